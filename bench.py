@@ -1,0 +1,151 @@
+#!/usr/bin/env python
+"""Headline benchmark: % partitions verified + partitions/s on the AC suite (BASELINE.json).
+
+Workload = the reference's ``src/AC`` experiment (Table V of the paper): the 12 Adult-census
+MLP architectures AC-1..AC-12, the full 16 000-partition grid per model (partition size 10),
+protected attribute ``sex``, 1 000 simulation points per partition, heuristic retry on
+UNKNOWN (HEURISTIC_PRUNE_THRESHOLD 5).  One *step* = verify the whole suite grid
+(192 000 partitions) once; with N GPUs the seeded partition order is sharded across the N
+ranks (strong scaling: total work fixed).  Weights are random-init (glorot-uniform, fixed
+seed) per BASELINE.json; ``--weights zoo`` uses the reference's trained weights instead.
+
+value  = decided partitions (SAT + UNSAT, every SAT confirmed exactly) per second, whole job.
+vs_baseline = value / 0.02497 decided partitions/s, the reference's AC/sex aggregate from
+Table V (553 decided in sum(#P x Total) = 22 144 s).
+
+    python bench.py --gpus 1 --steps 1 --warmup 1
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --steps 1 --warmup 1
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_DECIDED_PER_S = 553.0 / 22143.5
+METRIC = "% partitions verified + partitions/sec on AC suite at 1/2/4/8 MI355X"
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--preset", default="src/AC-sex")
+    ap.add_argument("--weights", default="random", choices=["random", "zoo"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--scope", default="suite", choices=["suite", "chunk"],
+                    help="suite: one step = whole grid of every model (strong scaling); "
+                         "chunk: one step = --chunk partitions per model per rank (weak scaling)")
+    ap.add_argument("--chunk", type=int, default=4096)
+    ap.add_argument("--node-budget", type=int, default=2048)
+    ap.add_argument("--sim-size", type=int, default=None)
+    ap.add_argument("--models", default=None, help="comma list (default: the preset's models)")
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+
+    import torch
+
+    from fairify_amd import presets
+    from fairify_amd.engine.pipeline import VerifyConfig, verify_chunk
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.ops.backend import Backend
+    from fairify_amd.parallel import dist as D
+    from fairify_amd.partition import processing_order
+
+    dev_type = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    info = D.init(dev_type)
+    pre = presets.get(args.preset)
+    grid = pre.grid()
+    q = pre.resolved()
+    order = processing_order(grid, seed=args.seed)
+    shard = order[info.rank::info.world]
+    names = args.models.split(",") if args.models else list(pre.models)
+    models = [get_model(n, weights=args.weights, seed=args.seed) for n in names]
+    backends = [Backend(m, device=info.device) for m in models]
+    cfg = VerifyConfig(sim_size=args.sim_size or pre.sim_size, seed=args.seed, chunk=args.chunk,
+                       soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
+                       node_budget=args.node_budget, heuristic=True, heuristic_p=pre.heuristic_p,
+                       heuristic_node_budget=args.node_budget)
+
+    def chunks_for_step(step: int):
+        if args.scope == "suite":
+            return [shard[s:s + args.chunk] for s in range(0, len(shard), args.chunk)]
+        n = len(shard)
+        start = (step * args.chunk) % max(1, n)
+        idx = (start + np.arange(args.chunk)) % max(1, n)
+        return [shard[idx]]
+
+    def run_step(step: int):
+        dec = att = sat = uns = 0
+        for m, be in zip(models, backends):
+            for ids in chunks_for_step(step):
+                recs = verify_chunk(be, m, q, grid, ids, cfg)
+                for r in recs:
+                    att += 1
+                    if r["verdict"] == "sat":
+                        sat += 1
+                    elif r["verdict"] == "unsat":
+                        uns += 1
+        dec = sat + uns
+        return np.array([att, dec, sat, uns], dtype=np.float64)
+
+    sync = (lambda: torch.cuda.synchronize(info.device)) if info.device.type == "cuda" else (lambda: None)
+    for w in range(args.warmup):
+        run_step(w)
+    sync()
+    D.barrier(info)
+    sync()
+    t0 = time.time()
+    tot = np.zeros(4)
+    for s in range(args.steps):
+        tot += run_step(args.warmup + s)
+    sync()
+    D.barrier(info)
+    sync()
+    dt = time.time() - t0
+    dt_max = D.all_reduce_max(info, dt)
+    tot = D.all_reduce_sum(info, tot)
+    att, dec, sat, uns = tot.tolist()
+    value = dec / dt_max if dt_max > 0 else 0.0
+    per_step = att / max(1, args.steps)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "decided partitions/s (SAT+UNSAT, whole job)",
+        "n_gpus": info.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * dt_max / max(1, args.steps), 3),
+        "higher_is_better": True,
+        "scaling": "strong" if args.scope == "suite" else "weak",
+        "vs_baseline": round(value / BASELINE_DECIDED_PER_S, 1),
+        "dtype": "fp32",
+        "data": f"synthetic: reference src/AC integer domain, {args.weights}-init AC-1..12 weights",
+        "config": {"model": f"AC suite ({','.join(names)})", "global_batch": int(per_step), "seq_len": None,
+                   "parallelism": f"dp{info.world}", "preset": args.preset, "grid_per_model": len(grid),
+                   "sim_size": cfg.sim_size, "node_budget": cfg.node_budget},
+        "pct_verified": round(100.0 * dec / max(1.0, att), 3),
+        "partitions_per_s": round(att / dt_max, 3) if dt_max > 0 else 0.0,
+        "sat": int(sat), "unsat": int(uns), "unknown": int(att - dec),
+        "baseline": {"decided_per_s": round(BASELINE_DECIDED_PER_S, 5), "pct_verified_of_attempted": 89.0,
+                     "coverage_of_grid_pct": 0.29},
+    }
+    if info.is_main:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    D.destroy(info)
+
+
+if __name__ == "__main__":
+    main()

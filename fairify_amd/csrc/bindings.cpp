@@ -1,0 +1,172 @@
+// pybind11 bindings of the fairify_amd HIP kernels (module fairify_amd._C).
+//
+// Tensors cross the boundary as raw device pointers (Python ints from Tensor.data_ptr()) plus
+// the caller's HIP stream (torch.cuda.current_stream().cuda_stream), so the extension has no
+// dependency on the torch C++ headers and launches onto whatever stream torch is using.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cmath>
+#include <cstdint>
+#include <stdexcept>
+#include <vector>
+
+#include "args.h"
+
+namespace py = pybind11;
+
+extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream);
+extern "C" int fa_forward_launch(const NetDesc& net, FwdArgs a, hipStream_t stream);
+extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream);
+extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
+
+template <typename T>
+static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+static float gamma_up(int k, double unit) {
+  const double ku = (k + 2) * unit;
+  return std::nextafter((float)(ku / (1.0 - ku)), INFINITY);
+}
+
+struct Net {
+  NetDesc d;
+  explicit Net(const std::vector<int>& dims, double unit) {
+    if (dims.size() < 2 || dims.size() > FA_MAX_LAYERS + 1) throw std::invalid_argument("bad layer count");
+    std::memset(&d, 0, sizeof(d));
+    d.n_layers = (int)dims.size() - 1;
+    int off = 0, noff = 0, mw = 0, mws = 0;
+    for (size_t i = 0; i < dims.size(); ++i) {
+      d.dims[i] = dims[i];
+      mw = std::max(mw, dims[i]);
+    }
+    for (int l = 0; l < d.n_layers; ++l) {
+      d.w_off[l] = off;
+      off += dims[l] * dims[l + 1];
+      d.b_off[l] = off;
+      off += dims[l + 1];
+      d.neuron_off[l] = noff;
+      noff += dims[l + 1];
+      mws = std::max(mws, dims[l] * dims[l + 1]);
+      d.g_gemm[l] = gamma_up(2 * dims[l] + 1, unit);
+      d.g_fwd[l] = gamma_up(dims[l] + 1, unit);
+    }
+    d.n_neurons = noff;
+    d.n_hidden = noff - dims.back();
+    d.max_width = mw;
+    d.max_wsize = mws;
+    d.unit = (float)unit;
+    d.g_conc = gamma_up(dims[0] + 1, unit);
+    n_params = off;
+  }
+  int n_params;
+};
+
+static void check(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + " launch failed, code " + std::to_string(rc));
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "fairify_amd CDNA4 (gfx950) kernels";
+  py::class_<Net>(m, "Net")
+      .def(py::init<const std::vector<int>&, double>())
+      .def_readonly("n_params", &Net::n_params)
+      .def_property_readonly("n_hidden", [](const Net& n) { return n.d.n_hidden; })
+      .def_property_readonly("n_neurons", [](const Net& n) { return n.d.n_neurons; });
+
+  m.def("bounds", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t dead_in, int R,
+                     int symbolic, uintptr_t out_lb, uintptr_t out_ub, uintptr_t Lc, uintptr_t L0, uintptr_t Le,
+                     uintptr_t Uc, uintptr_t U0, uintptr_t Ue, uintptr_t layer_lb, uintptr_t layer_ub,
+                     uintptr_t dead_out, int G, uintptr_t stream) {
+    NetDesc d = net.d;
+    d.g_conc = gamma_up(symbolic ? d.dims[0] + 1 : 1, d.unit);
+    BoundArgs a{};
+    a.flat = P<const float>(flat);
+    a.lo = P<const float>(lo);
+    a.hi = P<const float>(hi);
+    a.dead_in = P<const uint8_t>(dead_in);
+    a.R = R;
+    a.symbolic = symbolic;
+    a.G = G;
+    a.out_lb = P<float>(out_lb);
+    a.out_ub = P<float>(out_ub);
+    a.Lc = P<float>(Lc); a.L0 = P<float>(L0); a.Le = P<float>(Le);
+    a.Uc = P<float>(Uc); a.U0 = P<float>(U0); a.Ue = P<float>(Ue);
+    a.layer_lb = P<float>(layer_lb);
+    a.layer_ub = P<float>(layer_ub);
+    a.dead_out = P<uint8_t>(dead_out);
+    check(fa_bounds_launch(d, a, (hipStream_t)stream), "bounds");
+  });
+
+  m.def("forward", [](const Net& net, uintptr_t flat, uintptr_t x, int B, uintptr_t dead, uintptr_t out,
+                      uintptr_t stream) {
+    FwdArgs a{};
+    a.flat = P<const float>(flat);
+    a.x = P<const float>(x);
+    a.B = B;
+    a.dead = P<const uint8_t>(dead);
+    a.out = P<float>(out);
+    check(fa_forward_launch(net.d, a, (hipStream_t)stream), "forward");
+  });
+
+  m.def("sim", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t pids, int Pn, int n_samples,
+                  uint32_t seed, int V, const std::vector<int>& pa, uintptr_t values, int Pp, uintptr_t pairs,
+                  const std::vector<int>& ra, int tau, uintptr_t counts, uintptr_t found, uintptr_t wit_x,
+                  uintptr_t wit_xp, uintptr_t z0, uintptr_t stream) {
+    if (pa.size() > FA_MAX_PA || ra.size() > FA_MAX_RA) throw std::invalid_argument("too many PA/RA dims");
+    SimArgs a{};
+    a.flat = P<const float>(flat);
+    a.lo = P<const float>(lo);
+    a.hi = P<const float>(hi);
+    a.pids = P<const int64_t>(pids);
+    a.P = Pn;
+    a.n_samples = n_samples;
+    a.seed = seed;
+    a.V = V;
+    a.npa = (int)pa.size();
+    for (size_t i = 0; i < pa.size(); ++i) a.pa_idx[i] = pa[i];
+    a.values = P<const int64_t>(values);
+    a.Pp = Pp;
+    a.pairs = P<const int64_t>(pairs);
+    a.nra = (int)ra.size();
+    for (size_t i = 0; i < ra.size(); ++i) a.ra_idx[i] = ra[i];
+    a.tau = tau;
+    a.counts = P<int>(counts);
+    a.found = P<uint8_t>(found);
+    a.wit_x = P<float>(wit_x);
+    a.wit_xp = P<float>(wit_xp);
+    a.z0 = P<float>(z0);
+    check(fa_sim_launch(net.d, a, (hipStream_t)stream), "sim");
+  });
+
+  m.def("certify", [](int Nn, int n0, int V, int Pp, int norient, std::vector<uintptr_t> fx, std::vector<uintptr_t> fxp,
+                      uintptr_t xlo, uintptr_t xhi, uintptr_t xplo, uintptr_t xphi, uintptr_t pairs, uintptr_t values,
+                      const std::vector<int>& pa, uintptr_t shared, double unit, double gmarg, uintptr_t gmin,
+                      uintptr_t tstar, uintptr_t open, uintptr_t score, uintptr_t split_dim, uintptr_t cand_x,
+                      uintptr_t cand_xp, uintptr_t cand_v, uintptr_t cand_o, uintptr_t stream) {
+    if (pa.size() > FA_CMAX_PA) throw std::invalid_argument("too many PA dims");
+    if (fx.size() != 6 || fxp.size() != 6) throw std::invalid_argument("need 6 form pointers");
+    CertArgs a{};
+    a.Nn = Nn; a.n0 = n0; a.V = V; a.Pp = Pp; a.norient = norient;
+    a.Lc = P<const float>(fx[0]); a.L0 = P<const float>(fx[1]); a.Le = P<const float>(fx[2]);
+    a.Uc = P<const float>(fx[3]); a.U0 = P<const float>(fx[4]); a.Ue = P<const float>(fx[5]);
+    a.Lcp = P<const float>(fxp[0]); a.L0p = P<const float>(fxp[1]); a.Lep = P<const float>(fxp[2]);
+    a.Ucp = P<const float>(fxp[3]); a.U0p = P<const float>(fxp[4]); a.Uep = P<const float>(fxp[5]);
+    a.xlo = P<const float>(xlo); a.xhi = P<const float>(xhi);
+    a.xplo = P<const float>(xplo); a.xphi = P<const float>(xphi);
+    a.pairs = P<const int64_t>(pairs);
+    a.values = P<const int64_t>(values);
+    a.npa = (int)pa.size();
+    for (size_t i = 0; i < pa.size(); ++i) a.pa_idx[i] = pa[i];
+    a.shared = P<const uint8_t>(shared);
+    a.unit = (float)unit;
+    a.gmarg = std::nextafter((float)gmarg, INFINITY);
+    a.gmin = P<float>(gmin); a.tstar = P<float>(tstar);
+    a.open = P<uint8_t>(open); a.score = P<float>(score); a.split_dim = P<int64_t>(split_dim);
+    a.cand_x = P<float>(cand_x); a.cand_xp = P<float>(cand_xp);
+    a.cand_v = P<int64_t>(cand_v); a.cand_o = P<int64_t>(cand_o);
+    check(fa_certify_launch(a, (hipStream_t)stream), "certify");
+  });
+
+  m.def("arch", []() { return std::string("gfx950"); });
+}

@@ -1,0 +1,271 @@
+// Fused multi-layer bound propagation (IBP and forward-symbolic) on f32 MFMA.  gfx950.
+//
+// Replaces the reference's per-neuron Python triple loop `neuron_bounds`
+// (utils/prune.py:105-164) and its per-neuron Z3 "singular verification" (:276-364) with one
+// kernel over thousands of boxes; it is also the bounding primitive of the branch-and-bound
+// prover.  Algorithm and error accounting: ops/reference.py:bounds (same arithmetic).
+//
+// A workgroup (4 wave64) owns G box-rows.  Per row the linear forms U, L of the current layer
+// are kept in LDS as [2 blocks][rb rows][width] with rows = n0 coefficient rows (symbolic
+// mode only) + the constant row + the error row.  A layer is
+//     U' = [U | L] . [W+ ; W-]      L' = [L | U] . [W+ ; W-]
+// i.e. one GEMM of (G*2*rb) x (2*n_in) by (2*n_in) x n_out on v_mfma_f32_16x16x4_f32 with the
+// layer's W staged in LDS (W+/W- formed on the fly).  The error row rides along the same GEMM
+// (its second half is negated so it accumulates |W-|).  The epilogue (one thread per
+// (row, neuron)) concretises both forms over the box, applies the ReLU relaxation in place and
+// writes the error row for the next layer; only the logit forms (and, on request, per-neuron
+// bounds / dead flags) go back to HBM.
+#include "args.h"
+
+
+
+__global__ void __launch_bounds__(FA_THREADS)
+fa_bounds_kernel(NetDesc net, BoundArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int n0 = net.dims[0];
+  const int G = a.G;
+  const int nc = a.symbolic ? n0 + 1 : 1;      // coefficient rows incl. constant
+  const int rb = nc + 1;                        // + error row
+  const int crow = nc - 1;                      // constant row index
+  const int erow = nc;                          // error row index
+  const int S = a.stride;
+  float* s_lo = smem;                           // [G][n0]
+  float* s_hi = s_lo + G * n0;
+  float* s_m = s_hi + G * n0;
+  float* s_W = s_m + G * n0;                    // [n_in][wstride]
+  float* bufA = s_W + a.wfloats;
+  float* bufB = bufA + G * 2 * rb * S;
+  const int row0 = blockIdx.x * G;
+  const int tid = threadIdx.x;
+  const float unit = net.unit;
+
+  // ---- stage boxes
+  for (int i = tid; i < G * n0; i += FA_THREADS) {
+    int g = i / n0, d = i % n0;
+    int r = row0 + g;
+    float l = 0.f, h = 0.f;
+    if (r < a.R) { l = a.lo[(size_t)r * n0 + d]; h = a.hi[(size_t)r * n0 + d]; }
+    s_lo[i] = l; s_hi[i] = h; s_m[i] = fmaxf(fabsf(l), fabsf(h));
+  }
+  __syncthreads();
+  // ---- initial forms (layer-0 inputs): identity (symbolic) or [hi | lo] constants (IBP)
+  {
+    const float g0 = net.g_gemm[0];
+    for (int i = tid; i < G * 2 * rb * n0; i += FA_THREADS) {
+      int j = i % n0;
+      int rr = (i / n0) % rb;
+      int o = (i / (n0 * rb)) % 2;
+      int g = i / (n0 * rb * 2);
+      float v;
+      if (a.symbolic) {
+        if (rr < n0) v = (rr == j) ? 1.f : 0.f;
+        else if (rr == crow) v = 0.f;
+        else v = g0 * s_m[g * n0 + j];
+      } else {
+        float c = o == 0 ? s_hi[g * n0 + j] : s_lo[g * n0 + j];
+        v = (rr == crow) ? c : g0 * fabsf(c);
+      }
+      bufA[((g * 2 + o) * rb + rr) * S + j] = v;
+    }
+  }
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int M = G * 2 * rb;
+  for (int l = 0; l < net.n_layers; ++l) {
+    const int n_in = net.dims[l];
+    const int n_out = net.dims[l + 1];
+    const float* W = a.flat + net.w_off[l];
+    const float* bias = a.flat + net.b_off[l];
+    const int ws = a.wstride;
+    for (int i = tid; i < n_in * n_out; i += FA_THREADS) {
+      int k = i / n_out, j = i % n_out;
+      s_W[k * ws + j] = W[i];
+    }
+    __syncthreads();
+    // ---------------- GEMM on MFMA
+    const int mtiles = (M + 15) >> 4;
+    const int ntiles = (n_out + 15) >> 4;
+    for (int t = wave; t < mtiles * ntiles; t += 4) {
+      const int mt = t / ntiles, nt = t % ntiles;
+      const int m = mt * 16 + (lane & 15);
+      const int kq = lane >> 4;
+      const bool mval = m < M;
+      const int g = m / (2 * rb);
+      const int rem = m - g * 2 * rb;
+      const int o = rem / rb;
+      const int r = rem - o * rb;
+      const float* a_own = bufA + ((g * 2 + o) * rb + r) * S;
+      const float* a_oth = bufA + ((g * 2 + (1 - o)) * rb + r) * S;
+      const float sgn = (r == erow) ? -1.f : 1.f;
+      const int j = nt * 16 + (lane & 15);
+      const bool jval = j < n_out;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < n_in; k0 += 4) {
+        const int k = k0 + kq;
+        const bool kv = k < n_in;
+        float av = (mval && kv) ? a_own[k] : 0.f;
+        float wv = (jval && kv) ? s_W[k * ws + j] : 0.f;
+        acc = fa_mfma4(av, fmaxf(wv, 0.f), acc);
+      }
+      for (int k0 = 0; k0 < n_in; k0 += 4) {
+        const int k = k0 + kq;
+        const bool kv = k < n_in;
+        float av = (mval && kv) ? sgn * a_oth[k] : 0.f;
+        float wv = (jval && kv) ? s_W[k * ws + j] : 0.f;
+        acc = fa_mfma4(av, fminf(wv, 0.f), acc);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mr = mt * 16 + (lane >> 4) * 4 + i;
+        if (mr < M && jval) {
+          const int gg = mr / (2 * rb);
+          const int rm = mr - gg * 2 * rb;
+          const int oo = rm / rb;
+          const int rr = rm - oo * rb;
+          bufB[((gg * 2 + oo) * rb + rr) * S + j] = acc[i];
+        }
+      }
+    }
+    __syncthreads();
+    // ---------------- epilogue: concretise, relax, next-layer error rows
+    const bool last = (l == net.n_layers - 1);
+    const float gg_ = net.g_gemm[l];
+    const float gc = net.g_conc;
+    const float gnext = last ? 0.f : net.g_gemm[l + 1];
+    const int noff = net.neuron_off[l];
+    for (int it = tid; it < G * n_out; it += FA_THREADS) {
+      const int g = it / n_out, j = it % n_out;
+      const int rglob = row0 + g;
+      const bool rv = rglob < a.R;
+      float* cu = bufB + ((g * 2 + 0) * rb) * S + j;
+      float* cl = bufB + ((g * 2 + 1) * rb) * S + j;
+      const float* glo = s_lo + g * n0;
+      const float* ghi = s_hi + g * n0;
+      const float* gm = s_m + g * n0;
+      const float b = bias[j];
+      const float cU = cu[crow * S] + b, cL = cl[crow * S] + b;
+      float mnU = cU, mxU = cU, mgU = fabsf(cU);
+      float mnL = cL, mxL = cL, mgL = fabsf(cL);
+      if (a.symbolic) {
+        for (int i = 0; i < n0; ++i) {
+          const float u = cu[i * S], v = cl[i * S];
+          const float ul = u * glo[i], uh = u * ghi[i];
+          const float vl = v * glo[i], vh = v * ghi[i];
+          mnU += fminf(ul, uh); mxU += fmaxf(ul, uh); mgU += fabsf(u) * gm[i];
+          mnL += fminf(vl, vh); mxL += fmaxf(vl, vh); mgL += fabsf(v) * gm[i];
+        }
+      }
+      const float eU = cu[erow * S] * (1.f + 2.f * gg_) + gg_ * fabsf(b);
+      const float eL = cl[erow * S] * (1.f + 2.f * gg_) + gg_ * fabsf(b);
+      const float ub = mxU + gc * mgU + eU;
+      const float lb = mnL - gc * mgL - eL;
+      if (rv && a.layer_lb) {
+        a.layer_lb[(size_t)rglob * net.n_neurons + noff + j] = lb;
+        a.layer_ub[(size_t)rglob * net.n_neurons + noff + j] = ub;
+      }
+      if (last) {
+        if (rv) {
+          a.out_lb[rglob] = lb;
+          a.out_ub[rglob] = ub;
+          if (a.symbolic) {
+            for (int i = 0; i < n0; ++i) {
+              a.Lc[(size_t)rglob * n0 + i] = cl[i * S];
+              a.Uc[(size_t)rglob * n0 + i] = cu[i * S];
+            }
+            a.L0[rglob] = cL; a.Le[rglob] = eL;
+            a.U0[rglob] = cU; a.Ue[rglob] = eU;
+          }
+        }
+        continue;
+      }
+      bool forced = false;
+      if (a.dead_in && rv) forced = a.dead_in[(size_t)rglob * net.n_hidden + noff + j] != 0;
+      if (rv && a.dead_out) a.dead_out[(size_t)rglob * net.n_hidden + noff + j] = (ub <= 0.f) ? 1 : 0;
+      // upper relaxation: chord over [aa, ub] of T(x) = U(x) + eU
+      const float aa = mnU - gc * mgU + eU;
+      const bool zeroU = (ub <= 0.f) || forced;
+      const bool identU = !zeroU && (aa >= 0.f);
+      float s = 1.f, shift = 0.f, eUn, mgUn = 0.f;
+      if (zeroU) {
+        for (int i = 0; i < nc; ++i) cu[i * S] = 0.f;
+        eUn = 0.f;
+      } else if (identU) {
+        cu[crow * S] = cU;
+        eUn = eU;
+        mgUn = mgU;
+      } else {
+        s = (ub / (ub - aa)) * (1.f + 4.f * unit);
+        shift = eU - aa;
+        for (int i = 0; i < nc - 1; ++i) {
+          const float v = cu[i * S] * s;
+          cu[i * S] = v;
+          mgUn += fabsf(v) * gm[i];
+        }
+        const float c = cU * s + s * shift;
+        cu[crow * S] = c;
+        mgUn += fabsf(c);
+        eUn = 4.f * unit * s * (mgU + fabsf(shift));
+      }
+      // lower relaxation: lambda in {0,1} applied to L(x) - eL
+      const float aL = mnL - gc * mgL - eL;
+      const float bL = mxL + gc * mgL - eL;
+      const bool lam1 = !forced && ((aL >= 0.f) || ((bL > 0.f) && (bL > -aL)));
+      float eLn, mgLn = 0.f;
+      if (lam1) {
+        cl[crow * S] = cL;
+        eLn = eL;
+        mgLn = mgL;
+      } else {
+        for (int i = 0; i < nc; ++i) cl[i * S] = 0.f;
+        eLn = 0.f;
+      }
+      cu[erow * S] = eUn + gnext * mgUn;
+      cl[erow * S] = eLn + gnext * mgLn;
+    }
+    __syncthreads();
+    float* tmp = bufA; bufA = bufB; bufB = tmp;
+  }
+}
+
+extern "C" size_t fa_bounds_smem(const NetDesc& net, int symbolic, int G, int* stride, int* wstride,
+                                 int* wfloats) {
+  const int n0 = net.dims[0];
+  const int rb = (symbolic ? n0 + 1 : 1) + 1;
+  const int S = net.max_width | 1;            // odd stride: conflict-free column reads
+  int ws = 1;
+  for (int l = 0; l < net.n_layers; ++l) ws = ws > net.dims[l + 1] ? ws : net.dims[l + 1];
+  ws |= 1;
+  int wsz = 0;
+  for (int l = 0; l < net.n_layers; ++l) wsz = wsz > net.dims[l] * ws ? wsz : net.dims[l] * ws;
+  wsz = (wsz + 3) & ~3;
+  *stride = S;
+  *wstride = ws;
+  *wfloats = wsz;
+  size_t floats = 3 * (size_t)G * n0 + (size_t)wsz + 2 * (size_t)G * 2 * rb * S;
+  floats = (floats + 3) & ~(size_t)3;
+  return floats * sizeof(float);
+}
+
+extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream) {
+  if (args.R <= 0) return 0;
+  const size_t limit = 160 * 1024;
+  int G = args.G > 0 ? args.G : 16;
+  int S = 0, ws = 0, wf = 0;
+  size_t bytes = 0;
+  for (;;) {
+    bytes = fa_bounds_smem(net, args.symbolic, G, &S, &ws, &wf);
+    if (bytes <= 64 * 1024 || G == 1) break;
+    G--;
+  }
+  if (bytes > limit) return -1;
+  args.G = G;
+  args.stride = S;
+  args.wstride = ws;
+  args.wfloats = wf;
+  if (bytes > 64 * 1024)
+    FA_CHECK(hipFuncSetAttribute((const void*)fa_bounds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)bytes));
+  dim3 grid((args.R + G - 1) / G);
+  hipLaunchKernelGGL(fa_bounds_kernel, grid, dim3(FA_THREADS), bytes, stream, net, args);
+  return (int)hipGetLastError();
+}

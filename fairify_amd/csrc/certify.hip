@@ -1,0 +1,193 @@
+// Branch-and-bound node test: fairness-pair LP certificate (ops/reference.py:pair_certify).
+//
+// fa_pair_eval_kernel : one thread per (node, PA pair, orientation) evaluates the convex
+//                       piecewise-linear certificate g(t) at t in {0, 1} and at every breakpoint
+//                       of the shared-feature coefficients and keeps min_t g(t) and its argmin.
+// fa_pair_pick_kernel : one thread per node picks the most violating pair/orientation, and for
+//                       it emits the split dimension (largest |coef| x width contribution) and
+//                       the candidate vertex pair (x, x') that maximises the objective.
+#include "args.h"
+
+
+
+
+// Folded form of one row: coefficient i (0 on PA dims), constant (incl. err sign and PA terms),
+// |PA contribution| for the rounding margin.
+struct Form {
+  const float* c;
+  float c0;
+  float fmag;
+};
+
+__device__ __forceinline__ bool fa_is_pa(const CertArgs& a, int d) {
+  for (int k = 0; k < a.npa; ++k)
+    if (a.pa_idx[k] == d) return true;
+  return false;
+}
+
+__device__ __forceinline__ Form fa_fold(const CertArgs& a, const float* C, float c0, int v) {
+  Form f;
+  f.c = C;
+  float contrib = 0.f;
+  for (int k = 0; k < a.npa; ++k) contrib += C[a.pa_idx[k]] * (float)a.values[v * a.npa + k];
+  f.c0 = c0 + contrib;
+  f.fmag = fabsf(contrib);
+  return f;
+}
+
+// A / B forms of pair q (orientation o) of node n, with sign applied through sA / sB.
+__device__ __forceinline__ void fa_pair_forms(const CertArgs& a, int n, int q, int o, Form& A, float& sA,
+                                              Form& B, float& sB) {
+  const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+  const size_t ri = (size_t)n * a.V + vi, rj = (size_t)n * a.V + vj;
+  if (o == 0) {  // t * (-(L_v(x) - eL)) + (1-t) * (U_v'(x') + eU)
+    A = fa_fold(a, a.Lc + ri * a.n0, a.L0[ri] - a.Le[ri], vi);
+    sA = -1.f;
+    B = fa_fold(a, a.Ucp + rj * a.n0, a.U0p[rj] + a.Uep[rj], vj);
+    sB = 1.f;
+  } else {       // t * (U_v(x) + eU) + (1-t) * (-(L_v'(x') - eL))
+    A = fa_fold(a, a.Uc + ri * a.n0, a.U0[ri] + a.Ue[ri], vi);
+    sA = 1.f;
+    B = fa_fold(a, a.Lcp + rj * a.n0, a.L0p[rj] - a.Lep[rj], vj);
+    sB = -1.f;
+  }
+}
+
+__device__ float fa_g_at(const CertArgs& a, int n, const Form& A, float sA, const Form& B, float sB, float t,
+                         float magA, float magB) {
+  const float* xl = a.xlo + (size_t)n * a.n0;
+  const float* xh = a.xhi + (size_t)n * a.n0;
+  const float* pl = a.xplo + (size_t)n * a.n0;
+  const float* ph = a.xphi + (size_t)n * a.n0;
+  float val = 0.f;
+  for (int i = 0; i < a.n0; ++i) {
+    const float ai = fa_is_pa(a, i) ? 0.f : sA * A.c[i];
+    const float bi = fa_is_pa(a, i) ? 0.f : sB * B.c[i];
+    if (a.shared[i]) {
+      const float cs = t * ai + (1.f - t) * bi;
+      val += fmaxf(cs * xl[i], cs * xh[i]);
+    } else {
+      const float ca = t * ai, cb = (1.f - t) * bi;
+      val += fmaxf(ca * xl[i], ca * xh[i]) + fmaxf(cb * pl[i], cb * ph[i]);
+    }
+  }
+  const float A0 = sA * A.c0, B0 = sB * B.c0;
+  float g = val + t * A0 + (1.f - t) * B0;
+  g += a.gmarg * (t * magA + (1.f - t) * magB) + 8.f * a.unit * (magA + magB);
+  return g;
+}
+
+__device__ void fa_mags(const CertArgs& a, int n, const Form& A, const Form& B, float& magA, float& magB) {
+  const float* xl = a.xlo + (size_t)n * a.n0;
+  const float* xh = a.xhi + (size_t)n * a.n0;
+  const float* pl = a.xplo + (size_t)n * a.n0;
+  const float* ph = a.xphi + (size_t)n * a.n0;
+  magA = fabsf(A.c0) + A.fmag;
+  magB = fabsf(B.c0) + B.fmag;
+  for (int i = 0; i < a.n0; ++i) {
+    if (fa_is_pa(a, i)) continue;
+    magA += fabsf(A.c[i]) * fmaxf(fabsf(xl[i]), fabsf(xh[i]));
+    magB += fabsf(B.c[i]) * fmaxf(fabsf(pl[i]), fabsf(ph[i]));
+  }
+}
+
+__global__ void __launch_bounds__(FA_THREADS) fa_pair_eval_kernel(CertArgs a) {
+  const int Q = a.Pp * a.norient;
+  const int64_t idx = (int64_t)blockIdx.x * FA_THREADS + threadIdx.x;
+  if (idx >= (int64_t)a.Nn * Q) return;
+  const int n = (int)(idx / Q);
+  const int qq = (int)(idx % Q);
+  const int o = qq / a.Pp, q = qq % a.Pp;
+  Form A, B;
+  float sA, sB;
+  fa_pair_forms(a, n, q, o, A, sA, B, sB);
+  float magA, magB;
+  fa_mags(a, n, A, B, magA, magB);
+  // candidate t: 0, 1, breakpoints of shared dims (invalid -> 0 like the reference clamp)
+  float best = fa_g_at(a, n, A, sA, B, sB, 0.f, magA, magB);
+  float bt = 0.f;
+  {
+    const float g1 = fa_g_at(a, n, A, sA, B, sB, 1.f, magA, magB);
+    if (g1 < best) { best = g1; bt = 1.f; }
+  }
+  for (int i = 0; i < a.n0; ++i) {
+    if (!a.shared[i] || fa_is_pa(a, i)) continue;
+    const float ai = sA * A.c[i], bi = sB * B.c[i];
+    const float den = ai - bi;
+    if (den == 0.f) continue;
+    float t = -bi / den;
+    if (!(t > 0.f && t < 1.f)) continue;
+    const float g = fa_g_at(a, n, A, sA, B, sB, t, magA, magB);
+    if (g < best) { best = g; bt = t; }
+  }
+  a.gmin[idx] = best;
+  a.tstar[idx] = bt;
+}
+
+__global__ void __launch_bounds__(FA_THREADS) fa_pair_pick_kernel(CertArgs a) {
+  const int n = blockIdx.x * FA_THREADS + threadIdx.x;
+  if (n >= a.Nn) return;
+  const int Q = a.Pp * a.norient;
+  float bg = -INFINITY;
+  int bq = 0;
+  for (int qq = 0; qq < Q; ++qq) {
+    const float g = a.gmin[(size_t)n * Q + qq];
+    if (g > bg) { bg = g; bq = qq; }
+  }
+  const int o = bq / a.Pp, q = bq % a.Pp;
+  const float t = a.tstar[(size_t)n * Q + bq];
+  Form A, B;
+  float sA, sB;
+  fa_pair_forms(a, n, q, o, A, sA, B, sB);
+  const float* xl = a.xlo + (size_t)n * a.n0;
+  const float* xh = a.xhi + (size_t)n * a.n0;
+  const float* pl = a.xplo + (size_t)n * a.n0;
+  const float* ph = a.xphi + (size_t)n * a.n0;
+  float bs = -1.f;
+  int bd = 0;
+  for (int i = 0; i < a.n0; ++i) {
+    const float ai = fa_is_pa(a, i) ? 0.f : sA * A.c[i];
+    const float bi = fa_is_pa(a, i) ? 0.f : sB * B.c[i];
+    const float wx = xh[i] - xl[i];
+    const float cs = t * ai + (1.f - t) * bi;
+    float sx;
+    float cx;
+    if (a.shared[i]) {
+      sx = fabsf(cs) * wx;
+      cx = cs > 0.f ? xh[i] : xl[i];
+    } else {
+      sx = fabsf(t * ai) * wx;
+      cx = (t * ai > 0.f) ? xh[i] : xl[i];
+    }
+    sx += 1e-9f * wx;
+    if (sx > bs) { bs = sx; bd = i; }
+    a.cand_x[(size_t)n * a.n0 + i] = cx;
+    float cxp = cx;
+    if (!a.shared[i]) cxp = ((1.f - t) * bi > 0.f) ? ph[i] : pl[i];
+    a.cand_xp[(size_t)n * a.n0 + i] = cxp;
+  }
+  for (int i = 0; i < a.n0; ++i) {
+    float sxp = 0.f;
+    if (!a.shared[i]) {
+      const float bi = fa_is_pa(a, i) ? 0.f : sB * B.c[i];
+      const float wxp = ph[i] - pl[i];
+      sxp = fabsf((1.f - t) * bi) * wxp + 1e-9f * wxp;
+    }
+    if (sxp > bs) { bs = sxp; bd = a.n0 + i; }
+  }
+  a.open[n] = bg > 0.f ? 1 : 0;
+  a.score[n] = bg;
+  a.split_dim[n] = bd;
+  a.cand_v[n] = q;
+  a.cand_o[n] = o;
+}
+
+extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream) {
+  if (a.Nn <= 0) return 0;
+  if (a.npa > FA_CMAX_PA) return -3;
+  const int64_t tot = (int64_t)a.Nn * a.Pp * a.norient;
+  hipLaunchKernelGGL(fa_pair_eval_kernel, dim3((unsigned)((tot + FA_THREADS - 1) / FA_THREADS)), dim3(FA_THREADS), 0,
+                     stream, a);
+  hipLaunchKernelGGL(fa_pair_pick_kernel, dim3((a.Nn + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, a);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,62 @@
+// Shared device helpers for the fairify_amd CDNA4 (gfx950) kernels.
+//
+// Network descriptor, the counter-based RNG shared with ops/reference.py, and the f32 MFMA
+// wrapper.  All kernels use 256-thread workgroups = 4 wave64s.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FA_MAX_LAYERS 16
+#define FA_THREADS 256
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct NetDesc {
+  int n_layers;                       // number of weight layers L (last = linear logit)
+  int dims[FA_MAX_LAYERS + 1];        // dims[0] = n0 ; dims[l+1] = width of layer l
+  int w_off[FA_MAX_LAYERS];           // offset of W_l ([dims[l], dims[l+1]] row-major) in flat
+  int b_off[FA_MAX_LAYERS];           // offset of b_l in flat
+  int neuron_off[FA_MAX_LAYERS];      // first index of layer l in the all-neuron numbering
+  int n_hidden;                       // sum of hidden widths
+  int n_neurons;                      // n_hidden + 1
+  int max_width;                      // max(dims[0..L])
+  int max_wsize;                      // max dims[l]*dims[l+1]
+  float unit;                         // unit roundoff of the arithmetic (2^-24)
+  float g_gemm[FA_MAX_LAYERS];        // gamma for the layer-l GEMM (K = 2*dims[l] + 1)
+  float g_conc;                       // gamma for concretisation sums (K = rows per form)
+  float g_fwd[FA_MAX_LAYERS];         // gamma for the plain forward (K = dims[l] + 1)
+};
+
+// lowbias32 (Wellons) — identical to ops/reference.py:hash32
+__device__ __forceinline__ uint32_t fa_hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// ops/reference.py:rng_u32 (seed, partition id, sample index, feature index)
+__device__ __forceinline__ uint32_t fa_rng(uint32_t seed, int64_t pid, int64_t sample, int dim) {
+  uint32_t h = fa_hash32((uint32_t)((uint64_t)(sample * 64 + dim) & 0xFFFFFFFFull) ^ seed);
+  h = fa_hash32(h ^ (uint32_t)((uint64_t)pid & 0xFFFFFFFFull));
+  h = fa_hash32(h ^ (uint32_t)(((uint64_t)pid >> 32) & 0xFFFFFFFFull) ^ 0x5BD1E995u);
+  return h;
+}
+
+// One v_mfma_f32_16x16x4_f32: exact f32 fma chain.  Lane l supplies A[l&15][l>>4] and
+// B[l>>4][l&15]; D reg i is row (l>>4)*4+i, column l&15.
+__device__ __forceinline__ f32x4 fa_mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+#define FA_CHECK(x)                                                              \
+  do {                                                                           \
+    hipError_t e__ = (x);                                                        \
+    if (e__ != hipSuccess) {                                                     \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e__), __FILE__, \
+              __LINE__);                                                         \
+      abort();                                                                   \
+    }                                                                            \
+  } while (0)

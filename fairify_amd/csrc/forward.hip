@@ -1,0 +1,230 @@
+// Concrete MLP forward on f32 MFMA + the fused simulation/falsification kernel.  gfx950.
+//
+// fa_forward_kernel : logits of arbitrary rows (candidate replay, accuracy, hybrid routing,
+//                     causal testing; K7), with optional per-row dead-neuron masks
+//                     (heuristically pruned networks).
+// fa_sim_kernel     : one workgroup per partition; draws `S` lattice points with the counter
+//                     RNG (never written to HBM), counts per-neuron activations (reference
+//                     `candidate_dead_nodes`, utils/prune.py:168-192), re-evaluates each point
+//                     under every protected-attribute value (+ relaxed offsets) and records the
+//                     first strict sign flip (K3 + K8 fused).
+//
+// A 64-row tile goes through all layers in LDS; each layer is a 64 x n_in x n_out GEMM on
+// v_mfma_f32_16x16x4_f32 with bias / ReLU / mask / activation counting fused into the
+// accumulator epilogue (counts reduced across the 4 row-groups of a wave with shuffles, one LDS
+// atomic per column per tile).
+#include "args.h"
+
+#define FA_TR 64
+
+// rows [FA_TR][S] in bufA (cols 0..n0-1) -> logits in zout[FA_TR]; bufA/bufB clobbered.
+__device__ void fa_tile_forward(const NetDesc& net, const float* __restrict__ flat, float* bufA, float* bufB,
+                                int S, int nvalid, const uint8_t* __restrict__ dead_rows, int dead_stride,
+                                int* counts, float* zout) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  for (int l = 0; l < net.n_layers; ++l) {
+    const int n_in = net.dims[l];
+    const int n_out = net.dims[l + 1];
+    const float* __restrict__ W = flat + net.w_off[l];
+    const float* __restrict__ bias = flat + net.b_off[l];
+    const bool last = (l == net.n_layers - 1);
+    const int noff = net.neuron_off[l];
+    const int ntiles = (n_out + 15) >> 4;
+    for (int t = wave; t < 4 * ntiles; t += 4) {
+      const int mt = t / ntiles, nt = t % ntiles;
+      const int m = mt * 16 + (lane & 15);
+      const int kq = lane >> 4;
+      const int j = nt * 16 + (lane & 15);
+      const bool jval = j < n_out;
+      const float* arow = bufA + m * S;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < n_in; k0 += 4) {
+        const int k = k0 + kq;
+        const bool kv = k < n_in;
+        const float av = kv ? arow[k] : 0.f;
+        const float wv = (kv && jval) ? W[k * n_out + j] : 0.f;
+        acc = fa_mfma4(av, wv, acc);
+      }
+      const float b = jval ? bias[j] : 0.f;
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = mt * 16 + (lane >> 4) * 4 + i;
+        float v = acc[i] + b;
+        if (!last) {
+          v = fmaxf(v, 0.f);
+          if (dead_rows && jval && r < nvalid && dead_rows[(size_t)r * dead_stride + noff + j]) v = 0.f;
+        }
+        if (jval) {
+          if (last) zout[r] = v;
+          else bufB[r * S + j] = v;
+          cnt += (r < nvalid && v != 0.f) ? 1 : 0;
+        }
+      }
+      if (counts) {
+        cnt += __shfl_xor(cnt, 16);
+        cnt += __shfl_xor(cnt, 32);
+        if (lane < 16 && jval) atomicAdd(&counts[noff + j], cnt);
+      }
+    }
+    __syncthreads();
+    float* tmp = bufA; bufA = bufB; bufB = tmp;
+  }
+}
+
+
+
+__global__ void __launch_bounds__(FA_THREADS) fa_forward_kernel(NetDesc net, FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int S = a.S;
+  float* bufA = smem;
+  float* bufB = bufA + FA_TR * S;
+  float* z = bufB + FA_TR * S;
+  const int n0 = net.dims[0];
+  const int r0 = blockIdx.x * FA_TR;
+  const int nvalid = min(FA_TR, a.B - r0);
+  for (int i = threadIdx.x; i < FA_TR * n0; i += FA_THREADS) {
+    const int r = i / n0, d = i % n0;
+    bufA[r * S + d] = (r < nvalid) ? a.x[(size_t)(r0 + r) * n0 + d] : 0.f;
+  }
+  __syncthreads();
+  fa_tile_forward(net, a.flat, bufA, bufB, S, nvalid, a.dead ? a.dead + (size_t)r0 * net.n_hidden : nullptr,
+                  net.n_hidden, nullptr, z);
+  for (int i = threadIdx.x; i < nvalid; i += FA_THREADS) a.out[r0 + i] = z[i];
+}
+
+extern "C" int fa_forward_launch(const NetDesc& net, FwdArgs a, hipStream_t stream) {
+  if (a.B <= 0) return 0;
+  a.S = net.max_width | 1;
+  size_t bytes = (2 * (size_t)FA_TR * a.S + FA_TR) * sizeof(float);
+  if (bytes > 64 * 1024)
+    FA_CHECK(hipFuncSetAttribute((const void*)fa_forward_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)bytes));
+  hipLaunchKernelGGL(fa_forward_kernel, dim3((a.B + FA_TR - 1) / FA_TR), dim3(FA_THREADS), bytes, stream, net, a);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+#define FA_MAX_V 64
+
+
+
+__device__ __forceinline__ float fa_sample_coord(uint32_t seed, int64_t pid, int s, int d, float lo, float hi) {
+  const uint32_t h = fa_rng(seed, pid, s, d);
+  const uint32_t w = (uint32_t)(hi - lo) + 1u;
+  return lo + (float)(h % w);
+}
+
+__global__ void __launch_bounds__(FA_THREADS) fa_sim_kernel(NetDesc net, SimArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int S = a.S;
+  const int n0 = net.dims[0];
+  const int p = blockIdx.x;
+  const int tid = threadIdx.x;
+  float* bufA = smem;
+  float* bufB = bufA + FA_TR * S;
+  float* X = bufB + FA_TR * S;              // [FA_TR][n0]
+  float* z = X + FA_TR * n0;                // [FA_TR][V]
+  float* zp = z + FA_TR * a.V;              // [FA_TR][V]
+  float* zt = zp + FA_TR * a.V;             // [FA_TR]
+  float* s_lo = zt + FA_TR;                 // [n0]
+  float* s_hi = s_lo + n0;
+  int* cnt = (int*)(s_hi + n0);             // [n_neurons]
+  int* best = cnt + net.n_neurons;          // [1]
+  const int64_t pid = a.pids[p];
+  for (int i = tid; i < n0; i += FA_THREADS) {
+    s_lo[i] = a.lo[(size_t)p * n0 + i];
+    s_hi[i] = a.hi[(size_t)p * n0 + i];
+  }
+  for (int i = tid; i < net.n_neurons; i += FA_THREADS) cnt[i] = 0;
+  if (tid == 0) best[0] = 0x7FFFFFFF;
+  __syncthreads();
+  const uint32_t seed_ra = a.seed ^ 0x2545F491u;
+  for (int s0 = 0; s0 < a.n_samples; s0 += FA_TR) {
+    const int nvalid = min(FA_TR, a.n_samples - s0);
+    for (int i = tid; i < FA_TR * n0; i += FA_THREADS) {
+      const int r = i / n0, d = i % n0;
+      const float v = fa_sample_coord(a.seed, pid, s0 + r, d, s_lo[d], s_hi[d]);
+      X[i] = v;
+      bufA[r * S + d] = v;
+    }
+    __syncthreads();
+    // profile pass (reference semantics: the sampled PA value)
+    fa_tile_forward(net, a.flat, bufA, bufB, S, nvalid, nullptr, 0, cnt, zt);
+    // falsification: every PA assignment (x) and, for relaxed queries, every x' variant
+    const int passes = a.nra > 0 ? 2 : 1;
+    for (int ps = 0; ps < passes; ++ps) {
+      for (int v = 0; v < a.V; ++v) {
+        for (int i = tid; i < FA_TR * n0; i += FA_THREADS) {
+          const int r = i / n0, d = i % n0;
+          float val = X[i];
+          for (int k = 0; k < a.npa; ++k)
+            if (a.pa_idx[k] == d) val = (float)a.values[v * a.npa + k];
+          if (ps == 1) {
+            for (int k = 0; k < a.nra; ++k)
+              if (a.ra_idx[k] == d) {
+                const uint32_t h = fa_rng(seed_ra, pid, s0 + r, d);
+                val += (float)(h % (uint32_t)(2 * a.tau + 1)) - (float)a.tau;
+              }
+          }
+          bufA[r * S + d] = val;
+        }
+        __syncthreads();
+        float* zdst = (ps == 0) ? z : zp;
+        fa_tile_forward(net, a.flat, bufA, bufB, S, nvalid, nullptr, 0, nullptr, zt);
+        for (int r = tid; r < FA_TR; r += FA_THREADS) zdst[r * a.V + v] = zt[r];
+        __syncthreads();
+      }
+    }
+    const float* zq = (a.nra > 0) ? zp : z;
+    if (a.z0)
+      for (int r = tid; r < nvalid; r += FA_THREADS) a.z0[(size_t)p * a.n_samples + s0 + r] = z[r * a.V];
+    for (int i = tid; i < nvalid * a.Pp; i += FA_THREADS) {
+      const int r = i / a.Pp, q = i % a.Pp;
+      const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+      const float zi = z[r * a.V + vi], zj = zq[r * a.V + vj];
+      if ((zi < 0.f && zj > 0.f) || (zi > 0.f && zj < 0.f)) atomicMin(best, (s0 + r) * a.Pp + q);
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < net.n_neurons; i += FA_THREADS) a.counts[(size_t)p * net.n_neurons + i] = cnt[i];
+  const int key = best[0];
+  if (tid == 0) a.found[p] = key != 0x7FFFFFFF;
+  if (key != 0x7FFFFFFF) {
+    const int s = key / a.Pp, q = key % a.Pp;
+    const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+    for (int d = tid; d < n0; d += FA_THREADS) {
+      const float base = fa_sample_coord(a.seed, pid, s, d, s_lo[d], s_hi[d]);
+      float x = base, xp = base;
+      for (int k = 0; k < a.npa; ++k)
+        if (a.pa_idx[k] == d) {
+          x = (float)a.values[vi * a.npa + k];
+          xp = (float)a.values[vj * a.npa + k];
+        }
+      for (int k = 0; k < a.nra; ++k)
+        if (a.ra_idx[k] == d) {
+          const uint32_t h = fa_rng(seed_ra, pid, s, d);
+          xp += (float)(h % (uint32_t)(2 * a.tau + 1)) - (float)a.tau;
+        }
+      a.wit_x[(size_t)p * n0 + d] = x;
+      a.wit_xp[(size_t)p * n0 + d] = xp;
+    }
+  }
+}
+
+extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) {
+  if (a.P <= 0) return 0;
+  if (a.npa > FA_MAX_PA || a.nra > FA_MAX_RA) return -3;
+  a.S = net.max_width | 1;
+  const int n0 = net.dims[0];
+  size_t floats = 2 * (size_t)FA_TR * a.S + (size_t)FA_TR * n0 + 2 * (size_t)FA_TR * a.V + FA_TR + 2 * n0;
+  size_t bytes = floats * sizeof(float) + (net.n_neurons + 4) * sizeof(int);
+  bytes = (bytes + 15) & ~(size_t)15;
+  if (bytes > 160 * 1024) return -1;
+  if (bytes > 64 * 1024)
+    FA_CHECK(hipFuncSetAttribute((const void*)fa_sim_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  hipLaunchKernelGGL(fa_sim_kernel, dim3(a.P), dim3(FA_THREADS), bytes, stream, net, a);
+  return (int)hipGetLastError();
+}

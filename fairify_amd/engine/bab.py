@@ -1,0 +1,336 @@
+"""Batched branch-and-bound decision procedure for the fairness query (K8 + K9).
+
+The reference decides a partition with one Z3 ``check()`` under a soft timeout
+(src/AC/Verify-AC.py:127-163).  Z3 is not part of this framework; instead every partition of a
+chunk is decided *together* by a device-resident branch-and-bound over the integer lattice:
+
+* a node is an integer sub-box of the partition (plus, for relaxed attributes, a box for x');
+* its rows (one per protected-attribute assignment v) are bounded with the symbolic bound
+  propagation kernel, and :func:`pair_certify` proves "no violating pair inside" (node closed)
+  or returns the most violating pair, a split dimension and a candidate vertex pair;
+* candidates are evaluated with the fp32 forward + rounding bound and confirmed exactly on the
+  host (``engine.exact``), so SAT answers are true counterexamples;
+* leaves are single lattice points, evaluated exactly — the procedure is complete on the finite
+  domain, budgets (nodes per partition, wall clock) turn the remainder into UNKNOWN.
+
+All node bookkeeping is tensor code on the device; the only host round trip per iteration is
+the (tiny) SAT-candidate list.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..models.mlp import MLP
+from ..ops.backend import Backend
+from ..spec import ResolvedQuery
+from . import exact
+
+UNKNOWN, SAT, UNSAT, RUNNING = 0, 1, 2, 3
+VERDICT_NAMES = {UNKNOWN: "unknown", SAT: "sat", UNSAT: "unsat", RUNNING: "running"}
+
+
+@dataclass
+class BaBConfig:
+    node_budget: int = 4096          # max node expansions per partition (soft-timeout analogue)
+    batch_nodes: int = 32768         # nodes bounded per iteration
+    max_pool: int = 1 << 22          # live-node capacity (drop to UNKNOWN beyond)
+    time_budget: float = 1e9         # wall-clock seconds for the whole call
+    mode: str = "symbolic"
+
+
+@dataclass
+class BaBResult:
+    status: np.ndarray               # [P] int8 verdicts
+    cex_x: np.ndarray                # [P, n0] int64 (valid where SAT)
+    cex_xp: np.ndarray
+    nodes: np.ndarray                # [P] int64 nodes expanded
+    iters: int = 0
+    time: float = 0.0
+
+
+def _pa_table(q: ResolvedQuery, lo: np.ndarray, hi: np.ndarray):
+    """PA assignments shared by all partitions (PA ranges must be identical across the chunk)."""
+    pa = list(q.pa_idx)
+    if not np.all(lo[:, pa] == lo[:1, pa]) or not np.all(hi[:, pa] == hi[:1, pa]):
+        raise NotImplementedError("protected-attribute ranges differ between partitions of one chunk")
+    values = q.pa_values(lo[0], hi[0])
+    pairs = q.pa_pairs(values)
+    return values, pairs
+
+
+class BaBSolver:
+    def __init__(self, backend: Backend, query: ResolvedQuery, cfg: BaBConfig, dead: Optional[torch.Tensor] = None):
+        self.be = backend
+        self.q = query
+        self.cfg = cfg
+        self.dev = backend.device
+        self.dead = dead            # optional [P, N_hidden] bool (heuristically pruned nets)
+        n = query.n
+        self.pa = torch.tensor(list(query.pa_idx), dtype=torch.long, device=self.dev)
+        self.ra = torch.tensor(list(query.ra_idx), dtype=torch.long, device=self.dev)
+        shared = np.ones(n, dtype=bool)
+        shared[list(query.ra_idx)] = False
+        self.shared = torch.from_numpy(shared).to(self.dev)     # PA dims are fixed per row -> "shared" ok
+        self.relaxed = query.relaxed
+        self.tau = float(query.tau)
+        # mlp with dead-masks applied host-side for exact checks (per partition if masked)
+
+    # --------------------------------------------------------------------------------------
+    def _rows(self, lo: torch.Tensor, hi: torch.Tensor, values: torch.Tensor):
+        """Expand node boxes [N, n] into node-major rows [N*V, n] with PA dims set to v."""
+        N, n = lo.shape
+        V = values.shape[0]
+        rlo = lo[:, None, :].expand(N, V, n).clone()
+        rhi = hi[:, None, :].expand(N, V, n).clone()
+        vv = values.to(lo.dtype)[None, :, :].expand(N, V, values.shape[1])
+        rlo[:, :, self.pa] = vv
+        rhi[:, :, self.pa] = vv
+        return rlo.reshape(N * V, n), rhi.reshape(N * V, n)
+
+    def _eval_pairs(self, x: torch.Tensor, xp: torch.Tensor, part: torch.Tensor):
+        """Rigorous interval evaluation of point pairs (IBP on degenerate boxes keeps exact zeros
+        exact): returns (certain_violation, possible_but_uncertain) masks."""
+        d = self.dead[part] if self.dead is not None else None
+        rx = self.be.bounds(x, x, mode="ibp", dead=d)
+        rp = self.be.bounds(xp, xp, mode="ibp", dead=d)
+        sure = ((rx.out_ub < 0) & (rp.out_lb > 0)) | ((rx.out_lb > 0) & (rp.out_ub < 0))
+        poss = ((rx.out_lb < 0) & (rp.out_ub > 0)) | ((rx.out_ub > 0) & (rp.out_lb < 0))
+        return sure, poss & ~sure
+
+    # --------------------------------------------------------------------------------------
+    def solve(self, lo_np: np.ndarray, hi_np: np.ndarray, mlp_exact: MLP,
+              init_status: Optional[np.ndarray] = None,
+              exact_models: Optional[List[MLP]] = None) -> BaBResult:
+        """Decide every partition box ``[lo_np[p], hi_np[p]]``.
+
+        ``mlp_exact`` is the network used for exact confirmation (per-partition nets in
+        ``exact_models`` when heuristic masks are active).
+        """
+        t0 = time.time()
+        cfg = self.cfg
+        dev = self.dev
+        P, n = lo_np.shape
+        values_np, pairs_np = _pa_table(self.q, lo_np, hi_np)
+        values = torch.from_numpy(values_np).to(dev)
+        pairs = torch.from_numpy(pairs_np).to(dev)
+        V = values.shape[0]
+        status = np.full(P, RUNNING, dtype=np.int8) if init_status is None else init_status.astype(np.int8).copy()
+        cex_x = np.zeros((P, n), dtype=np.int64)
+        cex_xp = np.zeros((P, n), dtype=np.int64)
+        nodes_np = np.zeros(P, dtype=np.int64)
+        if pairs.shape[0] == 0:
+            status[status == RUNNING] = UNSAT   # a single PA value: no x' can differ
+            return BaBResult(status, cex_x, cex_xp, nodes_np, 0, time.time() - t0)
+
+        dt = torch.float32
+        run_idx = np.nonzero(status == RUNNING)[0]
+        xlo = torch.from_numpy(lo_np[run_idx]).to(dev, dt)
+        xhi = torch.from_numpy(hi_np[run_idx]).to(dev, dt)
+        part = torch.from_numpy(run_idx).to(dev)
+        if self.relaxed:
+            xplo = xlo.clone()
+            xphi = xhi.clone()
+            xplo[:, self.ra] -= self.tau
+            xphi[:, self.ra] += self.tau
+        else:
+            xplo, xphi = xlo, xhi
+        status_t = torch.from_numpy(status).to(dev)
+        nodes_t = torch.zeros(P, dtype=torch.long, device=dev)
+        it = 0
+        while xlo.shape[0] > 0:
+            if time.time() - t0 > cfg.time_budget:
+                break
+            it += 1
+            B = min(cfg.batch_nodes, xlo.shape[0])
+            blo, bhi, bpart = xlo[:B], xhi[:B], part[:B]
+            bplo, bphi = (xplo[:B], xphi[:B]) if self.relaxed else (blo, bhi)
+            # drop nodes of partitions that are already decided
+            alive = status_t[bpart] == RUNNING
+            if not bool(alive.all()):
+                blo, bhi, bpart, bplo, bphi = blo[alive], bhi[alive], bpart[alive], bplo[alive], bphi[alive]
+            rest = slice(B, None)
+            if blo.shape[0] == 0:
+                xlo, xhi, part = xlo[rest], xhi[rest], part[rest]
+                if self.relaxed:
+                    xplo, xphi = xplo[rest], xphi[rest]
+                continue
+            Nn = blo.shape[0]
+            nodes_t.index_add_(0, bpart, torch.ones_like(bpart))
+            dead_rows = None
+            if self.dead is not None:
+                dead_rows = self.dead[bpart].repeat_interleave(V, dim=0)
+            rlo, rhi = self._rows(blo, bhi, values)
+            res_x = self.be.bounds(rlo, rhi, mode=cfg.mode, dead=dead_rows)
+            if self.relaxed:
+                plo, phi = self._rows(bplo, bphi, values)
+                res_xp = self.be.bounds(plo, phi, mode=cfg.mode, dead=dead_rows)
+            else:
+                res_xp = res_x
+            dec = self.be.pair_certify(res_x, res_xp, blo, bhi, bplo, bphi, pairs, values, self.pa, self.shared,
+                                       self.relaxed)
+            open_ = dec.open_
+            # ---- candidate vertex pairs (falsification inside BaB)
+            pv = pairs[dec.cand_v]
+            cx = dec.cand_x.clone()
+            cxp = dec.cand_xp.clone()
+            cx[:, self.pa] = values[pv[:, 0]].to(cx.dtype)
+            cxp[:, self.pa] = values[pv[:, 1]].to(cx.dtype)
+            if self.relaxed:
+                r = self.ra
+                cxp[:, r] = torch.minimum(torch.maximum(cxp[:, r], cx[:, r] - self.tau), cx[:, r] + self.tau)
+                cxp[:, r] = torch.minimum(torch.maximum(cxp[:, r], bplo[:, r]), bphi[:, r])
+            # ---- leaves: single lattice points (x and x'); evaluate every pair exactly
+            width = (bhi - blo).amax(dim=1)
+            if self.relaxed:
+                width = torch.maximum(width, (bphi - bplo)[:, self.ra].amax(dim=1) if self.ra.numel() else width)
+            leaf = open_ & (width == 0)
+            sel = open_ & (status_t[bpart] == RUNNING)
+            cand_rows = torch.nonzero(sel & ~leaf).flatten()
+            found_idx: List[int] = []
+            found_x: List[np.ndarray] = []
+            found_xp: List[np.ndarray] = []
+            if cand_rows.numel():
+                sure, amb = self._eval_pairs(cx[cand_rows], cxp[cand_rows], bpart[cand_rows])
+                hit = cand_rows[sure | amb]
+                if hit.numel():
+                    found_idx.append(hit)
+            leaf_rows = torch.nonzero(leaf & sel).flatten()
+            if leaf_rows.numel():
+                # all pairs at the leaf point
+                L_ = leaf_rows.numel()
+                Pp = pairs.shape[0]
+                px = blo[leaf_rows][:, None, :].expand(L_, Pp, n).clone()
+                ppx = bplo[leaf_rows][:, None, :].expand(L_, Pp, n).clone()
+                px[:, :, self.pa] = values[pairs[:, 0]].to(px.dtype)[None].expand(L_, Pp, -1)
+                ppx[:, :, self.pa] = values[pairs[:, 1]].to(px.dtype)[None].expand(L_, Pp, -1)
+                lp = bpart[leaf_rows][:, None].expand(L_, Pp)
+                sure, amb = self._eval_pairs(px.reshape(-1, n), ppx.reshape(-1, n), lp.reshape(-1))
+                flag = (sure | amb).view(L_, Pp)
+                anyf = flag.any(dim=1)
+                if bool(anyf.any()):
+                    first = flag.float().argmax(dim=1)
+                    sel_l = torch.nonzero(anyf).flatten()
+                    found_idx.append(leaf_rows[sel_l])
+                    fx = px[sel_l, first[sel_l]]
+                    fxp = ppx[sel_l, first[sel_l]]
+                    cx[leaf_rows[sel_l]] = fx
+                    cxp[leaf_rows[sel_l]] = fxp
+            if found_idx:
+                rows = torch.cat(found_idx)
+                self._confirm(rows, cx, cxp, bpart, status, status_t, cex_x, cex_xp, mlp_exact, exact_models,
+                              lo_np, hi_np)
+            # ---- split open, non-leaf nodes of running partitions
+            nodes_np_now = nodes_t  # device
+            budget_ok = nodes_np_now[bpart] < cfg.node_budget
+            split = open_ & ~leaf & (status_t[bpart] == RUNNING) & budget_ok
+            # partitions that ran out of budget with open nodes -> UNKNOWN
+            over = open_ & ~leaf & (status_t[bpart] == RUNNING) & ~budget_ok
+            if bool(over.any()):
+                status_t[bpart[over]] = UNKNOWN
+            sidx = torch.nonzero(split).flatten()
+            new = self._split(blo[sidx], bhi[sidx], bplo[sidx], bphi[sidx], bpart[sidx], dec.split_dim[sidx])
+            # ---- next pool = rest + children
+            if self.relaxed:
+                clo, chi, cplo, cphi, cpart = new
+                xlo = torch.cat([xlo[rest], clo])
+                xhi = torch.cat([xhi[rest], chi])
+                xplo = torch.cat([xplo[rest], cplo])
+                xphi = torch.cat([xphi[rest], cphi])
+                part = torch.cat([part[rest], cpart])
+            else:
+                clo, chi, _, _, cpart = new
+                xlo = torch.cat([xlo[rest], clo])
+                xhi = torch.cat([xhi[rest], chi])
+                xplo, xphi = xlo, xhi
+                part = torch.cat([part[rest], cpart])
+            if xlo.shape[0] > cfg.max_pool:
+                # keep the oldest nodes; partitions losing nodes become UNKNOWN
+                lost = torch.unique(part[cfg.max_pool:])
+                status_t[lost[status_t[lost] == RUNNING]] = UNKNOWN
+                xlo, xhi, part = xlo[:cfg.max_pool], xhi[:cfg.max_pool], part[:cfg.max_pool]
+                if self.relaxed:
+                    xplo, xphi = xplo[:cfg.max_pool], xphi[:cfg.max_pool]
+                else:
+                    xplo, xphi = xlo, xhi
+        # partitions still running: no nodes left => UNSAT ; nodes left (time budget) => UNKNOWN
+        st = status_t.cpu().numpy()
+        remaining = set(part.cpu().numpy().tolist()) if xlo.shape[0] else set()
+        for p in np.nonzero(st == RUNNING)[0]:
+            st[p] = UNKNOWN if p in remaining else UNSAT
+        # SAT found on host overrides
+        st[status == SAT] = SAT
+        nodes_np = nodes_t.cpu().numpy()
+        return BaBResult(st.astype(np.int8), cex_x, cex_xp, nodes_np, it, time.time() - t0)
+
+    # --------------------------------------------------------------------------------------
+    def _confirm(self, rows, cx, cxp, bpart, status, status_t, cex_x, cex_xp, mlp_exact, exact_models,
+                 lo_np, hi_np):
+        r = rows.cpu().numpy()
+        X = cx[rows].cpu().numpy().round().astype(np.int64)
+        XP = cxp[rows].cpu().numpy().round().astype(np.int64)
+        parts = bpart[rows].cpu().numpy()
+        ok = exact.check_pair_constraints(X, XP, lo_np[parts], hi_np[parts], self.q.pa_idx, self.q.ra_idx,
+                                          self.q.tau)
+        if exact_models is None:
+            viol = exact.is_violation(mlp_exact, X, XP) & ok
+        else:
+            viol = np.zeros(len(parts), dtype=bool)
+            for k, p in enumerate(parts):
+                if ok[k]:
+                    viol[k] = exact.is_violation(exact_models[p], X[k:k + 1], XP[k:k + 1])[0]
+        newly = []
+        for k in np.nonzero(viol)[0]:
+            p = parts[k]
+            if status[p] != SAT:
+                status[p] = SAT
+                cex_x[p] = X[k]
+                cex_xp[p] = XP[k]
+                newly.append(p)
+        if newly:
+            status_t[torch.tensor(newly, device=status_t.device)] = SAT
+
+    def _split(self, lo, hi, plo, phi, part, dim):
+        n = lo.shape[1]
+        N = lo.shape[0]
+        if N == 0:
+            e = lo[:0]
+            return e, e, e, e, part[:0]
+        on_x = dim < n
+        d = torch.where(on_x, dim, dim - n)
+        ar = torch.arange(N, device=lo.device)
+        # children along x dim or x' dim
+        src_lo = torch.where(on_x, lo[ar, d], plo[ar, d])
+        src_hi = torch.where(on_x, hi[ar, d], phi[ar, d])
+        mid = torch.floor((src_lo + src_hi) / 2)
+        lo1, hi1, lo2, hi2 = lo.clone(), hi.clone(), lo.clone(), hi.clone()
+        plo1, phi1, plo2, phi2 = plo.clone(), phi.clone(), plo.clone(), phi.clone()
+        xs = torch.nonzero(on_x).flatten()
+        ps = torch.nonzero(~on_x).flatten()
+        hi1[xs, d[xs]] = mid[xs]
+        lo2[xs, d[xs]] = mid[xs] + 1
+        phi1[ps, d[ps]] = mid[ps]
+        plo2[ps, d[ps]] = mid[ps] + 1
+        clo = torch.cat([lo1, lo2])
+        chi = torch.cat([hi1, hi2])
+        cplo = torch.cat([plo1, plo2])
+        cphi = torch.cat([phi1, phi2])
+        cpart = torch.cat([part, part])
+        if not self.relaxed:
+            return clo, chi, clo, chi, cpart
+        # shared dims of x' follow x; tighten the |x_r - x'_r| <= tau coupling
+        sh = self.shared
+        cplo = torch.where(sh[None, :], clo, cplo)
+        cphi = torch.where(sh[None, :], chi, cphi)
+        r = self.ra
+        t = self.tau
+        cplo[:, r] = torch.maximum(cplo[:, r], clo[:, r] - t)
+        cphi[:, r] = torch.minimum(cphi[:, r], chi[:, r] + t)
+        clo[:, r] = torch.maximum(clo[:, r], cplo[:, r] - t)
+        chi[:, r] = torch.minimum(chi[:, r], cphi[:, r] + t)
+        ok = torch.all(clo <= chi, dim=1) & torch.all(cplo <= cphi, dim=1)
+        return clo[ok], chi[ok], cplo[ok], cphi[ok], cpart[ok]

@@ -1,0 +1,310 @@
+"""Per-model verification pipeline over a stream of partition chunks.
+
+Re-design of the per-partition loop of the reference drivers (``src/GC/Verify-GC.py:106-315``):
+sound prune -> SMT query -> heuristic prune + re-query on ``unknown`` -> counterexample replay
+-> one CSV row per partition -> hard timeout.  Here a *chunk* of partitions (thousands) goes
+through each stage at once on the device:
+
+  decode ids -> simulate/profile/falsify (K3+K8) -> IBP bounds (K2, B-compression) ->
+  symbolic bounds (K4, S-compression) -> branch-and-bound (K9) -> [heuristic masks (K5) +
+  BaB on the masked nets for UNKNOWN partitions] -> replay (K7) -> records.
+
+Per-partition timings are the chunk's stage times apportioned by each partition's share of
+the work (BaB node expansions), so the 24 CSV columns keep their meaning.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..models.mlp import MLP
+from ..ops.backend import Backend
+from ..partition import Grid
+from ..spec import ResolvedQuery
+from . import exact
+from . import prune as P_
+from .bab import SAT, UNKNOWN, UNSAT, RUNNING, VERDICT_NAMES, BaBConfig, BaBSolver, _pa_table
+from .sim import simulate
+
+
+@dataclass
+class VerifyConfig:
+    sim_size: int = 1000                 # reference sim_size (src/AC/Verify-AC.py:115)
+    seed: int = 0
+    chunk: int = 4096                    # partitions per device batch
+    soft_timeout: float = 100.0          # seconds (caps one chunk's BaB wall time)
+    hard_timeout: float = 30 * 60.0      # seconds per model (checked after each chunk)
+    node_budget: int = 4096              # BaB expansions per partition
+    batch_nodes: int = 32768
+    heuristic: bool = True               # reference behaviour: heuristic retry on unknown
+    heuristic_p: float = 5.0             # HEURISTIC_PRUNE_THRESHOLD
+    heuristic_node_budget: int = 4096
+    bisect_pairs: int = 16
+    bisect_steps: int = 12
+    sound_prune_stats: bool = True       # compute B/S compression (reference parity columns)
+
+
+@dataclass
+class PartitionRecord:
+    partition_id: int                    # 1-based position in processing order (reference)
+    grid_id: int
+    verdict: str
+    h_attempt: int = 0
+    h_success: int = 0
+    b_comp: float = 0.0
+    s_comp: float = 0.0
+    st_comp: float = 0.0
+    h_comp: float = 0.0
+    t_comp: float = 0.0
+    sv_time: float = 0.0
+    s_time: float = 0.0
+    hv_time: float = 0.0
+    h_time: float = 0.0
+    total_time: float = 0.0
+    c_check: int = 0
+    v_accurate: int = 0
+    orig_acc: Optional[float] = None
+    pruned_acc: float = 1.0
+    c1: Optional[np.ndarray] = None
+    c2: Optional[np.ndarray] = None
+    nodes: int = 0
+    stage: str = ""                      # which stage decided: sim / bab / heuristic
+
+
+@dataclass
+class ModelRun:
+    model: str
+    records: List[PartitionRecord] = field(default_factory=list)
+    attempted: int = 0
+    wall: float = 0.0
+    stopped_by_hard_timeout: bool = False
+
+    def counts(self) -> Dict[str, int]:
+        c = {"sat": 0, "unsat": 0, "unknown": 0}
+        for r in self.records:
+            c[r.verdict] += 1
+        return c
+
+
+def _amortize(total: float, work: np.ndarray) -> np.ndarray:
+    w = work.astype(np.float64) + 1.0
+    return total * w / w.sum()
+
+
+def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.ndarray, cfg: VerifyConfig,
+                 orig_acc: Optional[float] = None, time_budget: Optional[float] = None) -> List[dict]:
+    """Decide one chunk of partitions; returns per-partition dicts (no cumulative columns)."""
+    dev = be.device
+    lo_np, hi_np = grid.decode(ids)
+    Pn, n = lo_np.shape
+    widths = mlp.widths
+    Nh = int(sum(mlp.hidden))
+    t_start = time.time()
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+
+    values_np, pairs_np = _pa_table(q, lo_np, hi_np)
+    values = torch.from_numpy(values_np).to(dev)
+    pairs = torch.from_numpy(pairs_np).to(dev)
+    lo = torch.from_numpy(lo_np).to(dev, torch.float32)
+    hi = torch.from_numpy(hi_np).to(dev, torch.float32)
+    pids = torch.from_numpy(ids).to(dev)
+
+    # ---------------- stage 1: simulation (profile + falsify)
+    t0 = time.time()
+    sim = simulate(be, q, lo, hi, pids, cfg.sim_size, cfg.seed, values, pairs, cfg.bisect_pairs, cfg.bisect_steps)
+    cand, pos_prob = P_.candidates_from_counts(sim.counts, cfg.sim_size)
+    status = np.full(Pn, RUNNING, dtype=np.int8)
+    cex_x = np.zeros((Pn, n), dtype=np.int64)
+    cex_xp = np.zeros((Pn, n), dtype=np.int64)
+    stage = np.array([""] * Pn, dtype=object)
+    found = sim.found.cpu().numpy()
+    if found.any():
+        fi = np.nonzero(found)[0]
+        X = sim.wit_x[fi].cpu().numpy().round().astype(np.int64)
+        XP = sim.wit_xp[fi].cpu().numpy().round().astype(np.int64)
+        ok = exact.check_pair_constraints(X, XP, lo_np[fi], hi_np[fi], q.pa_idx, q.ra_idx, q.tau)
+        viol = exact.is_violation(mlp, X, XP) & ok
+        for k, p in enumerate(fi):
+            if viol[k]:
+                status[p] = SAT
+                cex_x[p], cex_xp[p] = X[k], XP[k]
+                stage[p] = "sim"
+    sync()
+    t_sim = time.time() - t0
+
+    # ---------------- stage 2: sound pruning statistics (IBP + symbolic on the partition box)
+    t0 = time.time()
+    b_dead = torch.zeros(Pn, mlp.n_neurons, dtype=torch.bool, device=dev)
+    s_dead = torch.zeros_like(b_dead)
+    st_dead = torch.zeros_like(b_dead)
+    s_cand = cand.clone()
+    ibp_lb = ibp_ub = None
+    if cfg.sound_prune_stats:
+        ibp = be.bounds(lo, hi, mode="ibp", keep_layers=True)
+        ibp_lb = torch.cat(ibp.layer_lb, dim=1)
+        ibp_ub = torch.cat(ibp.layer_ub, dim=1)
+        b_dead, b_rem = P_.bound_dead(cand, ibp_ub[:, :Nh], widths)
+        b_dead = P_.ensure_one_alive(b_dead, widths)
+        sym = be.bounds(lo, hi, mode="symbolic")
+        s_hid = b_rem[:, :Nh] & sym.dead
+        s_dead = torch.zeros_like(b_dead)
+        s_dead[:, :Nh] = s_hid
+        s_cand = b_rem.clone()
+        s_cand[:, :Nh] = b_rem[:, :Nh] & ~s_hid
+        st_dead = P_.ensure_one_alive(P_.merge(b_dead, s_dead), widths)
+    sync()
+    t_prune = time.time() - t0
+
+    # ---------------- stage 3: branch and bound on the original network
+    t0 = time.time()
+    budget = cfg.soft_timeout if time_budget is None else min(cfg.soft_timeout, time_budget)
+    solver = BaBSolver(be, q, BaBConfig(node_budget=cfg.node_budget, batch_nodes=cfg.batch_nodes,
+                                        time_budget=budget))
+    res = solver.solve(lo_np, hi_np, mlp, init_status=status)
+    newly_sat = (res.status == SAT) & (status != SAT)
+    stage[newly_sat] = "bab"
+    stage[(res.status == UNSAT)] = "bab"
+    cex_x[newly_sat] = res.cex_x[newly_sat]
+    cex_xp[newly_sat] = res.cex_xp[newly_sat]
+    status = res.status.copy()
+    nodes = res.nodes.copy()
+    sync()
+    t_bab = time.time() - t0
+
+    # ---------------- stage 4: heuristic retry for UNKNOWN partitions (unsound, flagged)
+    h_attempt = np.zeros(Pn, dtype=np.int64)
+    h_success = np.zeros(Pn, dtype=np.int64)
+    h_dead_np = np.zeros((Pn, mlp.n_neurons), dtype=bool)
+    t_dead_np = st_dead.cpu().numpy()
+    pruned_models: Dict[int, MLP] = {}
+    t_heur = 0.0
+    unk = np.nonzero(status == UNKNOWN)[0]
+    if cfg.heuristic and unk.size and ibp_ub is not None:
+        t0 = time.time()
+        h_attempt[unk] = 1
+        lb_np = ibp_lb.cpu().numpy()
+        ub_np = ibp_ub.cpu().numpy()
+        cand_np = cand.cpu().numpy()
+        scand_np = s_cand.cpu().numpy()
+        st_np = st_dead.cpu().numpy()
+        masks = np.zeros((unk.size, Nh), dtype=bool)
+        for k, p in enumerate(unk):
+            hd, md = P_.heuristic_prune_one(lb_np[p], ub_np[p], cand_np[p], scand_np[p], st_np[p], widths,
+                                            cfg.heuristic_p)
+            h_dead_np[p] = hd
+            t_dead_np[p] = md
+            masks[k] = md[:Nh]
+            pruned_models[p] = mlp.masked([md[s] for s in P_.layer_slices(widths)])
+        sub_lo, sub_hi = lo_np[unk], hi_np[unk]
+        dead_t = torch.from_numpy(masks).to(dev)
+        hsolver = BaBSolver(be, q, BaBConfig(node_budget=cfg.heuristic_node_budget, batch_nodes=cfg.batch_nodes,
+                                             time_budget=budget), dead=dead_t)
+        hres = hsolver.solve(sub_lo, sub_hi, mlp, exact_models=[pruned_models[p] for p in unk])
+        for k, p in enumerate(unk):
+            v = hres.status[k]
+            if v in (SAT, UNSAT):
+                h_success[p] = 1
+                status[p] = v
+                stage[p] = "heuristic"
+                if v == SAT:
+                    cex_x[p], cex_xp[p] = hres.cex_x[k], hres.cex_xp[k]
+            nodes[p] += hres.nodes[k]
+        sync()
+        t_heur = time.time() - t0
+
+    # ---------------- stage 5: replay / fidelity
+    t0 = time.time()
+    recs = []
+    sat_idx = np.nonzero(status == SAT)[0]
+    c_check = np.zeros(Pn, dtype=np.int64)
+    v_acc = np.zeros(Pn, dtype=np.int64)
+    if sat_idx.size:
+        xo = mlp.predict(cex_x[sat_idx])
+        xpo = mlp.predict(cex_xp[sat_idx])
+        v_acc[sat_idx] = (xo != xpo).astype(np.int64)
+        for k, p in enumerate(sat_idx):
+            net = pruned_models.get(p, mlp)
+            c1 = net.predict(cex_x[p:p + 1])[0]
+            c2 = net.predict(cex_xp[p:p + 1])[0]
+            c_check[p] = int(c1 == xo[k] and c2 == xpo[k])
+    pruned_acc = np.ones(Pn)
+    if pruned_models:
+        # agreement of the (heuristically) pruned net with the original on the sim points
+        for p, net in pruned_models.items():
+            X = torch.from_numpy(lo_np[p:p + 1]).to(torch.float32)
+            pts = sample_host(lo_np[p], hi_np[p], ids[p], cfg.sim_size, cfg.seed)
+            pruned_acc[p] = float(np.mean(net.predict(pts) == mlp.predict(pts)))
+    t_replay = time.time() - t0
+
+    # ---------------- records (timings apportioned by work)
+    work = nodes
+    s_share = _amortize(t_sim + t_prune + t_bab, work)
+    sv_share = _amortize(t_bab, work)
+    h_work = np.where(h_attempt > 0, nodes, 0)
+    hv_share = _amortize(t_heur, h_work) if t_heur > 0 else np.zeros(Pn)
+    rp_share = _amortize(t_replay, np.zeros(Pn))
+    b_c = P_.compression(b_dead).cpu().numpy()
+    s_c = P_.compression(s_dead).cpu().numpy()
+    st_c = P_.compression(st_dead).cpu().numpy()
+    h_c = h_dead_np.mean(axis=1)
+    t_c = t_dead_np.mean(axis=1)
+    for p in range(Pn):
+        v = VERDICT_NAMES[int(status[p])]
+        if v == "running":
+            v = "unknown"
+        sat = v == "sat"
+        recs.append(dict(
+            grid_id=int(ids[p]), verdict=v, h_attempt=int(h_attempt[p]), h_success=int(h_success[p]),
+            b_comp=float(b_c[p]), s_comp=float(s_c[p]), st_comp=float(st_c[p]),
+            h_comp=float(h_c[p]) if h_attempt[p] else 0.0,
+            t_comp=float(t_c[p]) if h_attempt[p] else float(st_c[p]),
+            sv_time=float(sv_share[p]), s_time=float(s_share[p]), hv_time=float(hv_share[p]),
+            h_time=float(hv_share[p]), total_time=float(s_share[p] + hv_share[p] + rp_share[p]),
+            c_check=int(c_check[p]), v_accurate=int(v_acc[p]), orig_acc=orig_acc,
+            pruned_acc=float(pruned_acc[p]),
+            c1=cex_x[p].astype(np.float32) if sat else None, c2=cex_xp[p].astype(np.float32) if sat else None,
+            nodes=int(nodes[p]), stage=stage[p] or ("bab" if v != "unknown" else ""),
+        ))
+    return recs
+
+
+def sample_host(lo: np.ndarray, hi: np.ndarray, pid: int, n_samples: int, seed: int) -> np.ndarray:
+    from ..ops.reference import sample_points
+
+    X = sample_points(torch.from_numpy(lo[None]).float(), torch.from_numpy(hi[None]).float(),
+                      torch.tensor([pid]), n_samples, seed)
+    return X[0].numpy().astype(np.int64)
+
+
+def verify_model(mlp: MLP, q: ResolvedQuery, grid: Grid, order: np.ndarray, cfg: VerifyConfig,
+                 device="cpu", orig_acc: Optional[float] = None,
+                 on_chunk: Optional[Callable[[List[PartitionRecord]], None]] = None,
+                 max_partitions: Optional[int] = None) -> ModelRun:
+    """Verify partitions of ``grid`` in ``order`` (ids) until done or the hard timeout."""
+    be = Backend(mlp, device=device)
+    run = ModelRun(model=mlp.name)
+    t0 = time.time()
+    total = len(order) if max_partitions is None else min(len(order), max_partitions)
+    pos = 0
+    while pos < total:
+        elapsed = time.time() - t0
+        if elapsed > cfg.hard_timeout:
+            run.stopped_by_hard_timeout = True
+            break
+        ids = order[pos:min(total, pos + cfg.chunk)]
+        recs = verify_chunk(be, mlp, q, grid, ids, cfg, orig_acc=orig_acc,
+                            time_budget=cfg.hard_timeout - elapsed)
+        out = []
+        for r in recs:
+            out.append(PartitionRecord(partition_id=pos + len(out) + 1, **r))
+        run.records.extend(out)
+        pos += len(ids)
+        if on_chunk is not None:
+            on_chunk(out)
+    run.attempted = len(run.records)
+    run.wall = time.time() - t0
+    return run

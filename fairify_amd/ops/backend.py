@@ -1,0 +1,78 @@
+"""Per-model compute backend: weights resident on the device + the hot ops.
+
+One ``Backend`` is created per (model, device).  Weights are uploaded once (≤ 90 KB fp32 for
+the largest zoo model) and, for the HIP path, packed into the flat layout the kernels read
+(``[W_0 | b_0 | W_1 | b_1 | ...]`` fp32, Keras ``[in, out]`` row-major).  Every method takes
+and returns device tensors; on CUDA/ROCm devices the HIP kernels run, on CPU the PyTorch
+reference in :mod:`fairify_amd.ops.reference`.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..models.mlp import MLP
+from . import reference as ref
+from . import use_hip
+
+
+class Backend:
+    def __init__(self, mlp: MLP, device="cpu", dtype=torch.float32):
+        self.mlp = mlp
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.ws = [torch.from_numpy(w).to(self.device, dtype) for w in mlp.weights]
+        self.bs = [torch.from_numpy(b).to(self.device, dtype) for b in mlp.biases]
+        self.widths = mlp.widths
+        self.n0 = mlp.n_in
+        self.n_hidden = int(sum(mlp.hidden))
+        probe = torch.empty(0, device=self.device)
+        self.hip = use_hip(probe) and dtype == torch.float32
+        if self.hip:
+            flat = np.concatenate([np.concatenate([w.reshape(-1), b]) for w, b in zip(mlp.weights, mlp.biases)])
+            self.flat = torch.from_numpy(flat.astype(np.float32)).to(self.device)
+            dims = [mlp.n_in] + mlp.widths
+            self.dims = torch.tensor(dims, dtype=torch.int32)
+        self.unit = ref.FP32_UNIT if dtype == torch.float32 else ref.FP64_UNIT
+
+    # ----------------------------------------------------------------------------- forward
+    def forward(self, x: torch.Tensor, dead: Optional[torch.Tensor] = None) -> torch.Tensor:
+        x = x.to(self.dtype)
+        if self.hip:
+            from . import hip
+
+            return hip.forward(self, x, dead)
+        return ref.forward(self.ws, self.bs, x, dead)
+
+    def forward_error(self, x: torch.Tensor) -> torch.Tensor:
+        return ref.forward_error_bound(self.ws, self.bs, x.to(self.dtype), self.unit)
+
+    def activation_counts(self, x: torch.Tensor) -> torch.Tensor:
+        """x [B, S, n0] -> [B, N] non-zero counts per neuron (all layers)."""
+        if self.hip:
+            from . import hip
+
+            return hip.activation_counts(self, x.to(self.dtype))
+        return ref.activation_counts(self.ws, self.bs, x.to(self.dtype))
+
+    # ----------------------------------------------------------------------------- bounds
+    def bounds(self, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic",
+               dead: Optional[torch.Tensor] = None, keep_layers: bool = False) -> ref.BoundResult:
+        lo = lo.to(self.dtype)
+        hi = hi.to(self.dtype)
+        if self.hip:
+            from . import hip
+
+            return hip.bounds(self, lo, hi, mode=mode, dead=dead, keep_layers=keep_layers)
+        return ref.bounds(self.ws, self.bs, lo, hi, mode=mode, dead=dead, unit=self.unit, keep_layers=keep_layers)
+
+    # ----------------------------------------------------------------------------- BaB node test
+    def pair_certify(self, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, shared, relaxed):
+        if self.hip:
+            from . import hip
+
+            return hip.pair_certify(self, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, shared, relaxed)
+        return ref.pair_certify(res_x, res_xp, xlo.to(self.dtype), xhi.to(self.dtype), xplo.to(self.dtype),
+                                xphi.to(self.dtype), pairs, values, pa, shared, relaxed, unit=self.unit)

@@ -1,0 +1,183 @@
+"""Thin Python wrappers launching the HIP kernels of ``fairify_amd._C`` on torch's stream.
+
+Every wrapper allocates its outputs with torch (caching allocator, current device), checks
+shapes/dtypes/contiguity on the host before launch (a mis-shaped launch must never reach the
+GPU), and passes raw pointers + ``torch.cuda.current_stream().cuda_stream``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import ext
+from . import reference as ref
+
+
+def _stream(dev) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _net(be):
+    n = getattr(be, "_hipnet", None)
+    if n is None:
+        dims = [be.mlp.n_in] + be.mlp.widths
+        n = ext().Net(dims, be.unit)
+        assert n.n_params == be.flat.numel(), (n.n_params, be.flat.numel())
+        be._hipnet = n
+    return n
+
+
+def _c(t: torch.Tensor, dtype, shape=None, name="tensor") -> torch.Tensor:
+    if t.dtype != dtype:
+        t = t.to(dtype)
+    t = t.contiguous()
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    return t
+
+
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+# ------------------------------------------------------------------------------------------------
+def forward(be, x: torch.Tensor, dead: Optional[torch.Tensor] = None) -> torch.Tensor:
+    shp = x.shape[:-1]
+    x2 = _c(x.reshape(-1, be.n0), torch.float32, name="x")
+    B = x2.shape[0]
+    out = torch.empty(B, dtype=torch.float32, device=x.device)
+    if B == 0:
+        return out.view(shp)
+    d = None
+    if dead is not None:
+        d = _c(dead.reshape(-1, be.n_hidden), torch.uint8, (B, be.n_hidden), "dead")
+    ext().forward(_net(be), be.flat.data_ptr(), x2.data_ptr(), B, _ptr(d), out.data_ptr(), _stream(x.device))
+    return out.view(shp)
+
+
+def activation_counts(be, x: torch.Tensor) -> torch.Tensor:
+    # generic rows: run the forward per layer through the reference on-device (rarely used on the
+    # GPU path; the fused sim kernel counts activations itself)
+    return ref.activation_counts(be.ws, be.bs, x)
+
+
+# ------------------------------------------------------------------------------------------------
+def bounds(be, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic", dead: Optional[torch.Tensor] = None,
+           keep_layers: bool = False, G: int = 0) -> ref.BoundResult:
+    R, n0 = lo.shape
+    if n0 != be.n0:
+        raise ValueError(f"box width {n0} != network input {be.n0}")
+    dev = lo.device
+    lo = _c(lo, torch.float32, (R, n0), "lo")
+    hi = _c(hi, torch.float32, (R, n0), "hi")
+    sym = 1 if mode == "symbolic" else 0
+    f32 = dict(dtype=torch.float32, device=dev)
+    out_lb = torch.empty(R, **f32)
+    out_ub = torch.empty(R, **f32)
+    res = ref.BoundResult(out_lb=out_lb, out_ub=out_ub)
+    forms = [None] * 6
+    if sym:
+        res.Lc = torch.empty(R, n0, **f32)
+        res.L0 = torch.empty(R, **f32)
+        res.Le = torch.empty(R, **f32)
+        res.Uc = torch.empty(R, n0, **f32)
+        res.U0 = torch.empty(R, **f32)
+        res.Ue = torch.empty(R, **f32)
+        forms = [res.Lc, res.L0, res.Le, res.Uc, res.U0, res.Ue]
+    N = be.mlp.n_neurons
+    lay_lb = lay_ub = None
+    if keep_layers:
+        lay_lb = torch.empty(R, N, **f32)
+        lay_ub = torch.empty(R, N, **f32)
+    dead_out = torch.empty(R, be.n_hidden, dtype=torch.uint8, device=dev) if be.n_hidden else None
+    d = None
+    if dead is not None:
+        d = _c(dead, torch.uint8, (R, be.n_hidden), "dead")
+    if R:
+        ext().bounds(_net(be), be.flat.data_ptr(), lo.data_ptr(), hi.data_ptr(), _ptr(d), R, sym,
+                     out_lb.data_ptr(), out_ub.data_ptr(), *[_ptr(t) for t in forms],
+                     _ptr(lay_lb), _ptr(lay_ub), _ptr(dead_out), G, _stream(dev))
+    if keep_layers:
+        widths = be.mlp.widths
+        offs = [0]
+        for w in widths:
+            offs.append(offs[-1] + w)
+        res.layer_lb = [lay_lb[:, offs[i]:offs[i + 1]] for i in range(len(widths))]
+        res.layer_ub = [lay_ub[:, offs[i]:offs[i + 1]] for i in range(len(widths))]
+    if dead_out is not None:
+        res.dead = dead_out.bool()
+    return res
+
+
+# ------------------------------------------------------------------------------------------------
+def pair_certify(be, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, shared, relaxed) -> ref.PairDecision:
+    Nn, n0 = xlo.shape
+    dev = xlo.device
+    V = values.shape[0]
+    Pp = pairs.shape[0]
+    norient = 2 if relaxed else 1
+    f32 = dict(dtype=torch.float32, device=dev)
+    xlo = _c(xlo, torch.float32, (Nn, n0), "xlo")
+    xhi = _c(xhi, torch.float32, (Nn, n0), "xhi")
+    xplo = _c(xplo, torch.float32, (Nn, n0), "xplo")
+    xphi = _c(xphi, torch.float32, (Nn, n0), "xphi")
+    for r in (res_x, res_xp):
+        if r.Lc is None or tuple(r.Lc.shape) != (Nn * V, n0):
+            raise ValueError("pair_certify needs symbolic forms for Nn*V rows")
+    pairs_c = _c(pairs, torch.int64, (Pp, 2), "pairs")
+    values_c = _c(values, torch.int64, None, "values")
+    sh = _c(shared, torch.uint8, (n0,), "shared")
+    Q = Pp * norient
+    gmin = torch.empty(Nn, Q, **f32)
+    tstar = torch.empty(Nn, Q, **f32)
+    open_ = torch.empty(Nn, dtype=torch.uint8, device=dev)
+    score = torch.empty(Nn, **f32)
+    split = torch.empty(Nn, dtype=torch.int64, device=dev)
+    cx = torch.empty(Nn, n0, **f32)
+    cxp = torch.empty(Nn, n0, **f32)
+    cv = torch.empty(Nn, dtype=torch.int64, device=dev)
+    co = torch.empty(Nn, dtype=torch.int64, device=dev)
+    fx = [res_x.Lc, res_x.L0, res_x.Le, res_x.Uc, res_x.U0, res_x.Ue]
+    fxp = [res_xp.Lc, res_xp.L0, res_xp.Le, res_xp.Uc, res_xp.U0, res_xp.Ue]
+    fx = [_c(t, torch.float32) for t in fx]
+    fxp = [_c(t, torch.float32) for t in fxp]
+    if Nn:
+        ext().certify(Nn, n0, V, Pp, norient, [t.data_ptr() for t in fx], [t.data_ptr() for t in fxp],
+                      xlo.data_ptr(), xhi.data_ptr(), xplo.data_ptr(), xphi.data_ptr(), pairs_c.data_ptr(),
+                      values_c.data_ptr(), [int(i) for i in pa.tolist()], sh.data_ptr(), be.unit,
+                      ref.gamma(2 * n0 + 4, be.unit), gmin.data_ptr(), tstar.data_ptr(), open_.data_ptr(),
+                      score.data_ptr(), split.data_ptr(), cx.data_ptr(), cxp.data_ptr(), cv.data_ptr(),
+                      co.data_ptr(), _stream(dev))
+    return ref.PairDecision(open_=open_.bool(), score=score, split_dim=split, cand_x=cx, cand_xp=cxp,
+                            cand_v=cv, cand_orient=co)
+
+
+# ------------------------------------------------------------------------------------------------
+def simulate(be, q, lo, hi, pids, n_samples, seed, values, pairs, bisect_pairs, bisect_steps, return_z0=False):
+    from ..engine.sim import SimResult, boundary_walk
+
+    P, n0 = lo.shape
+    dev = lo.device
+    lo_c = _c(lo, torch.float32, (P, n0), "lo")
+    hi_c = _c(hi, torch.float32, (P, n0), "hi")
+    pids_c = _c(pids, torch.int64, (P,), "pids")
+    V = values.shape[0]
+    Pp = pairs.shape[0]
+    values_c = _c(values, torch.int64, None, "values")
+    pairs_c = _c(pairs, torch.int64, (Pp, 2), "pairs")
+    counts = torch.empty(P, be.mlp.n_neurons, dtype=torch.int32, device=dev)
+    found = torch.zeros(P, dtype=torch.uint8, device=dev)
+    wx = torch.zeros(P, n0, dtype=torch.float32, device=dev)
+    wxp = torch.zeros(P, n0, dtype=torch.float32, device=dev)
+    z0 = torch.empty(P, n_samples, dtype=torch.float32, device=dev) if (bisect_pairs and bisect_steps) else None
+    if P and n_samples:
+        ext().sim(_net(be), be.flat.data_ptr(), lo_c.data_ptr(), hi_c.data_ptr(), pids_c.data_ptr(), P, n_samples,
+                  int(seed) & 0xFFFFFFFF, V, list(q.pa_idx), values_c.data_ptr(), Pp, pairs_c.data_ptr(),
+                  list(q.ra_idx) if q.relaxed else [], int(q.tau), counts.data_ptr(), found.data_ptr(),
+                  wx.data_ptr(), wxp.data_ptr(), _ptr(z0), _stream(dev))
+    res = SimResult(counts=counts, found=found.bool(), wit_x=wx, wit_xp=wxp)
+    if z0 is not None:
+        boundary_walk(be, q, lo_c, hi_c, pids_c, n_samples, seed, values_c, pairs_c, res, z0, bisect_pairs,
+                      bisect_steps)
+    return res

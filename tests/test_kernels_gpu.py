@@ -1,0 +1,137 @@
+"""HIP kernels vs the PyTorch reference (fp32 CPU / fp64 oracle) — run on a real MI355X."""
+import itertools
+
+import numpy as np
+import pytest
+import torch
+
+from fairify_amd.models.mlp import random_mlp
+from fairify_amd.models.zoo import get_model
+from fairify_amd.ops import reference as ref
+from fairify_amd.ops.backend import Backend
+from fairify_amd.spec import ADULT, Query
+
+pytestmark = pytest.mark.gpu
+
+
+def _boxes(n0, R, seed, span=6):
+    g = np.random.default_rng(seed)
+    lo = g.integers(-5, 20, size=(R, n0)).astype(np.float32)
+    hi = lo + g.integers(0, span, size=(R, n0)).astype(np.float32)
+    return torch.from_numpy(lo), torch.from_numpy(hi)
+
+
+NETS = [(13, [16, 8]), (16, [150, 100, 50]), (30, [16, 16, 16]), (6, [3]), (20, [64, 32, 16, 8, 4]), (13, [100, 100])]
+
+
+@pytest.mark.parametrize("n0,hidden", NETS)
+@pytest.mark.parametrize("mode", ["ibp", "symbolic"])
+def test_bounds_match_reference(cuda, n0, hidden, mode):
+    m = random_mlp(n0, hidden, seed=n0 + len(hidden), bias_scale=0.3)
+    lo, hi = _boxes(n0, 257, 1)
+    cpu = Backend(m, "cpu")
+    gpu = Backend(m, cuda)
+    assert gpu.hip
+    r_c = cpu.bounds(lo, hi, mode=mode, keep_layers=True)
+    r_g = gpu.bounds(lo.to(cuda), hi.to(cuda), mode=mode, keep_layers=True)
+    scale = (r_c.out_ub - r_c.out_lb).abs() + r_c.out_ub.abs() + 1e-3
+    assert torch.allclose(r_g.out_lb.cpu(), r_c.out_lb, rtol=1e-4, atol=1e-4 * float(scale.max()))
+    assert torch.allclose(r_g.out_ub.cpu(), r_c.out_ub, rtol=1e-4, atol=1e-4 * float(scale.max()))
+    for a, b in zip(r_g.layer_ub, r_c.layer_ub):
+        assert torch.allclose(a.cpu(), b, rtol=1e-4, atol=1e-3 * float(b.abs().max() + 1))
+    if mode == "symbolic":
+        assert torch.allclose(r_g.Lc.cpu(), r_c.Lc, rtol=1e-4, atol=1e-4 * float(r_c.Lc.abs().max() + 1))
+        assert torch.allclose(r_g.U0.cpu(), r_c.U0, rtol=1e-4, atol=1e-4 * float(r_c.U0.abs().max() + 1))
+
+
+@pytest.mark.parametrize("n0,hidden", NETS[:4])
+def test_bounds_sound_vs_bruteforce(cuda, n0, hidden):
+    m = random_mlp(n0, hidden, seed=7, bias_scale=0.5)
+    g = np.random.default_rng(3)
+    gpu = Backend(m, cuda)
+    for mode in ("ibp", "symbolic"):
+        for _ in range(4):
+            lo = g.integers(0, 5, size=(1, n0))
+            hi = lo.copy()
+            dims = g.choice(n0, size=min(n0, 4), replace=False)
+            hi[0, dims] += g.integers(1, 3, size=dims.size)
+            pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[0], hi[0])])))
+            z = m.logits(pts)
+            r = gpu.bounds(torch.tensor(lo, dtype=torch.float32, device=cuda),
+                           torch.tensor(hi, dtype=torch.float32, device=cuda), mode=mode)
+            assert float(r.out_lb[0]) <= z.min() + 1e-9
+            assert float(r.out_ub[0]) >= z.max() - 1e-9
+
+
+def test_forward_matches(cuda):
+    for n0, hidden in NETS:
+        m = random_mlp(n0, hidden, seed=11)
+        x = torch.randint(-3, 30, (1000, n0)).float()
+        z_ref = torch.from_numpy(m.logits(x.numpy().astype(np.float64))).float()
+        be = Backend(m, cuda)
+        z = be.forward(x.to(cuda)).cpu()
+        err = be.forward_error(x.to(cuda)).cpu()
+        assert torch.all((z - z_ref).abs() <= err + 1e-6)
+        # dead mask
+        dead = torch.rand(1000, m.n_neurons - 1) < 0.3
+        zd = be.forward(x.to(cuda), dead.to(cuda)).cpu()
+        zr = ref.forward([w.cpu() for w in be.ws], [b.cpu() for b in be.bs], x, dead)
+        assert torch.allclose(zd, zr, rtol=1e-4, atol=1e-3)
+
+
+def test_sim_kernel_matches_reference(cuda):
+    from fairify_amd.engine.sim import simulate
+    from fairify_amd.partition import Grid
+
+    q = Query(("race",)).resolve(ADULT)
+    grid = Grid.reference(ADULT, 10)
+    ids = np.arange(0, 16000, 97)[:128]
+    lo, hi = grid.decode(ids)
+    values = torch.from_numpy(q.pa_values(lo[0], hi[0]))
+    pairs = torch.from_numpy(q.pa_pairs(values.numpy()))
+    m = get_model("AC-3")
+    cpu = Backend(m, "cpu")
+    gpu = Backend(m, cuda)
+    lo_t = torch.from_numpy(lo).float()
+    hi_t = torch.from_numpy(hi).float()
+    pid = torch.from_numpy(ids)
+    a = simulate(cpu, q, lo_t, hi_t, pid, 300, 5, values, pairs, 0, 0)
+    b = simulate(gpu, q, lo_t.to(cuda), hi_t.to(cuda), pid.to(cuda), 300, 5, values.to(cuda), pairs.to(cuda), 0, 0)
+    diff = (a.counts - b.counts.cpu()).abs()
+    assert int(diff.max()) <= 2
+    agree = (a.found == b.found.cpu()).float().mean()
+    assert float(agree) > 0.97
+    both = a.found & b.found.cpu()
+    assert torch.equal(a.wit_x[both], b.wit_x.cpu()[both])
+
+
+def test_certify_matches_reference(cuda):
+    from fairify_amd.engine.bab import BaBSolver, BaBConfig
+
+    q = Query(("sex",), ("age",), 2).resolve(ADULT)
+    m = get_model("AC-1")
+    values = torch.tensor([[0], [1]])
+    pairs = torch.from_numpy(q.pa_pairs(values.numpy()))
+    lo, hi = _boxes(13, 64, 9, span=4)
+    lo[:, 8] = 0
+    hi[:, 8] = 1
+    plo, phi = lo.clone(), hi.clone()
+    plo[:, 0] -= 2
+    phi[:, 0] += 2
+    shared = torch.ones(13, dtype=torch.bool)
+    shared[0] = False
+    pa = torch.tensor([8])
+    outs = []
+    for dev in ("cpu", cuda):
+        be = Backend(m, dev)
+        rows = BaBSolver(be, q, BaBConfig())._rows
+        rl, rh = rows(lo.to(dev), hi.to(dev), values.to(dev))
+        pl, ph = rows(plo.to(dev), phi.to(dev), values.to(dev))
+        rx = be.bounds(rl, rh)
+        rxp = be.bounds(pl, ph)
+        outs.append(be.pair_certify(rx, rxp, lo.to(dev), hi.to(dev), plo.to(dev), phi.to(dev), pairs.to(dev),
+                                    values.to(dev), pa.to(dev), shared.to(dev), True))
+    a, b = outs
+    assert (a.open_ == b.open_.cpu()).float().mean() > 0.95
+    close = (a.score - b.score.cpu()).abs() <= 1e-3 * (a.score.abs() + 1)
+    assert close.float().mean() > 0.95
