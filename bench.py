@@ -49,6 +49,7 @@ def main() -> None:
     ap.add_argument("--models", default=None, help="comma list (default: the preset's models)")
     ap.add_argument("--device", default=None)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--profile", action="store_true", help="per-stage timing breakdown on stderr (syncs)")
     args = ap.parse_args()
 
     import torch
@@ -59,6 +60,7 @@ def main() -> None:
     from fairify_amd.ops.backend import Backend
     from fairify_amd.parallel import dist as D
     from fairify_amd.partition import processing_order
+    from fairify_amd.utils.timer import StageTimer
 
     dev_type = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
     info = D.init(dev_type)
@@ -83,11 +85,13 @@ def main() -> None:
         idx = (start + np.arange(args.chunk)) % max(1, n)
         return [shard[idx]]
 
+    timer = StageTimer(info.device, sync=args.profile)
+
     def run_step(step: int):
         dec = att = sat = uns = 0
         for m, be in zip(models, backends):
             for ids in chunks_for_step(step):
-                recs = verify_chunk(be, m, q, grid, ids, cfg)
+                recs = verify_chunk(be, m, q, grid, ids, cfg, timer=timer)
                 for r in recs:
                     att += 1
                     if r["verdict"] == "sat":
@@ -138,6 +142,8 @@ def main() -> None:
         "baseline": {"decided_per_s": round(BASELINE_DECIDED_PER_S, 5), "pct_verified_of_attempted": 89.0,
                      "coverage_of_grid_pct": 0.29},
     }
+    if args.profile and info.is_main:
+        print(timer.report(), file=sys.stderr, flush=True)
     if info.is_main:
         line = json.dumps(out)
         print(line, flush=True)

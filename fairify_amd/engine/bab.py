@@ -28,6 +28,7 @@ import torch
 from ..models.mlp import MLP
 from ..ops.backend import Backend
 from ..spec import ResolvedQuery
+from ..utils.timer import NULL, StageTimer
 from . import exact
 
 UNKNOWN, SAT, UNSAT, RUNNING = 0, 1, 2, 3
@@ -64,7 +65,9 @@ def _pa_table(q: ResolvedQuery, lo: np.ndarray, hi: np.ndarray):
 
 
 class BaBSolver:
-    def __init__(self, backend: Backend, query: ResolvedQuery, cfg: BaBConfig, dead: Optional[torch.Tensor] = None):
+    def __init__(self, backend: Backend, query: ResolvedQuery, cfg: BaBConfig, dead: Optional[torch.Tensor] = None,
+                 timer: StageTimer = NULL):
+        self.tm = timer
         self.be = backend
         self.q = query
         self.cfg = cfg
@@ -164,15 +167,17 @@ class BaBSolver:
             dead_rows = None
             if self.dead is not None:
                 dead_rows = self.dead[bpart].repeat_interleave(V, dim=0)
-            rlo, rhi = self._rows(blo, bhi, values)
-            res_x = self.be.bounds(rlo, rhi, mode=cfg.mode, dead=dead_rows)
-            if self.relaxed:
-                plo, phi = self._rows(bplo, bphi, values)
-                res_xp = self.be.bounds(plo, phi, mode=cfg.mode, dead=dead_rows)
-            else:
-                res_xp = res_x
-            dec = self.be.pair_certify(res_x, res_xp, blo, bhi, bplo, bphi, pairs, values, self.pa, self.shared,
-                                       self.relaxed)
+            with self.tm("bab.bounds"):
+                rlo, rhi = self._rows(blo, bhi, values)
+                res_x = self.be.bounds(rlo, rhi, mode=cfg.mode, dead=dead_rows)
+                if self.relaxed:
+                    plo, phi = self._rows(bplo, bphi, values)
+                    res_xp = self.be.bounds(plo, phi, mode=cfg.mode, dead=dead_rows)
+                else:
+                    res_xp = res_x
+            with self.tm("bab.certify"):
+                dec = self.be.pair_certify(res_x, res_xp, blo, bhi, bplo, bphi, pairs, values, self.pa, self.shared,
+                                           self.relaxed)
             open_ = dec.open_
             # ---- candidate vertex pairs (falsification inside BaB)
             pv = pairs[dec.cand_v]
@@ -195,7 +200,8 @@ class BaBSolver:
             found_x: List[np.ndarray] = []
             found_xp: List[np.ndarray] = []
             if cand_rows.numel():
-                sure, amb = self._eval_pairs(cx[cand_rows], cxp[cand_rows], bpart[cand_rows])
+                with self.tm("bab.eval_cand"):
+                    sure, amb = self._eval_pairs(cx[cand_rows], cxp[cand_rows], bpart[cand_rows])
                 hit = cand_rows[sure | amb]
                 if hit.numel():
                     found_idx.append(hit)
@@ -222,7 +228,8 @@ class BaBSolver:
                     cxp[leaf_rows[sel_l]] = fxp
             if found_idx:
                 rows = torch.cat(found_idx)
-                self._confirm(rows, cx, cxp, bpart, status, status_t, cex_x, cex_xp, mlp_exact, exact_models,
+                with self.tm("bab.confirm"):
+                    self._confirm(rows, cx, cxp, bpart, status, status_t, cex_x, cex_xp, mlp_exact, exact_models,
                               lo_np, hi_np)
             # ---- split open, non-leaf nodes of running partitions
             nodes_np_now = nodes_t  # device
@@ -233,7 +240,8 @@ class BaBSolver:
             if bool(over.any()):
                 status_t[bpart[over]] = UNKNOWN
             sidx = torch.nonzero(split).flatten()
-            new = self._split(blo[sidx], bhi[sidx], bplo[sidx], bphi[sidx], bpart[sidx], dec.split_dim[sidx])
+            with self.tm("bab.split"):
+                new = self._split(blo[sidx], bhi[sidx], bplo[sidx], bphi[sidx], bpart[sidx], dec.split_dim[sidx])
             # ---- next pool = rest + children
             if self.relaxed:
                 clo, chi, cplo, cphi, cpart = new

@@ -29,6 +29,7 @@ from . import exact
 from . import prune as P_
 from .bab import SAT, UNKNOWN, UNSAT, RUNNING, VERDICT_NAMES, BaBConfig, BaBSolver, _pa_table
 from .sim import simulate
+from ..utils.timer import StageTimer
 
 
 @dataclass
@@ -96,14 +97,15 @@ def _amortize(total: float, work: np.ndarray) -> np.ndarray:
 
 
 def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.ndarray, cfg: VerifyConfig,
-                 orig_acc: Optional[float] = None, time_budget: Optional[float] = None) -> List[dict]:
+                 orig_acc: Optional[float] = None, time_budget: Optional[float] = None,
+                 timer: Optional[StageTimer] = None) -> List[dict]:
     """Decide one chunk of partitions; returns per-partition dicts (no cumulative columns)."""
+    tm = timer if timer is not None else StageTimer()
     dev = be.device
     lo_np, hi_np = grid.decode(ids)
     Pn, n = lo_np.shape
     widths = mlp.widths
     Nh = int(sum(mlp.hidden))
-    t_start = time.time()
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
 
     values_np, pairs_np = _pa_table(q, lo_np, hi_np)
@@ -115,24 +117,26 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
 
     # ---------------- stage 1: simulation (profile + falsify)
     t0 = time.time()
-    sim = simulate(be, q, lo, hi, pids, cfg.sim_size, cfg.seed, values, pairs, cfg.bisect_pairs, cfg.bisect_steps)
-    cand, pos_prob = P_.candidates_from_counts(sim.counts, cfg.sim_size)
+    with tm("sim"):
+        sim = simulate(be, q, lo, hi, pids, cfg.sim_size, cfg.seed, values, pairs, cfg.bisect_pairs,
+                       cfg.bisect_steps)
+        cand, pos_prob = P_.candidates_from_counts(sim.counts, cfg.sim_size)
     status = np.full(Pn, RUNNING, dtype=np.int8)
     cex_x = np.zeros((Pn, n), dtype=np.int64)
     cex_xp = np.zeros((Pn, n), dtype=np.int64)
     stage = np.array([""] * Pn, dtype=object)
-    found = sim.found.cpu().numpy()
-    if found.any():
-        fi = np.nonzero(found)[0]
-        X = sim.wit_x[fi].cpu().numpy().round().astype(np.int64)
-        XP = sim.wit_xp[fi].cpu().numpy().round().astype(np.int64)
-        ok = exact.check_pair_constraints(X, XP, lo_np[fi], hi_np[fi], q.pa_idx, q.ra_idx, q.tau)
-        viol = exact.is_violation(mlp, X, XP) & ok
-        for k, p in enumerate(fi):
-            if viol[k]:
-                status[p] = SAT
-                cex_x[p], cex_xp[p] = X[k], XP[k]
-                stage[p] = "sim"
+    with tm("sim.confirm"):
+        found = sim.found.cpu().numpy()
+        if found.any():
+            fi = np.nonzero(found)[0]
+            X = sim.wit_x[fi].cpu().numpy().round().astype(np.int64)
+            XP = sim.wit_xp[fi].cpu().numpy().round().astype(np.int64)
+            ok = exact.check_pair_constraints(X, XP, lo_np[fi], hi_np[fi], q.pa_idx, q.ra_idx, q.tau)
+            viol = exact.is_violation(mlp, X, XP) & ok
+            hit = fi[viol]
+            status[hit] = SAT
+            cex_x[hit], cex_xp[hit] = X[viol], XP[viol]
+            stage[hit] = "sim"
     sync()
     t_sim = time.time() - t0
 
@@ -144,18 +148,19 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     s_cand = cand.clone()
     ibp_lb = ibp_ub = None
     if cfg.sound_prune_stats:
-        ibp = be.bounds(lo, hi, mode="ibp", keep_layers=True)
-        ibp_lb = torch.cat(ibp.layer_lb, dim=1)
-        ibp_ub = torch.cat(ibp.layer_ub, dim=1)
-        b_dead, b_rem = P_.bound_dead(cand, ibp_ub[:, :Nh], widths)
-        b_dead = P_.ensure_one_alive(b_dead, widths)
-        sym = be.bounds(lo, hi, mode="symbolic")
-        s_hid = b_rem[:, :Nh] & sym.dead
-        s_dead = torch.zeros_like(b_dead)
-        s_dead[:, :Nh] = s_hid
-        s_cand = b_rem.clone()
-        s_cand[:, :Nh] = b_rem[:, :Nh] & ~s_hid
-        st_dead = P_.ensure_one_alive(P_.merge(b_dead, s_dead), widths)
+        with tm("prune.bounds"):
+            ibp = be.bounds(lo, hi, mode="ibp", keep_layers=True)
+            ibp_lb = torch.cat(ibp.layer_lb, dim=1)
+            ibp_ub = torch.cat(ibp.layer_ub, dim=1)
+            b_dead, b_rem = P_.bound_dead(cand, ibp_ub[:, :Nh], widths)
+            b_dead = P_.ensure_one_alive(b_dead, widths)
+            sym = be.bounds(lo, hi, mode="symbolic")
+            s_hid = b_rem[:, :Nh] & sym.dead
+            s_dead = torch.zeros_like(b_dead)
+            s_dead[:, :Nh] = s_hid
+            s_cand = b_rem.clone()
+            s_cand[:, :Nh] = b_rem[:, :Nh] & ~s_hid
+            st_dead = P_.ensure_one_alive(P_.merge(b_dead, s_dead), widths)
     sync()
     t_prune = time.time() - t0
 
@@ -163,8 +168,9 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     t0 = time.time()
     budget = cfg.soft_timeout if time_budget is None else min(cfg.soft_timeout, time_budget)
     solver = BaBSolver(be, q, BaBConfig(node_budget=cfg.node_budget, batch_nodes=cfg.batch_nodes,
-                                        time_budget=budget))
-    res = solver.solve(lo_np, hi_np, mlp, init_status=status)
+                                        time_budget=budget), timer=tm)
+    with tm("bab"):
+        res = solver.solve(lo_np, hi_np, mlp, init_status=status)
     newly_sat = (res.status == SAT) & (status != SAT)
     stage[newly_sat] = "bab"
     stage[(res.status == UNSAT)] = "bab"
@@ -180,64 +186,76 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     h_success = np.zeros(Pn, dtype=np.int64)
     h_dead_np = np.zeros((Pn, mlp.n_neurons), dtype=bool)
     t_dead_np = st_dead.cpu().numpy()
-    pruned_models: Dict[int, MLP] = {}
+    masked: Dict[int, np.ndarray] = {}
     t_heur = 0.0
     unk = np.nonzero(status == UNKNOWN)[0]
     if cfg.heuristic and unk.size and ibp_ub is not None:
         t0 = time.time()
         h_attempt[unk] = 1
-        lb_np = ibp_lb.cpu().numpy()
-        ub_np = ibp_ub.cpu().numpy()
-        cand_np = cand.cpu().numpy()
-        scand_np = s_cand.cpu().numpy()
-        st_np = st_dead.cpu().numpy()
-        masks = np.zeros((unk.size, Nh), dtype=bool)
-        for k, p in enumerate(unk):
-            hd, md = P_.heuristic_prune_one(lb_np[p], ub_np[p], cand_np[p], scand_np[p], st_np[p], widths,
-                                            cfg.heuristic_p)
-            h_dead_np[p] = hd
-            t_dead_np[p] = md
-            masks[k] = md[:Nh]
-            pruned_models[p] = mlp.masked([md[s] for s in P_.layer_slices(widths)])
+        with tm("heuristic.masks"):
+            lb_np = ibp_lb.cpu().numpy()
+            ub_np = ibp_ub.cpu().numpy()
+            cand_np = cand.cpu().numpy()
+            scand_np = s_cand.cpu().numpy()
+            st_np = st_dead.cpu().numpy()
+            masks = np.zeros((unk.size, Nh), dtype=bool)
+            for k, p in enumerate(unk):
+                hd, md = P_.heuristic_prune_one(lb_np[p], ub_np[p], cand_np[p], scand_np[p], st_np[p], widths,
+                                                cfg.heuristic_p)
+                h_dead_np[p] = hd
+                t_dead_np[p] = md
+                masks[k] = md[:Nh]
+                masked[p] = md
+        # partitions whose heuristic mask equals the sound mask would re-run the same query
         sub_lo, sub_hi = lo_np[unk], hi_np[unk]
         dead_t = torch.from_numpy(masks).to(dev)
+        exact_models = [mlp.masked([masked[p][s] for s in P_.layer_slices(widths)]) for p in unk]
         hsolver = BaBSolver(be, q, BaBConfig(node_budget=cfg.heuristic_node_budget, batch_nodes=cfg.batch_nodes,
-                                             time_budget=budget), dead=dead_t)
-        hres = hsolver.solve(sub_lo, sub_hi, mlp, exact_models=[pruned_models[p] for p in unk])
-        for k, p in enumerate(unk):
-            v = hres.status[k]
-            if v in (SAT, UNSAT):
-                h_success[p] = 1
-                status[p] = v
-                stage[p] = "heuristic"
-                if v == SAT:
-                    cex_x[p], cex_xp[p] = hres.cex_x[k], hres.cex_xp[k]
-            nodes[p] += hres.nodes[k]
+                                             time_budget=budget), dead=dead_t, timer=tm)
+        with tm("heuristic.bab"):
+            hres = hsolver.solve(sub_lo, sub_hi, mlp, exact_models=exact_models)
+        dec = np.isin(hres.status, (SAT, UNSAT))
+        hp = unk[dec]
+        h_success[hp] = 1
+        status[hp] = hres.status[dec]
+        stage[hp] = "heuristic"
+        hs = unk[hres.status == SAT]
+        cex_x[hs] = hres.cex_x[hres.status == SAT]
+        cex_xp[hs] = hres.cex_xp[hres.status == SAT]
+        nodes[unk] += hres.nodes
         sync()
         t_heur = time.time() - t0
 
-    # ---------------- stage 5: replay / fidelity
+    # ---------------- stage 5: replay / fidelity (batched on the device)
     t0 = time.time()
-    recs = []
-    sat_idx = np.nonzero(status == SAT)[0]
-    c_check = np.zeros(Pn, dtype=np.int64)
-    v_acc = np.zeros(Pn, dtype=np.int64)
-    if sat_idx.size:
-        xo = mlp.predict(cex_x[sat_idx])
-        xpo = mlp.predict(cex_xp[sat_idx])
-        v_acc[sat_idx] = (xo != xpo).astype(np.int64)
-        for k, p in enumerate(sat_idx):
-            net = pruned_models.get(p, mlp)
-            c1 = net.predict(cex_x[p:p + 1])[0]
-            c2 = net.predict(cex_xp[p:p + 1])[0]
-            c_check[p] = int(c1 == xo[k] and c2 == xpo[k])
-    pruned_acc = np.ones(Pn)
-    if pruned_models:
-        # agreement of the (heuristically) pruned net with the original on the sim points
-        for p, net in pruned_models.items():
-            X = torch.from_numpy(lo_np[p:p + 1]).to(torch.float32)
-            pts = sample_host(lo_np[p], hi_np[p], ids[p], cfg.sim_size, cfg.seed)
-            pruned_acc[p] = float(np.mean(net.predict(pts) == mlp.predict(pts)))
+    with tm("replay"):
+        sat_idx = np.nonzero(status == SAT)[0]
+        c_check = np.zeros(Pn, dtype=np.int64)
+        v_acc = np.zeros(Pn, dtype=np.int64)
+        if sat_idx.size:
+            xo = mlp.predict(cex_x[sat_idx])
+            xpo = mlp.predict(cex_xp[sat_idx])
+            v_acc[sat_idx] = (xo != xpo).astype(np.int64)
+            dmask = np.zeros((sat_idx.size, Nh), dtype=bool)
+            for k, p in enumerate(sat_idx):
+                if p in masked:
+                    dmask[k] = masked[p][:Nh]
+            xt = torch.from_numpy(np.concatenate([cex_x[sat_idx], cex_xp[sat_idx]])).to(dev, torch.float32)
+            dt_ = torch.from_numpy(np.concatenate([dmask, dmask])).to(dev)
+            zp = be.forward(xt, dt_).cpu().numpy()
+            c1 = (zp[:sat_idx.size] > 0).astype(np.int64)
+            c2 = (zp[sat_idx.size:] > 0).astype(np.int64)
+            c_check[sat_idx] = ((c1 == xo) & (c2 == xpo)).astype(np.int64)
+        pruned_acc = np.ones(Pn)
+        if masked:
+            from ..ops.reference import sample_points
+
+            hp = np.array(sorted(masked))
+            X = sample_points(lo[hp], hi[hp], pids[hp], cfg.sim_size, cfg.seed)
+            dm = torch.from_numpy(np.stack([masked[p][:Nh] for p in hp])).to(dev)
+            z0 = be.forward(X)
+            z1 = be.forward(X, dm[:, None, :].expand(-1, X.shape[1], -1))
+            pruned_acc[hp] = ((z0 > 0) == (z1 > 0)).float().mean(dim=1).cpu().numpy()
     t_replay = time.time() - t0
 
     # ---------------- records (timings apportioned by work)
@@ -252,6 +270,7 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     st_c = P_.compression(st_dead).cpu().numpy()
     h_c = h_dead_np.mean(axis=1)
     t_c = t_dead_np.mean(axis=1)
+    recs = []
     for p in range(Pn):
         v = VERDICT_NAMES[int(status[p])]
         if v == "running":
