@@ -1,14 +1,15 @@
-// Kernel argument structs shared by the .hip kernels and the pybind11 bindings.
+// Kernel argument structs shared by the .hip kernels, the native BaB runtime and the bindings.
 #pragma once
 #include "common.h"
 
 #define FA_MAX_PA 8
 #define FA_MAX_RA 8
 #define FA_CMAX_PA 8
+#define FA_MAX_SPLIT 6      // at most 2^6 children per node and level
 
 struct BoundArgs {
   const float* flat;
-  const float* lo;          // [R, n0]
+  const float* lo;          // [R, n0]  (or node boxes [R/V, n0] when V > 0)
   const float* hi;          // [R, n0]
   const uint8_t* dead_in;   // [R, n_hidden] forced-zero neurons or nullptr
   int R;
@@ -24,6 +25,14 @@ struct BoundArgs {
   float* layer_lb;          // [R, n_neurons] or nullptr
   float* layer_ub;
   uint8_t* dead_out;        // [R, n_hidden] stable-inactive flags or nullptr
+  // node-row expansion: when V > 0, row r is node r / V with its PA dims set to values[r % V]
+  int V;
+  int npa;
+  int pa_idx[FA_MAX_PA];
+  const float* values;      // [V, npa]
+  // per-partition forced-dead masks (heuristic nets): dead = dead_part[node_part[node]]
+  const int* node_part;     // [R / max(V,1)]
+  const uint8_t* dead_part; // [P, n_hidden]
 };
 
 struct FwdArgs {
@@ -64,11 +73,15 @@ struct CertArgs {
   int Nn, n0, V, Pp, norient;
   const float *Lc, *L0, *Le, *Uc, *U0, *Ue;       // x rows   [Nn*V, n0] / [Nn*V]
   const float *Lcp, *L0p, *Lep, *Ucp, *U0p, *Uep; // x' rows
+  const float *olb, *oub, *olbp, *oubp;           // rigorous per-row logit bounds [Nn*V]
   const float *xlo, *xhi, *xplo, *xphi;           // [Nn, n0]
   const int64_t* pairs;                           // [Pp, 2]
   const int64_t* values;                          // [V, npa]
   int npa;
   int pa_idx[FA_CMAX_PA];
+  int nra;
+  int ra_idx[FA_MAX_RA];
+  float tau;
   const uint8_t* shared;                          // [n0]
   float unit;
   float gmarg;                                    // gamma(2*n0+4)
@@ -78,8 +91,44 @@ struct CertArgs {
   uint8_t* open;
   float* score;
   int64_t* split_dim;
-  float* cand_x;
+  float* cand_x;                                  // candidate pair with PA values set, x' clipped
   float* cand_xp;
   int64_t* cand_v;
   int64_t* cand_o;
+  float* scores;                                  // [Nn, 2*n0] split scores or nullptr
+  uint8_t* leaf;                                  // [Nn] single lattice point (x and x') or nullptr
+};
+
+// Branch step: close / flag / split the nodes of one sub-batch into the next BFS level.
+struct SplitArgs {
+  int Nn, n0, relaxed, nra, V, Pp, norient;
+  int ra_idx[FA_MAX_RA];
+  float tau;
+  const float *xlo, *xhi, *xplo, *xphi;   // input nodes [Nn, n0]
+  const int* part;                        // [Nn]
+  const uint8_t* open;                    // [Nn]
+  const uint8_t* leaf;                    // [Nn]
+  const float* scores;                    // [Nn, 2*n0]
+  const float* cand_x;                    // [Nn, n0]
+  const float* cand_xp;
+  const float* pe_lb;                     // point-eval bounds: [2*Nn] (x rows then x' rows)
+  const float* pe_ub;
+  const float *olb, *oub, *olbp, *oubp;   // per-row bounds of the node rows [Nn*V] (leaves)
+  const int64_t* pairs;
+  const int64_t* values;
+  int npa;
+  int pa_idx[FA_CMAX_PA];
+  const uint8_t* shared;
+  int8_t* status;                         // [P]
+  int* part_nodes;                        // [P]
+  int budget;
+  int m;                                  // requested split dims (children = 2^m)
+  float *oxlo, *oxhi, *oxplo, *oxphi;     // output pool
+  int* opart;
+  int* count_out;
+  int cap;
+  float* cand_buf;                        // [cand_cap, 2*n0] candidate (x, x') pairs
+  int* cand_part;                         // [cand_cap]
+  int* cand_count;
+  int cand_cap;
 };

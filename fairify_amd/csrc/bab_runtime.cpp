@@ -1,0 +1,379 @@
+// Native branch-and-bound driver (C++ host runtime around the HIP kernels).
+//
+// The reference decides each partition with one Z3 check() (src/AC/Verify-AC.py:127-163).  Here
+// all partitions of a chunk are decided together by a breadth-first branch-and-bound whose node
+// pool lives in device memory.  One BFS level = ceil(frontier / batch) sub-batches of
+//   bounds (symbolic, node-row expansion)  [+ bounds on x' boxes for relaxed queries]
+//   certify (pair LP certificate + pick)   -> open / leaf / split scores / candidate pair
+//   bounds (interval, candidate points)    -> rigorous point evaluation of the candidates
+//   split                                  -> children in the other pool, candidates flagged
+// followed by ONE host synchronisation (two counters).  Flagged candidates are confirmed
+// exactly by a Python callback (rational/fp64 check of the exact network); confirmed partitions
+// flip to SAT on the device.  Partitions whose nodes are all closed end UNSAT; budgets and the
+// time limit end the rest UNKNOWN.  The branching factor per level (2^m) grows when the
+// frontier is small so that tail levels still fill the GPU.
+#include <hip/hip_runtime.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "args.h"
+
+namespace py = pybind11;
+
+extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream);
+extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
+extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream);
+extern "C" int fa_mark_unknown_launch(const int* part, int n, int8_t* status, hipStream_t stream);
+extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_t v, hipStream_t stream);
+
+// defined in bindings.cpp
+const NetDesc& fa_net_desc(py::handle net);
+
+namespace {
+
+void ck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+void ckl(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + " launch failed, code " + std::to_string(rc));
+}
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void ensure(size_t cnt) {
+    if (cnt <= n) return;
+    if (p) hipFree(p);
+    p = nullptr;
+    ck(hipMalloc((void**)&p, std::max<size_t>(cnt, 1) * sizeof(T)), "hipMalloc");
+    n = cnt;
+  }
+  ~DevBuf() {
+    if (p) hipFree(p);
+  }
+};
+
+float gamma_up(int k, double unit) {
+  const double ku = (k + 2) * unit;
+  return std::nextafter((float)(ku / (1.0 - ku)), INFINITY);
+}
+
+}  // namespace
+
+class BabRuntime {
+ public:
+  BabRuntime(py::handle net, uintptr_t flat, std::vector<int> pa, std::vector<float> values_f,
+             std::vector<int64_t> values_i, std::vector<int64_t> pairs, std::vector<int> ra, float tau,
+             std::vector<uint8_t> shared, int capacity, int batch_nodes, int cand_cap, double unit)
+      : net_(fa_net_desc(net)),
+        flat_((const float*)flat),
+        pa_(std::move(pa)),
+        ra_(std::move(ra)),
+        tau_(tau),
+        cap_(capacity),
+        batch_(batch_nodes),
+        cand_cap_(cand_cap),
+        unit_(unit) {
+    n0_ = net_.dims[0];
+    npa_ = (int)pa_.size();
+    if (npa_ == 0 || npa_ > FA_CMAX_PA || (int)ra_.size() > FA_MAX_RA) throw std::invalid_argument("bad PA/RA");
+    V_ = (int)(values_i.size() / npa_);
+    Pp_ = (int)(pairs.size() / 2);
+    relaxed_ = !ra_.empty() && tau_ > 0;
+    norient_ = relaxed_ ? 2 : 1;
+    if ((int)shared.size() != n0_) throw std::invalid_argument("shared mask size");
+    vals_f_.ensure(values_f.size());
+    vals_i_.ensure(values_i.size());
+    pairs_.ensure(pairs.size());
+    shared_.ensure(shared.size());
+    ck(hipMemcpy(vals_f_.p, values_f.data(), values_f.size() * sizeof(float), hipMemcpyHostToDevice), "cp");
+    ck(hipMemcpy(vals_i_.p, values_i.data(), values_i.size() * sizeof(int64_t), hipMemcpyHostToDevice), "cp");
+    ck(hipMemcpy(pairs_.p, pairs.data(), pairs.size() * sizeof(int64_t), hipMemcpyHostToDevice), "cp");
+    ck(hipMemcpy(shared_.p, shared.data(), shared.size(), hipMemcpyHostToDevice), "cp");
+    const size_t cn = (size_t)cap_ * n0_;
+    for (int i = 0; i < 2; ++i) {
+      lo_[i].ensure(cn);
+      hi_[i].ensure(cn);
+      part_[i].ensure(cap_);
+      if (relaxed_) {
+        plo_[i].ensure(cn);
+        phi_[i].ensure(cn);
+      }
+    }
+    const size_t R = (size_t)batch_ * V_;
+    for (int s = 0; s < (relaxed_ ? 2 : 1); ++s) {
+      Lc_[s].ensure(R * n0_);
+      Uc_[s].ensure(R * n0_);
+      L0_[s].ensure(R); Le_[s].ensure(R); U0_[s].ensure(R); Ue_[s].ensure(R);
+      olb_[s].ensure(R); oub_[s].ensure(R);
+    }
+    const size_t Q = (size_t)Pp_ * norient_;
+    gmin_.ensure(batch_ * Q);
+    tstar_.ensure(batch_ * Q);
+    open_.ensure(batch_);
+    leaf_.ensure(batch_);
+    score_.ensure(batch_);
+    split_.ensure(batch_);
+    cv_.ensure(batch_);
+    co_.ensure(batch_);
+    cand_.ensure((size_t)2 * batch_ * n0_);
+    scores_.ensure((size_t)batch_ * 2 * n0_);
+    pe_lb_.ensure(2 * (size_t)batch_);
+    pe_ub_.ensure(2 * (size_t)batch_);
+    pe_part_.ensure(2 * (size_t)batch_);
+    cand_buf_.ensure((size_t)cand_cap_ * 2 * n0_);
+    cand_part_.ensure(cand_cap_);
+    counters_.ensure(2);
+    ck(hipHostMalloc((void**)&hcount_, 2 * sizeof(int)), "hipHostMalloc");
+  }
+  ~BabRuntime() {
+    if (hcount_) hipHostFree(hcount_);
+  }
+
+  py::tuple solve(py::array_t<float, py::array::c_style | py::array::forcecast> lo,
+                  py::array_t<float, py::array::c_style | py::array::forcecast> hi,
+                  py::array_t<int8_t, py::array::c_style | py::array::forcecast> status0, int budget,
+                  double time_budget, uintptr_t dead_part, py::object confirm, uintptr_t stream_i) {
+    hipStream_t st = (hipStream_t)stream_i;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int P = (int)lo.shape(0);
+    if (lo.ndim() != 2 || lo.shape(1) != n0_ || hi.shape(0) != P || status0.shape(0) != P)
+      throw std::invalid_argument("solve: shape mismatch");
+    status_.ensure(P);
+    nodes_.ensure(P);
+    std::vector<int8_t> hstatus(status0.data(), status0.data() + P);
+    ck(hipMemcpyAsync(status_.p, hstatus.data(), P, hipMemcpyHostToDevice, st), "cp status");
+    ck(hipMemsetAsync(nodes_.p, 0, P * sizeof(int), st), "memset nodes");
+    // initial pool: running partitions
+    std::vector<int> run;
+    for (int p = 0; p < P; ++p)
+      if (hstatus[p] == 3) run.push_back(p);
+    if ((int)run.size() > cap_) throw std::invalid_argument("more partitions than pool capacity");
+    std::vector<float> hl((size_t)run.size() * n0_), hh((size_t)run.size() * n0_);
+    for (size_t i = 0; i < run.size(); ++i)
+      for (int d = 0; d < n0_; ++d) {
+        hl[i * n0_ + d] = lo.data()[(size_t)run[i] * n0_ + d];
+        hh[i * n0_ + d] = hi.data()[(size_t)run[i] * n0_ + d];
+      }
+    int cur = 0;
+    int n_in = (int)run.size();
+    if (n_in) {
+      ck(hipMemcpyAsync(lo_[0].p, hl.data(), hl.size() * sizeof(float), hipMemcpyHostToDevice, st), "cp lo");
+      ck(hipMemcpyAsync(hi_[0].p, hh.data(), hh.size() * sizeof(float), hipMemcpyHostToDevice, st), "cp hi");
+      ck(hipMemcpyAsync(part_[0].p, run.data(), run.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp part");
+      if (relaxed_) {
+        for (size_t i = 0; i < run.size(); ++i)
+          for (int r : ra_) {
+            hl[i * n0_ + r] -= tau_;
+            hh[i * n0_ + r] += tau_;
+          }
+        ck(hipMemcpyAsync(plo_[0].p, hl.data(), hl.size() * sizeof(float), hipMemcpyHostToDevice, st), "cp");
+        ck(hipMemcpyAsync(phi_[0].p, hh.data(), hh.size() * sizeof(float), hipMemcpyHostToDevice, st), "cp");
+      }
+    }
+    // host result buffers
+    py::array_t<int64_t> cex_x({P, n0_}), cex_xp({P, n0_});
+    std::memset(cex_x.mutable_data(), 0, sizeof(int64_t) * (size_t)P * n0_);
+    std::memset(cex_xp.mutable_data(), 0, sizeof(int64_t) * (size_t)P * n0_);
+    std::vector<char> got(P, 0);
+    int levels = 0, launches = 0;
+    long long total_nodes = 0;
+    bool timed_out = false;
+    const int target = std::max(batch_, 1);
+    while (n_in > 0) {
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > time_budget) {
+        ckl(fa_mark_unknown_launch(part_[cur].p, n_in, status_.p, st), "mark");
+        timed_out = true;
+        break;
+      }
+      int m = 1;
+      while (m < FA_MAX_SPLIT && (long long)n_in << (m + 1) <= (long long)target) ++m;
+      ck(hipMemsetAsync(counters_.p, 0, 2 * sizeof(int), st), "memset counters");
+      const int nxt = cur ^ 1;
+      for (int s = 0; s < n_in; s += batch_) {
+        const int nb = std::min(batch_, n_in - s);
+        const float* blo = lo_[cur].p + (size_t)s * n0_;
+        const float* bhi = hi_[cur].p + (size_t)s * n0_;
+        const float* bplo = relaxed_ ? plo_[cur].p + (size_t)s * n0_ : blo;
+        const float* bphi = relaxed_ ? phi_[cur].p + (size_t)s * n0_ : bhi;
+        const int* bpart = part_[cur].p + s;
+        launch_bounds(blo, bhi, bpart, nb, 0, dead_part, st);
+        if (relaxed_) launch_bounds(bplo, bphi, bpart, nb, 1, dead_part, st);
+        const int sx = relaxed_ ? 1 : 0;
+        CertArgs c{};
+        c.Nn = nb; c.n0 = n0_; c.V = V_; c.Pp = Pp_; c.norient = norient_;
+        c.Lc = Lc_[0].p; c.L0 = L0_[0].p; c.Le = Le_[0].p; c.Uc = Uc_[0].p; c.U0 = U0_[0].p; c.Ue = Ue_[0].p;
+        c.Lcp = Lc_[sx].p; c.L0p = L0_[sx].p; c.Lep = Le_[sx].p;
+        c.Ucp = Uc_[sx].p; c.U0p = U0_[sx].p; c.Uep = Ue_[sx].p;
+        c.olb = olb_[0].p; c.oub = oub_[0].p; c.olbp = olb_[sx].p; c.oubp = oub_[sx].p;
+        c.xlo = blo; c.xhi = bhi; c.xplo = bplo; c.xphi = bphi;
+        c.pairs = pairs_.p; c.values = vals_i_.p; c.npa = npa_;
+        for (int k = 0; k < npa_; ++k) c.pa_idx[k] = pa_[k];
+        c.nra = relaxed_ ? (int)ra_.size() : 0;
+        for (int k = 0; k < c.nra; ++k) c.ra_idx[k] = ra_[k];
+        c.tau = tau_;
+        c.shared = shared_.p;
+        c.unit = (float)unit_;
+        c.gmarg = gamma_up(2 * n0_ + 4, unit_);
+        c.gmin = gmin_.p; c.tstar = tstar_.p;
+        c.open = open_.p; c.score = score_.p; c.split_dim = split_.p;
+        c.cand_x = cand_.p; c.cand_xp = cand_.p + (size_t)nb * n0_;
+        c.cand_v = cv_.p; c.cand_o = co_.p;
+        c.scores = scores_.p; c.leaf = leaf_.p;
+        ckl(fa_certify_launch(c, st), "certify");
+        // rigorous interval evaluation of the candidate pairs (rows: x then x')
+        ck(hipMemcpyAsync(pe_part_.p, bpart, nb * sizeof(int), hipMemcpyDeviceToDevice, st), "cp");
+        ck(hipMemcpyAsync(pe_part_.p + nb, bpart, nb * sizeof(int), hipMemcpyDeviceToDevice, st), "cp");
+        BoundArgs b{};
+        b.flat = flat_; b.lo = cand_.p; b.hi = cand_.p; b.R = 2 * nb; b.symbolic = 0;
+        b.out_lb = pe_lb_.p; b.out_ub = pe_ub_.p;
+        if (dead_part) { b.node_part = pe_part_.p; b.dead_part = (const uint8_t*)dead_part; }
+        ckl(fa_bounds_launch(net_, b, st), "bounds(points)");
+        SplitArgs sa{};
+        sa.Nn = nb; sa.n0 = n0_; sa.relaxed = relaxed_ ? 1 : 0; sa.nra = relaxed_ ? (int)ra_.size() : 0;
+        for (int k = 0; k < sa.nra; ++k) sa.ra_idx[k] = ra_[k];
+        sa.V = V_; sa.Pp = Pp_; sa.norient = norient_; sa.tau = tau_;
+        sa.xlo = blo; sa.xhi = bhi; sa.xplo = bplo; sa.xphi = bphi; sa.part = bpart;
+        sa.open = open_.p; sa.leaf = leaf_.p; sa.scores = scores_.p;
+        sa.cand_x = c.cand_x; sa.cand_xp = c.cand_xp; sa.pe_lb = pe_lb_.p; sa.pe_ub = pe_ub_.p;
+        sa.olb = c.olb; sa.oub = c.oub; sa.olbp = c.olbp; sa.oubp = c.oubp;
+        sa.pairs = pairs_.p; sa.values = vals_i_.p; sa.npa = npa_;
+        for (int k = 0; k < npa_; ++k) sa.pa_idx[k] = pa_[k];
+        sa.shared = shared_.p;
+        sa.status = status_.p; sa.part_nodes = nodes_.p; sa.budget = budget; sa.m = m;
+        sa.oxlo = lo_[nxt].p; sa.oxhi = hi_[nxt].p;
+        sa.oxplo = relaxed_ ? plo_[nxt].p : nullptr; sa.oxphi = relaxed_ ? phi_[nxt].p : nullptr;
+        sa.opart = part_[nxt].p; sa.count_out = counters_.p; sa.cap = cap_;
+        sa.cand_buf = cand_buf_.p; sa.cand_part = cand_part_.p; sa.cand_count = counters_.p + 1;
+        sa.cand_cap = cand_cap_;
+        ckl(fa_split_launch(sa, st), "split");
+        launches += relaxed_ ? 6 : 5;
+      }
+      ck(hipMemcpyAsync(hcount_, counters_.p, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "cp counters");
+      ck(hipStreamSynchronize(st), "sync");
+      total_nodes += n_in;
+      const int n_out = std::min(hcount_[0], cap_);
+      const int n_cand = std::min(hcount_[1], cand_cap_);
+      ++levels;
+      if (n_cand > 0) confirm_candidates(n_cand, confirm, got, cex_x, cex_xp, st);
+      cur = nxt;
+      n_in = n_out;
+    }
+    std::vector<int8_t> sout(P);
+    std::vector<int> nout(P);
+    ck(hipMemcpyAsync(sout.data(), status_.p, P, hipMemcpyDeviceToHost, st), "cp");
+    ck(hipMemcpyAsync(nout.data(), nodes_.p, P * sizeof(int), hipMemcpyDeviceToHost, st), "cp");
+    ck(hipStreamSynchronize(st), "sync");
+    py::array_t<int8_t> status_out(P);
+    py::array_t<int64_t> nodes_out(P);
+    for (int p = 0; p < P; ++p) {
+      int8_t v = sout[p];
+      if (got[p]) v = 1;
+      else if (v == 3) v = timed_out ? 0 : 2;   // all nodes closed => UNSAT
+      status_out.mutable_data()[p] = v;
+      nodes_out.mutable_data()[p] = nout[p];
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    py::dict stats;
+    stats["levels"] = levels;
+    stats["launches"] = launches;
+    stats["nodes"] = total_nodes;
+    stats["time"] = el;
+    stats["timed_out"] = timed_out;
+    return py::make_tuple(status_out, cex_x, cex_xp, nodes_out, stats);
+  }
+
+ private:
+  void launch_bounds(const float* lo, const float* hi, const int* part, int nb, int slot, uintptr_t dead_part,
+                     hipStream_t st) {
+    BoundArgs b{};
+    b.flat = flat_;
+    b.lo = lo;
+    b.hi = hi;
+    b.R = nb * V_;
+    b.symbolic = 1;
+    b.out_lb = olb_[slot].p; b.out_ub = oub_[slot].p;
+    b.Lc = Lc_[slot].p; b.L0 = L0_[slot].p; b.Le = Le_[slot].p;
+    b.Uc = Uc_[slot].p; b.U0 = U0_[slot].p; b.Ue = Ue_[slot].p;
+    b.V = V_;
+    b.npa = npa_;
+    for (int k = 0; k < npa_; ++k) b.pa_idx[k] = pa_[k];
+    b.values = vals_f_.p;
+    if (dead_part) {
+      b.node_part = part;
+      b.dead_part = (const uint8_t*)dead_part;
+    }
+    ckl(fa_bounds_launch(net_, b, st), "bounds");
+  }
+
+  void confirm_candidates(int n_cand, py::object& confirm, std::vector<char>& got, py::array_t<int64_t>& cex_x,
+                          py::array_t<int64_t>& cex_xp, hipStream_t st) {
+    py::array_t<float> buf({n_cand, 2 * n0_});
+    py::array_t<int> parts(n_cand);
+    ck(hipMemcpyAsync(buf.mutable_data(), cand_buf_.p, sizeof(float) * (size_t)n_cand * 2 * n0_,
+                      hipMemcpyDeviceToHost, st), "cp cand");
+    ck(hipMemcpyAsync(parts.mutable_data(), cand_part_.p, sizeof(int) * n_cand, hipMemcpyDeviceToHost, st), "cp");
+    ck(hipStreamSynchronize(st), "sync");
+    py::array_t<bool> ok = confirm(parts, buf).cast<py::array_t<bool>>();
+    std::vector<int> newly;
+    const float* B = buf.data();
+    for (int i = 0; i < n_cand; ++i) {
+      const int p = parts.data()[i];
+      if (!ok.data()[i] || got[p]) continue;
+      got[p] = 1;
+      newly.push_back(p);
+      for (int d = 0; d < n0_; ++d) {
+        cex_x.mutable_data()[(size_t)p * n0_ + d] = (int64_t)std::llround(B[(size_t)i * 2 * n0_ + d]);
+        cex_xp.mutable_data()[(size_t)p * n0_ + d] = (int64_t)std::llround(B[(size_t)i * 2 * n0_ + n0_ + d]);
+      }
+    }
+    if (!newly.empty()) {
+      idx_.ensure(newly.size());
+      ck(hipMemcpyAsync(idx_.p, newly.data(), newly.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp idx");
+      ckl(fa_set_status_launch(idx_.p, (int)newly.size(), status_.p, 1, st), "set_status");
+      ck(hipStreamSynchronize(st), "sync");
+    }
+  }
+
+  NetDesc net_;
+  const float* flat_;
+  std::vector<int> pa_, ra_;
+  float tau_;
+  int cap_, batch_, cand_cap_;
+  double unit_;
+  int n0_ = 0, npa_ = 0, V_ = 0, Pp_ = 0, norient_ = 1;
+  bool relaxed_ = false;
+  DevBuf<float> vals_f_;
+  DevBuf<int64_t> vals_i_, pairs_;
+  DevBuf<uint8_t> shared_;
+  DevBuf<float> lo_[2], hi_[2], plo_[2], phi_[2];
+  DevBuf<int> part_[2];
+  DevBuf<float> Lc_[2], Uc_[2], L0_[2], Le_[2], U0_[2], Ue_[2], olb_[2], oub_[2];
+  DevBuf<float> gmin_, tstar_, score_, cand_, scores_, pe_lb_, pe_ub_, cand_buf_;
+  DevBuf<uint8_t> open_, leaf_;
+  DevBuf<int64_t> split_, cv_, co_;
+  DevBuf<int> pe_part_, cand_part_, counters_, nodes_, idx_;
+  DevBuf<int8_t> status_;
+  int* hcount_ = nullptr;
+};
+
+void register_bab(py::module& m) {
+  py::class_<BabRuntime>(m, "BabRuntime")
+      .def(py::init<py::handle, uintptr_t, std::vector<int>, std::vector<float>, std::vector<int64_t>,
+                    std::vector<int64_t>, std::vector<int>, float, std::vector<uint8_t>, int, int, int, double>(),
+           py::arg("net"), py::arg("flat"), py::arg("pa"), py::arg("values_f"), py::arg("values_i"),
+           py::arg("pairs"), py::arg("ra"), py::arg("tau"), py::arg("shared"), py::arg("capacity"),
+           py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"))
+      .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
+           py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"));
+}

@@ -57,10 +57,14 @@ struct Net {
     d.max_wsize = mws;
     d.unit = (float)unit;
     d.g_conc = gamma_up(dims[0] + 1, unit);
+    d.g_one = gamma_up(1, unit);
     n_params = off;
   }
   int n_params;
 };
+
+const NetDesc& fa_net_desc(py::handle h) { return h.cast<const Net&>().d; }
+void register_bab(py::module& m);
 
 static void check(int rc, const char* what) {
   if (rc != 0) throw std::runtime_error(std::string(what) + " launch failed, code " + std::to_string(rc));
@@ -79,7 +83,6 @@ PYBIND11_MODULE(_C, m) {
                      uintptr_t Uc, uintptr_t U0, uintptr_t Ue, uintptr_t layer_lb, uintptr_t layer_ub,
                      uintptr_t dead_out, int G, uintptr_t stream) {
     NetDesc d = net.d;
-    d.g_conc = gamma_up(symbolic ? d.dims[0] + 1 : 1, d.unit);
     BoundArgs a{};
     a.flat = P<const float>(flat);
     a.lo = P<const float>(lo);
@@ -141,23 +144,29 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("certify", [](int Nn, int n0, int V, int Pp, int norient, std::vector<uintptr_t> fx, std::vector<uintptr_t> fxp,
                       uintptr_t xlo, uintptr_t xhi, uintptr_t xplo, uintptr_t xphi, uintptr_t pairs, uintptr_t values,
-                      const std::vector<int>& pa, uintptr_t shared, double unit, double gmarg, uintptr_t gmin,
-                      uintptr_t tstar, uintptr_t open, uintptr_t score, uintptr_t split_dim, uintptr_t cand_x,
-                      uintptr_t cand_xp, uintptr_t cand_v, uintptr_t cand_o, uintptr_t stream) {
-    if (pa.size() > FA_CMAX_PA) throw std::invalid_argument("too many PA dims");
-    if (fx.size() != 6 || fxp.size() != 6) throw std::invalid_argument("need 6 form pointers");
+                      const std::vector<int>& pa, const std::vector<int>& ra, double tau, uintptr_t shared,
+                      double unit, double gmarg, uintptr_t gmin, uintptr_t tstar, uintptr_t open, uintptr_t score,
+                      uintptr_t split_dim, uintptr_t cand_x, uintptr_t cand_xp, uintptr_t cand_v, uintptr_t cand_o,
+                      uintptr_t scores, uintptr_t leaf, uintptr_t stream) {
+    if (pa.size() > FA_CMAX_PA || ra.size() > FA_MAX_RA) throw std::invalid_argument("too many PA/RA dims");
+    if (fx.size() != 8 || fxp.size() != 8) throw std::invalid_argument("need 8 form pointers (6 forms + lb/ub)");
     CertArgs a{};
     a.Nn = Nn; a.n0 = n0; a.V = V; a.Pp = Pp; a.norient = norient;
     a.Lc = P<const float>(fx[0]); a.L0 = P<const float>(fx[1]); a.Le = P<const float>(fx[2]);
     a.Uc = P<const float>(fx[3]); a.U0 = P<const float>(fx[4]); a.Ue = P<const float>(fx[5]);
+    a.olb = P<const float>(fx[6]); a.oub = P<const float>(fx[7]);
     a.Lcp = P<const float>(fxp[0]); a.L0p = P<const float>(fxp[1]); a.Lep = P<const float>(fxp[2]);
     a.Ucp = P<const float>(fxp[3]); a.U0p = P<const float>(fxp[4]); a.Uep = P<const float>(fxp[5]);
+    a.olbp = P<const float>(fxp[6]); a.oubp = P<const float>(fxp[7]);
     a.xlo = P<const float>(xlo); a.xhi = P<const float>(xhi);
     a.xplo = P<const float>(xplo); a.xphi = P<const float>(xphi);
     a.pairs = P<const int64_t>(pairs);
     a.values = P<const int64_t>(values);
     a.npa = (int)pa.size();
     for (size_t i = 0; i < pa.size(); ++i) a.pa_idx[i] = pa[i];
+    a.nra = (int)ra.size();
+    for (size_t i = 0; i < ra.size(); ++i) a.ra_idx[i] = ra[i];
+    a.tau = (float)tau;
     a.shared = P<const uint8_t>(shared);
     a.unit = (float)unit;
     a.gmarg = std::nextafter((float)gmarg, INFINITY);
@@ -165,8 +174,10 @@ PYBIND11_MODULE(_C, m) {
     a.open = P<uint8_t>(open); a.score = P<float>(score); a.split_dim = P<int64_t>(split_dim);
     a.cand_x = P<float>(cand_x); a.cand_xp = P<float>(cand_xp);
     a.cand_v = P<int64_t>(cand_v); a.cand_o = P<int64_t>(cand_o);
+    a.scores = P<float>(scores); a.leaf = P<uint8_t>(leaf);
     check(fa_certify_launch(a, (hipStream_t)stream), "certify");
   });
 
   m.def("arch", []() { return std::string("gfx950"); });
+  register_bab(m);
 }

@@ -5,29 +5,30 @@
 // kernel over thousands of boxes; it is also the bounding primitive of the branch-and-bound
 // prover.  Algorithm and error accounting: ops/reference.py:bounds (same arithmetic).
 //
-// A workgroup (4 wave64) owns G box-rows.  Per row the linear forms U, L of the current layer
-// are kept in LDS as [2 blocks][rb rows][width] with rows = n0 coefficient rows (symbolic
-// mode only) + the constant row + the error row.  A layer is
-//     U' = [U | L] . [W+ ; W-]      L' = [L | U] . [W+ ; W-]
-// i.e. one GEMM of (G*2*rb) x (2*n_in) by (2*n_in) x n_out on v_mfma_f32_16x16x4_f32 with the
-// layer's W staged in LDS (W+/W- formed on the fly).  The error row rides along the same GEMM
-// (its second half is negated so it accumulates |W-|).  The epilogue (one thread per
-// (row, neuron)) concretises both forms over the box, applies the ReLU relaxation in place and
-// writes the error row for the next layer; only the logit forms (and, on request, per-neuron
-// bounds / dead flags) go back to HBM.
+// A workgroup (4 wave64) owns G box-rows.  Per row, two blocks (upper U / lower L) of rows are
+// kept in LDS, each [rb rows][width]:
+//   symbolic: n0 coefficient rows, constant row, error row, interval row, interval-error row
+//   ibp     : interval row, interval-error row
+// A layer is ONE GEMM   out_U = [U | L] . [W+ ; W-],   out_L = [L | U] . [W+ ; W-]
+// of (G*2*rb) x (2*n_in) by (2*n_in) x n_out on v_mfma_f32_16x16x4_f32 with the layer's W staged
+// in LDS (W+/W- formed on the fly; error rows negated in the second half so they accumulate
+// |W-|).  The epilogue (one thread per (row, neuron)) intersects the symbolic and interval
+// bounds, applies the ReLU relaxation to the forms in place, re-seeds the interval rows with
+// max(0, bound) and writes the error rows for the next layer.  Only the logit forms (and, on
+// request, per-neuron bounds / dead flags) go back to HBM.
 #include "args.h"
-
-
 
 __global__ void __launch_bounds__(FA_THREADS)
 fa_bounds_kernel(NetDesc net, BoundArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int n0 = net.dims[0];
   const int G = a.G;
-  const int nc = a.symbolic ? n0 + 1 : 1;      // coefficient rows incl. constant
-  const int rb = nc + 1;                        // + error row
-  const int crow = nc - 1;                      // constant row index
-  const int erow = nc;                          // error row index
+  const bool sym = a.symbolic != 0;
+  const int crow = n0;                          // constant row (symbolic)
+  const int erow = n0 + 1;                      // form error row (symbolic)
+  const int irow = sym ? n0 + 2 : 0;            // interval row
+  const int ierow = irow + 1;                   // interval error row
+  const int rb = irow + 2;
   const int S = a.stride;
   float* s_lo = smem;                           // [G][n0]
   float* s_hi = s_lo + G * n0;
@@ -44,27 +45,36 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
     int g = i / n0, d = i % n0;
     int r = row0 + g;
     float l = 0.f, h = 0.f;
-    if (r < a.R) { l = a.lo[(size_t)r * n0 + d]; h = a.hi[(size_t)r * n0 + d]; }
+    if (r < a.R) {
+      if (a.V > 0) {  // node-row expansion: PA dims take the row's assignment
+        const int node = r / a.V, v = r - node * a.V;
+        l = a.lo[(size_t)node * n0 + d];
+        h = a.hi[(size_t)node * n0 + d];
+        for (int k = 0; k < a.npa; ++k)
+          if (a.pa_idx[k] == d) l = h = a.values[v * a.npa + k];
+      } else {
+        l = a.lo[(size_t)r * n0 + d];
+        h = a.hi[(size_t)r * n0 + d];
+      }
+    }
     s_lo[i] = l; s_hi[i] = h; s_m[i] = fmaxf(fabsf(l), fabsf(h));
   }
   __syncthreads();
-  // ---- initial forms (layer-0 inputs): identity (symbolic) or [hi | lo] constants (IBP)
+  // ---- layer-0 inputs: identity forms + [hi | lo] interval rows
   {
     const float g0 = net.g_gemm[0];
     for (int i = tid; i < G * 2 * rb * n0; i += FA_THREADS) {
-      int j = i % n0;
-      int rr = (i / n0) % rb;
-      int o = (i / (n0 * rb)) % 2;
-      int g = i / (n0 * rb * 2);
+      const int j = i % n0;
+      const int rr = (i / n0) % rb;
+      const int o = (i / (n0 * rb)) % 2;
+      const int g = i / (n0 * rb * 2);
+      const float c = o == 0 ? s_hi[g * n0 + j] : s_lo[g * n0 + j];
       float v;
-      if (a.symbolic) {
-        if (rr < n0) v = (rr == j) ? 1.f : 0.f;
-        else if (rr == crow) v = 0.f;
-        else v = g0 * s_m[g * n0 + j];
-      } else {
-        float c = o == 0 ? s_hi[g * n0 + j] : s_lo[g * n0 + j];
-        v = (rr == crow) ? c : g0 * fabsf(c);
-      }
+      if (rr == irow) v = c;
+      else if (rr == ierow) v = g0 * fabsf(c);
+      else if (rr < n0) v = (rr == j) ? 1.f : 0.f;
+      else if (rr == crow) v = 0.f;
+      else v = g0 * s_m[g * n0 + j];           // erow
       bufA[((g * 2 + o) * rb + rr) * S + j] = v;
     }
   }
@@ -78,7 +88,7 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
     const float* bias = a.flat + net.b_off[l];
     const int ws = a.wstride;
     for (int i = tid; i < n_in * n_out; i += FA_THREADS) {
-      int k = i / n_out, j = i % n_out;
+      const int k = i / n_out, j = i % n_out;
       s_W[k * ws + j] = W[i];
     }
     __syncthreads();
@@ -96,22 +106,22 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
       const int r = rem - o * rb;
       const float* a_own = bufA + ((g * 2 + o) * rb + r) * S;
       const float* a_oth = bufA + ((g * 2 + (1 - o)) * rb + r) * S;
-      const float sgn = (r == erow) ? -1.f : 1.f;
+      const float sgn = (r == ierow || (sym && r == erow)) ? -1.f : 1.f;
       const int j = nt * 16 + (lane & 15);
       const bool jval = j < n_out;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       for (int k0 = 0; k0 < n_in; k0 += 4) {
         const int k = k0 + kq;
         const bool kv = k < n_in;
-        float av = (mval && kv) ? a_own[k] : 0.f;
-        float wv = (jval && kv) ? s_W[k * ws + j] : 0.f;
+        const float av = (mval && kv) ? a_own[k] : 0.f;
+        const float wv = (jval && kv) ? s_W[k * ws + j] : 0.f;
         acc = fa_mfma4(av, fmaxf(wv, 0.f), acc);
       }
       for (int k0 = 0; k0 < n_in; k0 += 4) {
         const int k = k0 + kq;
         const bool kv = k < n_in;
-        float av = (mval && kv) ? sgn * a_oth[k] : 0.f;
-        float wv = (jval && kv) ? s_W[k * ws + j] : 0.f;
+        const float av = (mval && kv) ? sgn * a_oth[k] : 0.f;
+        const float wv = (jval && kv) ? s_W[k * ws + j] : 0.f;
         acc = fa_mfma4(av, fminf(wv, 0.f), acc);
       }
 #pragma unroll
@@ -127,10 +137,11 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
       }
     }
     __syncthreads();
-    // ---------------- epilogue: concretise, relax, next-layer error rows
+    // ---------------- epilogue: intersect, relax, re-seed interval rows, next error rows
     const bool last = (l == net.n_layers - 1);
     const float gg_ = net.g_gemm[l];
     const float gc = net.g_conc;
+    const float gi = net.g_one;
     const float gnext = last ? 0.f : net.g_gemm[l + 1];
     const int noff = net.neuron_off[l];
     for (int it = tid; it < G * n_out; it += FA_THREADS) {
@@ -139,14 +150,24 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
       const bool rv = rglob < a.R;
       float* cu = bufB + ((g * 2 + 0) * rb) * S + j;
       float* cl = bufB + ((g * 2 + 1) * rb) * S + j;
-      const float* glo = s_lo + g * n0;
-      const float* ghi = s_hi + g * n0;
-      const float* gm = s_m + g * n0;
       const float b = bias[j];
-      const float cU = cu[crow * S] + b, cL = cl[crow * S] + b;
-      float mnU = cU, mxU = cU, mgU = fabsf(cU);
-      float mnL = cL, mxL = cL, mgL = fabsf(cL);
-      if (a.symbolic) {
+      // interval rows
+      const float hI = cu[irow * S] + b, lI = cl[irow * S] + b;
+      const float eIh = cu[ierow * S] * (1.f + 2.f * gg_) + gg_ * fabsf(b);
+      const float eIl = cl[ierow * S] * (1.f + 2.f * gg_) + gg_ * fabsf(b);
+      float ub = hI + gi * fabsf(hI) + eIh;
+      float lb = lI - gi * fabsf(lI) - eIl;
+      // symbolic forms
+      float cU = 0.f, cL = 0.f, mnU = 0.f, mxU = 0.f, mgU = 0.f, mnL = 0.f, mxL = 0.f, mgL = 0.f;
+      float eU = 0.f, eL = 0.f;
+      if (sym) {
+        const float* glo = s_lo + g * n0;
+        const float* ghi = s_hi + g * n0;
+        const float* gm = s_m + g * n0;
+        cU = cu[crow * S] + b;
+        cL = cl[crow * S] + b;
+        mnU = cU; mxU = cU; mgU = fabsf(cU);
+        mnL = cL; mxL = cL; mgL = fabsf(cL);
         for (int i = 0; i < n0; ++i) {
           const float u = cu[i * S], v = cl[i * S];
           const float ul = u * glo[i], uh = u * ghi[i];
@@ -154,11 +175,11 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
           mnU += fminf(ul, uh); mxU += fmaxf(ul, uh); mgU += fabsf(u) * gm[i];
           mnL += fminf(vl, vh); mxL += fmaxf(vl, vh); mgL += fabsf(v) * gm[i];
         }
+        eU = cu[erow * S] * (1.f + 2.f * gg_) + gg_ * fabsf(b);
+        eL = cl[erow * S] * (1.f + 2.f * gg_) + gg_ * fabsf(b);
+        ub = fminf(ub, mxU + gc * mgU + eU);
+        lb = fmaxf(lb, mnL - gc * mgL - eL);
       }
-      const float eU = cu[erow * S] * (1.f + 2.f * gg_) + gg_ * fabsf(b);
-      const float eL = cl[erow * S] * (1.f + 2.f * gg_) + gg_ * fabsf(b);
-      const float ub = mxU + gc * mgU + eU;
-      const float lb = mnL - gc * mgL - eL;
       if (rv && a.layer_lb) {
         a.layer_lb[(size_t)rglob * net.n_neurons + noff + j] = lb;
         a.layer_ub[(size_t)rglob * net.n_neurons + noff + j] = ub;
@@ -167,7 +188,7 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
         if (rv) {
           a.out_lb[rglob] = lb;
           a.out_ub[rglob] = ub;
-          if (a.symbolic) {
+          if (sym) {
             for (int i = 0; i < n0; ++i) {
               a.Lc[(size_t)rglob * n0 + i] = cl[i * S];
               a.Uc[(size_t)rglob * n0 + i] = cu[i * S];
@@ -180,23 +201,36 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
       }
       bool forced = false;
       if (a.dead_in && rv) forced = a.dead_in[(size_t)rglob * net.n_hidden + noff + j] != 0;
-      if (rv && a.dead_out) a.dead_out[(size_t)rglob * net.n_hidden + noff + j] = (ub <= 0.f) ? 1 : 0;
-      // upper relaxation: chord over [aa, ub] of T(x) = U(x) + eU
-      const float aa = mnU - gc * mgU + eU;
-      const bool zeroU = (ub <= 0.f) || forced;
-      const bool identU = !zeroU && (aa >= 0.f);
-      float s = 1.f, shift = 0.f, eUn, mgUn = 0.f;
-      if (zeroU) {
-        for (int i = 0; i < nc; ++i) cu[i * S] = 0.f;
-        eUn = 0.f;
-      } else if (identU) {
+      else if (a.dead_part && rv) {
+        const int node = a.V > 0 ? rglob / a.V : rglob;
+        forced = a.dead_part[(size_t)a.node_part[node] * net.n_hidden + noff + j] != 0;
+      }
+      const bool isdead = ub <= 0.f;
+      const bool isact = lb >= 0.f;
+      if (rv && a.dead_out) a.dead_out[(size_t)rglob * net.n_hidden + noff + j] = isdead ? 1 : 0;
+      const bool zero = isdead || forced;
+      const float ih = zero ? 0.f : fmaxf(ub, 0.f);
+      const float il = zero ? 0.f : fmaxf(lb, 0.f);
+      cu[irow * S] = ih;
+      cl[irow * S] = il;
+      cu[ierow * S] = gnext * ih;
+      cl[ierow * S] = gnext * il;
+      if (!sym) continue;
+      const float* gm = s_m + g * n0;
+      // upper relaxation: identity (stable active) / zero / chord over [aa, bb] of T = U + eU
+      float eUn = 0.f, mgUn = 0.f;
+      if (zero) {
+        for (int i = 0; i <= crow; ++i) cu[i * S] = 0.f;
+      } else if (isact) {
         cu[crow * S] = cU;
         eUn = eU;
         mgUn = mgU;
       } else {
-        s = (ub / (ub - aa)) * (1.f + 4.f * unit);
-        shift = eU - aa;
-        for (int i = 0; i < nc - 1; ++i) {
+        const float aa = mnU - gc * mgU + eU;
+        const float bb = mxU + gc * mgU + eU;
+        const float s = (bb / (bb - aa)) * (1.f + 4.f * unit);
+        const float shift = eU - aa;
+        for (int i = 0; i < n0; ++i) {
           const float v = cu[i * S] * s;
           cu[i * S] = v;
           mgUn += fabsf(v) * gm[i];
@@ -209,15 +243,14 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
       // lower relaxation: lambda in {0,1} applied to L(x) - eL
       const float aL = mnL - gc * mgL - eL;
       const float bL = mxL + gc * mgL - eL;
-      const bool lam1 = !forced && ((aL >= 0.f) || ((bL > 0.f) && (bL > -aL)));
-      float eLn, mgLn = 0.f;
+      const bool lam1 = !zero && (isact || ((bL > 0.f) && (bL > -aL)));
+      float eLn = 0.f, mgLn = 0.f;
       if (lam1) {
         cl[crow * S] = cL;
         eLn = eL;
         mgLn = mgL;
       } else {
-        for (int i = 0; i < nc; ++i) cl[i * S] = 0.f;
-        eLn = 0.f;
+        for (int i = 0; i <= crow; ++i) cl[i * S] = 0.f;
       }
       cu[erow * S] = eUn + gnext * mgUn;
       cl[erow * S] = eLn + gnext * mgLn;
@@ -230,7 +263,7 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
 extern "C" size_t fa_bounds_smem(const NetDesc& net, int symbolic, int G, int* stride, int* wstride,
                                  int* wfloats) {
   const int n0 = net.dims[0];
-  const int rb = (symbolic ? n0 + 1 : 1) + 1;
+  const int rb = symbolic ? n0 + 4 : 2;
   const int S = net.max_width | 1;            // odd stride: conflict-free column reads
   int ws = 1;
   for (int l = 0; l < net.n_layers; ++l) ws = ws > net.dims[l + 1] ? ws : net.dims[l + 1];

@@ -2,14 +2,13 @@
 //
 // fa_pair_eval_kernel : one thread per (node, PA pair, orientation) evaluates the convex
 //                       piecewise-linear certificate g(t) at t in {0, 1} and at every breakpoint
-//                       of the shared-feature coefficients and keeps min_t g(t) and its argmin.
+//                       of the shared-feature coefficients and keeps min_t g(t) and its argmin;
+//                       pairs already excluded by the rows' rigorous sign bounds get g = -1.
 // fa_pair_pick_kernel : one thread per node picks the most violating pair/orientation, and for
-//                       it emits the split dimension (largest |coef| x width contribution) and
-//                       the candidate vertex pair (x, x') that maximises the objective.
+//                       it emits the per-dimension split scores (|coef| x width at t*), the best
+//                       split dimension, the leaf flag and the candidate vertex pair (x, x') that
+//                       maximises the objective (PA values set, relaxed features clipped to tau).
 #include "args.h"
-
-
-
 
 // Folded form of one row: coefficient i (0 on PA dims), constant (incl. err sign and PA terms),
 // |PA contribution| for the rounding margin.
@@ -61,8 +60,9 @@ __device__ float fa_g_at(const CertArgs& a, int n, const Form& A, float sA, cons
   const float* ph = a.xphi + (size_t)n * a.n0;
   float val = 0.f;
   for (int i = 0; i < a.n0; ++i) {
-    const float ai = fa_is_pa(a, i) ? 0.f : sA * A.c[i];
-    const float bi = fa_is_pa(a, i) ? 0.f : sB * B.c[i];
+    if (fa_is_pa(a, i)) continue;
+    const float ai = sA * A.c[i];
+    const float bi = sB * B.c[i];
     if (a.shared[i]) {
       const float cs = t * ai + (1.f - t) * bi;
       val += fmaxf(cs * xl[i], cs * xh[i]);
@@ -98,12 +98,22 @@ __global__ void __launch_bounds__(FA_THREADS) fa_pair_eval_kernel(CertArgs a) {
   const int n = (int)(idx / Q);
   const int qq = (int)(idx % Q);
   const int o = qq / a.Pp, q = qq % a.Pp;
+  // exact-sign shortcut from the rigorous per-row bounds
+  {
+    const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+    const size_t ri = (size_t)n * a.V + vi, rj = (size_t)n * a.V + vj;
+    const bool imp = (o == 0) ? (a.olb[ri] >= 0.f || a.oubp[rj] <= 0.f) : (a.oub[ri] <= 0.f || a.olbp[rj] >= 0.f);
+    if (imp) {
+      a.gmin[idx] = -1.f;
+      a.tstar[idx] = 0.f;
+      return;
+    }
+  }
   Form A, B;
   float sA, sB;
   fa_pair_forms(a, n, q, o, A, sA, B, sB);
   float magA, magB;
   fa_mags(a, n, A, B, magA, magB);
-  // candidate t: 0, 1, breakpoints of shared dims (invalid -> 0 like the reference clamp)
   float best = fa_g_at(a, n, A, sA, B, sB, 0.f, magA, magB);
   float bt = 0.f;
   {
@@ -115,7 +125,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_pair_eval_kernel(CertArgs a) {
     const float ai = sA * A.c[i], bi = sB * B.c[i];
     const float den = ai - bi;
     if (den == 0.f) continue;
-    float t = -bi / den;
+    const float t = -bi / den;
     if (!(t > 0.f && t < 1.f)) continue;
     const float g = fa_g_at(a, n, A, sA, B, sB, t, magA, magB);
     if (g < best) { best = g; bt = t; }
@@ -139,19 +149,24 @@ __global__ void __launch_bounds__(FA_THREADS) fa_pair_pick_kernel(CertArgs a) {
   Form A, B;
   float sA, sB;
   fa_pair_forms(a, n, q, o, A, sA, B, sB);
-  const float* xl = a.xlo + (size_t)n * a.n0;
-  const float* xh = a.xhi + (size_t)n * a.n0;
-  const float* pl = a.xplo + (size_t)n * a.n0;
-  const float* ph = a.xphi + (size_t)n * a.n0;
+  const int n0 = a.n0;
+  const float* xl = a.xlo + (size_t)n * n0;
+  const float* xh = a.xhi + (size_t)n * n0;
+  const float* pl = a.xplo + (size_t)n * n0;
+  const float* ph = a.xphi + (size_t)n * n0;
+  float* cxo = a.cand_x + (size_t)n * n0;
+  float* cpo = a.cand_xp + (size_t)n * n0;
+  float* sco = a.scores ? a.scores + (size_t)n * 2 * n0 : nullptr;
   float bs = -1.f;
   int bd = 0;
-  for (int i = 0; i < a.n0; ++i) {
-    const float ai = fa_is_pa(a, i) ? 0.f : sA * A.c[i];
-    const float bi = fa_is_pa(a, i) ? 0.f : sB * B.c[i];
+  bool leaf = true;
+  for (int i = 0; i < n0; ++i) {
+    const bool pa = fa_is_pa(a, i);
+    const float ai = pa ? 0.f : sA * A.c[i];
+    const float bi = pa ? 0.f : sB * B.c[i];
     const float wx = xh[i] - xl[i];
     const float cs = t * ai + (1.f - t) * bi;
-    float sx;
-    float cx;
+    float sx, cx;
     if (a.shared[i]) {
       sx = fabsf(cs) * wx;
       cx = cs > 0.f ? xh[i] : xl[i];
@@ -160,31 +175,50 @@ __global__ void __launch_bounds__(FA_THREADS) fa_pair_pick_kernel(CertArgs a) {
       cx = (t * ai > 0.f) ? xh[i] : xl[i];
     }
     sx += 1e-9f * wx;
+    if (pa || wx <= 0.f) sx = -1.f;
+    if (!pa && wx > 0.f) leaf = false;
     if (sx > bs) { bs = sx; bd = i; }
-    a.cand_x[(size_t)n * a.n0 + i] = cx;
+    if (sco) sco[i] = sx;
     float cxp = cx;
     if (!a.shared[i]) cxp = ((1.f - t) * bi > 0.f) ? ph[i] : pl[i];
-    a.cand_xp[(size_t)n * a.n0 + i] = cxp;
+    cxo[i] = cx;
+    cpo[i] = cxp;
   }
-  for (int i = 0; i < a.n0; ++i) {
-    float sxp = 0.f;
-    if (!a.shared[i]) {
-      const float bi = fa_is_pa(a, i) ? 0.f : sB * B.c[i];
+  for (int i = 0; i < n0; ++i) {
+    float sxp = -1.f;
+    if (!a.shared[i] && !fa_is_pa(a, i)) {
+      const float bi = sB * B.c[i];
       const float wxp = ph[i] - pl[i];
-      sxp = fabsf((1.f - t) * bi) * wxp + 1e-9f * wxp;
+      if (wxp > 0.f) {
+        sxp = fabsf((1.f - t) * bi) * wxp + 1e-9f * wxp;
+        leaf = false;
+      }
     }
-    if (sxp > bs) { bs = sxp; bd = a.n0 + i; }
+    if (sco) sco[n0 + i] = sxp;
+    if (sxp > bs) { bs = sxp; bd = n0 + i; }
+  }
+  // candidate pair: PA values of the chosen pair, relaxed features within tau of x (and in x' box)
+  const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+  for (int k = 0; k < a.npa; ++k) {
+    cxo[a.pa_idx[k]] = (float)a.values[vi * a.npa + k];
+    cpo[a.pa_idx[k]] = (float)a.values[vj * a.npa + k];
+  }
+  for (int k = 0; k < a.nra; ++k) {
+    const int r = a.ra_idx[k];
+    float v = fminf(fmaxf(cpo[r], cxo[r] - a.tau), cxo[r] + a.tau);
+    cpo[r] = fminf(fmaxf(v, pl[r]), ph[r]);
   }
   a.open[n] = bg > 0.f ? 1 : 0;
   a.score[n] = bg;
   a.split_dim[n] = bd;
   a.cand_v[n] = q;
   a.cand_o[n] = o;
+  if (a.leaf) a.leaf[n] = leaf ? 1 : 0;
 }
 
 extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream) {
   if (a.Nn <= 0) return 0;
-  if (a.npa > FA_CMAX_PA) return -3;
+  if (a.npa > FA_CMAX_PA || a.nra > FA_MAX_RA) return -3;
   const int64_t tot = (int64_t)a.Nn * a.Pp * a.norient;
   hipLaunchKernelGGL(fa_pair_eval_kernel, dim3((unsigned)((tot + FA_THREADS - 1) / FA_THREADS)), dim3(FA_THREADS), 0,
                      stream, a);

@@ -24,6 +24,7 @@ struct NetDesc {
   float unit;                         // unit roundoff of the arithmetic (2^-24)
   float g_gemm[FA_MAX_LAYERS];        // gamma for the layer-l GEMM (K = 2*dims[l] + 1)
   float g_conc;                       // gamma for concretisation sums (K = rows per form)
+  float g_one;                        // gamma_1 (interval-row final addition)
   float g_fwd[FA_MAX_LAYERS];         // gamma for the plain forward (K = dims[l] + 1)
 };
 

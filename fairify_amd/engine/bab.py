@@ -18,6 +18,7 @@ the (tiny) SAT-candidate list.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -42,6 +43,7 @@ class BaBConfig:
     max_pool: int = 1 << 22          # live-node capacity (drop to UNKNOWN beyond)
     time_budget: float = 1e9         # wall-clock seconds for the whole call
     mode: str = "symbolic"
+    cand_cap: int = 1 << 17          # candidate pairs confirmed per BFS level (native runtime)
 
 
 @dataclass
@@ -129,6 +131,8 @@ class BaBSolver:
         if pairs.shape[0] == 0:
             status[status == RUNNING] = UNSAT   # a single PA value: no x' can differ
             return BaBResult(status, cex_x, cex_xp, nodes_np, 0, time.time() - t0)
+        if self.be.hip and os.environ.get("FAIRIFY_TORCH_BAB") != "1":
+            return self._solve_native(lo_np, hi_np, status, values_np, pairs_np, mlp_exact, exact_models, t0)
 
         dt = torch.float32
         run_idx = np.nonzero(status == RUNNING)[0]
@@ -190,7 +194,9 @@ class BaBSolver:
                 cxp[:, r] = torch.minimum(torch.maximum(cxp[:, r], cx[:, r] - self.tau), cx[:, r] + self.tau)
                 cxp[:, r] = torch.minimum(torch.maximum(cxp[:, r], bplo[:, r]), bphi[:, r])
             # ---- leaves: single lattice points (x and x'); evaluate every pair exactly
-            width = (bhi - blo).amax(dim=1)
+            wmask = torch.ones(blo.shape[1], dtype=torch.bool, device=blo.device)
+            wmask[self.pa] = False
+            width = (bhi - blo)[:, wmask].amax(dim=1)
             if self.relaxed:
                 width = torch.maximum(width, (bphi - bplo)[:, self.ra].amax(dim=1) if self.ra.numel() else width)
             leaf = open_ & (width == 0)
@@ -274,6 +280,63 @@ class BaBSolver:
         st[status == SAT] = SAT
         nodes_np = nodes_t.cpu().numpy()
         return BaBResult(st.astype(np.int8), cex_x, cex_xp, nodes_np, it, time.time() - t0)
+
+    # --------------------------------------------------------------------------------------
+    def _runtime(self, values_np: np.ndarray, pairs_np: np.ndarray, n_run: int):
+        """Native (C++/HIP) BaB runtime, cached on the backend per query signature."""
+        from ..ops import ext
+        from ..ops.hip import _net
+
+        key = (tuple(self.q.pa_idx), tuple(self.q.ra_idx), self.q.tau, values_np.tobytes(), pairs_np.tobytes())
+        cache = self.be.__dict__.setdefault("_bab_rt", {})
+        cap = max(self.cfg.max_pool, n_run)
+        rt = cache.get(key)
+        if rt is None or rt[1] < cap:
+            shared = np.ones(self.q.n, dtype=np.uint8)
+            shared[list(self.q.ra_idx)] = 0
+            rt = (ext().BabRuntime(_net(self.be), self.be.flat.data_ptr(), list(self.q.pa_idx),
+                                   values_np.astype(np.float32).reshape(-1).tolist(),
+                                   values_np.astype(np.int64).reshape(-1).tolist(),
+                                   pairs_np.astype(np.int64).reshape(-1).tolist(),
+                                   list(self.q.ra_idx) if self.relaxed else [], float(self.q.tau),
+                                   shared.tolist(), int(cap), int(self.cfg.batch_nodes), int(self.cfg.cand_cap),
+                                   float(self.be.unit)), cap)
+            cache[key] = rt
+        return rt[0]
+
+    def _solve_native(self, lo_np, hi_np, status, values_np, pairs_np, mlp_exact, exact_models, t0) -> BaBResult:
+        n_run = int((status == RUNNING).sum())
+        rt = self._runtime(values_np, pairs_np, n_run)
+        q = self.q
+
+        def confirm(parts: np.ndarray, buf: np.ndarray) -> np.ndarray:
+            with self.tm("bab.confirm"):
+                n = q.n
+                X = np.rint(buf[:, :n]).astype(np.int64)
+                XP = np.rint(buf[:, n:]).astype(np.int64)
+                ok = exact.check_pair_constraints(X, XP, lo_np[parts], hi_np[parts], q.pa_idx, q.ra_idx, q.tau)
+                out = np.zeros(len(parts), dtype=bool)
+                if exact_models is None:
+                    idx = np.nonzero(ok)[0]
+                    if idx.size:
+                        out[idx] = exact.is_violation(mlp_exact, X[idx], XP[idx])
+                else:
+                    for k in np.nonzero(ok)[0]:
+                        out[k] = exact.is_violation(exact_models[int(parts[k])], X[k:k + 1], XP[k:k + 1])[0]
+                return out
+
+        dead_ptr = 0
+        if self.dead is not None:
+            self._dead_u8 = self.dead.to(torch.uint8).contiguous()
+            dead_ptr = self._dead_u8.data_ptr()
+        stream = torch.cuda.current_stream(self.dev).cuda_stream
+        with self.tm("bab.native"):
+            st, cx, cxp, nodes, stats = rt.solve(lo_np.astype(np.float32), hi_np.astype(np.float32), status,
+                                                  int(self.cfg.node_budget), float(self.cfg.time_budget), dead_ptr,
+                                                  confirm, stream)
+        self.stats = dict(stats)
+        return BaBResult(np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes),
+                         int(stats["levels"]), time.time() - t0)
 
     # --------------------------------------------------------------------------------------
     def _confirm(self, rows, cx, cxp, bpart, status, status_t, cex_x, cex_xp, mlp_exact, exact_models,

@@ -91,6 +91,23 @@ class ModelRun:
         return c
 
 
+class _LazyMasked:
+    """Per-partition heuristically pruned networks, materialised only when a SAT candidate of
+    that partition needs exact confirmation."""
+
+    def __init__(self, mlp: MLP, masks: List[np.ndarray], widths):
+        self.mlp, self.masks, self.sls = mlp, masks, P_.layer_slices(widths)
+        self.cache: Dict[int, MLP] = {}
+
+    def __getitem__(self, k: int) -> MLP:
+        if k not in self.cache:
+            self.cache[k] = self.mlp.masked([self.masks[k][s] for s in self.sls])
+        return self.cache[k]
+
+    def __len__(self) -> int:
+        return len(self.masks)
+
+
 def _amortize(total: float, work: np.ndarray) -> np.ndarray:
     w = work.astype(np.float64) + 1.0
     return total * w / w.sum()
@@ -193,23 +210,20 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
         t0 = time.time()
         h_attempt[unk] = 1
         with tm("heuristic.masks"):
-            lb_np = ibp_lb.cpu().numpy()
-            ub_np = ibp_ub.cpu().numpy()
-            cand_np = cand.cpu().numpy()
-            scand_np = s_cand.cpu().numpy()
-            st_np = st_dead.cpu().numpy()
-            masks = np.zeros((unk.size, Nh), dtype=bool)
+            ut = torch.from_numpy(unk).to(dev)
+            hd_t, md_t = P_.heuristic_prune_batch(ibp_lb[ut], ibp_ub[ut], cand[ut], s_cand[ut], st_dead[ut],
+                                                  widths, cfg.heuristic_p)
+            hd_np = hd_t.cpu().numpy()
+            md_np = md_t.cpu().numpy()
+            h_dead_np[unk] = hd_np
+            t_dead_np[unk] = md_np
+            masks = md_np[:, :Nh]
             for k, p in enumerate(unk):
-                hd, md = P_.heuristic_prune_one(lb_np[p], ub_np[p], cand_np[p], scand_np[p], st_np[p], widths,
-                                                cfg.heuristic_p)
-                h_dead_np[p] = hd
-                t_dead_np[p] = md
-                masks[k] = md[:Nh]
-                masked[p] = md
+                masked[p] = md_np[k]
         # partitions whose heuristic mask equals the sound mask would re-run the same query
         sub_lo, sub_hi = lo_np[unk], hi_np[unk]
         dead_t = torch.from_numpy(masks).to(dev)
-        exact_models = [mlp.masked([masked[p][s] for s in P_.layer_slices(widths)]) for p in unk]
+        exact_models = _LazyMasked(mlp, [masked[p] for p in unk], widths)
         hsolver = BaBSolver(be, q, BaBConfig(node_budget=cfg.heuristic_node_budget, batch_nodes=cfg.batch_nodes,
                                              time_budget=budget), dead=dead_t, timer=tm)
         with tm("heuristic.bab"):

@@ -70,6 +70,62 @@ def compression(dead: torch.Tensor) -> torch.Tensor:
     return dead.to(torch.float32).mean(dim=1)
 
 
+def _masked_percentile(vals: torch.Tensor, mask: torch.Tensor, q: float):
+    """Row-wise NumPy-'linear' percentile of ``vals`` over entries where ``mask`` (>=1 entry)."""
+    inf = torch.full_like(vals, float("inf"))
+    srt = torch.sort(torch.where(mask, vals, inf), dim=1).values
+    k = mask.sum(dim=1).clamp(min=1)
+    pos = (k - 1).to(vals.dtype) * (q / 100.0)
+    lo = pos.floor().long()
+    hi = torch.minimum(lo + 1, k - 1)
+    frac = pos - lo.to(vals.dtype)
+    a = srt.gather(1, lo[:, None])[:, 0]
+    b = srt.gather(1, hi[:, None])[:, 0]
+    return a + (b - a) * frac
+
+
+def heuristic_prune_batch(ws_lb: torch.Tensor, ws_ub: torch.Tensor, cand: torch.Tensor, s_cand: torch.Tensor,
+                          deads: torch.Tensor, widths: Sequence[int], perc: float):
+    """Vectorised :func:`heuristic_prune_one` over a batch of partitions (rows).
+
+    Same decisions as the reference ``heuristic_prune`` (utils/prune.py:862-939): per hidden
+    layer compare the candidates' and non-candidates' ``ws_ub`` distributions (mean, median,
+    NumPy-linear percentiles) and mark harsh outliers dead.  Returns (new, merged) [P, N] bool.
+    """
+    dt = torch.float64
+    lb = ws_lb.to(dt)
+    ub = ws_ub.to(dt)
+    new = torch.zeros_like(cand, dtype=torch.bool)
+    sls = layer_slices(widths)
+    for sl in sls[:-1]:
+        c = cand[:, sl].bool()
+        u = ub[:, sl]
+        l = lb[:, sl]
+        nc = ~c
+        kc = c.sum(1)
+        kn = nc.sum(1)
+        zero = torch.zeros_like(u)
+        mean_c = torch.where(c, u, zero).sum(1) / kc.clamp(min=1)
+        mean_n = torch.where(nc, u, zero).sum(1) / kn.clamp(min=1)
+        med_c = _masked_percentile(u, c, 50.0)
+        med_n = _masked_percentile(u, nc, 50.0)
+        p5 = _masked_percentile(u, nc, perc)
+        p95 = _masked_percentile(u, nc, 100.0 - perc)
+        differ = (mean_n > 2 * mean_c) & (med_n > 2 * med_c) & (kn > 0) & (kc > 0)
+        hit = s_cand[:, sl].bool() & (u < p5[:, None]) & (u < 0.1 * p95[:, None]) & (u < l.abs())
+        layer_new = torch.where(differ[:, None], hit, torch.zeros_like(hit))
+        layer_new = layer_new | (kn == 0)[:, None]
+        new[:, sl] = layer_new
+    for sl in sls:
+        alld = new[:, sl].all(1)
+        new[alld, sl.start] = False
+    merged = deads.bool() | new
+    for sl in sls:
+        alld = merged[:, sl].all(1)
+        merged[alld, sl.start] = False
+    return new, merged
+
+
 def heuristic_prune_one(ws_lb: np.ndarray, ws_ub: np.ndarray, cand: np.ndarray, s_cand: np.ndarray,
                         deads: np.ndarray, widths: Sequence[int], perc: float) -> Tuple[np.ndarray, np.ndarray]:
     """Reference ``heuristic_prune`` for ONE partition; arrays over all N neurons.

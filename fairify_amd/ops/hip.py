@@ -138,17 +138,19 @@ def pair_certify(be, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, sha
     cxp = torch.empty(Nn, n0, **f32)
     cv = torch.empty(Nn, dtype=torch.int64, device=dev)
     co = torch.empty(Nn, dtype=torch.int64, device=dev)
-    fx = [res_x.Lc, res_x.L0, res_x.Le, res_x.Uc, res_x.U0, res_x.Ue]
-    fxp = [res_xp.Lc, res_xp.L0, res_xp.Le, res_xp.Uc, res_xp.U0, res_xp.Ue]
+    fx = [res_x.Lc, res_x.L0, res_x.Le, res_x.Uc, res_x.U0, res_x.Ue, res_x.out_lb, res_x.out_ub]
+    fxp = [res_xp.Lc, res_xp.L0, res_xp.Le, res_xp.Uc, res_xp.U0, res_xp.Ue, res_xp.out_lb, res_xp.out_ub]
     fx = [_c(t, torch.float32) for t in fx]
     fxp = [_c(t, torch.float32) for t in fxp]
+    scores = torch.empty(Nn, 2 * n0, **f32)
+    leaf = torch.empty(Nn, dtype=torch.uint8, device=dev)
     if Nn:
         ext().certify(Nn, n0, V, Pp, norient, [t.data_ptr() for t in fx], [t.data_ptr() for t in fxp],
                       xlo.data_ptr(), xhi.data_ptr(), xplo.data_ptr(), xphi.data_ptr(), pairs_c.data_ptr(),
-                      values_c.data_ptr(), [int(i) for i in pa.tolist()], sh.data_ptr(), be.unit,
+                      values_c.data_ptr(), [int(i) for i in pa.tolist()], [], 0.0, sh.data_ptr(), be.unit,
                       ref.gamma(2 * n0 + 4, be.unit), gmin.data_ptr(), tstar.data_ptr(), open_.data_ptr(),
                       score.data_ptr(), split.data_ptr(), cx.data_ptr(), cxp.data_ptr(), cv.data_ptr(),
-                      co.data_ptr(), _stream(dev))
+                      co.data_ptr(), scores.data_ptr(), leaf.data_ptr(), _stream(dev))
     return ref.PairDecision(open_=open_.bool(), score=score, split_dim=split, cand_x=cx, cand_xp=cxp,
                             cand_v=cv, cand_orient=co)
 

@@ -438,6 +438,8 @@ def pair_certify(res_x: BoundResult, res_xp: BoundResult, xlo: torch.Tensor, xhi
     # tie-break toward the widest dim so that zero-coefficient dims still get split eventually
     sx = sx + 1e-9 * wx
     sxp = sxp + 1e-9 * wxp
+    sx[:, pa] = -1.0                      # PA coordinates are enumerated, never split
+    sxp[:, pa] = -1.0
     split_dim = torch.cat([sx, sxp], dim=1).argmax(dim=1)
     # candidate vertex maximising the objective at t*
     cx_s = torch.where(cs > 0, xhi, xlo)
