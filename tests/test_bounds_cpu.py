@@ -1,0 +1,80 @@
+"""Reference bound propagation: soundness vs brute force, exact zeros, fp64 tightness."""
+import itertools
+
+import numpy as np
+import pytest
+import torch
+
+from fairify_amd.models.mlp import random_mlp
+from fairify_amd.ops import reference as ref
+from fairify_amd.ops.backend import Backend
+
+
+def _brute(m, lo, hi):
+    pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo, hi)])))
+    return m.layer_outputs(pts)
+
+
+@pytest.mark.parametrize("mode", ["ibp", "symbolic"])
+@pytest.mark.parametrize("seed", range(6))
+def test_bounds_sound(mode, seed):
+    m = random_mlp(5, [8, 6, 4], seed=seed, bias_scale=0.5 if seed % 2 else 0.0)
+    be = Backend(m)
+    g = np.random.default_rng(seed)
+    lo = g.integers(-3, 5, (6, 5))
+    hi = lo + g.integers(0, 4, (6, 5))
+    r = be.bounds(torch.tensor(lo).float(), torch.tensor(hi).float(), mode=mode, keep_layers=True)
+    for k in range(6):
+        outs = _brute(m, lo[k], hi[k])
+        for l, o in enumerate(outs):
+            pre = o if l == len(outs) - 1 else None
+            if pre is not None:
+                assert float(r.out_lb[k]) <= o[:, 0].min() and float(r.out_ub[k]) >= o[:, 0].max()
+        # hidden post-activations are within relu(bounds)
+        for l, o in enumerate(outs[:-1]):
+            assert np.all(o <= np.maximum(r.layer_ub[l][k].numpy(), 0) + 1e-6)
+
+
+def test_symbolic_tighter_than_ibp_on_average():
+    m = random_mlp(13, [50, 50], seed=4, bias_scale=0.2)
+    be = Backend(m)
+    g = np.random.default_rng(1)
+    lo = g.integers(0, 20, (64, 13))
+    hi = lo + 3
+    a = be.bounds(torch.tensor(lo).float(), torch.tensor(hi).float(), mode="ibp")
+    b = be.bounds(torch.tensor(lo).float(), torch.tensor(hi).float(), mode="symbolic")
+    assert float((b.out_ub - b.out_lb).mean()) < float((a.out_ub - a.out_lb).mean())
+    assert torch.all(b.out_ub - b.out_lb <= a.out_ub - a.out_lb + 1e-4)
+
+
+def test_exact_zero_kept_exact():
+    # zero biases + non-positive output weights: N <= 0 exactly everywhere
+    m = random_mlp(4, [6, 5], seed=2)
+    m.weights[-1] = -np.abs(m.weights[-1])
+    be = Backend(m)
+    lo = torch.zeros(3, 4)
+    hi = torch.full((3, 4), 7.0)
+    r = be.bounds(lo, hi, mode="symbolic")
+    assert torch.all(r.out_ub <= 0)
+
+
+def test_fp64_matches_fp32_within_margin():
+    m = random_mlp(6, [16, 8], seed=9, bias_scale=0.3)
+    g = np.random.default_rng(2)
+    lo = torch.tensor(g.integers(0, 50, (32, 6))).float()
+    hi = lo + 5
+    r32 = Backend(m).bounds(lo, hi)
+    r64 = Backend(m, dtype=torch.float64).bounds(lo.double(), hi.double())
+    assert torch.all(r32.out_lb <= r64.out_lb.float() + 1e-3)
+    assert torch.all(r32.out_ub >= r64.out_ub.float() - 1e-3)
+
+
+def test_rng_stream_is_stable():
+    lo = torch.zeros(2, 3)
+    hi = torch.tensor([[5.0, 9.0, 1.0], [100.0, 3.0, 7.0]])
+    a = ref.sample_points(lo, hi, torch.tensor([3, 4]), 50, seed=11)
+    b = ref.sample_points(lo, hi, torch.tensor([3, 4]), 50, seed=11)
+    assert torch.equal(a, b)
+    assert torch.all(a >= lo[:, None]) and torch.all(a <= hi[:, None])
+    c = ref.sample_points_at(lo, hi, torch.tensor([3, 4]), torch.tensor([[7, 8], [0, 49]]), seed=11)
+    assert torch.equal(c[0], a[0, 7:9]) and torch.equal(c[1, 1], a[1, 49])
