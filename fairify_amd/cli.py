@@ -1,0 +1,168 @@
+"""Command line interface (replaces ``src/fairify.sh`` + the per-family copied driver scripts).
+
+    python -m fairify_amd.cli presets
+    python -m fairify_amd.cli verify --preset src/GC-age --models GC-1,GC-3 --out results/gc
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m fairify_amd.cli verify --preset stress/AC ...
+    python -m fairify_amd.cli zoo [--import-dir /path/to/models]
+    python -m fairify_amd.cli analyze --preset experiment/AC-3 --model AC-3 --fairer AC-3 ...
+    python -m fairify_amd.cli repair --model AC-3 --counterexamples results/ac3/counterexamples.csv ...
+    python -m fairify_amd.cli export-cex --preset src/AC-sex --model AC-3 --results results/ac
+
+The reference's only flag is ``sys.argv[1]`` = soft timeout (src/AC/Verify-AC.py:147-148);
+every other constant is a preset field here and can be overridden on the command line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from dataclasses import replace
+
+
+def _device(arg):
+    import torch
+
+    if arg:
+        return arg
+    return "cuda" if torch.cuda.is_available() else "cpu"
+
+
+def cmd_presets(args):
+    from . import presets
+
+    for name, p in sorted(presets.PRESETS.items()):
+        g = p.grid()
+        print(f"{name:20s} suite={p.suite:9s} PA={','.join(p.query.pa):22s} RA={','.join(p.query.ra) or '-':9s} "
+              f"tau={p.query.tau:<2d} P={p.partition_size:<4d} partitions={len(g):<9d} soft={p.soft_timeout:g}s "
+              f"hard={p.hard_timeout:g}s models={len(p.models)}  [{p.source}]")
+
+
+def cmd_verify(args):
+    from . import presets
+    from .engine.pipeline import VerifyConfig
+    from .engine.runner import run_preset
+    from .parallel import dist as D
+
+    pre = presets.get(args.preset)
+    if args.partition_size:
+        pre = replace(pre, partition_size=args.partition_size)
+    info = D.init(_device(args.device))
+    cfg = VerifyConfig(sim_size=args.sim_size or pre.sim_size, seed=args.seed, chunk=args.chunk,
+                       soft_timeout=args.soft_timeout if args.soft_timeout is not None else pre.soft_timeout,
+                       hard_timeout=args.hard_timeout if args.hard_timeout is not None else pre.hard_timeout,
+                       node_budget=args.node_budget, heuristic=not args.no_heuristic,
+                       heuristic_p=args.heuristic_p if args.heuristic_p is not None else pre.heuristic_p,
+                       heuristic_node_budget=args.node_budget)
+    models = args.models.split(",") if args.models else None
+    run_preset(pre, models=models, weights=args.weights, out_dir=args.out, cfg=cfg, info=info,
+               max_partitions=args.max_partitions, resume=args.resume, seed=args.seed,
+               accuracy=not args.no_accuracy)
+    D.destroy(info)
+
+
+def cmd_zoo(args):
+    from .models.zoo import ZOO, get_model, has_weights
+
+    if args.import_dir:
+        import subprocess
+
+        tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "import_zoo.py")
+        subprocess.run([sys.executable, tool, args.import_dir], check=True)
+    for name, (suite, n_in, hidden) in sorted(ZOO.items()):
+        print(f"{name:10s} suite={suite:9s} {n_in}->{'-'.join(map(str, hidden))}->1 "
+              f"weights={'shipped' if has_weights(name) else 'random-only'}")
+
+
+def cmd_analyze(args):
+    from .analysis.report import analyze_model
+
+    out = analyze_model(args.preset, args.model, fairer=args.fairer, results=args.results, weights=args.weights,
+                        seed=args.seed, out_dir=args.out, device=_device(args.device),
+                        causal_samples=args.causal_max)
+    print(json.dumps(out, indent=2, default=float))
+
+
+def cmd_repair(args):
+    from .repair.retrain import repair_model
+
+    out = repair_model(args.model, counterexamples=args.counterexamples, method=args.method, out=args.out,
+                       top_k=args.top_k, epochs=args.epochs, weights=args.weights, seed=args.seed,
+                       device=_device(args.device))
+    print(json.dumps(out, indent=2, default=float))
+
+
+def cmd_export(args):
+    from .report.counterexamples import export_counterexamples
+
+    path = export_counterexamples(args.preset, args.model, args.results, out=args.out, weights=args.weights)
+    print(path)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="fairify_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    sub.add_parser("presets").set_defaults(fn=cmd_presets)
+
+    v = sub.add_parser("verify", help="verify a preset's models (torchrun for multi-GPU)")
+    v.add_argument("--preset", required=True)
+    v.add_argument("--models", default=None)
+    v.add_argument("--weights", default="zoo", help="zoo | random | path/to/model.h5")
+    v.add_argument("--out", default="results")
+    v.add_argument("--partition-size", type=int, default=None)
+    v.add_argument("--soft-timeout", type=float, default=None)
+    v.add_argument("--hard-timeout", type=float, default=None)
+    v.add_argument("--heuristic-p", type=float, default=None)
+    v.add_argument("--no-heuristic", action="store_true")
+    v.add_argument("--node-budget", type=int, default=4096)
+    v.add_argument("--sim-size", type=int, default=None)
+    v.add_argument("--chunk", type=int, default=4096)
+    v.add_argument("--seed", type=int, default=0)
+    v.add_argument("--max-partitions", type=int, default=None)
+    v.add_argument("--resume", action="store_true")
+    v.add_argument("--no-accuracy", action="store_true")
+    v.add_argument("--device", default=None)
+    v.set_defaults(fn=cmd_verify)
+
+    z = sub.add_parser("zoo", help="list the model zoo / import Keras .h5 models")
+    z.add_argument("--import-dir", default=None)
+    z.set_defaults(fn=cmd_zoo)
+
+    a = sub.add_parser("analyze", help="group metrics, causal discrimination, hybrid routing")
+    a.add_argument("--preset", required=True)
+    a.add_argument("--model", required=True)
+    a.add_argument("--fairer", default=None)
+    a.add_argument("--results", default=None, help="results dir of a verify run (partition verdicts)")
+    a.add_argument("--weights", default="zoo")
+    a.add_argument("--seed", type=int, default=0)
+    a.add_argument("--out", default=None)
+    a.add_argument("--causal-max", type=int, default=1000)
+    a.add_argument("--device", default=None)
+    a.set_defaults(fn=cmd_analyze)
+
+    r = sub.add_parser("repair", help="bias localisation + masked fine-tune / counterexample retraining")
+    r.add_argument("--model", required=True)
+    r.add_argument("--counterexamples", required=True)
+    r.add_argument("--method", default="masked", choices=["masked", "retrain"])
+    r.add_argument("--out", required=True)
+    r.add_argument("--top-k", type=int, default=10)
+    r.add_argument("--epochs", type=int, default=5)
+    r.add_argument("--weights", default="zoo")
+    r.add_argument("--seed", type=int, default=0)
+    r.add_argument("--device", default=None)
+    r.set_defaults(fn=cmd_repair)
+
+    e = sub.add_parser("export-cex", help="decode counterexamples of a verify run to category labels")
+    e.add_argument("--preset", required=True)
+    e.add_argument("--model", required=True)
+    e.add_argument("--results", required=True)
+    e.add_argument("--out", default=None)
+    e.add_argument("--weights", default="zoo")
+    e.set_defaults(fn=cmd_export)
+
+    args = ap.parse_args(argv)
+    args.fn(args)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+"""Preset runner: data-parallel verification of a model list with checkpoint/resume.
+
+Reference flow: ``for model_file in os.listdir(model_dir): for p in p_list: ...`` with one CSV
+append per partition and a per-model hard timeout (src/AC/Verify-AC.py:78-320).  Here:
+
+* the seeded processing order is split into *rounds*; in every round each rank verifies its
+  strided share (``chunk`` partitions) on its own GPU;
+* per-partition records are packed into fixed-width rows and ``all_gather``-ed (RCCL) to rank 0,
+  which appends them to the reference-format CSV in processing order and checkpoints the set
+  of finished positions (``state/<model>.npz``) so ``--resume`` skips them;
+* the hard timeout is a global decision (``all_reduce(MAX)`` of elapsed time), so all ranks
+  stop at the same round;
+* rank 0 prints/writes the Table-V row of every model (``summary.json``).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from dataclasses import asdict, replace
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..models.zoo import get_model
+from ..ops.backend import Backend
+from ..parallel import dist as D
+from ..partition import processing_order
+from ..presets import Preset
+from ..report.csv_report import PartitionCSV, format_table, table_v_row, write_summary
+from ..utils.timer import StageTimer
+from .pipeline import PartitionRecord, VerifyConfig, verify_chunk
+
+VCODE = {"sat": 1, "unsat": 2, "unknown": 0}
+VNAME = {v: k for k, v in VCODE.items()}
+STAGES = ["", "sim", "bab", "heuristic"]
+_SCALARS = ["h_attempt", "h_success", "b_comp", "s_comp", "st_comp", "h_comp", "t_comp", "sv_time", "s_time",
+            "hv_time", "h_time", "total_time", "c_check", "v_accurate", "pruned_acc", "nodes"]
+
+
+def pack(records: List[dict], positions: np.ndarray, n0: int) -> np.ndarray:
+    """Fixed-width float64 rows: [pos, grid_id, verdict, stage, scalars..., has_cex, c1[n0], c2[n0]]."""
+    w = 4 + len(_SCALARS) + 1 + 2 * n0
+    out = np.zeros((len(records), w), dtype=np.float64)
+    for i, (r, pos) in enumerate(zip(records, positions)):
+        out[i, 0] = pos
+        out[i, 1] = r["grid_id"]
+        out[i, 2] = VCODE[r["verdict"]]
+        out[i, 3] = STAGES.index(r.get("stage", "")) if r.get("stage", "") in STAGES else 0
+        for k, name in enumerate(_SCALARS):
+            out[i, 4 + k] = float(r[name])
+        if r["c1"] is not None:
+            out[i, 4 + len(_SCALARS)] = 1
+            out[i, 5 + len(_SCALARS):5 + len(_SCALARS) + n0] = r["c1"]
+            out[i, 5 + len(_SCALARS) + n0:] = r["c2"]
+    return out
+
+
+def unpack(rows: np.ndarray, n0: int, orig_acc: Optional[float]) -> List[PartitionRecord]:
+    recs = []
+    for row in rows:
+        kw = {name: row[4 + k] for k, name in enumerate(_SCALARS)}
+        for name in ("h_attempt", "h_success", "c_check", "v_accurate", "nodes"):
+            kw[name] = int(kw[name])
+        has = row[4 + len(_SCALARS)] > 0
+        c1 = row[5 + len(_SCALARS):5 + len(_SCALARS) + n0].astype(np.float32) if has else None
+        c2 = row[5 + len(_SCALARS) + n0:].astype(np.float32) if has else None
+        recs.append(PartitionRecord(partition_id=int(row[0]) + 1, grid_id=int(row[1]), verdict=VNAME[int(row[2])],
+                                    stage=STAGES[int(row[3])], c1=c1, c2=c2, orig_acc=orig_acc, **kw))
+    return recs
+
+
+def model_accuracy(mlp, suite: str, seed: int = 0) -> Optional[float]:
+    """``Original-acc`` column: test accuracy on the suite's dataset (real when available)."""
+    from ..data import tabular
+
+    try:
+        ds = tabular.load(suite, seed=seed)
+    except Exception:
+        return None
+    if ds.X_test.shape[1] != mlp.n_in:
+        return None
+    return float(np.mean(mlp.predict(ds.X_test) == ds.y_test))
+
+
+def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str = "zoo", out_dir: str = "results",
+               cfg: Optional[VerifyConfig] = None, info: Optional[D.DistInfo] = None,
+               max_partitions: Optional[int] = None, resume: bool = False, seed: int = 0,
+               accuracy: bool = True, verbose: bool = True) -> List[Dict]:
+    info = info or D.DistInfo()
+    grid = preset.grid(seed=seed)
+    q = preset.resolved()
+    order = processing_order(grid, seed=seed)
+    total = len(order) if max_partitions is None else min(len(order), int(max_partitions))
+    cfg = cfg or VerifyConfig(sim_size=preset.sim_size, soft_timeout=preset.soft_timeout,
+                              hard_timeout=preset.hard_timeout, heuristic_p=preset.heuristic_p, seed=seed)
+    n0 = q.n
+    rows_out: List[Dict] = []
+    pa_name = ",".join(a for a in preset.query.pa if preset.domain().has(a))
+    for name in (models or list(preset.models)):
+        mlp = get_model(name, weights=weights, seed=seed)
+        be = Backend(mlp, device=info.device)
+        acc = model_accuracy(mlp, preset.suite, seed) if accuracy else None
+        state_path = os.path.join(out_dir, "state", f"{name}.npz")
+        csv_path = os.path.join(out_dir, f"{name}.csv")
+        done = np.zeros(0, dtype=np.int64)
+        if resume and os.path.exists(state_path):
+            done = np.load(state_path)["done"]
+        todo = np.setdiff1d(np.arange(total), done)
+        mine = todo[info.rank::info.world]
+        writer = PartitionCSV(csv_path, resume=resume) if info.is_main else None
+        all_records: List[PartitionRecord] = []
+        timer = StageTimer(info.device)
+        t0 = time.time()
+        rounds = int(np.ceil(len(todo) / max(1, cfg.chunk * info.world))) if len(todo) else 0
+        stopped = False
+        for r in range(rounds):
+            elapsed = D.all_reduce_max(info, time.time() - t0)
+            if elapsed > cfg.hard_timeout:
+                stopped = True
+                break
+            pos = mine[r * cfg.chunk:(r + 1) * cfg.chunk]
+            if len(pos):
+                recs = verify_chunk(be, mlp, q, grid, order[pos], cfg, orig_acc=acc,
+                                    time_budget=cfg.hard_timeout - elapsed, timer=timer)
+                packed = pack(recs, pos, n0)
+            else:
+                packed = np.zeros((0, 4 + len(_SCALARS) + 1 + 2 * n0))
+            gathered = D.all_gather_rows(info, packed)
+            if info.is_main:
+                gathered = gathered[np.argsort(gathered[:, 0], kind="stable")]
+                recs_all = unpack(gathered, n0, acc)
+                writer.write(recs_all)
+                all_records.extend(recs_all)
+                done = np.union1d(done, gathered[:, 0].astype(np.int64))
+                os.makedirs(os.path.dirname(state_path), exist_ok=True)
+                np.savez(state_path, done=done)
+        wall = D.all_reduce_max(info, time.time() - t0)
+        if info.is_main:
+            row = table_v_row(name, pa_name, all_records, len(grid), wall=wall)
+            row["stopped_by_hard_timeout"] = stopped
+            row["original_acc"] = acc
+            rows_out.append(row)
+            if verbose:
+                print(f"[{preset.name}] {name}: {row['SAT']} sat / {row['UNSAT']} unsat / {row['UNK']} unknown "
+                      f"of {row['#P']} (grid {len(grid)}, cov {row['Cov%']}%) in {wall:.2f}s "
+                      f"= {row['partitions_per_s']} partitions/s", flush=True)
+    if info.is_main:
+        write_summary(os.path.join(out_dir, "summary.json"), rows_out,
+                      {"preset": preset.name, "weights": weights, "n_ranks": info.world, "seed": seed,
+                       "config": asdict(cfg)})
+        if verbose and rows_out:
+            print(format_table(rows_out), flush=True)
+    return rows_out
