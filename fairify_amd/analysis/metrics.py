@@ -1,0 +1,88 @@
+"""Group-fairness metrics of a classifier's predictions (C28; AIF360-equivalent, K10).
+
+The fork computes them with AIF360's ``ClassificationMetric`` / ``BinaryLabelDatasetMetric``
+(src/AC/Verify-AC-experiment-new.py:482-542; src/AC/detect_bias.py:51-116).  AIF360 is not
+available here, so the definitions are re-implemented directly (privileged group = PA == 1):
+
+* DI  = P(yhat=1 | unpriv) / P(yhat=1 | priv)                (disparate impact)
+* SPD = P(yhat=1 | unpriv) - P(yhat=1 | priv)                (statistical parity difference)
+* EOD = TPR_unpriv - TPR_priv                                (equal opportunity difference)
+* AOD = ((FPR_u - FPR_p) + (TPR_u - TPR_p)) / 2              (average odds difference)
+* ERD = ERR_u - ERR_p                                        (error rate difference)
+* CNT = 1 - mean_i |yhat_i - mean(yhat over the 5 nearest neighbours of x_i, incl. itself)|
+* TI  = generalized entropy index alpha=1 of b_i = yhat_i - y_i + 1  (Theil index)
+
+The consistency kNN (the only super-linear part) runs as tiled distance GEMMs + top-k on the
+device (torch on ROCm, i.e. hipBLASLt GEMMs; chunked so [chunk, n] distances stay small).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+
+def _rate(mask: np.ndarray, num: np.ndarray) -> float:
+    d = mask.sum()
+    return float(num[mask].sum() / d) if d else float("nan")
+
+
+def group_metrics(y_true: np.ndarray, y_pred: np.ndarray, protected: np.ndarray, privileged_value=1) -> Dict[str, float]:
+    y_true = np.asarray(y_true).astype(int)
+    y_pred = np.asarray(y_pred).astype(int)
+    priv = np.asarray(protected) == privileged_value
+    unp = ~priv
+    pos_u = _rate(unp, y_pred == 1)
+    pos_p = _rate(priv, y_pred == 1)
+    tpr_u = _rate(unp & (y_true == 1), y_pred == 1)
+    tpr_p = _rate(priv & (y_true == 1), y_pred == 1)
+    fpr_u = _rate(unp & (y_true == 0), y_pred == 1)
+    fpr_p = _rate(priv & (y_true == 0), y_pred == 1)
+    err_u = _rate(unp, y_pred != y_true)
+    err_p = _rate(priv, y_pred != y_true)
+    return {
+        "DI": pos_u / pos_p if pos_p else float("nan"),
+        "SPD": pos_u - pos_p,
+        "EOD": tpr_u - tpr_p,
+        "AOD": 0.5 * ((fpr_u - fpr_p) + (tpr_u - tpr_p)),
+        "ERD": err_u - err_p,
+    }
+
+
+def consistency(X: np.ndarray, y_pred: np.ndarray, k: int = 5, device=None, chunk: int = 4096) -> float:
+    """AIF360 ``consistency()`` (kNN over features, neighbours include the point itself)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    Xt = torch.as_tensor(np.asarray(X, dtype=np.float32), device=dev)
+    yp = torch.as_tensor(np.asarray(y_pred, dtype=np.float32), device=dev)
+    n = Xt.shape[0]
+    sq = (Xt * Xt).sum(1)
+    acc = 0.0
+    for s in range(0, n, chunk):
+        q = Xt[s:s + chunk]
+        d = sq[s:s + chunk, None] - 2.0 * (q @ Xt.T) + sq[None, :]
+        # exact self-distance 0 (avoid fp cancellation noise moving the point itself out of the k set)
+        ar = torch.arange(q.shape[0], device=dev)
+        d[ar, s + ar] = -1.0
+        idx = d.topk(k, dim=1, largest=False).indices
+        acc += float((yp[s:s + chunk] - yp[idx].mean(1)).abs().sum())
+    return 1.0 - acc / max(1, n)
+
+
+def theil_index(y_true: np.ndarray, y_pred: np.ndarray) -> float:
+    b = np.asarray(y_pred, dtype=np.float64) - np.asarray(y_true, dtype=np.float64) + 1.0
+    mu = b.mean()
+    r = b / mu
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t = np.where(r > 0, r * np.log(r), 0.0)
+    return float(t.mean())
+
+
+def all_metrics(X: np.ndarray, y_true: np.ndarray, y_pred: np.ndarray, pa_index: int, device=None) -> Dict[str, float]:
+    from sklearn.metrics import accuracy_score, f1_score
+
+    out = {"accuracy": float(accuracy_score(y_true, y_pred)), "f1": float(f1_score(y_true, y_pred, zero_division=0))}
+    out.update(group_metrics(y_true, y_pred, X[:, pa_index]))
+    out["CNT"] = consistency(X, y_pred, device=device)
+    out["TI"] = theil_index(y_true, y_pred)
+    return out

@@ -1,0 +1,187 @@
+"""Bias localisation and repair (C30, C31) in PyTorch-ROCm.
+
+Reference:
+* ``src/AC/detect_bias.py:204-437`` — for counterexample pairs (rows 2i, 2i+1 differing only in
+  the protected attribute) average |activation(x) - activation(x')| over every neuron of every
+  layer (K13), take the top-k "biased" neurons, map them to (layer, neuron), and fine-tune only
+  their incoming weights/bias with masked-gradient Adam (lr 5e-4, 5 epochs, batch 32); then
+  relabel each pair with the max of its labels and fit again; save ``AC-16``.
+* ``src/AC/new_model.py:179-263`` — two-stage retraining: original data, then counterexample
+  batches with an accuracy floor.
+
+Both are re-implemented on ``torch.nn`` (the network is an :class:`~fairify_amd.models.MLP`);
+activations for the localisation come from one batched forward of all pairs.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..models.mlp import MLP
+
+
+def load_pairs(path: str, n_features: int, pa_index: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Counterexample pairs from a CSV of encoded rows (x, x' consecutive; optional label col)
+    or from a ``*.npz`` with arrays ``x``, ``xp`` (and optional ``y``)."""
+    if path.endswith(".npz"):
+        z = np.load(path, allow_pickle=False)
+        X = np.stack([z["x"], z["xp"]], axis=1).reshape(-1, n_features)
+        y = np.repeat(z["y"], 2) if "y" in z.files else None
+        return X.astype(np.float64), y
+    import pandas as pd
+
+    df = pd.read_csv(path)
+    num = df.select_dtypes(include=[np.number])
+    if num.shape[1] >= n_features + 1:
+        X = num.iloc[:, :n_features].to_numpy(dtype=np.float64)
+        y = num.iloc[:, n_features].to_numpy().astype(int)
+    else:
+        X = num.iloc[:, :n_features].to_numpy(dtype=np.float64)
+        y = None
+    return X, y
+
+
+def activation_deltas(mlp: MLP, X: np.ndarray, pa_index: int, device="cpu") -> np.ndarray:
+    """Mean |act(x) - act(x')| per neuron (all layers) over valid consecutive pairs."""
+    net = mlp.to_torch(device)
+    xs = torch.as_tensor(X[0::2], dtype=torch.float32, device=device)
+    xps = torch.as_tensor(X[1::2], dtype=torch.float32, device=device)
+    n = min(len(xs), len(xps))
+    xs, xps = xs[:n], xps[:n]
+    mask = torch.ones(xs.shape[1], dtype=torch.bool, device=device)
+    mask[pa_index] = False
+    valid = torch.isclose(xs[:, mask], xps[:, mask], atol=1e-5).all(dim=1)
+    xs, xps = xs[valid], xps[valid]
+    if len(xs) == 0:
+        return np.zeros(mlp.n_neurons)
+
+    def acts(x):
+        out = []
+        h = x
+        for mod in net:
+            h = mod(h)
+            if isinstance(mod, (torch.nn.ReLU,)) or mod is net[-1]:
+                out.append(h)
+        return torch.cat(out, dim=1)
+
+    with torch.no_grad():
+        d = (acts(xs) - acts(xps)).abs().mean(0)
+    return d.cpu().numpy()
+
+
+def map_neurons(mlp: MLP, idx: Sequence[int]) -> List[Tuple[int, int]]:
+    offs = np.cumsum([0] + mlp.widths)
+    out = []
+    for g in idx:
+        l = int(np.searchsorted(offs, g, side="right") - 1)
+        out.append((l, int(g - offs[l])))
+    return out
+
+
+def masked_finetune(mlp: MLP, X: np.ndarray, y: np.ndarray, neurons: List[Tuple[int, int]], epochs: int = 5,
+                    lr: float = 5e-4, batch: int = 32, device="cpu", seed: int = 0) -> MLP:
+    """Adam on BCE, gradients masked to the incoming weights/bias of ``neurons`` only."""
+    torch.manual_seed(seed)
+    net = mlp.to_torch(device)
+    lins = [m for m in net if isinstance(m, torch.nn.Linear)]
+    masks = []
+    for l, lin in enumerate(lins):
+        wm = torch.zeros_like(lin.weight)
+        bm = torch.zeros_like(lin.bias)
+        for (ll, j) in neurons:
+            if ll == l:
+                wm[j, :] = 1
+                bm[j] = 1
+        masks.append((wm, bm))
+    params = [p for lin in lins for p in (lin.weight, lin.bias)]
+    opt = torch.optim.Adam(params, lr=lr)
+    Xt = torch.as_tensor(X, dtype=torch.float32, device=device)
+    yt = torch.as_tensor(y, dtype=torch.float32, device=device)
+    lossf = torch.nn.BCEWithLogitsLoss()
+    for _ in range(epochs):
+        for s in range(0, len(Xt), batch):
+            opt.zero_grad()
+            loss = lossf(net(Xt[s:s + batch])[:, 0], yt[s:s + batch])
+            loss.backward()
+            for lin, (wm, bm) in zip(lins, masks):
+                lin.weight.grad *= wm
+                lin.bias.grad *= bm
+            opt.step()
+    return MLP.from_torch(net, name=mlp.name + "-repaired")
+
+
+def fit(mlp: MLP, X: np.ndarray, y: np.ndarray, epochs: int = 5, lr: float = 1e-3, batch: int = 32, device="cpu",
+        seed: int = 0, acc_floor: Optional[Tuple[np.ndarray, np.ndarray, float]] = None) -> MLP:
+    """Plain full-network fine-tune (``model.fit``); optional accuracy floor on held-out data."""
+    torch.manual_seed(seed)
+    net = mlp.to_torch(device)
+    opt = torch.optim.Adam(net.parameters(), lr=lr)
+    Xt = torch.as_tensor(X, dtype=torch.float32, device=device)
+    yt = torch.as_tensor(y, dtype=torch.float32, device=device)
+    lossf = torch.nn.BCEWithLogitsLoss()
+    best = MLP.from_torch(net, name=mlp.name)
+    for _ in range(epochs):
+        perm = torch.randperm(len(Xt), device=device)
+        for s in range(0, len(Xt), batch):
+            b = perm[s:s + batch]
+            opt.zero_grad()
+            lossf(net(Xt[b])[:, 0], yt[b]).backward()
+            opt.step()
+        cur = MLP.from_torch(net, name=mlp.name)
+        if acc_floor is not None:
+            Xv, yv, floor = acc_floor
+            if np.mean(cur.predict(Xv) == yv) < floor:
+                break
+        best = cur
+    return best
+
+
+def relabel_pairs(X: np.ndarray, y: np.ndarray) -> np.ndarray:
+    """Each counterexample pair gets the max of its two labels (detect_bias.py:412-430)."""
+    y = np.asarray(y).copy()
+    for i in range(0, len(y) - 1, 2):
+        m = max(y[i], y[i + 1])
+        y[i] = y[i + 1] = m
+    return y
+
+
+def repair_model(model: str, counterexamples: str, method: str = "masked", out: str = "repaired.npz",
+                 top_k: int = 10, epochs: int = 5, weights: str = "zoo", seed: int = 0, device: str = "cpu") -> Dict:
+    from ..data import tabular
+    from ..models.zoo import get_model, suite_of
+    from ..presets import PRESETS
+    from ..spec import DOMAINS
+
+    mlp = get_model(model, weights=weights, seed=seed)
+    suite = suite_of(model)
+    pre = next(p for p in PRESETS.values() if p.suite == suite and model in p.models)
+    q = pre.resolved()
+    pa = q.pa_idx[0]
+    X, y = load_pairs(counterexamples, mlp.n_in, pa)
+    if y is None:
+        y = mlp.predict(X)
+    ds = tabular.load(suite, seed=seed, mlp=mlp)
+    before = float(np.mean(mlp.predict(ds.X_test) == ds.y_test))
+    scores = activation_deltas(mlp, X, pa, device)
+    top = np.argsort(-scores)[:top_k]
+    if method == "masked":
+        neurons = map_neurons(mlp, top[:1] if top_k == 1 else top)
+        rep = masked_finetune(mlp, X, y, neurons, epochs=epochs, device=device, seed=seed)
+        rep = fit(rep, X, relabel_pairs(X, y), epochs=epochs, lr=5e-4, device=device, seed=seed)
+    else:  # two-stage retraining (new_model.py): original data, then counterexample batches with a floor
+        rep = fit(mlp, ds.X_train, ds.y_train, epochs=max(1, epochs), lr=1e-2 if epochs > 5 else 1e-3,
+                  batch=256, device=device, seed=seed)
+        rep = fit(rep, X, relabel_pairs(X, y), epochs=epochs, lr=1e-3, batch=16, device=device, seed=seed,
+                  acc_floor=(ds.X_test, ds.y_test, 0.80))
+    rep.name = os.path.splitext(os.path.basename(out))[0]
+    rep.save_npz(out)
+    after = float(np.mean(rep.predict(ds.X_test) == ds.y_test))
+    pair_flip_before = float(np.mean(mlp.predict(X[0::2]) != mlp.predict(X[1::2])))
+    pair_flip_after = float(np.mean(rep.predict(X[0::2]) != rep.predict(X[1::2])))
+    return {"model": model, "repaired": out, "method": method, "top_neurons": map_neurons(mlp, top),
+            "top_scores": scores[top].tolist(), "acc_before": before, "acc_after": after,
+            "pair_disagreement_before": pair_flip_before, "pair_disagreement_after": pair_flip_after,
+            "data": "synthetic" if ds.synthetic else ds.name}

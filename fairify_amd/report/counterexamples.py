@@ -1,0 +1,69 @@
+"""Counterexample export with label decoding (C26).
+
+Reference: ``decode_counterexample`` + ``counterexample.csv`` writers of the fork
+(src/AC/Verify-AC-experiment-new2.py:344-407, src/GC/...-new2.py:318-467,
+src/BM/...-new2.py:343-404): encoded integers are mapped back to category strings with the
+training LabelEncoders, KBins bins to their midpoints, and each row gets the model output
+(sigmoid) and the predicted class.  Rows that cannot be decoded (codes outside the encoder's
+classes) are dropped, like the reference's BM variant.  An ``.npz`` with the raw pairs is
+written next to it (input of ``repair``).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+import pandas as pd
+
+
+def _decode_column(vals: np.ndarray, enc) -> Optional[np.ndarray]:
+    if enc is None:
+        return vals
+    if hasattr(enc, "classes_"):            # LabelEncoder
+        codes = np.rint(vals).astype(int)
+        ok = (codes >= 0) & (codes < len(enc.classes_))
+        out = np.empty(len(vals), dtype=object)
+        out[ok] = enc.classes_[codes[ok]]
+        out[~ok] = None
+        return out
+    if hasattr(enc, "bin_edges_"):          # KBinsDiscretizer -> bin midpoints
+        e = enc.bin_edges_[0]
+        b = np.clip(np.rint(vals).astype(int), 0, len(e) - 2)
+        return 0.5 * (e[b] + e[b + 1])
+    return vals
+
+
+def export_counterexamples(preset: str, model: str, results: str, out: Optional[str] = None,
+                           weights: str = "zoo") -> str:
+    from .. import presets
+    from ..data import tabular
+    from ..models.zoo import get_model
+    from .csv_report import read_csv
+
+    pre = presets.get(preset)
+    dom = pre.domain()
+    mlp = get_model(model, weights=weights)
+    rows = [r for r in read_csv(os.path.join(results, f"{model}.csv")) if r["Verification"] == "sat" and r["C1"]]
+
+    def parse(s):
+        return np.array([float(t) for t in s.replace("[", " ").replace("]", " ").split()])
+
+    X = np.array([parse(r["C1"]) for r in rows]).reshape(-1, dom.n)
+    XP = np.array([parse(r["C2"]) for r in rows]).reshape(-1, dom.n)
+    pairs = np.stack([X, XP], axis=1).reshape(-1, dom.n)
+    try:
+        enc = tabular.load(pre.suite, allow_synthetic=False).encoders
+    except Exception:
+        enc = {}
+    z = mlp.logits(pairs)
+    out_df = pd.DataFrame({name: _decode_column(pairs[:, i], enc.get(name)) for i, name in enumerate(dom.names)})
+    out_df["output"] = 0.5 * (1 + np.tanh(0.5 * z))
+    out_df["prediction"] = (z > 0).astype(int)
+    keep = ~out_df[dom.names].isna().any(axis=1).to_numpy()
+    keep = keep.reshape(-1, 2).all(axis=1).repeat(2)
+    out_df = out_df[keep]
+    out = out or os.path.join(results, f"{model}-counterexample.csv")
+    out_df.to_csv(out, index=False)
+    np.savez(os.path.splitext(out)[0] + ".npz", x=X, xp=XP, y=np.maximum(z[0::2] > 0, z[1::2] > 0).astype(int))
+    return out

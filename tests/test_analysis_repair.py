@@ -1,0 +1,82 @@
+"""Group metrics, causal detector, hybrid routing, counterexample export, repair (CPU)."""
+import os
+
+import numpy as np
+import pytest
+
+from fairify_amd import presets
+from fairify_amd.analysis.causal import CausalDiscriminationDetector
+from fairify_amd.analysis.hybrid import V_SAT, V_UNSAT, VerdictTable, hybrid_predict
+from fairify_amd.analysis.metrics import consistency, group_metrics, theil_index
+from fairify_amd.engine.pipeline import VerifyConfig
+from fairify_amd.engine.runner import run_preset
+from fairify_amd.models.mlp import random_mlp
+
+
+def test_group_metrics_hand_computed():
+    y = np.array([1, 1, 0, 0, 1, 0, 1, 0])
+    p = np.array([1, 0, 0, 1, 1, 1, 1, 0])
+    a = np.array([1, 1, 1, 1, 0, 0, 0, 0])      # privileged = 1
+    m = group_metrics(y, p, a)
+    # priv: pos rate 2/4, unpriv: 3/4 ; TPR priv 1/2, unpriv 2/2 ; FPR priv 1/2, unpriv 1/2
+    assert m["SPD"] == pytest.approx(0.25)
+    assert m["DI"] == pytest.approx(1.5)
+    assert m["EOD"] == pytest.approx(0.5)
+    assert m["AOD"] == pytest.approx(0.25)
+
+
+def test_consistency_matches_bruteforce():
+    rng = np.random.default_rng(0)
+    X = rng.integers(0, 10, (200, 4)).astype(float) + rng.random((200, 4)) * 1e-3
+    yp = rng.integers(0, 2, 200)
+    d = ((X[:, None] - X[None]) ** 2).sum(-1)
+    nn = np.argsort(d, axis=1)[:, :5]
+    ref = 1 - np.mean(np.abs(yp - yp[nn].mean(1)))
+    assert consistency(X, yp, chunk=37) == pytest.approx(ref)
+    assert theil_index(np.array([1, 0, 1]), np.array([1, 0, 1])) == pytest.approx(0.0)
+
+
+def test_causal_detector_extremes():
+    names = ["a", "s", "b"]
+    X = np.array([[0, 0, 0], [1, 1, 1], [2, 0, 2]], dtype=float)
+    fair = CausalDiscriminationDetector.from_data(lambda Z: (Z[:, 0] > 0).astype(int), X, names, max_samples=300)
+    assert fair.causal_discrimination(["s"])[1] == 0.0
+    unfair = CausalDiscriminationDetector.from_data(lambda Z: Z[:, 1].astype(int), X, names, max_samples=300)
+    assert unfair.causal_discrimination(["s"])[1] == 1.0
+
+
+def test_verdict_table_and_hybrid():
+    pre = presets.get("src/GC-age")
+    g = pre.grid()
+    t = VerdictTable(g)
+    t.set(np.array([0, 1]), ["sat", "unsat"])
+    lo, hi = g.decode(np.array([0, 1, 2]))
+    v = t.lookup(lo)
+    assert v.tolist() == [V_SAT, V_UNSAT, -1]
+    yh = hybrid_predict(lo, t, lambda X: np.zeros(len(X), int), lambda X: np.ones(len(X), int))
+    assert yh.tolist() == [1, 0, 0]
+
+
+def test_export_and_repair_roundtrip(tmp_path):
+    from fairify_amd.report.counterexamples import export_counterexamples
+    from fairify_amd.repair.retrain import activation_deltas, masked_finetune, map_neurons, relabel_pairs
+
+    out = str(tmp_path)
+    run_preset(presets.get("src/GC-age"), models=["GC-1"], out_dir=out, accuracy=False, verbose=False,
+               cfg=VerifyConfig(sim_size=200, node_budget=256), max_partitions=12, weights="random")
+    path = export_counterexamples("src/GC-age", "GC-1", out, weights="random")
+    z = np.load(os.path.splitext(path)[0] + ".npz")
+    assert z["x"].shape == z["xp"].shape and len(z["x"]) > 0
+    from fairify_amd.models.zoo import get_model
+
+    m = get_model("GC-1", weights="random")
+    X = np.stack([z["x"], z["xp"]], 1).reshape(-1, 20)
+    sc = activation_deltas(m, X, pa_index=11)
+    assert sc.shape == (m.n_neurons,) and sc.max() > 0
+    neurons = map_neurons(m, np.argsort(-sc)[:3])
+    y = relabel_pairs(X, m.predict(X))
+    rep = masked_finetune(m, X, y, neurons, epochs=2)
+    # only the selected neurons' incoming weights changed
+    changed = [np.nonzero(np.any(a != b, axis=0))[0].tolist() for a, b in zip(m.weights, rep.weights)]
+    for l, cols in enumerate(changed):
+        assert set(cols) <= {j for (ll, j) in neurons if ll == l}
