@@ -63,13 +63,13 @@ def test_export_and_repair_roundtrip(tmp_path):
 
     out = str(tmp_path)
     run_preset(presets.get("src/GC-age"), models=["GC-1"], out_dir=out, accuracy=False, verbose=False,
-               cfg=VerifyConfig(sim_size=200, node_budget=256), max_partitions=12, weights="random")
-    path = export_counterexamples("src/GC-age", "GC-1", out, weights="random")
+               cfg=VerifyConfig(sim_size=200, node_budget=256), max_partitions=12, weights="zoo")
+    path = export_counterexamples("src/GC-age", "GC-1", out, weights="zoo")
     z = np.load(os.path.splitext(path)[0] + ".npz")
     assert z["x"].shape == z["xp"].shape and len(z["x"]) > 0
     from fairify_amd.models.zoo import get_model
 
-    m = get_model("GC-1", weights="random")
+    m = get_model("GC-1", weights="zoo")
     X = np.stack([z["x"], z["xp"]], 1).reshape(-1, 20)
     sc = activation_deltas(m, X, pa_index=11)
     assert sc.shape == (m.n_neurons,) and sc.max() > 0
