@@ -181,14 +181,15 @@ class BabRuntime {
       }
     }
     // host result buffers
-    py::array_t<int64_t> cex_x({P, n0_}), cex_xp({P, n0_});
-    std::memset(cex_x.mutable_data(), 0, sizeof(int64_t) * (size_t)P * n0_);
-    std::memset(cex_xp.mutable_data(), 0, sizeof(int64_t) * (size_t)P * n0_);
+    std::vector<int64_t> cex_x((size_t)P * n0_, 0), cex_xp((size_t)P * n0_, 0);
     std::vector<char> got(P, 0);
     int levels = 0, launches = 0;
     long long total_nodes = 0;
     bool timed_out = false;
     const int target = std::max(batch_, 1);
+    {
+    // the level loop runs without the GIL: several models/streams can be driven from Python threads
+    py::gil_scoped_release nogil;
     while (n_in > 0) {
       const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (el > time_budget) {
@@ -269,6 +270,7 @@ class BabRuntime {
       cur = nxt;
       n_in = n_out;
     }
+    }
     std::vector<int8_t> sout(P);
     std::vector<int> nout(P);
     ck(hipMemcpyAsync(sout.data(), status_.p, P, hipMemcpyDeviceToHost, st), "cp");
@@ -290,7 +292,10 @@ class BabRuntime {
     stats["nodes"] = total_nodes;
     stats["time"] = el;
     stats["timed_out"] = timed_out;
-    return py::make_tuple(status_out, cex_x, cex_xp, nodes_out, stats);
+    py::array_t<int64_t> ax({P, n0_}), axp({P, n0_});
+    std::memcpy(ax.mutable_data(), cex_x.data(), sizeof(int64_t) * cex_x.size());
+    std::memcpy(axp.mutable_data(), cex_xp.data(), sizeof(int64_t) * cex_xp.size());
+    return py::make_tuple(status_out, ax, axp, nodes_out, stats);
   }
 
  private:
@@ -316,25 +321,34 @@ class BabRuntime {
     ckl(fa_bounds_launch(net_, b, st), "bounds");
   }
 
-  void confirm_candidates(int n_cand, py::object& confirm, std::vector<char>& got, py::array_t<int64_t>& cex_x,
-                          py::array_t<int64_t>& cex_xp, hipStream_t st) {
-    py::array_t<float> buf({n_cand, 2 * n0_});
-    py::array_t<int> parts(n_cand);
-    ck(hipMemcpyAsync(buf.mutable_data(), cand_buf_.p, sizeof(float) * (size_t)n_cand * 2 * n0_,
-                      hipMemcpyDeviceToHost, st), "cp cand");
-    ck(hipMemcpyAsync(parts.mutable_data(), cand_part_.p, sizeof(int) * n_cand, hipMemcpyDeviceToHost, st), "cp");
+  // called WITHOUT the GIL; takes it only around the Python confirmation callback
+  void confirm_candidates(int n_cand, py::object& confirm, std::vector<char>& got, std::vector<int64_t>& cex_x,
+                          std::vector<int64_t>& cex_xp, hipStream_t st) {
+    std::vector<float> buf((size_t)n_cand * 2 * n0_);
+    std::vector<int> parts(n_cand);
+    ck(hipMemcpyAsync(buf.data(), cand_buf_.p, sizeof(float) * buf.size(), hipMemcpyDeviceToHost, st), "cp cand");
+    ck(hipMemcpyAsync(parts.data(), cand_part_.p, sizeof(int) * n_cand, hipMemcpyDeviceToHost, st), "cp");
     ck(hipStreamSynchronize(st), "sync");
-    py::array_t<bool> ok = confirm(parts, buf).cast<py::array_t<bool>>();
+    std::vector<char> ok(n_cand, 0);
+    {
+      py::gil_scoped_acquire gil;
+      py::array_t<float> abuf({n_cand, 2 * n0_});
+      py::array_t<int> aparts(n_cand);
+      std::memcpy(abuf.mutable_data(), buf.data(), sizeof(float) * buf.size());
+      std::memcpy(aparts.mutable_data(), parts.data(), sizeof(int) * parts.size());
+      py::array_t<bool> res = confirm(aparts, abuf).cast<py::array_t<bool>>();
+      for (int i = 0; i < n_cand; ++i) ok[i] = res.data()[i] ? 1 : 0;
+    }
     std::vector<int> newly;
     const float* B = buf.data();
     for (int i = 0; i < n_cand; ++i) {
-      const int p = parts.data()[i];
-      if (!ok.data()[i] || got[p]) continue;
+      const int p = parts[i];
+      if (!ok[i] || got[p]) continue;
       got[p] = 1;
       newly.push_back(p);
       for (int d = 0; d < n0_; ++d) {
-        cex_x.mutable_data()[(size_t)p * n0_ + d] = (int64_t)std::llround(B[(size_t)i * 2 * n0_ + d]);
-        cex_xp.mutable_data()[(size_t)p * n0_ + d] = (int64_t)std::llround(B[(size_t)i * 2 * n0_ + n0_ + d]);
+        cex_x[(size_t)p * n0_ + d] = (int64_t)std::llround(B[(size_t)i * 2 * n0_ + d]);
+        cex_xp[(size_t)p * n0_ + d] = (int64_t)std::llround(B[(size_t)i * 2 * n0_ + n0_ + d]);
       }
     }
     if (!newly.empty()) {

@@ -123,7 +123,7 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     Pn, n = lo_np.shape
     widths = mlp.widths
     Nh = int(sum(mlp.hidden))
-    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    sync = (lambda: torch.cuda.current_stream(dev).synchronize()) if dev.type == "cuda" else (lambda: None)
 
     values_np, pairs_np = _pa_table(q, lo_np, hi_np)
     values = torch.from_numpy(values_np).to(dev)

@@ -29,7 +29,7 @@ class StageTimer:
     @contextlib.contextmanager
     def __call__(self, name: str):
         if self.sync:
-            torch.cuda.synchronize(self.device)
+            torch.cuda.current_stream(self.device).synchronize()
         if _ROCTX and torch.cuda.is_available():
             torch.cuda.nvtx.range_push(name)
         t0 = time.perf_counter()
@@ -37,7 +37,7 @@ class StageTimer:
             yield
         finally:
             if self.sync:
-                torch.cuda.synchronize(self.device)
+                torch.cuda.current_stream(self.device).synchronize()
             self.t[name] += time.perf_counter() - t0
             self.n[name] += 1
             if _ROCTX and torch.cuda.is_available():
