@@ -99,6 +99,42 @@ def cmd_export(args):
     print(path)
 
 
+def cmd_export_smt(args):
+    """Write the SMT-LIB2 query of partitions (sound-pruned on the box) for external solvers."""
+    import numpy as np
+    import torch
+
+    from . import presets
+    from .engine import prune as P_
+    from .models.zoo import get_model
+    from .ops.backend import Backend
+    from .partition import processing_order
+    from .smt import encode_partition, pruned_network
+
+    pre = presets.get(args.preset)
+    grid = pre.grid()
+    q = pre.resolved()
+    m = get_model(args.model, weights=args.weights, seed=args.seed)
+    order = processing_order(grid, seed=args.seed)
+    ids = order[:args.count] if args.ids is None else np.array([int(x) for x in args.ids.split(",")])
+    lo, hi = grid.decode(ids)
+    be = Backend(m, device=_device(args.device))
+    r = be.bounds(torch.from_numpy(lo).float().to(be.device), torch.from_numpy(hi).float().to(be.device),
+                  mode="ibp", keep_layers=True)
+    nh = int(sum(m.hidden))
+    dead = torch.cat(r.layer_ub, dim=1)[:, :nh] <= 0
+    dead = P_.ensure_one_alive(torch.cat([dead, torch.zeros_like(dead[:, :1])], dim=1), m.widths)[:, :nh]
+    dead = dead.cpu().numpy()
+    os.makedirs(args.out, exist_ok=True)
+    for k, gid in enumerate(ids):
+        net = pruned_network(m, dead[k])
+        text = encode_partition(net, q, lo[k], hi[k], timeout_s=args.timeout, fork_params=args.fork_params).text
+        path = os.path.join(args.out, f"{args.model}-p{int(gid)}.smt2")
+        with open(path, "w") as f:
+            f.write(text)
+        print(path, f"(pruned {m.n_neurons - net.n_neurons} of {m.n_neurons} neurons)")
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="fairify_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -159,6 +195,19 @@ def main(argv=None):
     e.add_argument("--out", default=None)
     e.add_argument("--weights", default="zoo")
     e.set_defaults(fn=cmd_export)
+
+    x = sub.add_parser("export-smt", help="write SMT-LIB2 partition queries (GPU-pruned) for external solvers")
+    x.add_argument("--preset", required=True)
+    x.add_argument("--model", required=True)
+    x.add_argument("--out", required=True)
+    x.add_argument("--count", type=int, default=4, help="first N partitions of the seeded order")
+    x.add_argument("--ids", default=None, help="comma list of grid ids (overrides --count)")
+    x.add_argument("--timeout", type=float, default=100.0)
+    x.add_argument("--fork-params", action="store_true")
+    x.add_argument("--weights", default="zoo")
+    x.add_argument("--seed", type=int, default=0)
+    x.add_argument("--device", default=None)
+    x.set_defaults(fn=cmd_export_smt)
 
     args = ap.parse_args(argv)
     args.fn(args)

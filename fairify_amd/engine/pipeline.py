@@ -47,6 +47,10 @@ class VerifyConfig:
     bisect_pairs: int = 16
     bisect_steps: int = 12
     sound_prune_stats: bool = True       # compute B/S compression (reference parity columns)
+    smt_backend: str = "auto"            # host SMT on the BaB residue: auto | z3py | z3bin | none
+    smt_workers: int = 8
+    smt_timeout: Optional[float] = None  # per query; defaults to soft_timeout
+    smt_fork_params: bool = False        # Z3 seed/restart/phase options of the fork's drivers
 
 
 @dataclass
@@ -106,6 +110,19 @@ class _LazyMasked:
 
     def __len__(self) -> int:
         return len(self.masks)
+
+
+_HOST_SMT: Dict[tuple, object] = {}
+
+
+def _host_smt(cfg: VerifyConfig):
+    """Host SMT pool for the residue (cached per configuration; inactive without a back-end)."""
+    from ..smt.host import HostSMT
+
+    key = (cfg.smt_backend, cfg.smt_workers, cfg.smt_timeout or cfg.soft_timeout, cfg.smt_fork_params)
+    if key not in _HOST_SMT:
+        _HOST_SMT[key] = HostSMT(cfg.smt_backend, cfg.smt_workers, key[2], cfg.smt_fork_params)
+    return _HOST_SMT[key]
 
 
 def _amortize(total: float, work: np.ndarray) -> np.ndarray:
@@ -197,6 +214,32 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     nodes = res.nodes.copy()
     sync()
     t_bab = time.time() - t0
+
+    # ---------------- stage 3b: host SMT on the sound-pruned subnetworks of the residue
+    # (the reference's Z3 check, src/AC/Verify-AC.py:145-158; no-op without a back-end)
+    t_smt = 0.0
+    if cfg.smt_backend != "none":
+        hs = _host_smt(cfg)
+        unk = np.nonzero(status == UNKNOWN)[0]
+        if hs.active and unk.size:
+            t0 = time.time()
+            with tm("smt"):
+                ut = torch.from_numpy(unk).to(dev)
+                futs = hs.submit(mlp, q, lo_np[unk], hi_np[unk], st_dead[ut][:, :Nh])
+                for k, f in zip(unk, futs):
+                    verdict, pair = f.result()
+                    if verdict == "unsat":
+                        status[k], stage[k] = UNSAT, "smt"
+                    elif verdict == "sat" and pair is not None:
+                        X = np.array([pair[0]], dtype=np.int64)
+                        XP = np.array([pair[1]], dtype=np.int64)
+                        ok = exact.check_pair_constraints(X, XP, lo_np[k:k + 1], hi_np[k:k + 1], q.pa_idx,
+                                                          q.ra_idx, q.tau)
+                        if ok[0] and exact.is_violation(mlp, X, XP)[0]:
+                            status[k], stage[k] = SAT, "smt"
+                            cex_x[k], cex_xp[k] = X[0], XP[0]
+            t_smt = time.time() - t0
+    t_bab += t_smt
 
     # ---------------- stage 4: heuristic retry for UNKNOWN partitions (unsound, flagged)
     h_attempt = np.zeros(Pn, dtype=np.int64)

@@ -1,0 +1,84 @@
+"""Host SMT stage: residual (UNKNOWN) partitions -> GPU-pruned subnetworks -> host solver pool.
+
+The reference solves every partition with Z3 on the CPU (src/AC/Verify-AC.py:127-212).  Here
+the GPU decides the bulk; only partitions that are still UNKNOWN after the device
+branch-and-bound (and the heuristic retry) reach this stage:
+
+1. the sound dead-neuron masks of those partitions (computed on the GPU by the IBP/symbolic
+   pruner) are copied device -> pinned host memory with a non-blocking copy on a dedicated
+   side stream, so the copy overlaps whatever the compute stream does next;
+2. host worker threads wait on that copy's event, delete the dead neurons
+   (``prune_neurons``, utils/prune.py:950-977), emit the SMT-LIB2 query
+   (:mod:`fairify_amd.smt.encode`) and run the configured back-end with the soft timeout;
+3. ``sat`` models are re-confirmed with the exact checker on the ORIGINAL network before
+   they count (the reference's ``V-accurate`` / ``C-check`` replay, src/AC/Verify-AC.py:225-258).
+
+With no back-end available (this image ships no Z3) the stage is a no-op.
+"""
+from __future__ import annotations
+
+from concurrent.futures import Future, ThreadPoolExecutor
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..models.mlp import MLP
+from ..spec import ResolvedQuery
+from .encode import encode_partition, pruned_network
+from .solver import resolve, solve
+
+
+class HostSMT:
+    def __init__(self, backend: str = "auto", workers: int = 8, timeout_s: float = 100.0, fork_params: bool = False):
+        self.backend = resolve(backend)
+        self.timeout_s = float(timeout_s)
+        self.fork_params = fork_params
+        self.pool = ThreadPoolExecutor(max_workers=max(1, workers)) if self.backend != "none" else None
+        self._streams: Dict[int, torch.cuda.Stream] = {}
+
+    @property
+    def active(self) -> bool:
+        return self.pool is not None
+
+    def _side_stream(self, dev: torch.device):
+        k = dev.index or 0
+        if k not in self._streams:
+            self._streams[k] = torch.cuda.Stream(dev)
+        return self._streams[k]
+
+    def stage_masks(self, masks: torch.Tensor):
+        """Device bool [K, Nh] -> (pinned host uint8 tensor, event or None)."""
+        m = masks.to(torch.uint8)
+        if m.device.type != "cuda":
+            return m.cpu(), None
+        host = torch.empty(m.shape, dtype=torch.uint8, pin_memory=True)
+        side = self._side_stream(m.device)
+        side.wait_stream(torch.cuda.current_stream(m.device))
+        with torch.cuda.stream(side):
+            host.copy_(m, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        m.record_stream(side)
+        return host, ev
+
+    def submit(self, mlp: MLP, q: ResolvedQuery, lo: np.ndarray, hi: np.ndarray, masks: torch.Tensor
+               ) -> List[Future]:
+        """One future per partition (rows of lo/hi/masks) -> (verdict, pair or None)."""
+        if not self.active or len(lo) == 0:
+            return []
+        host, ev = self.stage_masks(masks)
+
+        def work(k: int):
+            if ev is not None:
+                ev.synchronize()
+            net = pruned_network(mlp, host[k].numpy().astype(bool))
+            script = encode_partition(net, q, lo[k], hi[k], timeout_s=self.timeout_s,
+                                      fork_params=self.fork_params).text
+            return solve(script, q.n, self.backend, self.timeout_s)
+
+        return [self.pool.submit(work, k) for k in range(len(lo))]
+
+    def shutdown(self):
+        if self.pool is not None:
+            self.pool.shutdown(wait=True)
