@@ -33,6 +33,9 @@ struct BoundArgs {
   // per-partition forced-dead masks (heuristic nets): dead = dead_part[node_part[node]]
   const int* node_part;     // [R / max(V,1)]
   const uint8_t* dead_part; // [P, n_hidden]
+  // input dims degenerate (lo == hi) in EVERY row: folded into the constant by the
+  // register-resident symbolic kernel (PA dims are added automatically when V > 0)
+  unsigned long long fold;
 };
 
 struct FwdArgs {

@@ -81,7 +81,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bounds", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t dead_in, int R,
                      int symbolic, uintptr_t out_lb, uintptr_t out_ub, uintptr_t Lc, uintptr_t L0, uintptr_t Le,
                      uintptr_t Uc, uintptr_t U0, uintptr_t Ue, uintptr_t layer_lb, uintptr_t layer_ub,
-                     uintptr_t dead_out, int G, uintptr_t stream) {
+                     uintptr_t dead_out, int G, uintptr_t stream, unsigned long long fold) {
     NetDesc d = net.d;
     BoundArgs a{};
     a.flat = P<const float>(flat);
@@ -98,8 +98,12 @@ PYBIND11_MODULE(_C, m) {
     a.layer_lb = P<float>(layer_lb);
     a.layer_ub = P<float>(layer_ub);
     a.dead_out = P<uint8_t>(dead_out);
+    a.fold = fold;
     check(fa_bounds_launch(d, a, (hipStream_t)stream), "bounds");
-  });
+  }, py::arg("net"), py::arg("flat"), py::arg("lo"), py::arg("hi"), py::arg("dead_in"), py::arg("R"),
+     py::arg("symbolic"), py::arg("out_lb"), py::arg("out_ub"), py::arg("Lc"), py::arg("L0"), py::arg("Le"),
+     py::arg("Uc"), py::arg("U0"), py::arg("Ue"), py::arg("layer_lb"), py::arg("layer_ub"), py::arg("dead_out"),
+     py::arg("G"), py::arg("stream"), py::arg("fold") = 0ull);
 
   m.def("forward", [](const Net& net, uintptr_t flat, uintptr_t x, int B, uintptr_t dead, uintptr_t out,
                       uintptr_t stream) {

@@ -16,6 +16,8 @@
 // bounds, applies the ReLU relaxation to the forms in place, re-seeds the interval rows with
 // max(0, bound) and writes the error rows for the next layer.  Only the logit forms (and, on
 // request, per-neuron bounds / dead flags) go back to HBM.
+#include <stdlib.h>
+
 #include "args.h"
 
 __global__ void __launch_bounds__(FA_THREADS)
@@ -279,8 +281,28 @@ extern "C" size_t fa_bounds_smem(const NetDesc& net, int symbolic, int G, int* s
   return floats * sizeof(float);
 }
 
+extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long long fold_mask,
+                                 hipStream_t stream);
+
+static int fa_lds_only() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("FAIRIFY_BOUNDS_KERNEL");
+    v = (e && e[0] == 'l') ? 1 : 0;   // "lds": force the LDS-tiled kernel (A/B comparisons)
+  }
+  return v;
+}
+
 extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream) {
   if (args.R <= 0) return 0;
+  if (args.symbolic && !fa_lds_only()) {
+    unsigned long long fold = args.fold;
+    if (args.V > 0)
+      for (int k = 0; k < args.npa; ++k) fold |= 1ull << args.pa_idx[k];
+    const int rc = fa_sym_try_launch(net, args, fold, stream);
+    if (rc == 1) return 0;
+    if (rc < 0) return -rc;
+  }
   const size_t limit = 160 * 1024;
   int G = args.G > 0 ? args.G : 16;
   int S = 0, ws = 0, wf = 0;

@@ -1,0 +1,469 @@
+// Register-resident forward-symbolic bound propagation (K4/K9 bounding primitive).  gfx950.
+//
+// Same arithmetic and error accounting as fa_bounds_kernel / ops/reference.py:bounds (symbolic
+// mode), re-tiled for CDNA4:
+//
+// * ONE box-row per wave64 (many waves per CU, persistent grid), no __syncthreads after the
+//   one-time staging of every layer's W and b into LDS.
+// * A layer's linear forms are kept TRANSPOSED in MFMA accumulators: rows = neurons, columns =
+//   form columns [coefficients of the non-folded input dims | constant | error | interval |
+//   interval error].  Input dims that are degenerate for every row (the protected attribute
+//   in the node-row expansion, V > 0) are folded into the constant column, so Adult's
+//   13-input forms (12 coefficients + 4) fill exactly one 16-wide column tile.
+// * Layer l is   U' = W+^T U + W-^T L,   L' = W+^T L + W-^T U   on v_mfma_f32_16x16x4_f32.
+//   The L block stores its two error columns NEGATED, so the same four plain MFMAs make both
+//   error columns accumulate |W-| (U_err' = W+ eU + |W-| eL, -L_err' = -(W+ eL + |W-| eU)).
+//   The previous layer's accumulator tile IS the next layer's B operand (reg i of tile t holds
+//   neurons 16t + 4*(lane>>4) + i); W^T is staged in LDS pre-permuted into that MFMA operand
+//   order, one ds_read_b128 per (output tile, K tile), so forms never touch LDS or HBM
+//   between layers.
+// * The epilogue works on the accumulators: constant/error/interval columns are broadcast and
+//   the concretisation sums reduced within each 16-lane row with DPP (quad_perm, row
+//   half-mirror, row mirror: a butterfly, so every lane holds the bitwise-identical sum), and
+//   the ReLU relaxation rescales each lane's own column.
+//
+// Shapes outside the register budget (wide layers with > 1 column tile) keep using the
+// LDS-tiled fa_bounds_kernel; see fa_sym_try_launch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "args.h"
+
+#define FA_SYM_MAXC 48   // at most 3 column tiles
+
+struct SymCfg {
+  int nc;                          // coefficient columns (non-folded input dims)
+  int cdim[FA_SYM_MAXC];           // column -> input dim (c < nc)
+  unsigned long long fold;         // bitmask of folded (degenerate) input dims
+  int w_lds[FA_MAX_LAYERS];        // LDS float offset of W_l, MFMA operand order:
+                                   //   [jt][t][lane][i] = W[16t + 4(lane>>4) + i][16jt + (lane&15)]
+  int b_lds[FA_MAX_LAYERS];        // LDS float offset of b_l
+  int lds_floats;
+};
+
+struct SymBox {
+  const BoundArgs* a;
+  int node, v, n0;
+  __device__ __forceinline__ float lo(int d) const {
+    float x = a->lo[(size_t)node * n0 + d];
+    if (a->V > 0)
+      for (int k = 0; k < a->npa; ++k)
+        if (a->pa_idx[k] == d) x = a->values[v * a->npa + k];
+    return x;
+  }
+  __device__ __forceinline__ float hi(int d) const {
+    float x = a->hi[(size_t)node * n0 + d];
+    if (a->V > 0)
+      for (int k = 0; k < a->npa; ++k)
+        if (a->pa_idx[k] == d) x = a->values[v * a->npa + k];
+    return x;
+  }
+};
+
+// per-wave LDS slab: tile staging T[2 blocks][16 neurons][TS] + box values [3][48]
+template <int NT>
+struct SymSlab {
+  static constexpr int TS = 16 * NT + 4;                 // padded row stride (floats)
+  static constexpr int TILE = 2 * 16 * TS;
+  static constexpr int BOX = 3 * FA_SYM_MAXC;
+  static constexpr int FLOATS = (TILE + BOX + 3) & ~3;
+};
+
+template <int NT, int TM>
+__device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
+                                             const float* smem, float* T, const float* bxv, const int* cdim_s,
+                                             int l, int r,
+                                             int node, int lane, const float (&B)[NT][TM][2][4],
+                                             float (&A)[NT][TM][2][4]) {
+  constexpr int TS = SymSlab<NT>::TS;
+  const int col = lane & 15, grp = lane >> 4;
+  const int n_in = net.dims[l], n_out = net.dims[l + 1];
+  const int tin = (n_in + 15) >> 4, tout = (n_out + 15) >> 4;
+  const float* sw = smem + cfg.w_lds[l];
+  const float* sb = smem + cfg.b_lds[l];
+  const bool last = l == net.n_layers - 1;
+  const float gg = net.g_gemm[l];
+  const float gc = net.g_conc;
+  const float gi = net.g_one;
+  const float unit = net.unit;
+  const float gnext = last ? 0.f : net.g_gemm[l + 1];
+  const int noff = net.neuron_off[l];
+  const int nc = cfg.nc;
+  const int n0 = net.dims[0];
+  // neuron lane role in the epilogue: lanes 0-15 = U block, 16-31 = L block of neuron (lane & 15)
+  const bool nl_act = lane < 32;
+  const int ob = (lane >> 4) & 1;
+  float* Trow = T + (ob * 16 + col) * TS;
+#pragma unroll
+  for (int jt = 0; jt < TM; ++jt) {
+    if (jt >= tout) break;
+    f32x4 U[NT], Lq[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+      U[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      Lq[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const float4* wq = reinterpret_cast<const float4*>(sw) + (size_t)jt * tin * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      if (t >= tin) break;
+      const float4 w4 = wq[t * 64];
+      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          const float bu = B[ct][t][0][i], bl = B[ct][t][1][i];
+          U[ct] = fa_mfma4(wp, bu, U[ct]);
+          Lq[ct] = fa_mfma4(wp, bl, Lq[ct]);
+          U[ct] = fa_mfma4(wn, bl, U[ct]);
+          Lq[ct] = fa_mfma4(wn, bu, Lq[ct]);
+        }
+      }
+    }
+    // ---------------- spill the tile: T[block][neuron][column]
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        T[(4 * grp + i) * TS + ct * 16 + col] = U[ct][i];
+        T[(16 + 4 * grp + i) * TS + ct * 16 + col] = Lq[ct][i];
+      }
+    __builtin_amdgcn_wave_barrier();
+    // ---------------- one lane per (neuron, block): bounds, relaxation, new form row
+    const int j = 16 * jt + col;
+    const bool jv = j < n_out;
+    float v[16 * NT];
+#pragma unroll
+    for (int q = 0; q < 4 * NT; ++q) {
+      const float4 x = reinterpret_cast<const float4*>(Trow)[q];
+      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+    }
+    const float b = jv ? sb[j] : 0.f;
+    // concretisation of the coefficient part over the box (Σ min, Σ max, Σ |c| m); padding
+    // columns hold 0 coefficients and a [0, 0] box, so they add exact zeros
+    float mn = 0.f, mx = 0.f, mg = 0.f;
+#pragma unroll
+    for (int c = 4; c < 16 * NT; ++c) {
+      const float p = v[c] * bxv[c], h = v[c] * bxv[FA_SYM_MAXC + c];
+      mn += fminf(p, h);
+      mx += fmaxf(p, h);
+      mg += fabsf(v[c]) * bxv[2 * FA_SYM_MAXC + c];
+    }
+    const float cr = v[0];
+    float er = v[1], ivr = v[2], ier = v[3];
+    const float sgn = ob ? -1.f : 1.f;            // L block: error columns stored negated
+    er *= sgn;
+    ier *= sgn;
+    const float c0 = cr + b;
+    const float mgc = mg;                         // coefficient part of the magnitude
+    mn += c0; mx += c0; mg += fabsf(c0);
+    const float iv = ivr + b;
+    const float eI = ier * (1.f + 2.f * gg) + gg * fabsf(b);
+    const float e = er * (1.f + 2.f * gg) + gg * fabsf(b);
+    float bound;
+    if (ob == 0) bound = fminf(iv + gi * fabsf(iv) + eI, mx + gc * mg + e);   // ub (U block)
+    else bound = fmaxf(iv - gi * fabsf(iv) - eI, mn - gc * mg - e);           // lb (L block)
+    const float other = __shfl_xor(bound, 16, 64);
+    const float ub = ob == 0 ? bound : other;
+    const float lb = ob == 0 ? other : bound;
+    if (nl_act && jv && a.layer_lb) {
+      if (ob == 0) a.layer_ub[(size_t)r * net.n_neurons + noff + j] = ub;
+      else a.layer_lb[(size_t)r * net.n_neurons + noff + j] = lb;
+    }
+    if (last) {
+      if (nl_act && j == 0) {   // logit: rigorous bounds + output forms (folded dims -> 0)
+        float* Cf = ob == 0 ? a.Uc : a.Lc;
+        if (ob == 0) {
+          a.out_ub[r] = ub; a.U0[r] = c0; a.Ue[r] = e;
+        } else {
+          a.out_lb[r] = lb; a.L0[r] = c0; a.Le[r] = e;
+        }
+        for (int d = 0; d < n0; ++d)
+          if ((cfg.fold >> d) & 1ull) Cf[(size_t)r * n0 + d] = 0.f;
+        for (int c = 0; c < nc; ++c) Cf[(size_t)r * n0 + cdim_s[c]] = Trow[4 + c];
+      }
+      continue;
+    }
+    bool forced = false;
+    if (nl_act && jv) {
+      if (a.dead_in) forced = a.dead_in[(size_t)r * net.n_hidden + noff + j] != 0;
+      else if (a.dead_part) forced = a.dead_part[(size_t)a.node_part[node] * net.n_hidden + noff + j] != 0;
+    }
+    const bool isdead = ub <= 0.f;
+    const bool isact = lb >= 0.f;
+    if (nl_act && ob == 0 && jv && a.dead_out) a.dead_out[(size_t)r * net.n_hidden + noff + j] = isdead ? 1 : 0;
+    const bool zero = isdead || forced || !jv;
+    float s, cnew, en, mgn, ivn;
+    if (ob == 0) {
+      // upper: identity (stable active) / zero / chord over [aa, bb] of T = U + eU
+      ivn = zero ? 0.f : fmaxf(ub, 0.f);
+      s = 1.f; cnew = c0; en = e; mgn = mg;
+      if (zero) {
+        s = 0.f; cnew = 0.f; en = 0.f; mgn = 0.f;
+      } else if (!isact) {
+        const float aa = mn - gc * mg + e;
+        const float bb = mx + gc * mg + e;
+        s = (bb / (bb - aa)) * (1.f + 4.f * unit);
+        const float shift = e - aa;
+        cnew = c0 * s + s * shift;
+        mgn = s * mgc * (1.f + 8.f * unit) + fabsf(cnew);
+        en = 4.f * unit * s * (mg + fabsf(shift));
+      }
+    } else {
+      // lower: lambda in {0,1} applied to L(x) - eL
+      ivn = zero ? 0.f : fmaxf(lb, 0.f);
+      const float aL = mn - gc * mg - e;
+      const float bL = mx + gc * mg - e;
+      const bool lam1 = !zero && (isact || ((bL > 0.f) && (bL > -aL)));
+      s = lam1 ? 1.f : 0.f;
+      cnew = lam1 ? c0 : 0.f;
+      en = lam1 ? e : 0.f;
+      mgn = lam1 ? mg : 0.f;
+    }
+    // new row: constant, error, interval, interval error (L errors negated), scaled coefficients
+    v[0] = cnew;
+    v[1] = sgn * (en + gnext * mgn);
+    v[2] = ivn;
+    v[3] = sgn * (gnext * ivn);
+#pragma unroll
+    for (int c = 4; c < 16 * NT; ++c) v[c] *= s;
+    if (nl_act) {
+#pragma unroll
+      for (int q = 0; q < 4 * NT; ++q)
+        reinterpret_cast<float4*>(Trow)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---------------- reload in MFMA operand layout: next layer's B
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        A[ct][jt][0][i] = T[(4 * grp + i) * TS + ct * 16 + col];
+        A[ct][jt][1][i] = T[(16 + 4 * grp + i) * TS + ct * 16 + col];
+      }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int NT, int TM>
+__global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  // ---- stage every layer's W in MFMA operand order (zero padded) and b
+  for (int l = 0; l < net.n_layers; ++l) {
+    const int n_in = net.dims[l], n_out = net.dims[l + 1];
+    const int tin = (n_in + 15) >> 4, tout = (n_out + 15) >> 4;
+    const float* W = a.flat + net.w_off[l];
+    float* sw = smem + cfg.w_lds[l];
+    for (int e = tid; e < tout * tin * 256; e += FA_THREADS) {
+      const int i = e & 3, ln = (e >> 2) & 63, blk = e >> 8;
+      const int jt = blk / tin, t = blk - jt * tin;
+      const int k = 16 * t + 4 * (ln >> 4) + i, j = 16 * jt + (ln & 15);
+      sw[e] = (k < n_in && j < n_out) ? W[k * n_out + j] : 0.f;
+    }
+    for (int j = tid; j < n_out; j += FA_THREADS) smem[cfg.b_lds[l] + j] = a.flat[net.b_off[l] + j];
+  }
+  int* cdim_s = reinterpret_cast<int*>(smem + cfg.lds_floats - FA_SYM_MAXC);
+  for (int c = tid; c < FA_SYM_MAXC; c += FA_THREADS) cdim_s[c] = c < cfg.nc ? cfg.cdim[c] : -1;
+  __syncthreads();
+  const int lane = tid & 63;
+  const int grp = lane >> 4;
+  const int wave = tid >> 6;
+  const int nw = FA_THREADS / 64;
+  const int n0 = net.dims[0];
+  const int nc = cfg.nc;
+  const float g0 = net.g_gemm[0];
+  float* T = smem + cfg.lds_floats + wave * SymSlab<NT>::FLOATS;
+  float* bxv = T + SymSlab<NT>::TILE;             // [lo | hi | max(|lo|,|hi|)] per coefficient column
+  const int tin0 = (n0 + 15) >> 4;
+  // column layout: 0 constant, 1 error, 2 interval, 3 interval error, 4.. coefficients
+  int role[NT], cdm[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) {
+    const int c = ct * 16 + (lane & 15);
+    role[ct] = c == 0 ? 1 : c == 1 ? 2 : c == 2 ? 3 : c == 3 ? 4 : (c - 4 < nc ? 0 : 5);
+    cdm[ct] = (role[ct] == 0) ? cdim_s[c - 4] : -1;
+  }
+  for (int r0 = blockIdx.x * nw + wave; r0 < a.R; r0 += gridDim.x * nw) {
+    const int r = __builtin_amdgcn_readfirstlane(r0);
+    SymBox bx;
+    bx.a = &a;
+    bx.n0 = n0;
+    bx.node = a.V > 0 ? r / a.V : r;
+    bx.v = a.V > 0 ? r - bx.node * a.V : 0;
+    if (lane < FA_SYM_MAXC) {   // box values per column (0 on non-coefficient columns)
+      const int d = (lane >= 4 && lane - 4 < nc) ? cdim_s[lane - 4] : -1;
+      const float l0 = d >= 0 ? bx.lo(d) : 0.f, h0 = d >= 0 ? bx.hi(d) : 0.f;
+      bxv[lane] = l0;
+      bxv[FA_SYM_MAXC + lane] = h0;
+      bxv[2 * FA_SYM_MAXC + lane] = fmaxf(fabsf(l0), fabsf(h0));
+    }
+    float XA[NT][TM][2][4], XB[NT][TM][2][4];
+    // ---- layer-0 operands: identity forms (folded dims -> constant) + [hi | lo] interval rows;
+    //      L-block error columns negated
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      if (t >= tin0) break;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 16 * t + 4 * grp + i;
+        float xl = 0.f, xh = 0.f;
+        const bool kv = k < n0;
+        if (kv) {
+          xl = bx.lo(k);
+          xh = bx.hi(k);
+        }
+        const bool folded = kv && ((cfg.fold >> k) & 1ull);
+        const float m = fmaxf(fabsf(xl), fabsf(xh));
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          float vu = 0.f, vl = 0.f;
+          if (kv) {
+            switch (role[ct]) {
+              case 0: vu = vl = (!folded && cdm[ct] == k) ? 1.f : 0.f; break;
+              case 1: vu = vl = folded ? xl : 0.f; break;
+              case 2: vu = g0 * m; vl = -vu; break;
+              case 3: vu = xh; vl = xl; break;
+              case 4: vu = g0 * fabsf(xh); vl = -(g0 * fabsf(xl)); break;
+              default: break;
+            }
+          }
+          XA[ct][t][0][i] = vu;
+          XA[ct][t][1][i] = vl;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int l = 0; l < net.n_layers; ++l) {
+      if (l & 1)
+        fa_sym_layer<NT, TM>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, lane, XB, XA);
+      else
+        fa_sym_layer<NT, TM>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, lane, XA, XB);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+namespace {
+
+typedef void (*SymKernel)(NetDesc, BoundArgs, SymCfg);
+
+template <int NT, int TM>
+SymKernel sym_ptr() {
+  return fa_sym_kernel<NT, TM>;
+}
+
+SymKernel select_kernel(int NT, int TM) {
+  switch (NT) {
+    case 1:
+      if (TM <= 1) return sym_ptr<1, 1>();
+      if (TM <= 2) return sym_ptr<1, 2>();
+      if (TM <= 4) return sym_ptr<1, 4>();
+      if (TM <= 7) return sym_ptr<1, 7>();
+      return nullptr;
+    case 2:
+      if (TM <= 1) return sym_ptr<2, 1>();
+      if (TM <= 2) return sym_ptr<2, 2>();
+      if (TM <= 4) return sym_ptr<2, 4>();
+      return nullptr;
+    case 3:
+      if (TM <= 1) return sym_ptr<3, 1>();
+      if (TM <= 2) return sym_ptr<3, 2>();
+      return nullptr;
+    default:
+      return nullptr;
+  }
+}
+
+int device_cus() {
+  static int cus = 0;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  });
+  return cus;
+}
+
+}  // namespace
+
+// Launch the register-resident kernel if the shape fits; returns 1 if launched, 0 if the caller
+// must use the LDS-tiled kernel, <0 on a launch error.  fold_mask: input dims degenerate in
+// every row (PA dims under node-row expansion).
+extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long long fold_mask,
+                                 hipStream_t stream) {
+  if (!a.symbolic || a.R <= 0) return 0;
+  const int n0 = net.dims[0];
+  if (n0 > 64) return 0;
+  SymCfg cfg{};
+  cfg.fold = fold_mask;
+  int nc = 0;
+  for (int d = 0; d < n0; ++d)
+    if (!((fold_mask >> d) & 1ull)) {
+      if (nc >= FA_SYM_MAXC) return 0;
+      cfg.cdim[nc++] = d;
+    }
+  cfg.nc = nc;
+  const int cols = nc + 4;
+  const int NT = (cols + 15) / 16;
+  int TM = 1;
+  for (int l = 0; l < net.n_layers; ++l) TM = std::max(TM, (net.dims[l] + 15) / 16);
+  TM = std::max(TM, (net.dims[net.n_layers] + 15) / 16);
+  SymKernel k = select_kernel(NT, TM);
+  if (!k) return 0;
+  int off = 0;
+  for (int l = 0; l < net.n_layers; ++l) {
+    cfg.w_lds[l] = off;
+    off += ((net.dims[l] + 15) / 16) * ((net.dims[l + 1] + 15) / 16) * 256;
+  }
+  for (int l = 0; l < net.n_layers; ++l) {
+    cfg.b_lds[l] = off;
+    off += net.dims[l + 1];
+  }
+  off = ((off + 3) & ~3) + FA_SYM_MAXC;         // + column -> input-dim table (ints)
+  cfg.lds_floats = off;
+  int slab = 0;
+  switch (NT) {
+    case 1: slab = SymSlab<1>::FLOATS; break;
+    case 2: slab = SymSlab<2>::FLOATS; break;
+    default: slab = SymSlab<3>::FLOATS; break;
+  }
+  const size_t bytes = (size_t)(off + (FA_THREADS / 64) * slab) * sizeof(float);
+  if (bytes > 150 * 1024) return 0;
+  // per (kernel, LDS bytes): raise the dynamic-LDS limit once and cache the occupancy
+  static std::mutex mu;
+  static std::map<std::pair<const void*, size_t>, int> occ;
+  int per_cu = 0;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    const auto key = std::make_pair((const void*)k, bytes);
+    auto it = occ.find(key);
+    if (it == occ.end()) {
+      if (bytes > 64 * 1024) {
+        const hipError_t e =
+            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return -(int)e;
+      }
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, FA_THREADS, bytes) != hipSuccess || per_cu <= 0)
+        per_cu = 1;
+      occ[key] = per_cu;
+    } else {
+      per_cu = it->second;
+    }
+  }
+  const long long waves_needed = a.R;
+  long long blocks = (waves_needed + 3) / 4;
+  const long long cap = (long long)device_cus() * per_cu;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(FA_THREADS), bytes, stream, net, a, cfg);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 1 : -(int)e;
+}

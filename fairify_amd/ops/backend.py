@@ -59,13 +59,14 @@ class Backend:
 
     # ----------------------------------------------------------------------------- bounds
     def bounds(self, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic",
-               dead: Optional[torch.Tensor] = None, keep_layers: bool = False) -> ref.BoundResult:
+               dead: Optional[torch.Tensor] = None, keep_layers: bool = False, fold=()) -> ref.BoundResult:
+        """``fold``: dims degenerate (lo == hi) in every row — a HIP-kernel layout hint only."""
         lo = lo.to(self.dtype)
         hi = hi.to(self.dtype)
         if self.hip:
             from . import hip
 
-            return hip.bounds(self, lo, hi, mode=mode, dead=dead, keep_layers=keep_layers)
+            return hip.bounds(self, lo, hi, mode=mode, dead=dead, keep_layers=keep_layers, fold=fold)
         return ref.bounds(self.ws, self.bs, lo, hi, mode=mode, dead=dead, unit=self.unit, keep_layers=keep_layers)
 
     # ----------------------------------------------------------------------------- BaB node test

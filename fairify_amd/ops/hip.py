@@ -6,7 +6,7 @@ GPU), and passes raw pointers + ``torch.cuda.current_stream().cuda_stream``.
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Optional, Sequence
 
 import torch
 
@@ -37,6 +37,15 @@ def _c(t: torch.Tensor, dtype, shape=None, name="tensor") -> torch.Tensor:
     return t
 
 
+def _fold_mask(fold: Sequence[int], n0: int) -> int:
+    m = 0
+    for d in fold:
+        if not 0 <= int(d) < min(n0, 64):
+            raise ValueError(f"fold dim {d} out of range")
+        m |= 1 << int(d)
+    return m
+
+
 def _ptr(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else t.data_ptr()
 
@@ -64,7 +73,9 @@ def activation_counts(be, x: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------------------------
 def bounds(be, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic", dead: Optional[torch.Tensor] = None,
-           keep_layers: bool = False, G: int = 0) -> ref.BoundResult:
+           keep_layers: bool = False, G: int = 0, fold: Sequence[int] = ()) -> ref.BoundResult:
+    """``fold``: input dims with lo == hi in EVERY row (folded into the constant column of the
+    register-resident symbolic kernel; the caller guarantees degeneracy)."""
     R, n0 = lo.shape
     if n0 != be.n0:
         raise ValueError(f"box width {n0} != network input {be.n0}")
@@ -97,7 +108,7 @@ def bounds(be, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic", dead:
     if R:
         ext().bounds(_net(be), be.flat.data_ptr(), lo.data_ptr(), hi.data_ptr(), _ptr(d), R, sym,
                      out_lb.data_ptr(), out_ub.data_ptr(), *[_ptr(t) for t in forms],
-                     _ptr(lay_lb), _ptr(lay_ub), _ptr(dead_out), G, _stream(dev))
+                     _ptr(lay_lb), _ptr(lay_ub), _ptr(dead_out), G, _stream(dev), _fold_mask(fold, n0))
     if keep_layers:
         widths = be.mlp.widths
         offs = [0]

@@ -1,0 +1,128 @@
+"""Register-resident symbolic bound kernel (csrc/symbolic.hip) vs the PyTorch reference.
+
+Covers every template shape the dispatcher can pick (column tiles NT = 1..3, row tiles
+TM = 1..7), folded degenerate input dims (the node-row expansion of the BaB runtime), forced
+dead neurons, and soundness against brute-force enumeration.  Run on a real MI355X.
+"""
+import itertools
+
+import numpy as np
+import pytest
+import torch
+
+from fairify_amd.models.mlp import random_mlp
+from fairify_amd.ops.backend import Backend
+
+pytestmark = pytest.mark.gpu
+
+# (n0, hidden, folded dims): NT = ceil((n0 - |fold| + 4) / 16), TM = ceil(max width / 16)
+SHAPES = [
+    (13, [100, 100], (8,)),            # AC-4 with PA folded: NT=1, TM=7
+    (13, [64, 32, 16, 8, 4], (8,)),    # AC-7: NT=1, TM=4
+    (13, [50], (7,)),                  # AC-3: NT=1, TM=4
+    (13, [5] * 9, (8,)),               # AC-12: NT=1, TM=1
+    (13, [16, 8], ()),                 # no fold: NT=2, TM=1
+    (20, [50], (11,)),                 # GC-1: NT=2, TM=4
+    (16, [64, 16], (0,)),              # BM-1: NT=2, TM=4
+    (30, [16, 16, 16], (20,)),         # DF: NT=3, TM=2
+    (6, [16, 8], (3,)),                # CP-1: NT=1, TM=1
+    (12, [32, 32], (3, 4)),            # two folded dims
+]
+
+
+def _boxes(n0, R, seed, fold, span=6):
+    g = np.random.default_rng(seed)
+    lo = g.integers(-5, 20, size=(R, n0)).astype(np.float32)
+    hi = lo + g.integers(0, span, size=(R, n0)).astype(np.float32)
+    for d in fold:
+        hi[:, d] = lo[:, d]
+    return torch.from_numpy(lo), torch.from_numpy(hi)
+
+
+@pytest.mark.parametrize("n0,hidden,fold", SHAPES)
+def test_symbolic_kernel_matches_reference(cuda, n0, hidden, fold):
+    m = random_mlp(n0, hidden, seed=n0 + 3 * len(hidden), bias_scale=0.3)
+    lo, hi = _boxes(n0, 300, 5, fold)
+    cpu = Backend(m, "cpu")
+    gpu = Backend(m, cuda)
+    assert gpu.hip
+    rc = cpu.bounds(lo, hi, mode="symbolic", keep_layers=True)
+    rg = gpu.bounds(lo.to(cuda), hi.to(cuda), mode="symbolic", keep_layers=True, fold=fold)
+    scale = float(((rc.out_ub - rc.out_lb).abs() + rc.out_ub.abs()).max() + 1e-3)
+    assert torch.allclose(rg.out_lb.cpu(), rc.out_lb, rtol=1e-4, atol=1e-4 * scale)
+    assert torch.allclose(rg.out_ub.cpu(), rc.out_ub, rtol=1e-4, atol=1e-4 * scale)
+    for a, b in zip(rg.layer_ub, rc.layer_ub):
+        assert torch.allclose(a.cpu(), b, rtol=1e-4, atol=1e-3 * float(b.abs().max() + 1))
+    for a, b in zip(rg.layer_lb, rc.layer_lb):
+        assert torch.allclose(a.cpu(), b, rtol=1e-4, atol=1e-3 * float(b.abs().max() + 1))
+    # folded dims move into the constant: compare the forms evaluated on the folded value
+    keep = [d for d in range(n0) if d not in fold]
+    for C_g, c_g, C_c, c_c in ((rg.Lc, rg.L0, rc.Lc, rc.L0), (rg.Uc, rg.U0, rc.Uc, rc.U0)):
+        C_g, c_g = C_g.cpu(), c_g.cpu()
+        tol = 1e-4 * float(C_c.abs().max() + 1)
+        assert torch.allclose(C_g[:, keep], C_c[:, keep], rtol=1e-4, atol=tol)
+        if fold:
+            assert float(C_g[:, list(fold)].abs().max()) == 0.0
+        folded_c = c_c + (C_c[:, list(fold)] * lo[:, list(fold)]).sum(1) if fold else c_c
+        assert torch.allclose(c_g, folded_c, rtol=1e-4, atol=1e-4 * float(folded_c.abs().max() + 1))
+    # dead flags agree except on neurons whose bound is within rounding of 0
+    assert rg.dead is not None
+
+
+@pytest.mark.parametrize("n0,hidden,fold", [SHAPES[0], SHAPES[5], SHAPES[7]])
+def test_symbolic_kernel_forced_dead(cuda, n0, hidden, fold):
+    m = random_mlp(n0, hidden, seed=11, bias_scale=0.3)
+    lo, hi = _boxes(n0, 128, 7, fold)
+    dead = torch.rand(128, m.n_neurons - 1, generator=torch.Generator().manual_seed(0)) < 0.3
+    rc = Backend(m, "cpu").bounds(lo, hi, mode="symbolic", dead=dead)
+    rg = Backend(m, cuda).bounds(lo.to(cuda), hi.to(cuda), mode="symbolic", dead=dead.to(cuda), fold=fold)
+    scale = float(((rc.out_ub - rc.out_lb).abs() + rc.out_ub.abs()).max() + 1e-3)
+    assert torch.allclose(rg.out_lb.cpu(), rc.out_lb, rtol=1e-4, atol=1e-4 * scale)
+    assert torch.allclose(rg.out_ub.cpu(), rc.out_ub, rtol=1e-4, atol=1e-4 * scale)
+
+
+@pytest.mark.parametrize("n0,hidden", [(13, [100, 100]), (13, [16, 8]), (20, [50]), (6, [16, 8])])
+def test_symbolic_kernel_sound_vs_bruteforce(cuda, n0, hidden):
+    m = random_mlp(n0, hidden, seed=3, bias_scale=0.5)
+    g = np.random.default_rng(4)
+    be = Backend(m, cuda)
+    pa = n0 // 2
+    for _ in range(6):
+        lo = g.integers(0, 5, size=(1, n0))
+        hi = lo.copy()
+        dims = [d for d in g.choice(n0, size=min(n0, 5), replace=False) if d != pa]
+        hi[0, dims] += g.integers(1, 3, size=len(dims))
+        pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[0], hi[0])])))
+        z = m.logits(pts)
+        r = be.bounds(torch.tensor(lo, dtype=torch.float32, device=cuda),
+                      torch.tensor(hi, dtype=torch.float32, device=cuda), mode="symbolic", fold=(pa,))
+        assert float(r.out_lb[0]) <= z.min() + 1e-9
+        assert float(r.out_ub[0]) >= z.max() - 1e-9
+
+
+def test_native_bab_agrees_with_torch_bab_ac4(cuda):
+    """AC-4 (the TM=7 shape) through the native BaB runtime (node-row expansion, PA folded) vs
+    the tensor BaB (explicit rows, nothing folded): decided verdicts must agree."""
+    import os
+
+    from fairify_amd import presets
+    from fairify_amd.engine.bab import BaBConfig, BaBSolver
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.partition import processing_order
+
+    pre = presets.get("src/AC-sex")
+    grid = pre.grid()
+    q = pre.resolved()
+    ids = processing_order(grid, 0)[:192]
+    lo, hi = grid.decode(ids)
+    m = get_model("AC-4", weights="random", seed=0)
+    be = Backend(m, cuda)
+    nat = BaBSolver(be, q, BaBConfig(node_budget=1024)).solve(lo, hi, m)
+    os.environ["FAIRIFY_TORCH_BAB"] = "1"
+    try:
+        tor = BaBSolver(be, q, BaBConfig(node_budget=1024)).solve(lo, hi, m)
+    finally:
+        del os.environ["FAIRIFY_TORCH_BAB"]
+    decided = (nat.status != 0) & (tor.status != 0)
+    assert np.array_equal(nat.status[decided], tor.status[decided])
+    assert decided.mean() > 0.5
