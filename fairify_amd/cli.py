@@ -53,11 +53,11 @@ def cmd_verify(args):
                        hard_timeout=args.hard_timeout if args.hard_timeout is not None else pre.hard_timeout,
                        node_budget=args.node_budget, heuristic=not args.no_heuristic,
                        heuristic_p=args.heuristic_p if args.heuristic_p is not None else pre.heuristic_p,
-                       heuristic_node_budget=args.node_budget)
+                       heuristic_node_budget=args.node_budget, smt_backend=args.smt)
     models = args.models.split(",") if args.models else None
     run_preset(pre, models=models, weights=args.weights, out_dir=args.out, cfg=cfg, info=info,
                max_partitions=args.max_partitions, resume=args.resume, seed=args.seed,
-               accuracy=not args.no_accuracy)
+               accuracy=not args.no_accuracy, escalate=args.escalate)
     D.destroy(info)
 
 
@@ -156,6 +156,9 @@ def main(argv=None):
     v.add_argument("--seed", type=int, default=0)
     v.add_argument("--max-partitions", type=int, default=None)
     v.add_argument("--resume", action="store_true")
+    v.add_argument("--escalate", type=int, default=1,
+                   help="retry each round's UNKNOWN partitions on all ranks with N x the node budget")
+    v.add_argument("--smt", default="auto", help="host SMT back-end for the residue: auto | z3py | z3bin | none")
     v.add_argument("--no-accuracy", action="store_true")
     v.add_argument("--device", default=None)
     v.set_defaults(fn=cmd_verify)

@@ -29,6 +29,7 @@
 namespace py = pybind11;
 
 extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream);
+extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
 extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream);
 extern "C" int fa_mark_unknown_launch(const int* part, int n, int8_t* status, hipStream_t stream);
@@ -239,7 +240,9 @@ class BabRuntime {
         b.flat = flat_; b.lo = cand_.p; b.hi = cand_.p; b.R = 2 * nb; b.symbolic = 0;
         b.out_lb = pe_lb_.p; b.out_ub = pe_ub_.p;
         if (dead_part) { b.node_part = pe_part_.p; b.dead_part = (const uint8_t*)dead_part; }
-        ckl(fa_bounds_launch(net_, b, st), "bounds(points)");
+        const int prc = fa_point_try_launch(net_, b, st);
+        if (prc < 0) ckl(-prc, "points");
+        if (prc == 0) ckl(fa_bounds_launch(net_, b, st), "bounds(points)");
         SplitArgs sa{};
         sa.Nn = nb; sa.n0 = n0_; sa.relaxed = relaxed_ ? 1 : 0; sa.nra = relaxed_ ? (int)ra_.size() : 0;
         for (int k = 0; k < sa.nra; ++k) sa.ra_idx[k] = ra_[k];

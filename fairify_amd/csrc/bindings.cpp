@@ -17,6 +17,7 @@
 namespace py = pybind11;
 
 extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream);
+extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_forward_launch(const NetDesc& net, FwdArgs a, hipStream_t stream);
 extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream);
 extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
@@ -104,6 +105,21 @@ PYBIND11_MODULE(_C, m) {
      py::arg("symbolic"), py::arg("out_lb"), py::arg("out_ub"), py::arg("Lc"), py::arg("L0"), py::arg("Le"),
      py::arg("Uc"), py::arg("U0"), py::arg("Ue"), py::arg("layer_lb"), py::arg("layer_ub"), py::arg("dead_out"),
      py::arg("G"), py::arg("stream"), py::arg("fold") = 0ull);
+
+  m.def("point_bounds", [](const Net& net, uintptr_t flat, uintptr_t x, uintptr_t dead_in, int R, uintptr_t out_lb,
+                           uintptr_t out_ub, uintptr_t stream) {
+    BoundArgs a{};
+    a.flat = P<const float>(flat);
+    a.lo = P<const float>(x);
+    a.hi = P<const float>(x);
+    a.dead_in = P<const uint8_t>(dead_in);
+    a.R = R;
+    a.out_lb = P<float>(out_lb);
+    a.out_ub = P<float>(out_ub);
+    int rc = fa_point_try_launch(net.d, a, (hipStream_t)stream);
+    if (rc < 0) check(-rc, "point_bounds");
+    if (rc == 0) check(fa_bounds_launch(net.d, a, (hipStream_t)stream), "point_bounds(ibp)");
+  });
 
   m.def("forward", [](const Net& net, uintptr_t flat, uintptr_t x, int B, uintptr_t dead, uintptr_t out,
                       uintptr_t stream) {

@@ -98,13 +98,13 @@ class BaBSolver:
         return rlo.reshape(N * V, n), rhi.reshape(N * V, n)
 
     def _eval_pairs(self, x: torch.Tensor, xp: torch.Tensor, part: torch.Tensor):
-        """Rigorous interval evaluation of point pairs (IBP on degenerate boxes keeps exact zeros
-        exact): returns (certain_violation, possible_but_uncertain) masks."""
+        """Rigorous evaluation of point pairs (value + running error bound that keeps exact
+        zeros exact): returns (certain_violation, possible_but_uncertain) masks."""
         d = self.dead[part] if self.dead is not None else None
-        rx = self.be.bounds(x, x, mode="ibp", dead=d)
-        rp = self.be.bounds(xp, xp, mode="ibp", dead=d)
-        sure = ((rx.out_ub < 0) & (rp.out_lb > 0)) | ((rx.out_lb > 0) & (rp.out_ub < 0))
-        poss = ((rx.out_lb < 0) & (rp.out_ub > 0)) | ((rx.out_ub > 0) & (rp.out_lb < 0))
+        xlb, xub = self.be.point_bounds(x, d)
+        plb, pub = self.be.point_bounds(xp, d)
+        sure = ((xub < 0) & (plb > 0)) | ((xlb > 0) & (pub < 0))
+        poss = ((xlb < 0) & (pub > 0)) | ((xub > 0) & (plb < 0))
         return sure, poss & ~sure
 
     # --------------------------------------------------------------------------------------

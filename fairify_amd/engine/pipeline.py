@@ -29,6 +29,7 @@ from . import exact
 from . import prune as P_
 from .bab import SAT, UNKNOWN, UNSAT, RUNNING, VERDICT_NAMES, BaBConfig, BaBSolver, _pa_table
 from .sim import simulate
+from ..utils import faults
 from ..utils.timer import StageTimer
 
 
@@ -212,6 +213,12 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     cex_xp[newly_sat] = res.cex_xp[newly_sat]
     status = res.status.copy()
     nodes = res.nodes.copy()
+    forced = faults.forced_unknown(ids) & (stage == "bab")      # fault injection: solver "timeouts"
+    if forced.any():
+        status[forced] = UNKNOWN
+        stage[forced] = ""
+        cex_x[forced] = 0
+        cex_xp[forced] = 0
     sync()
     t_bab = time.time() - t0
 

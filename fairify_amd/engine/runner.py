@@ -28,6 +28,7 @@ from ..parallel import dist as D
 from ..partition import processing_order
 from ..presets import Preset
 from ..report.csv_report import PartitionCSV, format_table, table_v_row, write_summary
+from ..utils import faults
 from ..utils.timer import StageTimer
 from .pipeline import PartitionRecord, VerifyConfig, verify_chunk
 
@@ -83,10 +84,39 @@ def model_accuracy(mlp, suite: str, seed: int = 0) -> Optional[float]:
     return float(np.mean(mlp.predict(ds.X_test) == ds.y_test))
 
 
+def _residual_pass(be, mlp, q, grid, order, gathered: np.ndarray, cfg: VerifyConfig, escalate: int, acc,
+                   info: D.DistInfo, timer, budget: float) -> np.ndarray:
+    """Residual re-distribution ("work stealing"): the UNKNOWN partitions of the
+    round — wherever they fell — are re-sharded evenly over the ranks and retried with an
+    escalated node budget; every rank sees the same gathered rows, so the split needs no
+    extra coordination.  Returns the round's rows with the retried ones replaced."""
+    n0 = q.n
+    unk = np.nonzero(gathered[:, 2] == VCODE["unknown"])[0] if len(gathered) else np.zeros(0, np.int64)
+    if unk.size == 0 or budget <= 0:
+        return gathered
+    pos_all = gathered[unk, 0].astype(np.int64)
+    share = pos_all[info.rank::info.world]
+    c2 = replace(cfg, node_budget=cfg.node_budget * escalate,
+                 heuristic_node_budget=cfg.heuristic_node_budget * escalate)
+    if len(share):
+        recs = verify_chunk(be, mlp, q, grid, order[share], c2, orig_acc=acc, time_budget=budget, timer=timer)
+        packed = pack(recs, share, n0)
+    else:
+        packed = np.zeros((0, gathered.shape[1]))
+    retried = D.all_gather_rows(info, packed)
+    if len(retried):
+        idx = {int(p): k for k, p in enumerate(gathered[:, 0].astype(np.int64))}
+        for row in retried:
+            gathered[idx[int(row[0])]] = row
+    return gathered
+
+
 def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str = "zoo", out_dir: str = "results",
                cfg: Optional[VerifyConfig] = None, info: Optional[D.DistInfo] = None,
                max_partitions: Optional[int] = None, resume: bool = False, seed: int = 0,
-               accuracy: bool = True, verbose: bool = True) -> List[Dict]:
+               accuracy: bool = True, verbose: bool = True, escalate: int = 1) -> List[Dict]:
+    """``escalate`` > 1: every round's UNKNOWN partitions are re-distributed over all ranks and
+    retried with ``escalate`` x the node budget (residual work stealing)."""
     info = info or D.DistInfo()
     grid = preset.grid(seed=seed)
     q = preset.resolved()
@@ -127,6 +157,9 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             else:
                 packed = np.zeros((0, 4 + len(_SCALARS) + 1 + 2 * n0))
             gathered = D.all_gather_rows(info, packed)
+            if escalate > 1:
+                gathered = _residual_pass(be, mlp, q, grid, order, gathered, cfg, escalate, acc, info, timer,
+                                          cfg.hard_timeout - elapsed)
             if info.is_main:
                 gathered = gathered[np.argsort(gathered[:, 0], kind="stable")]
                 recs_all = unpack(gathered, n0, acc)
@@ -135,6 +168,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                 done = np.union1d(done, gathered[:, 0].astype(np.int64))
                 os.makedirs(os.path.dirname(state_path), exist_ok=True)
                 np.savez(state_path, done=done)
+            faults.maybe_crash(r + 1, info.rank)
         wall = D.all_reduce_max(info, time.time() - t0)
         if info.is_main:
             row = table_v_row(name, pa_name, all_records, len(grid), wall=wall)

@@ -69,6 +69,15 @@ class Backend:
             return hip.bounds(self, lo, hi, mode=mode, dead=dead, keep_layers=keep_layers, fold=fold)
         return ref.bounds(self.ws, self.bs, lo, hi, mode=mode, dead=dead, unit=self.unit, keep_layers=keep_layers)
 
+    def point_bounds(self, x: torch.Tensor, dead: Optional[torch.Tensor] = None):
+        """Rigorous [lb, ub] of the logit at points x [R, n0] (candidate-pair screening)."""
+        x = x.to(self.dtype)
+        if self.hip:
+            from . import hip
+
+            return hip.point_bounds(self, x, dead)
+        return ref.point_bounds(self.ws, self.bs, x, dead, unit=self.unit)
+
     # ----------------------------------------------------------------------------- BaB node test
     def pair_certify(self, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, shared, relaxed):
         if self.hip:

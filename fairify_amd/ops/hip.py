@@ -72,6 +72,21 @@ def activation_counts(be, x: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------------------------
+def point_bounds(be, x: torch.Tensor, dead: Optional[torch.Tensor] = None):
+    R = x.shape[0]
+    x2 = _c(x, torch.float32, (R, be.n0), "x")
+    lb = torch.empty(R, dtype=torch.float32, device=x.device)
+    ub = torch.empty(R, dtype=torch.float32, device=x.device)
+    d = None
+    if dead is not None:
+        d = _c(dead, torch.uint8, (R, be.n_hidden), "dead")
+    if R:
+        ext().point_bounds(_net(be), be.flat.data_ptr(), x2.data_ptr(), _ptr(d), R, lb.data_ptr(), ub.data_ptr(),
+                           _stream(x.device))
+    return lb, ub
+
+
+# ------------------------------------------------------------------------------------------------
 def bounds(be, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic", dead: Optional[torch.Tensor] = None,
            keep_layers: bool = False, G: int = 0, fold: Sequence[int] = ()) -> ref.BoundResult:
     """``fold``: input dims with lo == hi in EVERY row (folded into the constant column of the

@@ -141,6 +141,41 @@ def forward_error_bound(ws, bs, x: torch.Tensor, unit: float = FP32_UNIT) -> tor
     return e[..., 0] * (1 + 1e-6) + 1e-30
 
 
+def point_bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], x: torch.Tensor,
+                 dead: Optional[torch.Tensor] = None, unit: Optional[float] = None):
+    """Rigorous logit interval at points ``x`` [R, n0] (csrc/points.hip, same arithmetic).
+
+    Per layer: z = h W + b, d = (|W|^T (e + g|h|)) (1 + 2g) + g|b| + g1|z| bounds |v - z|;
+    ReLU keeps exact zeros (z + d <= 0 or forced dead -> 0 with error 0)."""
+    dt = x.dtype
+    if unit is None:
+        unit = FP64_UNIT if dt == torch.float64 else FP32_UNIT
+    gi = gamma(1, unit)
+    h = x
+    L = len(ws)
+    g0 = gamma(ws[0].shape[0] + 1, unit)
+    eo = g0 * h.abs()
+    off = 0
+    for l in range(L):
+        W = ws[l].to(dt)
+        b = bs[l].to(dt)
+        g = gamma(W.shape[0] + 1, unit)
+        z = h @ W + b
+        d = (eo @ W.abs()) * (1 + 2 * g) + g * b.abs() + gi * z.abs()
+        if l == L - 1:
+            return (z - d)[:, 0], (z + d)[:, 0]
+        n = W.shape[1]
+        zero = (z + d) <= 0
+        if dead is not None:
+            zero = zero | dead[:, off:off + n].bool()
+        off += n
+        h = torch.where(zero, torch.zeros_like(z), z.clamp(min=0))
+        e = torch.where(zero, torch.zeros_like(d), d)
+        gn = gamma(ws[l + 1].shape[0] + 1, unit)
+        eo = e + gn * h
+    raise AssertionError("unreachable")
+
+
 # ======================================================================================
 # Bound propagation (IBP and forward symbolic) with rigorous fp error terms
 # ======================================================================================

@@ -78,3 +78,24 @@ def test_rng_stream_is_stable():
     assert torch.all(a >= lo[:, None]) and torch.all(a <= hi[:, None])
     c = ref.sample_points_at(lo, hi, torch.tensor([3, 4]), torch.tensor([[7, 8], [0, 49]]), seed=11)
     assert torch.equal(c[0], a[0, 7:9]) and torch.equal(c[1, 1], a[1, 49])
+
+
+def test_point_bounds_contain_exact_logits():
+    """ops.reference.point_bounds (= csrc/points.hip arithmetic) brackets the exact logit and
+    keeps exact zeros: a neuron provably dead at the point contributes exactly nothing."""
+    import numpy as np
+    import torch
+
+    from fairify_amd.engine import exact
+    from fairify_amd.models.mlp import random_mlp
+    from fairify_amd.ops import reference as ref
+
+    for seed, (n0, hidden) in enumerate([(13, [100, 100]), (6, [16, 8]), (20, [64, 32, 16, 8, 4])]):
+        m = random_mlp(n0, hidden, seed=seed, bias_scale=0.5)
+        x = torch.randint(-3, 40, (500, n0)).float()
+        lb, ub = ref.point_bounds([torch.from_numpy(w) for w in m.weights], [torch.from_numpy(b) for b in m.biases], x)
+        z = m.logits(x.numpy().astype(np.float64))
+        assert np.all(lb.numpy() <= z) and np.all(z <= ub.numpy())
+        assert float((ub - lb).max()) < 1e-2 * (1 + float(np.abs(z).max()))
+        s = exact.exact_signs(m, x.numpy().astype(np.int64))
+        assert np.all(s[lb.numpy() > 0] == 1) and np.all(s[ub.numpy() < 0] == -1)

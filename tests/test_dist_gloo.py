@@ -78,3 +78,86 @@ def test_resume_skips_finished(tmp_path):
     assert len(csv_rows) == 40
     assert sorted(int(r["Partition_ID"]) for r in csv_rows) == list(range(1, 41))
     assert rows[0]["#P"] == 20          # this invocation verified only the new ones
+
+
+def _worker_escalate(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch
+
+    torch.set_num_threads(1)
+    from fairify_amd import presets
+    from fairify_amd.engine.pipeline import VerifyConfig
+    from fairify_amd.engine.runner import run_preset
+    from fairify_amd.parallel import dist as D
+
+    info = D.init("cpu")
+    cfg = VerifyConfig(sim_size=100, chunk=24, node_budget=16, heuristic=False)
+    run_preset(presets.get("src/AC-sex"), models=["AC-7"], weights="random", out_dir=out, cfg=cfg, info=info,
+               max_partitions=48, accuracy=False, verbose=False, escalate=8)
+    D.destroy(info)
+
+
+def test_residual_redistribution_matches_one_rank(tmp_path):
+    """UNKNOWN partitions re-sharded over the ranks and retried with 8x budget: the result
+    table is independent of the rank count."""
+    one, two = str(tmp_path / "one"), str(tmp_path / "two")
+    for w, out in ((1, one), (2, two)):
+        port = _free_port()
+        mp.spawn(_worker_escalate, args=(w, port, out), nprocs=w, join=True)
+    a = read_csv(os.path.join(one, "AC-7.csv"))
+    b = read_csv(os.path.join(two, "AC-7.csv"))
+    assert len(a) == len(b) == 48
+    for ra, rb in zip(a, b):
+        for col in ["Partition_ID", "Verification", "C1", "C2"]:
+            assert ra[col] == rb[col], col
+
+
+def test_injected_crash_then_resume_matches_uninterrupted(tmp_path, monkeypatch):
+    from fairify_amd import presets
+    from fairify_amd.engine.pipeline import VerifyConfig
+    from fairify_amd.engine.runner import run_preset
+    from fairify_amd.utils.faults import InjectedFault
+
+    pre = presets.get("src/GC-age")
+    cfg = VerifyConfig(sim_size=100, chunk=8, node_budget=256)
+    ref_dir, out = str(tmp_path / "ref"), str(tmp_path / "crash")
+    run_preset(pre, models=["GC-4"], out_dir=ref_dir, cfg=cfg, max_partitions=40, accuracy=False, verbose=False)
+    monkeypatch.setenv("FAIRIFY_FAULT_CRASH_AFTER", "2")
+    with pytest.raises(InjectedFault):
+        run_preset(pre, models=["GC-4"], out_dir=out, cfg=cfg, max_partitions=40, accuracy=False, verbose=False)
+    assert len(read_csv(os.path.join(out, "GC-4.csv"))) == 16      # two checkpointed rounds of 8
+    monkeypatch.delenv("FAIRIFY_FAULT_CRASH_AFTER")
+    run_preset(pre, models=["GC-4"], out_dir=out, cfg=cfg, max_partitions=40, resume=True, accuracy=False,
+               verbose=False)
+    a = read_csv(os.path.join(ref_dir, "GC-4.csv"))
+    b = read_csv(os.path.join(out, "GC-4.csv"))
+    assert len(a) == len(b) == 40
+    for ra, rb in zip(a, b):
+        for col in ["Partition_ID", "Verification", "SAT_count", "UNSAT_count", "UNK_count", "C1", "C2"]:
+            assert ra[col] == rb[col], col
+
+
+def test_forced_unknown_injection(monkeypatch):
+    from fairify_amd import presets
+    from fairify_amd.engine.pipeline import VerifyConfig, verify_chunk
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.ops.backend import Backend
+    from fairify_amd.partition import processing_order
+    from fairify_amd.utils.faults import forced_unknown
+
+    pre = presets.get("src/GC-age")
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, 0)[:32]
+    m = get_model("GC-4")
+    cfg = VerifyConfig(sim_size=100, node_budget=256, heuristic=False)
+    base = [r["verdict"] for r in verify_chunk(Backend(m), m, q, grid, ids, cfg)]
+    monkeypatch.setenv("FAIRIFY_FAULT_FORCE_UNKNOWN", "0.5")
+    mask = forced_unknown(ids)
+    assert 0 < mask.sum() < len(ids)
+    recs = verify_chunk(Backend(m), m, q, grid, ids, cfg)
+    for r, b, f in zip(recs, base, mask):
+        if f and r["stage"] != "sim" and b != "unknown":
+            assert r["verdict"] == "unknown"
+        elif not f:
+            assert r["verdict"] == b

@@ -126,3 +126,24 @@ def test_native_bab_agrees_with_torch_bab_ac4(cuda):
     decided = (nat.status != 0) & (tor.status != 0)
     assert np.array_equal(nat.status[decided], tor.status[decided])
     assert decided.mean() > 0.5
+
+
+@pytest.mark.parametrize("n0,hidden", [(13, [100, 100]), (13, [64, 32, 16, 8, 4]), (6, [16, 8]), (20, [50]),
+                                       (16, [150, 100, 50])])
+def test_point_kernel_matches_reference(cuda, n0, hidden):
+    from fairify_amd.ops import reference as ref
+
+    m = random_mlp(n0, hidden, seed=n0, bias_scale=0.5)
+    x = torch.randint(-3, 40, (1000, n0)).float()
+    dead = torch.rand(1000, m.n_neurons - 1, generator=torch.Generator().manual_seed(1)) < 0.2
+    be = Backend(m, cuda)
+    for d in (None, dead):
+        lb, ub = be.point_bounds(x.to(cuda), None if d is None else d.to(cuda))
+        rl, ru = ref.point_bounds([torch.from_numpy(w) for w in m.weights], [torch.from_numpy(b) for b in m.biases],
+                                  x, d)
+        z = ref.forward([torch.from_numpy(w).double() for w in m.weights],
+                        [torch.from_numpy(b).double() for b in m.biases], x.double(), d)
+        assert torch.all(lb.cpu().double() <= z) and torch.all(z <= ub.cpu().double())
+        if max(hidden) <= 112:      # wider nets fall back to interval propagation (different bound)
+            tol = 1e-4 * (1 + float(z.abs().max()))
+            assert torch.allclose(lb.cpu(), rl, atol=tol) and torch.allclose(ub.cpu(), ru, atol=tol)
