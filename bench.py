@@ -23,6 +23,7 @@ import contextlib
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -51,8 +52,11 @@ def main() -> None:
     ap.add_argument("--models", default=None, help="comma list (default: the preset's models)")
     ap.add_argument("--device", default=None)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--emulate-shard", default=None,
+                    help="r/N: run only rank r's shard of an N-rank job on this one process (diagnostics)")
     ap.add_argument("--profile", action="store_true", help="per-stage timing breakdown on stderr (syncs)")
-    ap.add_argument("--concurrency", type=int, default=0, help="models verified concurrently (HIP streams)")
+    ap.add_argument("--concurrency", type=int, default=0,
+                    help="host threads / HIP streams verifying (model, chunk) items concurrently (default 8 on GPU)")
     args = ap.parse_args()
 
     import torch
@@ -72,6 +76,9 @@ def main() -> None:
     q = pre.resolved()
     order = processing_order(grid, seed=args.seed)
     shard = order[info.rank::info.world]
+    if args.emulate_shard:
+        er, en = (int(v) for v in args.emulate_shard.split("/"))
+        shard = order[er::en]
     names = args.models.split(",") if args.models else list(pre.models)
     models = [get_model(n, weights=args.weights, seed=args.seed) for n in names]
     backends = [Backend(m, device=info.device) for m in models]
@@ -90,32 +97,37 @@ def main() -> None:
 
     timer = StageTimer(info.device, sync=args.profile)
 
-    conc = args.concurrency or (4 if info.device.type == "cuda" else 1)
-    streams = [torch.cuda.Stream(info.device) for _ in range(conc)] if info.device.type == "cuda" else []
+    # Work items = (model, chunk of its shard), largest models first; a pool of host threads,
+    # each driving its own HIP stream (the native BaB loop releases the GIL), so one chunk's
+    # host phases overlap other chunks' kernels and big models no longer serialise the tail.
+    conc = args.concurrency or (8 if info.device.type == "cuda" else 1)
+    tls = threading.local()
+
+    def thread_stream():
+        if info.device.type != "cuda":
+            return contextlib.nullcontext()
+        if getattr(tls, "stream", None) is None:
+            tls.stream = torch.cuda.Stream(info.device)
+        return torch.cuda.stream(tls.stream)
+
     pool = ThreadPoolExecutor(max_workers=conc) if conc > 1 else None
 
-    def one_model(k: int, step: int):
+    def one_item(k: int, ids: np.ndarray):
         m, be = models[k], backends[k]
-        ctx = torch.cuda.stream(streams[k % conc]) if streams else contextlib.nullcontext()
-        out = np.zeros(4)
-        with ctx:
-            for ids in chunks_for_step(step):
-                recs = verify_chunk(be, m, q, grid, ids, cfg, timer=timer)
-                v = [r["verdict"] for r in recs]
-                s, u = v.count("sat"), v.count("unsat")
-                out += np.array([len(v), s + u, s, u], dtype=np.float64)
-            if streams:
+        with thread_stream():
+            recs = verify_chunk(be, m, q, grid, ids, cfg, timer=timer)
+            if info.device.type == "cuda":
                 torch.cuda.current_stream(info.device).synchronize()
-        return out
+        v = [r["verdict"] for r in recs]
+        s_, u_ = v.count("sat"), v.count("unsat")
+        return np.array([len(v), s_ + u_, s_, u_], dtype=np.float64)
 
     def run_step(step: int):
-        # models run concurrently (one HIP stream each; the native BaB loop releases the GIL), so
-        # one model's host syncs overlap the other models' kernels
-        if pool is None:
-            return sum(one_model(k, step) for k in range(len(models)))
-        # largest models first to shorten the tail
         order_k = sorted(range(len(models)), key=lambda k: -models[k].n_neurons)
-        return sum(f.result() for f in [pool.submit(one_model, k, step) for k in order_k])
+        items = [(k, ids) for k in order_k for ids in chunks_for_step(step)]
+        if pool is None:
+            return sum(one_item(k, ids) for k, ids in items)
+        return sum(f.result() for f in [pool.submit(one_item, k, ids) for k, ids in items])
 
     sync = (lambda: torch.cuda.synchronize(info.device)) if info.device.type == "cuda" else (lambda: None)
     for w in range(args.warmup):

@@ -28,8 +28,9 @@ __device__ __forceinline__ void fa_tighten(const SplitArgs& a, float* lo, float*
   }
 }
 
-__global__ void __launch_bounds__(FA_THREADS) fa_split_kernel(SplitArgs a) {
-  const int n = blockIdx.x * FA_THREADS + threadIdx.x;
+#define FA_SPLIT_THREADS 64
+__global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a) {
+  const int n = blockIdx.x * FA_SPLIT_THREADS + threadIdx.x;
   if (n >= a.Nn) return;
   const int p = a.part[n];
   if (a.status[p] != ST_RUNNING || !a.open[n]) return;
@@ -198,7 +199,8 @@ __global__ void fa_set_status_kernel(const int* idx, int n, int8_t* status, int8
 extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream) {
   if (a.Nn <= 0) return 0;
   if (a.nra > FA_MAX_RA || a.npa > FA_CMAX_PA || a.n0 > 64) return -3;
-  hipLaunchKernelGGL(fa_split_kernel, dim3((a.Nn + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(fa_split_kernel, dim3((a.Nn + FA_SPLIT_THREADS - 1) / FA_SPLIT_THREADS), dim3(FA_SPLIT_THREADS),
+                     0, stream, a);
   return (int)hipGetLastError();
 }
 

@@ -100,16 +100,8 @@ class BabRuntime {
     ck(hipMemcpy(vals_i_.p, values_i.data(), values_i.size() * sizeof(int64_t), hipMemcpyHostToDevice), "cp");
     ck(hipMemcpy(pairs_.p, pairs.data(), pairs.size() * sizeof(int64_t), hipMemcpyHostToDevice), "cp");
     ck(hipMemcpy(shared_.p, shared.data(), shared.size(), hipMemcpyHostToDevice), "cp");
-    const size_t cn = (size_t)cap_ * n0_;
-    for (int i = 0; i < 2; ++i) {
-      lo_[i].ensure(cn);
-      hi_[i].ensure(cn);
-      part_[i].ensure(cap_);
-      if (relaxed_) {
-        plo_[i].ensure(cn);
-        phi_[i].ensure(cn);
-      }
-    }
+    // node pools grow on demand (geometrically) up to cap_ = the configured maximum
+    pool_[0] = pool_[1] = 0;
     const size_t R = (size_t)batch_ * V_;
     for (int s = 0; s < (relaxed_ ? 2 : 1); ++s) {
       Lc_[s].ensure(R * n0_);
@@ -159,6 +151,7 @@ class BabRuntime {
     for (int p = 0; p < P; ++p)
       if (hstatus[p] == 3) run.push_back(p);
     if ((int)run.size() > cap_) throw std::invalid_argument("more partitions than pool capacity");
+    ensure_pool(0, std::max<long long>((long long)run.size(), 1));
     std::vector<float> hl((size_t)run.size() * n0_), hh((size_t)run.size() * n0_);
     for (size_t i = 0; i < run.size(); ++i)
       for (int d = 0; d < n0_; ++d) {
@@ -202,6 +195,9 @@ class BabRuntime {
       while (m < FA_MAX_SPLIT && (long long)n_in << (m + 1) <= (long long)target) ++m;
       ck(hipMemsetAsync(counters_.p, 0, 2 * sizeof(int), st), "memset counters");
       const int nxt = cur ^ 1;
+      // every kernel of the previous level has finished (level-end sync), so the next pool
+      // can be re-allocated safely: children <= n_in * 2^m
+      ensure_pool(nxt, (long long)n_in << m);
       for (int s = 0; s < n_in; s += batch_) {
         const int nb = std::min(batch_, n_in - s);
         const float* blo = lo_[cur].p + (size_t)s * n0_;
@@ -257,7 +253,7 @@ class BabRuntime {
         sa.status = status_.p; sa.part_nodes = nodes_.p; sa.budget = budget; sa.m = m;
         sa.oxlo = lo_[nxt].p; sa.oxhi = hi_[nxt].p;
         sa.oxplo = relaxed_ ? plo_[nxt].p : nullptr; sa.oxphi = relaxed_ ? phi_[nxt].p : nullptr;
-        sa.opart = part_[nxt].p; sa.count_out = counters_.p; sa.cap = cap_;
+        sa.opart = part_[nxt].p; sa.count_out = counters_.p; sa.cap = pool_[nxt];
         sa.cand_buf = cand_buf_.p; sa.cand_part = cand_part_.p; sa.cand_count = counters_.p + 1;
         sa.cand_cap = cand_cap_;
         ckl(fa_split_launch(sa, st), "split");
@@ -266,7 +262,7 @@ class BabRuntime {
       ck(hipMemcpyAsync(hcount_, counters_.p, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "cp counters");
       ck(hipStreamSynchronize(st), "sync");
       total_nodes += n_in;
-      const int n_out = std::min(hcount_[0], cap_);
+      const int n_out = std::min(hcount_[0], pool_[nxt]);
       const int n_cand = std::min(hcount_[1], cand_cap_);
       ++levels;
       if (n_cand > 0) confirm_candidates(n_cand, confirm, got, cex_x, cex_xp, st);
@@ -324,6 +320,25 @@ class BabRuntime {
     ckl(fa_bounds_launch(net_, b, st), "bounds");
   }
 
+  // grow pool `i` to hold at least `need` nodes (clamped to cap_; over-capacity children make
+  // their partition UNKNOWN in the split kernel, which stays sound)
+  void ensure_pool(int i, long long need) {
+    const int want = (int)std::min<long long>(std::max<long long>(need, 1), cap_);
+    if (want <= pool_[i]) return;
+    int n = std::max(pool_[i], 1 << 16);
+    while (n < want) n = (n > cap_ / 2) ? cap_ : n * 2;
+    n = std::min(n, cap_);
+    const size_t cn = (size_t)n * n0_;
+    lo_[i].ensure(cn);
+    hi_[i].ensure(cn);
+    part_[i].ensure(n);
+    if (relaxed_) {
+      plo_[i].ensure(cn);
+      phi_[i].ensure(cn);
+    }
+    pool_[i] = n;
+  }
+
   // called WITHOUT the GIL; takes it only around the Python confirmation callback
   void confirm_candidates(int n_cand, py::object& confirm, std::vector<char>& got, std::vector<int64_t>& cex_x,
                           std::vector<int64_t>& cex_xp, hipStream_t st) {
@@ -367,6 +382,7 @@ class BabRuntime {
   std::vector<int> pa_, ra_;
   float tau_;
   int cap_, batch_, cand_cap_;
+  int pool_[2] = {0, 0};
   double unit_;
   int n0_ = 0, npa_ = 0, V_ = 0, Pp_ = 0, norient_ = 1;
   bool relaxed_ = false;

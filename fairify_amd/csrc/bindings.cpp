@@ -60,8 +60,15 @@ struct Net {
     d.g_conc = gamma_up(dims[0] + 1, unit);
     d.g_one = gamma_up(1, unit);
     n_params = off;
+    d.wperm_off = (off + 3) & ~3;
+    int wp = 0;
+    for (int l = 0; l < d.n_layers; ++l) wp += ((dims[l] + 15) / 16) * ((dims[l + 1] + 15) / 16) * 256;
+    for (int l = 0; l < d.n_layers; ++l) wp += dims[l + 1];
+    d.wperm_floats = (wp + 3) & ~3;
+    total_floats = d.wperm_off + d.wperm_floats;
   }
   int n_params;
+  int total_floats;
 };
 
 const NetDesc& fa_net_desc(py::handle h) { return h.cast<const Net&>().d; }
@@ -76,6 +83,8 @@ PYBIND11_MODULE(_C, m) {
   py::class_<Net>(m, "Net")
       .def(py::init<const std::vector<int>&, double>())
       .def_readonly("n_params", &Net::n_params)
+      .def_readonly("total_floats", &Net::total_floats)
+      .def_property_readonly("wperm_off", [](const Net& n) { return n.d.wperm_off; })
       .def_property_readonly("n_hidden", [](const Net& n) { return n.d.n_hidden; })
       .def_property_readonly("n_neurons", [](const Net& n) { return n.d.n_neurons; });
 

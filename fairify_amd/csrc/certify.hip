@@ -91,16 +91,20 @@ __device__ void fa_mags(const CertArgs& a, int n, const Form& A, const Form& B, 
   }
 }
 
-__global__ void __launch_bounds__(FA_THREADS) fa_pair_eval_kernel(CertArgs a) {
+// Register-resident evaluation: the pair's two folded forms and the node boxes are loaded once
+// (NM >= n0, compile-time), then g(t) is evaluated at t in {0, 1} and at every breakpoint of a
+// shared feature without touching memory again.  Same arithmetic as fa_g_at / fa_mags.
+#define FA_CERT_THREADS 64
+template <int NM>
+__global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_eval_kernel(CertArgs a) {
   const int Q = a.Pp * a.norient;
-  const int64_t idx = (int64_t)blockIdx.x * FA_THREADS + threadIdx.x;
+  const int64_t idx = (int64_t)blockIdx.x * FA_CERT_THREADS + threadIdx.x;
   if (idx >= (int64_t)a.Nn * Q) return;
   const int n = (int)(idx / Q);
   const int qq = (int)(idx % Q);
   const int o = qq / a.Pp, q = qq % a.Pp;
-  // exact-sign shortcut from the rigorous per-row bounds
-  {
-    const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+  const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+  {  // exact-sign shortcut from the rigorous per-row bounds
     const size_t ri = (size_t)n * a.V + vi, rj = (size_t)n * a.V + vj;
     const bool imp = (o == 0) ? (a.olb[ri] >= 0.f || a.oubp[rj] <= 0.f) : (a.oub[ri] <= 0.f || a.olbp[rj] >= 0.f);
     if (imp) {
@@ -112,30 +116,69 @@ __global__ void __launch_bounds__(FA_THREADS) fa_pair_eval_kernel(CertArgs a) {
   Form A, B;
   float sA, sB;
   fa_pair_forms(a, n, q, o, A, sA, B, sB);
-  float magA, magB;
-  fa_mags(a, n, A, B, magA, magB);
-  float best = fa_g_at(a, n, A, sA, B, sB, 0.f, magA, magB);
-  float bt = 0.f;
+  const int n0 = a.n0;
+  const float* xlp = a.xlo + (size_t)n * n0;
+  const float* xhp = a.xhi + (size_t)n * n0;
+  const float* plp = a.xplo + (size_t)n * n0;
+  const float* php = a.xphi + (size_t)n * n0;
+  float ca[NM], cb[NM], xl[NM], xh[NM], pl[NM], ph[NM];
+  bool sh[NM], un[NM];
+  float magA = fabsf(A.c0) + A.fmag, magB = fabsf(B.c0) + B.fmag;
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    const bool v = i < n0 && !fa_is_pa(a, i);
+    ca[i] = v ? sA * A.c[i] : 0.f;
+    cb[i] = v ? sB * B.c[i] : 0.f;
+    xl[i] = v ? xlp[i] : 0.f;
+    xh[i] = v ? xhp[i] : 0.f;
+    pl[i] = v ? plp[i] : 0.f;
+    ph[i] = v ? php[i] : 0.f;
+    sh[i] = v && a.shared[i];
+    un[i] = v && !a.shared[i];
+    magA += fabsf(ca[i]) * fmaxf(fabsf(xl[i]), fabsf(xh[i]));
+    magB += fabsf(cb[i]) * fmaxf(fabsf(pl[i]), fabsf(ph[i]));
+  }
+  const float A0 = sA * A.c0, B0 = sB * B.c0;
+  const float marg0 = 8.f * a.unit * (magA + magB);
+  auto g_at = [&](float t) {
+    float val = 0.f;
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const float cs = t * ca[i] + (1.f - t) * cb[i];
+      const float c1 = t * ca[i], c2 = (1.f - t) * cb[i];
+      const float vs = fmaxf(cs * xl[i], cs * xh[i]);
+      const float vu = fmaxf(c1 * xl[i], c1 * xh[i]) + fmaxf(c2 * pl[i], c2 * ph[i]);
+      val += sh[i] ? vs : (un[i] ? vu : 0.f);
+    }
+    return val + t * A0 + (1.f - t) * B0 + a.gmarg * (t * magA + (1.f - t) * magB) + marg0;
+  };
+  float best = g_at(0.f), bt = 0.f;
   {
-    const float g1 = fa_g_at(a, n, A, sA, B, sB, 1.f, magA, magB);
+    const float g1 = g_at(1.f);
     if (g1 < best) { best = g1; bt = 1.f; }
   }
-  for (int i = 0; i < a.n0; ++i) {
-    if (!a.shared[i] || fa_is_pa(a, i)) continue;
-    const float ai = sA * A.c[i], bi = sB * B.c[i];
+#pragma unroll 1
+  for (int i = 0; i < n0; ++i) {
+    // runtime loop over breakpoints; the register arrays are read through a select chain
+    float ai = 0.f, bi = 0.f;
+    bool s_i = false;
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      if (k == i) { ai = ca[k]; bi = cb[k]; s_i = sh[k]; }
+    if (!s_i) continue;
     const float den = ai - bi;
     if (den == 0.f) continue;
     const float t = -bi / den;
     if (!(t > 0.f && t < 1.f)) continue;
-    const float g = fa_g_at(a, n, A, sA, B, sB, t, magA, magB);
+    const float g = g_at(t);
     if (g < best) { best = g; bt = t; }
   }
   a.gmin[idx] = best;
   a.tstar[idx] = bt;
 }
 
-__global__ void __launch_bounds__(FA_THREADS) fa_pair_pick_kernel(CertArgs a) {
-  const int n = blockIdx.x * FA_THREADS + threadIdx.x;
+__global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_pick_kernel(CertArgs a) {
+  const int n = blockIdx.x * FA_CERT_THREADS + threadIdx.x;
   if (n >= a.Nn) return;
   const int Q = a.Pp * a.norient;
   float bg = -INFINITY;
@@ -220,8 +263,11 @@ extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream) {
   if (a.Nn <= 0) return 0;
   if (a.npa > FA_CMAX_PA || a.nra > FA_MAX_RA) return -3;
   const int64_t tot = (int64_t)a.Nn * a.Pp * a.norient;
-  hipLaunchKernelGGL(fa_pair_eval_kernel, dim3((unsigned)((tot + FA_THREADS - 1) / FA_THREADS)), dim3(FA_THREADS), 0,
-                     stream, a);
-  hipLaunchKernelGGL(fa_pair_pick_kernel, dim3((a.Nn + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, a);
+  const dim3 ge((unsigned)((tot + FA_CERT_THREADS - 1) / FA_CERT_THREADS));
+  if (a.n0 <= 16) hipLaunchKernelGGL(fa_pair_eval_kernel<16>, ge, dim3(FA_CERT_THREADS), 0, stream, a);
+  else if (a.n0 <= 32) hipLaunchKernelGGL(fa_pair_eval_kernel<32>, ge, dim3(FA_CERT_THREADS), 0, stream, a);
+  else return -4;
+  hipLaunchKernelGGL(fa_pair_pick_kernel, dim3((a.Nn + FA_CERT_THREADS - 1) / FA_CERT_THREADS),
+                     dim3(FA_CERT_THREADS), 0, stream, a);
   return (int)hipGetLastError();
 }

@@ -26,6 +26,11 @@ struct NetDesc {
   float g_conc;                       // gamma for concretisation sums (K = rows per form)
   float g_one;                        // gamma_1 (interval-row final addition)
   float g_fwd[FA_MAX_LAYERS];         // gamma for the plain forward (K = dims[l] + 1)
+  // float offset (multiple of 4) of the MFMA-operand-order copy of the weights in `flat`:
+  // per layer [jt][t][lane][i] = W[16t + 4(lane>>4) + i][16jt + (lane&15)] (zero padded), then
+  // every layer's bias; staged into LDS by the register-resident kernels with float4 copies
+  int wperm_off;
+  int wperm_floats;                   // size of that block (multiple of 4)
 };
 
 // lowbias32 (Wellons) — identical to ops/reference.py:hash32

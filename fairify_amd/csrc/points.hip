@@ -95,18 +95,11 @@ template <int TM>
 __global__ void __launch_bounds__(FA_THREADS) fa_point_kernel(NetDesc net, BoundArgs a, PointCfg cfg) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
-  for (int l = 0; l < net.n_layers; ++l) {
-    const int n_in = net.dims[l], n_out = net.dims[l + 1];
-    const int tin = (n_in + 15) >> 4, tout = (n_out + 15) >> 4;
-    const float* W = a.flat + net.w_off[l];
-    float* sw = smem + cfg.w_lds[l];
-    for (int e = tid; e < tout * tin * 256; e += FA_THREADS) {
-      const int i = e & 3, ln = (e >> 2) & 63, blk = e >> 8;
-      const int jt = blk / tin, t = blk - jt * tin;
-      const int k = 16 * t + 4 * (ln >> 4) + i, j = 16 * jt + (ln & 15);
-      sw[e] = (k < n_in && j < n_out) ? W[k * n_out + j] : 0.f;
-    }
-    for (int j = tid; j < n_out; j += FA_THREADS) smem[cfg.b_lds[l] + j] = a.flat[net.b_off[l] + j];
+  // ---- stage the MFMA-operand-order weights + biases (pre-permuted in `flat`) into LDS
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.flat + net.wperm_off);
+    float4* dst = reinterpret_cast<float4*>(smem);
+    for (int e = tid; e < (net.wperm_floats >> 2); e += FA_THREADS) dst[e] = src[e];
   }
   __syncthreads();
   const int lane = tid & 63, col = lane & 15, grp = lane >> 4;
@@ -180,6 +173,7 @@ extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t 
     cfg.b_lds[l] = off;
     off += net.dims[l + 1];
   }
+  if (((off + 3) & ~3) != net.wperm_floats) return -1;   // layout mismatch with the pre-permuted block
   const size_t bytes = (size_t)((off + 3) & ~3) * sizeof(float);
   if (bytes > 150 * 1024) return 0;
   static std::mutex mu;

@@ -255,19 +255,11 @@ template <int NT, int TM>
 __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
-  // ---- stage every layer's W in MFMA operand order (zero padded) and b
-  for (int l = 0; l < net.n_layers; ++l) {
-    const int n_in = net.dims[l], n_out = net.dims[l + 1];
-    const int tin = (n_in + 15) >> 4, tout = (n_out + 15) >> 4;
-    const float* W = a.flat + net.w_off[l];
-    float* sw = smem + cfg.w_lds[l];
-    for (int e = tid; e < tout * tin * 256; e += FA_THREADS) {
-      const int i = e & 3, ln = (e >> 2) & 63, blk = e >> 8;
-      const int jt = blk / tin, t = blk - jt * tin;
-      const int k = 16 * t + 4 * (ln >> 4) + i, j = 16 * jt + (ln & 15);
-      sw[e] = (k < n_in && j < n_out) ? W[k * n_out + j] : 0.f;
-    }
-    for (int j = tid; j < n_out; j += FA_THREADS) smem[cfg.b_lds[l] + j] = a.flat[net.b_off[l] + j];
+  // ---- stage the MFMA-operand-order weights + biases (pre-permuted in `flat`) into LDS
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.flat + net.wperm_off);
+    float4* dst = reinterpret_cast<float4*>(smem);
+    for (int e = tid; e < (net.wperm_floats >> 2); e += FA_THREADS) dst[e] = src[e];
   }
   int* cdim_s = reinterpret_cast<int*>(smem + cfg.lds_floats - FA_SYM_MAXC);
   for (int c = tid; c < FA_SYM_MAXC; c += FA_THREADS) cdim_s[c] = c < cfg.nc ? cfg.cdim[c] : -1;
@@ -428,7 +420,9 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
     cfg.b_lds[l] = off;
     off += net.dims[l + 1];
   }
-  off = ((off + 3) & ~3) + FA_SYM_MAXC;         // + column -> input-dim table (ints)
+  off = ((off + 3) & ~3);
+  if (off != net.wperm_floats) return -1;       // layout mismatch with the pre-permuted block
+  off += FA_SYM_MAXC;                           // + column -> input-dim table (ints)
   cfg.lds_floats = off;
   int slab = 0;
   switch (NT) {

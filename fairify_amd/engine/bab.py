@@ -19,6 +19,7 @@ the (tiny) SAT-candidate list.
 from __future__ import annotations
 
 import os
+import threading
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -40,7 +41,7 @@ VERDICT_NAMES = {UNKNOWN: "unknown", SAT: "sat", UNSAT: "unsat", RUNNING: "runni
 class BaBConfig:
     node_budget: int = 4096          # max node expansions per partition (soft-timeout analogue)
     batch_nodes: int = 32768         # nodes bounded per iteration
-    max_pool: int = 1 << 22          # live-node capacity (drop to UNKNOWN beyond)
+    max_pool: int = 1 << 24          # live-node capacity per runtime (grown lazily; UNKNOWN beyond)
     time_budget: float = 1e9         # wall-clock seconds for the whole call
     mode: str = "symbolic"
     cand_cap: int = 1 << 17          # candidate pairs confirmed per BFS level (native runtime)
@@ -287,7 +288,10 @@ class BaBSolver:
         from ..ops import ext
         from ..ops.hip import _net
 
-        key = (tuple(self.q.pa_idx), tuple(self.q.ra_idx), self.q.tau, values_np.tobytes(), pairs_np.tobytes())
+        # one runtime per (query, host thread): concurrent chunks of one model on several
+        # streams must not share device work buffers
+        key = (tuple(self.q.pa_idx), tuple(self.q.ra_idx), self.q.tau, values_np.tobytes(), pairs_np.tobytes(),
+               threading.get_ident())
         cache = self.be.__dict__.setdefault("_bab_rt", {})
         cap = max(self.cfg.max_pool, n_run)
         rt = cache.get(key)

@@ -28,6 +28,7 @@ from ..spec import ResolvedQuery
 from . import exact
 from . import prune as P_
 from .bab import SAT, UNKNOWN, UNSAT, RUNNING, VERDICT_NAMES, BaBConfig, BaBSolver, _pa_table
+from .falsify import residual_falsify
 from .sim import simulate
 from ..utils import faults
 from ..utils.timer import StageTimer
@@ -48,6 +49,9 @@ class VerifyConfig:
     bisect_pairs: int = 16
     bisect_steps: int = 12
     sound_prune_stats: bool = True       # compute B/S compression (reference parity columns)
+    residual_samples: int = 8192         # residual falsifier on BaB-UNKNOWN partitions (0 = off)
+    residual_starts: int = 16
+    residual_iters: int = 24
     smt_backend: str = "auto"            # host SMT on the BaB residue: auto | z3py | z3bin | none
     smt_workers: int = 8
     smt_timeout: Optional[float] = None  # per query; defaults to soft_timeout
@@ -221,6 +225,32 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
         cex_xp[forced] = 0
     sync()
     t_bab = time.time() - t0
+
+    # ---------------- stage 3a: residual falsifier (heavy sampling + lattice local search) on
+    # the partitions the BaB left UNKNOWN; candidates are confirmed exactly
+    if cfg.residual_samples > 0:
+        unk = np.nonzero(status == UNKNOWN)[0]
+        if unk.size:
+            t0 = time.time()
+            with tm("falsify"):
+                ut = torch.from_numpy(unk).to(dev)
+                fr = residual_falsify(be, q, lo[ut], hi[ut], pids[ut], values, pairs, cfg.seed,
+                                      n_samples=cfg.residual_samples, k_starts=cfg.residual_starts,
+                                      iters=cfg.residual_iters)
+                fnd = fr.found.cpu().numpy()
+                if fnd.any():
+                    fi = np.nonzero(fnd)[0]
+                    X = fr.wit_x[fi].cpu().numpy().round().astype(np.int64)
+                    XP = fr.wit_xp[fi].cpu().numpy().round().astype(np.int64)
+                    pi = unk[fi]
+                    ok = exact.check_pair_constraints(X, XP, lo_np[pi], hi_np[pi], q.pa_idx, q.ra_idx, q.tau)
+                    viol = exact.is_violation(mlp, X, XP) & ok
+                    hit = pi[viol]
+                    status[hit] = SAT
+                    cex_x[hit], cex_xp[hit] = X[viol], XP[viol]
+                    stage[hit] = "falsify"
+            sync()
+            t_bab += time.time() - t0
 
     # ---------------- stage 3b: host SMT on the sound-pruned subnetworks of the residue
     # (the reference's Z3 check, src/AC/Verify-AC.py:145-158; no-op without a back-end)

@@ -34,7 +34,7 @@ from .pipeline import PartitionRecord, VerifyConfig, verify_chunk
 
 VCODE = {"sat": 1, "unsat": 2, "unknown": 0}
 VNAME = {v: k for k, v in VCODE.items()}
-STAGES = ["", "sim", "bab", "heuristic", "smt"]
+STAGES = ["", "sim", "bab", "heuristic", "smt", "falsify"]
 _SCALARS = ["h_attempt", "h_success", "b_comp", "s_comp", "st_comp", "h_comp", "t_comp", "sv_time", "s_time",
             "hv_time", "h_time", "total_time", "c_check", "v_accurate", "pruned_acc", "nodes"]
 

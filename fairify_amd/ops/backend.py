@@ -18,6 +18,24 @@ from . import reference as ref
 from . import use_hip
 
 
+def mfma_weight_block(weights, biases) -> np.ndarray:
+    """Weights in MFMA operand order for the register-resident kernels (csrc/symbolic.hip,
+    csrc/points.hip): per layer [jt][t][lane][i] = W[16t + 4(lane>>4) + i][16jt + (lane&15)]
+    (zero padded to 16-neuron tiles), then every layer's bias; total padded to 4 floats."""
+    parts = []
+    lane = np.arange(64)
+    for W in weights:
+        n_in, n_out = W.shape
+        tin, tout = (n_in + 15) // 16, (n_out + 15) // 16
+        Wp = np.zeros((16 * tin, 16 * tout), np.float32)
+        Wp[:n_in, :n_out] = W
+        jt, t, ln, i = np.meshgrid(np.arange(tout), np.arange(tin), lane, np.arange(4), indexing="ij")
+        parts.append(Wp[16 * t + 4 * (ln >> 4) + i, 16 * jt + (ln & 15)].reshape(-1))
+    parts += [np.asarray(b, np.float32).reshape(-1) for b in biases]
+    out = np.concatenate(parts)
+    return np.concatenate([out, np.zeros((-len(out)) % 4, np.float32)])
+
+
 class Backend:
     def __init__(self, mlp: MLP, device="cpu", dtype=torch.float32):
         self.mlp = mlp
@@ -32,7 +50,9 @@ class Backend:
         self.hip = use_hip(probe) and dtype == torch.float32
         if self.hip:
             flat = np.concatenate([np.concatenate([w.reshape(-1), b]) for w, b in zip(mlp.weights, mlp.biases)])
-            self.flat = torch.from_numpy(flat.astype(np.float32)).to(self.device)
+            flat = np.concatenate([flat.astype(np.float32), np.zeros((-len(flat)) % 4, np.float32),
+                                   mfma_weight_block(mlp.weights, mlp.biases)])
+            self.flat = torch.from_numpy(flat).to(self.device)
             dims = [mlp.n_in] + mlp.widths
             self.dims = torch.tensor(dims, dtype=torch.int32)
         self.unit = ref.FP32_UNIT if dtype == torch.float32 else ref.FP64_UNIT

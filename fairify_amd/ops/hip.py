@@ -23,7 +23,7 @@ def _net(be):
     if n is None:
         dims = [be.mlp.n_in] + be.mlp.widths
         n = ext().Net(dims, be.unit)
-        assert n.n_params == be.flat.numel(), (n.n_params, be.flat.numel())
+        assert n.total_floats == be.flat.numel(), (n.total_floats, be.flat.numel())
         be._hipnet = n
     return n
 

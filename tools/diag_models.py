@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--no-heuristic", action="store_true")
     ap.add_argument("--weights", default="random")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--residual-samples", type=int, default=8192)
+    ap.add_argument("--residual-iters", type=int, default=24)
+    ap.add_argument("--residual-starts", type=int, default=16)
     args = ap.parse_args()
     import torch
 
@@ -49,7 +52,8 @@ def main():
     names = args.models.split(",") if args.models else list(pre.models)
     cfg = VerifyConfig(sim_size=pre.sim_size, chunk=args.chunk, node_budget=args.node_budget,
                        heuristic=not args.no_heuristic, heuristic_p=pre.heuristic_p,
-                       heuristic_node_budget=args.node_budget)
+                       heuristic_node_budget=args.node_budget, residual_samples=args.residual_samples,
+                       residual_iters=args.residual_iters, residual_starts=args.residual_starts)
     out = []
     for name in names:
         m = get_model(name, weights=args.weights, seed=0)
