@@ -48,6 +48,8 @@ def main() -> None:
                          "chunk: one step = --chunk partitions per model per rank (weak scaling)")
     ap.add_argument("--chunk", type=int, default=4096)
     ap.add_argument("--node-budget", type=int, default=2048)
+    ap.add_argument("--residual-samples", type=int, default=None, help="residual falsifier samples (0 = off)")
+    ap.add_argument("--residual-iters", type=int, default=None)
     ap.add_argument("--sim-size", type=int, default=None)
     ap.add_argument("--models", default=None, help="comma list (default: the preset's models)")
     ap.add_argument("--device", default=None)
@@ -86,6 +88,10 @@ def main() -> None:
                        soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
                        node_budget=args.node_budget, heuristic=True, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=args.node_budget)
+    if args.residual_samples is not None:
+        cfg.residual_samples = args.residual_samples
+    if args.residual_iters is not None:
+        cfg.residual_iters = args.residual_iters
 
     def chunks_for_step(step: int):
         if args.scope == "suite":

@@ -49,9 +49,9 @@ class VerifyConfig:
     bisect_pairs: int = 16
     bisect_steps: int = 12
     sound_prune_stats: bool = True       # compute B/S compression (reference parity columns)
-    residual_samples: int = 8192         # residual falsifier on BaB-UNKNOWN partitions (0 = off)
-    residual_starts: int = 16
-    residual_iters: int = 24
+    residual_samples: int = 2048         # residual falsifier on BaB-UNKNOWN partitions (0 = off)
+    residual_starts: int = 16            # local-search starts per partition
+    residual_iters: int = 12             # coordinate-ascent rounds
     smt_backend: str = "auto"            # host SMT on the BaB residue: auto | z3py | z3bin | none
     smt_workers: int = 8
     smt_timeout: Optional[float] = None  # per query; defaults to soft_timeout

@@ -44,8 +44,11 @@ def init(device_type: Optional[str] = None) -> DistInfo:
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        # one process per GPU; ranks beyond the visible devices (rehearsals with several ranks
+        # on one GPU) share devices round-robin
+        n_dev = max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local % n_dev)
+        dev = torch.device("cuda", local % n_dev)
     else:
         dev = torch.device("cpu")
     info = DistInfo(rank=rank, world=world, local_rank=local, device=dev)
@@ -53,6 +56,9 @@ def init(device_type: Optional[str] = None) -> DistInfo:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         backend = "nccl" if device_type == "cuda" else "gloo"
+        # FAIRIFY_DIST_BACKEND=gloo: host collectives (e.g. several ranks sharing one GPU, where
+        # RCCL refuses duplicate devices); the default on GPUs is nccl == RCCL over xGMI
+        backend = os.environ.get("FAIRIFY_DIST_BACKEND", backend)
         if backend == "nccl":
             dist.init_process_group(backend, rank=rank, world_size=world, device_id=dev)
         else:
@@ -65,14 +71,17 @@ def init(device_type: Optional[str] = None) -> DistInfo:
 
 def barrier(info: DistInfo) -> None:
     if info.initialized:
-        if info.device.type == "cuda":
+        if _dev(info).type == "cuda":
             dist.barrier(device_ids=[info.device.index])
         else:
             dist.barrier()
 
 
 def _dev(info: DistInfo) -> torch.device:
-    return info.device if info.device.type == "cuda" else torch.device("cpu")
+    """Device of collective buffers: the GPU for RCCL, the host for gloo."""
+    if info.device.type == "cuda" and dist.is_initialized() and dist.get_backend() == "nccl":
+        return info.device
+    return torch.device("cpu")
 
 
 def all_reduce_max(info: DistInfo, x: float) -> float:
