@@ -230,8 +230,10 @@ class BabRuntime {
         c.scores = scores_.p; c.leaf = leaf_.p;
         ckl(fa_certify_launch(c, st), "certify");
         // rigorous interval evaluation of the candidate pairs (rows: x then x')
-        ck(hipMemcpyAsync(pe_part_.p, bpart, nb * sizeof(int), hipMemcpyDeviceToDevice, st), "cp");
-        ck(hipMemcpyAsync(pe_part_.p + nb, bpart, nb * sizeof(int), hipMemcpyDeviceToDevice, st), "cp");
+        if (dead_part) {   // per-point partition ids only matter for the heuristic (masked) nets
+          ck(hipMemcpyAsync(pe_part_.p, bpart, nb * sizeof(int), hipMemcpyDeviceToDevice, st), "cp");
+          ck(hipMemcpyAsync(pe_part_.p + nb, bpart, nb * sizeof(int), hipMemcpyDeviceToDevice, st), "cp");
+        }
         BoundArgs b{};
         b.flat = flat_; b.lo = cand_.p; b.hi = cand_.p; b.R = 2 * nb; b.symbolic = 0;
         b.out_lb = pe_lb_.p; b.out_ub = pe_ub_.p;

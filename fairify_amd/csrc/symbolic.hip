@@ -26,6 +26,8 @@
 // LDS-tiled fa_bounds_kernel; see fa_sym_try_launch.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <map>
 #include <mutex>
@@ -73,17 +75,18 @@ struct SymSlab {
   static constexpr int FLOATS = (TILE + BOX + 3) & ~3;
 };
 
-template <int NT, int TM>
-__device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
-                                             const float* smem, float* T, const float* bxv, const int* cdim_s,
-                                             int l, int r,
-                                             int node, int lane, const float (&B)[NT][TM][2][4],
-                                             float (&A)[NT][TM][2][4]) {
+// Epilogue of one 16-neuron output tile (accumulators U, Lq of tile jt): spill to the wave's
+// LDS slab, one lane per (neuron, block) computes the rigorous bounds and the ReLU relaxation
+// once, the new form rows are reloaded in MFMA operand layout into (nu, nlo).  Returns false on
+// the last layer (outputs written, nothing to reload).
+template <int NT>
+__device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
+                                                const float* smem, float* T, const float* bxv, const int* cdim_s,
+                                                int l, int r, int node, int lane, int jt, const f32x4 (&U)[NT],
+                                                const f32x4 (&Lq)[NT], float (&nu)[NT][4], float (&nlo)[NT][4]) {
   constexpr int TS = SymSlab<NT>::TS;
   const int col = lane & 15, grp = lane >> 4;
-  const int n_in = net.dims[l], n_out = net.dims[l + 1];
-  const int tin = (n_in + 15) >> 4, tout = (n_out + 15) >> 4;
-  const float* sw = smem + cfg.w_lds[l];
+  const int n_out = net.dims[l + 1];
   const float* sb = smem + cfg.b_lds[l];
   const bool last = l == net.n_layers - 1;
   const float gg = net.g_gemm[l];
@@ -98,34 +101,6 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
   const bool nl_act = lane < 32;
   const int ob = (lane >> 4) & 1;
   float* Trow = T + (ob * 16 + col) * TS;
-#pragma unroll
-  for (int jt = 0; jt < TM; ++jt) {
-    if (jt >= tout) break;
-    f32x4 U[NT], Lq[NT];
-#pragma unroll
-    for (int ct = 0; ct < NT; ++ct) {
-      U[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-      Lq[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const float4* wq = reinterpret_cast<const float4*>(sw) + (size_t)jt * tin * 64 + lane;
-#pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      if (t >= tin) break;
-      const float4 w4 = wq[t * 64];
-      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
-          const float bu = B[ct][t][0][i], bl = B[ct][t][1][i];
-          U[ct] = fa_mfma4(wp, bu, U[ct]);
-          Lq[ct] = fa_mfma4(wp, bl, Lq[ct]);
-          U[ct] = fa_mfma4(wn, bl, U[ct]);
-          Lq[ct] = fa_mfma4(wn, bu, Lq[ct]);
-        }
-      }
-    }
     // ---------------- spill the tile: T[block][neuron][column]
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct)
@@ -188,7 +163,7 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
           if ((cfg.fold >> d) & 1ull) Cf[(size_t)r * n0 + d] = 0.f;
         for (int c = 0; c < nc; ++c) Cf[(size_t)r * n0 + cdim_s[c]] = Trow[4 + c];
       }
-      continue;
+      return false;
     }
     bool forced = false;
     if (nl_act && jv) {
@@ -244,10 +219,75 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
     for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        A[ct][jt][0][i] = T[(4 * grp + i) * TS + ct * 16 + col];
-        A[ct][jt][1][i] = T[(16 + 4 * grp + i) * TS + ct * 16 + col];
+        nu[ct][i] = T[(4 * grp + i) * TS + ct * 16 + col];
+        nlo[ct][i] = T[(16 + 4 * grp + i) * TS + ct * 16 + col];
       }
     __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
+template <int NT, int TM>
+__device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
+                                             const float* smem, float* T, const float* bxv, const int* cdim_s,
+                                             int l, int r,
+                                             int node, int lane, const float (&B)[NT][TM][2][4],
+                                             float (&A)[NT][TM][2][4]) {
+  constexpr int TS = SymSlab<NT>::TS;
+  const int col = lane & 15, grp = lane >> 4;
+  const int n_in = net.dims[l], n_out = net.dims[l + 1];
+  const int tin = (n_in + 15) >> 4, tout = (n_out + 15) >> 4;
+  const float* sw = smem + cfg.w_lds[l];
+  const float* sb = smem + cfg.b_lds[l];
+  const bool last = l == net.n_layers - 1;
+  const float gg = net.g_gemm[l];
+  const float gc = net.g_conc;
+  const float gi = net.g_one;
+  const float unit = net.unit;
+  const float gnext = last ? 0.f : net.g_gemm[l + 1];
+  const int noff = net.neuron_off[l];
+  const int nc = cfg.nc;
+  const int n0 = net.dims[0];
+  // neuron lane role in the epilogue: lanes 0-15 = U block, 16-31 = L block of neuron (lane & 15)
+  const bool nl_act = lane < 32;
+  const int ob = (lane >> 4) & 1;
+  float* Trow = T + (ob * 16 + col) * TS;
+#pragma unroll
+  for (int jt = 0; jt < TM; ++jt) {
+    if (jt >= tout) break;
+    f32x4 U[NT], Lq[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+      U[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      Lq[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const float4* wq = reinterpret_cast<const float4*>(sw) + (size_t)jt * tin * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      if (t >= tin) break;
+      const float4 w4 = wq[t * 64];
+      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          const float bu = B[ct][t][0][i], bl = B[ct][t][1][i];
+          U[ct] = fa_mfma4(wp, bu, U[ct]);
+          Lq[ct] = fa_mfma4(wp, bl, Lq[ct]);
+          U[ct] = fa_mfma4(wn, bl, U[ct]);
+          Lq[ct] = fa_mfma4(wn, bu, Lq[ct]);
+        }
+      }
+    }
+    float nu[NT][4], nlo[NT][4];
+    if (!fa_sym_epilogue<NT>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, lane, jt, U, Lq, nu, nlo)) continue;
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        A[ct][jt][0][i] = nu[ct][i];
+        A[ct][jt][1][i] = nlo[ct][i];
+      }
   }
 }
 
@@ -342,6 +382,11 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundAr
   }
 }
 
+// (A K-split variant with two waves per box -- each wave holding half of the K tiles and
+// exchanging partial sums through LDS, two workgroup barriers per layer -- reached 2 waves/SIMD
+// for the 100-wide layers but measured 10-75 % SLOWER than one wave per box on every AC shape:
+// profiles/experiments/r1_bounds_microbench_ksplit_2waves_per_box.json.  Not kept.)
+
 namespace {
 
 typedef void (*SymKernel)(NetDesc, BoundArgs, SymCfg);
@@ -430,8 +475,9 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
     case 2: slab = SymSlab<2>::FLOATS; break;
     default: slab = SymSlab<3>::FLOATS; break;
   }
+  const int threads = FA_THREADS, rows_per_block = FA_THREADS / 64;
   const size_t bytes = (size_t)(off + (FA_THREADS / 64) * slab) * sizeof(float);
-  if (bytes > 150 * 1024) return 0;
+  if (bytes > 160 * 1024) return 0;
   // per (kernel, LDS bytes): raise the dynamic-LDS limit once and cache the occupancy
   static std::mutex mu;
   static std::map<std::pair<const void*, size_t>, int> occ;
@@ -446,18 +492,17 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
             hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         if (e != hipSuccess) return -(int)e;
       }
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, FA_THREADS, bytes) != hipSuccess || per_cu <= 0)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, bytes) != hipSuccess || per_cu <= 0)
         per_cu = 1;
       occ[key] = per_cu;
     } else {
       per_cu = it->second;
     }
   }
-  const long long waves_needed = a.R;
-  long long blocks = (waves_needed + 3) / 4;
+  long long blocks = (a.R + rows_per_block - 1) / rows_per_block;
   const long long cap = (long long)device_cus() * per_cu;
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(FA_THREADS), bytes, stream, net, a, cfg);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(threads), bytes, stream, net, a, cfg);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 1 : -(int)e;
 }

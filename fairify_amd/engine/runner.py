@@ -43,6 +43,19 @@ def pack(records: List[dict], positions: np.ndarray, n0: int) -> np.ndarray:
     """Fixed-width float64 rows: [pos, grid_id, verdict, stage, scalars..., has_cex, c1[n0], c2[n0]]."""
     w = 4 + len(_SCALARS) + 1 + 2 * n0
     out = np.zeros((len(records), w), dtype=np.float64)
+    cols = getattr(records, "cols", None)
+    if cols is not None:            # columnar chunk result: vectorised packing
+        out[:, 0] = positions
+        out[:, 1] = cols["grid_id"]
+        out[:, 2] = np.select([cols["verdict"] == "sat", cols["verdict"] == "unsat"], [1, 2], 0)
+        out[:, 3] = [STAGES.index(x) if x in STAGES else 0 for x in cols["stage"]]
+        for k, name in enumerate(_SCALARS):
+            out[:, 4 + k] = cols[name]
+        sat = cols["verdict"] == "sat"
+        out[:, 4 + len(_SCALARS)] = sat
+        out[sat, 5 + len(_SCALARS):5 + len(_SCALARS) + n0] = cols["cex_x"][sat]
+        out[sat, 5 + len(_SCALARS) + n0:] = cols["cex_xp"][sat]
+        return out
     for i, (r, pos) in enumerate(zip(records, positions)):
         out[i, 0] = pos
         out[i, 1] = r["grid_id"]

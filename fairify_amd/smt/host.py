@@ -17,6 +17,7 @@ With no back-end available (this image ships no Z3) the stage is a no-op.
 """
 from __future__ import annotations
 
+import threading
 from concurrent.futures import Future, ThreadPoolExecutor
 from typing import Dict, List, Optional, Tuple
 
@@ -36,6 +37,22 @@ class HostSMT:
         self.fork_params = fork_params
         self.pool = ThreadPoolExecutor(max_workers=max(1, workers)) if self.backend != "none" else None
         self._streams: Dict[int, torch.cuda.Stream] = {}
+        self._cache: Dict[tuple, MLP] = {}
+        self._lock = threading.Lock()
+
+    def _pruned(self, mlp: MLP, dead: np.ndarray) -> MLP:
+        """Mask dedup: partitions of a chunk share few distinct dead-neuron masks,
+        so each distinct mask's pruned subnetwork is built once (keyed by the packed bits)."""
+        key = (id(mlp), np.packbits(dead).tobytes())
+        with self._lock:
+            net = self._cache.get(key)
+        if net is None:
+            net = pruned_network(mlp, dead)
+            with self._lock:
+                if len(self._cache) > 4096:
+                    self._cache.clear()
+                self._cache[key] = net
+        return net
 
     @property
     def active(self) -> bool:
@@ -72,7 +89,7 @@ class HostSMT:
         def work(k: int):
             if ev is not None:
                 ev.synchronize()
-            net = pruned_network(mlp, host[k].numpy().astype(bool))
+            net = self._pruned(mlp, host[k].numpy().astype(bool))
             script = encode_partition(net, q, lo[k], hi[k], timeout_s=self.timeout_s,
                                       fork_params=self.fork_params).text
             return solve(script, q.n, self.backend, self.timeout_s)

@@ -1,0 +1,14 @@
+#!/bin/bash
+set -eo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/ks
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || { tail -60 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python tools/bench_bounds.py --json-out gpurun_out/ks/bb_ksplit.json
+FAIRIFY_SYM_KSPLIT=0 timeout -k 10 300 python tools/bench_bounds.py --json-out gpurun_out/ks/bb_v3.json
+timeout -k 10 600 python bench.py --json-out gpurun_out/ks/bench.json
+FAIRIFY_SYM_KSPLIT=0 timeout -k 10 600 python bench.py --json-out gpurun_out/ks/bench_v3.json
+for v in "--bisect-steps 0" "--concurrency 12"; do
+  timeout -k 10 600 python bench.py $v --json-out gpurun_out/ks/x.json > /dev/null 2>&1
+  python -c "import json;r=json.load(open('gpurun_out/ks/x.json'));print('$v', r['value'], r['ms_per_step'], r['pct_verified'])"
+done
