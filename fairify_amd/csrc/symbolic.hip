@@ -70,7 +70,8 @@ struct SymBox {
 template <int NT>
 struct SymSlab {
   static constexpr int TS = 16 * NT + 4;                 // padded row stride (floats)
-  static constexpr int TILE = 2 * 16 * TS;
+  static constexpr int TILE1 = 2 * 16 * TS;             // one 16-neuron tile, U and L blocks
+  static constexpr int TILE = 2 * TILE1;                 // two tiles per epilogue pass
   static constexpr int BOX = 3 * FA_SYM_MAXC;
   static constexpr int FLOATS = (TILE + BOX + 3) & ~3;
 };
@@ -82,8 +83,9 @@ struct SymSlab {
 template <int NT>
 __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
                                                 const float* smem, float* T, const float* bxv, const int* cdim_s,
-                                                int l, int r, int node, int lane, int jt, const f32x4 (&U)[NT],
-                                                const f32x4 (&Lq)[NT], float (&nu)[NT][4], float (&nlo)[NT][4]) {
+                                                int l, int r, int node, int lane, int jt0, const f32x4 (&U)[2][NT],
+                                                const f32x4 (&Lq)[2][NT], float (&nu)[2][NT][4],
+                                                float (&nlo)[2][NT][4]) {
   constexpr int TS = SymSlab<NT>::TS;
   const int col = lane & 15, grp = lane >> 4;
   const int n_out = net.dims[l + 1];
@@ -97,20 +99,26 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
   const int noff = net.neuron_off[l];
   const int nc = cfg.nc;
   const int n0 = net.dims[0];
-  // neuron lane role in the epilogue: lanes 0-15 = U block, 16-31 = L block of neuron (lane & 15)
-  const bool nl_act = lane < 32;
+  // neuron lane role in the epilogue: tile jt0 + (lane >> 5); within it lanes 0-15 = U block,
+  // 16-31 = L block of neuron (lane & 15) -- all 64 lanes busy for two output tiles
+  const int tsub = lane >> 5;
+  const int jt = jt0 + tsub;
+  const int n_out_t = net.dims[l + 1];
+  const bool nl_act = 16 * jt < n_out_t;
   const int ob = (lane >> 4) & 1;
-  float* Trow = T + (ob * 16 + col) * TS;
-    // ---------------- spill the tile: T[block][neuron][column]
+  float* Trow = T + tsub * SymSlab<NT>::TILE1 + (ob * 16 + col) * TS;
+    // ---------------- spill both tiles: T[tile][block][neuron][column]
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct)
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        T[(4 * grp + i) * TS + ct * 16 + col] = U[ct][i];
-        T[(16 + 4 * grp + i) * TS + ct * 16 + col] = Lq[ct][i];
-      }
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          T[u * SymSlab<NT>::TILE1 + (4 * grp + i) * TS + ct * 16 + col] = U[u][ct][i];
+          T[u * SymSlab<NT>::TILE1 + (16 + 4 * grp + i) * TS + ct * 16 + col] = Lq[u][ct][i];
+        }
     __builtin_amdgcn_wave_barrier();
-    // ---------------- one lane per (neuron, block): bounds, relaxation, new form row
+    // ---------------- one lane per (tile, neuron, block): bounds, relaxation, new form row
     const int j = 16 * jt + col;
     const bool jv = j < n_out;
     float v[16 * NT];
@@ -214,14 +222,16 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
         reinterpret_cast<float4*>(Trow)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     }
     __builtin_amdgcn_wave_barrier();
-    // ---------------- reload in MFMA operand layout: next layer's B
+    // ---------------- reload both tiles in MFMA operand layout: next layer's B
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct)
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        nu[ct][i] = T[(4 * grp + i) * TS + ct * 16 + col];
-        nlo[ct][i] = T[(16 + 4 * grp + i) * TS + ct * 16 + col];
-      }
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          nu[u][ct][i] = T[u * SymSlab<NT>::TILE1 + (4 * grp + i) * TS + ct * 16 + col];
+          nlo[u][ct][i] = T[u * SymSlab<NT>::TILE1 + (16 + 4 * grp + i) * TS + ct * 16 + col];
+        }
     __builtin_amdgcn_wave_barrier();
     return true;
 }
@@ -252,42 +262,68 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
   const int ob = (lane >> 4) & 1;
   float* Trow = T + (ob * 16 + col) * TS;
 #pragma unroll
-  for (int jt = 0; jt < TM; ++jt) {
-    if (jt >= tout) break;
-    f32x4 U[NT], Lq[NT];
+  for (int jt0 = 0; jt0 < TM; jt0 += 2) {
+    if (jt0 >= tout) break;
+    f32x4 U[2][NT], Lq[2][NT];
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct) {
-      U[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-      Lq[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const float4* wq = reinterpret_cast<const float4*>(sw) + (size_t)jt * tin * 64 + lane;
+    for (int u = 0; u < 2; ++u) {
+      const int jt = jt0 + u;
 #pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      if (t >= tin) break;
-      const float4 w4 = wq[t * 64];
-      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+      for (int ct = 0; ct < NT; ++ct) {
+        U[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        Lq[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (jt >= tout || jt >= TM) continue;
+      const float4* wq = reinterpret_cast<const float4*>(sw) + (size_t)jt * tin * 64 + lane;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
+      for (int t = 0; t < TM; ++t) {
+        if (t >= tin) break;
+        const float4 w4 = wq[t * 64];
+        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
-          const float bu = B[ct][t][0][i], bl = B[ct][t][1][i];
-          U[ct] = fa_mfma4(wp, bu, U[ct]);
-          Lq[ct] = fa_mfma4(wp, bl, Lq[ct]);
-          U[ct] = fa_mfma4(wn, bl, U[ct]);
-          Lq[ct] = fa_mfma4(wn, bu, Lq[ct]);
+        for (int i = 0; i < 4; ++i) {
+          const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
+#pragma unroll
+          for (int ct = 0; ct < NT; ++ct) {
+            const float bu = B[ct][t][0][i], bl = B[ct][t][1][i];
+            U[u][ct] = fa_mfma4(wp, bu, U[u][ct]);
+            Lq[u][ct] = fa_mfma4(wp, bl, Lq[u][ct]);
+            U[u][ct] = fa_mfma4(wn, bl, U[u][ct]);
+            Lq[u][ct] = fa_mfma4(wn, bu, Lq[u][ct]);
+          }
         }
       }
     }
-    float nu[NT][4], nlo[NT][4];
-    if (!fa_sym_epilogue<NT>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, lane, jt, U, Lq, nu, nlo)) continue;
+    float nu[2][NT][4], nlo[2][NT][4];
+#ifdef FA_SYM_TIMING_NO_EPILOGUE
+    // timing-only build (tools/symk_timing.cpp): GEMM + operand hand-off without the epilogue
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct)
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        A[ct][jt][0][i] = nu[ct][i];
-        A[ct][jt][1][i] = nlo[ct][i];
-      }
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          nu[u][ct][i] = U[u][ct][i] * 1e-3f;
+          nlo[u][ct][i] = Lq[u][ct][i] * 1e-3f;
+        }
+    if (l == net.n_layers - 1) {
+      if (lane == 0) a.out_lb[r] = nu[0][0][0] + nlo[0][0][1];
+      continue;
+    }
+#else
+    if (!fa_sym_epilogue<NT>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, lane, jt0, U, Lq, nu, nlo)) continue;
+#endif
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (jt0 + u >= TM) break;
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          A[ct][jt0 + u][0][i] = nu[u][ct][i];
+          A[ct][jt0 + u][1][i] = nlo[u][ct][i];
+        }
+    }
   }
 }
 
