@@ -50,6 +50,7 @@ def main() -> None:
     ap.add_argument("--node-budget", type=int, default=2048)
     ap.add_argument("--residual-samples", type=int, default=None, help="residual falsifier samples (0 = off)")
     ap.add_argument("--residual-iters", type=int, default=None)
+    ap.add_argument("--bisect-steps", type=int, default=None, help="boundary-walk bisection steps (0 = off)")
     ap.add_argument("--sim-size", type=int, default=None)
     ap.add_argument("--models", default=None, help="comma list (default: the preset's models)")
     ap.add_argument("--device", default=None)
@@ -92,6 +93,8 @@ def main() -> None:
         cfg.residual_samples = args.residual_samples
     if args.residual_iters is not None:
         cfg.residual_iters = args.residual_iters
+    if args.bisect_steps is not None:
+        cfg.bisect_steps = args.bisect_steps
 
     def chunks_for_step(step: int):
         if args.scope == "suite":
@@ -124,9 +127,8 @@ def main() -> None:
             recs = verify_chunk(be, m, q, grid, ids, cfg, timer=timer)
             if info.device.type == "cuda":
                 torch.cuda.current_stream(info.device).synchronize()
-        v = [r["verdict"] for r in recs]
-        s_, u_ = v.count("sat"), v.count("unsat")
-        return np.array([len(v), s_ + u_, s_, u_], dtype=np.float64)
+        c = recs.counts()
+        return np.array([len(recs), c["sat"] + c["unsat"], c["sat"], c["unsat"]], dtype=np.float64)
 
     def run_step(step: int):
         order_k = sorted(range(len(models)), key=lambda k: -models[k].n_neurons)

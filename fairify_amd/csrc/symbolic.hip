@@ -261,6 +261,46 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
   const bool nl_act = lane < 32;
   const int ob = (lane >> 4) & 1;
   float* Trow = T + (ob * 16 + col) * TS;
+#ifndef FA_SYM_TIMING_NO_EPILOGUE
+  if (last && n_out == 1) {
+    // single-neuron output layer: a VALU dot product instead of a 16-row MFMA tile of which
+    // 15 rows are padding.  Lane (grp, col) sums its 4*tin neurons k = 16t + 4 grp + i for its
+    // form column; two cross-group butterflies finish the sum (any summation order stays within
+    // the layer's gamma_{2 n_in + 1} bound).  W[k][0] is lane (grp*16) of the permuted block.
+    float su[NT], sl[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) su[ct] = sl[ct] = 0.f;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      if (t >= tin) break;
+      const float4 w4 = reinterpret_cast<const float4*>(sw)[t * 64 + grp * 16];
+      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          su[ct] = fmaf(wp, B[ct][t][0][i], fmaf(wn, B[ct][t][1][i], su[ct]));
+          sl[ct] = fmaf(wp, B[ct][t][1][i], fmaf(wn, B[ct][t][0][i], sl[ct]));
+        }
+      }
+    }
+    f32x4 U[2][NT], Lq[2][NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+      su[ct] += __shfl_xor(su[ct], 16, 64);
+      sl[ct] += __shfl_xor(sl[ct], 16, 64);
+      su[ct] += __shfl_xor(su[ct], 32, 64);
+      sl[ct] += __shfl_xor(sl[ct], 32, 64);
+      U[0][ct] = f32x4{grp == 0 ? su[ct] : 0.f, 0.f, 0.f, 0.f};     // row 0 of tile 0 = neuron 0
+      Lq[0][ct] = f32x4{grp == 0 ? sl[ct] : 0.f, 0.f, 0.f, 0.f};
+      U[1][ct] = Lq[1][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float nu[2][NT][4], nlo[2][NT][4];
+    fa_sym_epilogue<NT>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, lane, 0, U, Lq, nu, nlo);
+    return;
+  }
+#endif
 #pragma unroll
   for (int jt0 = 0; jt0 < TM; jt0 += 2) {
     if (jt0 >= tout) break;

@@ -65,16 +65,23 @@ def main():
     for name in (args.models.split(",") if args.models else list(pre.models)):
         m = get_model(name, weights="random", seed=0)
         be = Backend(m, device=dev)
+        def run():
+            if args.mode == "points":
+                be.point_bounds(lo)
+            else:
+                be.bounds(lo, hi, mode=args.mode, fold=fold)
+
         for _ in range(3):
-            be.bounds(lo, hi, mode=args.mode, fold=fold)
+            run()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.iters):
-            be.bounds(lo, hi, mode=args.mode, fold=fold)
+            run()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.iters
         dims = [m.n_in] + m.widths
-        fl = gemm_flops(dims, args.rows, args.mode == "symbolic")
+        fl = gemm_flops(dims, args.rows, args.mode == "symbolic") if args.mode != "points" else \
+            sum(2 * 2 * dims[l] * dims[l + 1] for l in range(len(dims) - 1)) * args.rows
         row = dict(model=name, dims=dims, rows=args.rows, mode=args.mode, ms=round(dt * 1e3, 4),
                    mrows_per_s=round(args.rows / dt / 1e6, 3), gemm_tflops=round(fl / dt / 1e12, 2))
         out.append(row)
