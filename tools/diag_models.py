@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--residual-samples", type=int, default=8192)
     ap.add_argument("--residual-iters", type=int, default=24)
     ap.add_argument("--residual-starts", type=int, default=16)
+    ap.add_argument("--deep-budget", type=int, default=0,
+                    help="re-run the sound BaB with this node budget on the partitions left UNKNOWN "
+                         "before the heuristic stage, and report how they resolve")
     args = ap.parse_args()
     import torch
 
@@ -78,6 +81,22 @@ def main():
                    by_stage={k: int((st == k).sum()) for k in set(st.tolist())},
                    nodes_sum=int(nodes.sum()), nodes_p50=float(np.median(nodes)), nodes_p99=float(np.percentile(nodes, 99)),
                    nodes_max=int(nodes.max()), stages={k: round(t, 3) for k, t in tm.t.items()})
+        if args.deep_budget:
+            from fairify_amd.engine.bab import SAT, UNSAT, BaBConfig, BaBSolver
+
+            unk = np.nonzero((v == "unknown") | (st == "heuristic"))[0]
+            if unk.size:
+                ids = order[unk]
+                lo_np, hi_np = grid.decode(ids)
+                t1 = time.time()
+                res = BaBSolver(be, q, BaBConfig(node_budget=args.deep_budget)).solve(lo_np, hi_np, m)
+                if dev.type == "cuda":
+                    torch.cuda.synchronize()
+                row["deep"] = dict(budget=args.deep_budget, n=int(unk.size), wall=round(time.time() - t1, 3),
+                                   sat=int((res.status == SAT).sum()), unsat=int((res.status == UNSAT).sum()),
+                                   unk=int(((res.status != SAT) & (res.status != UNSAT)).sum()),
+                                   nodes_p50=float(np.median(res.nodes)),
+                                   nodes_p90=float(np.percentile(res.nodes, 90)))
         out.append(row)
         print(json.dumps(row), flush=True)
     if args.json_out:
