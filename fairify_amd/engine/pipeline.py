@@ -42,6 +42,8 @@ class VerifyConfig:
     soft_timeout: float = 100.0          # seconds (caps one chunk's BaB wall time)
     hard_timeout: float = 30 * 60.0      # seconds per model (checked after each chunk)
     node_budget: int = 4096              # BaB expansions per partition
+    escalate_budget: int = 0             # second sound BaB pass on the residue with this node
+                                         # budget (0 = off); runs after the residual falsifier
     batch_nodes: int = 32768
     heuristic: bool = True               # reference behaviour: heuristic retry on unknown
     heuristic_p: float = 5.0             # HEURISTIC_PRUNE_THRESHOLD
@@ -141,6 +143,7 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
                  timer: Optional[StageTimer] = None) -> List[dict]:
     """Decide one chunk of partitions; returns per-partition dicts (no cumulative columns)."""
     tm = timer if timer is not None else StageTimer()
+    t_start = time.time()
     dev = be.device
     lo_np, hi_np = grid.decode(ids)
     Pn, n = lo_np.shape
@@ -253,7 +256,29 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
             sync()
             t_bab += time.time() - t0
 
-    # ---------------- stage 3b: host SMT on the sound-pruned subnetworks of the residue
+    # ---------------- stage 3b: escalated sound BaB on what is still UNKNOWN (the cheap first
+    # pass decides the bulk; only the residue pays for the deep budget)
+    if cfg.escalate_budget > cfg.node_budget:
+        unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+        if unk.size:
+            t0 = time.time()
+            el = time.time() - t_start
+            esolver = BaBSolver(be, q, BaBConfig(node_budget=cfg.escalate_budget, batch_nodes=cfg.batch_nodes,
+                                                 time_budget=max(0.0, budget - el)), timer=tm)
+            with tm("bab.escalate"):
+                eres = esolver.solve(lo_np[unk], hi_np[unk], mlp)
+            dec_e = np.isin(eres.status, (SAT, UNSAT))
+            hit = unk[dec_e]
+            status[hit] = eres.status[dec_e]
+            stage[hit] = "bab"
+            es = eres.status == SAT
+            cex_x[unk[es]] = eres.cex_x[es]
+            cex_xp[unk[es]] = eres.cex_xp[es]
+            nodes[unk] += eres.nodes
+            sync()
+            t_bab += time.time() - t0
+
+    # ---------------- stage 3c: host SMT on the sound-pruned subnetworks of the residue
     # (the reference's Z3 check, src/AC/Verify-AC.py:145-158; no-op without a back-end)
     t_smt = 0.0
     if cfg.smt_backend != "none":

@@ -70,3 +70,28 @@ def test_exact_signs_fraction_fallback():
     m.biases = [np.zeros_like(b) for b in m.biases]
     x = np.zeros((2, 3), dtype=np.int64)
     assert np.all(exact.exact_signs(m, x) == 0)
+
+
+def test_escalated_pass_is_sound_and_monotone():
+    """The escalated second BaB pass (VerifyConfig.escalate_budget) only turns UNKNOWN into
+    verdicts that agree with brute force, and never decides fewer partitions than one pass."""
+    from fairify_amd.engine.pipeline import VerifyConfig, verify_chunk
+    from fairify_amd.partition import Grid
+
+    q = Query(pa=("f2",)).resolve(DOM)
+    grid = Grid.reference(DOM, 3)
+    ids = np.arange(len(grid))
+    lo_all, hi_all = grid.decode(ids)
+    for seed in range(3):
+        m = random_mlp(5, [8, 6], seed=500 + seed, bias_scale=0.3)
+        be = Backend(m)
+        base = dict(sim_size=16, node_budget=2, heuristic=False, residual_samples=0, smt_backend="none")
+        one = verify_chunk(be, m, q, grid, ids, VerifyConfig(**base))
+        two = verify_chunk(be, m, q, grid, ids, VerifyConfig(escalate_budget=10 ** 5, **base))
+        v1 = one.cols["verdict"]
+        v2 = two.cols["verdict"]
+        assert (v2 != "unknown").sum() >= (v1 != "unknown").sum()
+        assert np.all((v1 == "unknown") | (v1 == v2))
+        for k in np.nonzero(v2 != "unknown")[0]:
+            want = "sat" if brute(m, q, lo_all[k], hi_all[k]) == SAT else "unsat"
+            assert v2[k] == want, (seed, k)
