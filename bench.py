@@ -46,7 +46,9 @@ def main() -> None:
     ap.add_argument("--scope", default="suite", choices=["suite", "chunk"],
                     help="suite: one step = whole grid of every model (strong scaling); "
                          "chunk: one step = --chunk partitions per model per rank (weak scaling)")
-    ap.add_argument("--chunk", type=int, default=4096)
+    ap.add_argument("--chunk", type=int, default=4096,
+                    help="partitions per work item (big chunks win even for small per-rank shards: a 1/8 "
+                         "shard takes 1.02 s per step at 4096 vs 1.76 s at 667, profiles/scaling_emulation.md)")
     ap.add_argument("--node-budget", type=int, default=2048)
     ap.add_argument("--escalate-budget", type=int, default=8192,
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
@@ -106,12 +108,13 @@ def main() -> None:
         idx = (start + np.arange(args.chunk)) % max(1, n)
         return [shard[idx]]
 
+    conc = args.concurrency or (8 if info.device.type == "cuda" else 1)
+
     timer = StageTimer(info.device, sync=args.profile)
 
     # Work items = (model, chunk of its shard), largest models first; a pool of host threads,
     # each driving its own HIP stream (the native BaB loop releases the GIL), so one chunk's
     # host phases overlap other chunks' kernels and big models no longer serialise the tail.
-    conc = args.concurrency or (8 if info.device.type == "cuda" else 1)
     tls = threading.local()
 
     def thread_stream():
@@ -174,7 +177,7 @@ def main() -> None:
         "config": {"model": f"AC suite ({','.join(names)})", "global_batch": int(per_step), "seq_len": None,
                    "parallelism": f"dp{info.world}", "preset": args.preset, "grid_per_model": len(grid),
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
-                   "escalate_budget": cfg.escalate_budget},
+                   "escalate_budget": cfg.escalate_budget, "chunk": args.chunk},
         "pct_verified": round(100.0 * dec / max(1.0, att), 3),
         "partitions_per_s": round(att / dt_max, 3) if dt_max > 0 else 0.0,
         "sat": int(sat), "unsat": int(uns), "unknown": int(att - dec),

@@ -53,11 +53,13 @@ def cmd_verify(args):
                        hard_timeout=args.hard_timeout if args.hard_timeout is not None else pre.hard_timeout,
                        node_budget=args.node_budget, heuristic=not args.no_heuristic,
                        heuristic_p=args.heuristic_p if args.heuristic_p is not None else pre.heuristic_p,
-                       heuristic_node_budget=args.node_budget, smt_backend=args.smt)
+                       heuristic_node_budget=args.node_budget, smt_backend=args.smt,
+                       escalate_budget=args.escalate_budget)
     models = args.models.split(",") if args.models else None
     run_preset(pre, models=models, weights=args.weights, out_dir=args.out, cfg=cfg, info=info,
                max_partitions=args.max_partitions, resume=args.resume, seed=args.seed,
-               accuracy=not args.no_accuracy, escalate=args.escalate)
+               accuracy=not args.no_accuracy, escalate=args.escalate,
+               concurrency=args.concurrency or (4 if info.device.type == "cuda" else 1))
     D.destroy(info)
 
 
@@ -158,6 +160,10 @@ def main(argv=None):
     v.add_argument("--resume", action="store_true")
     v.add_argument("--escalate", type=int, default=1,
                    help="retry each round's UNKNOWN partitions on all ranks with N x the node budget")
+    v.add_argument("--escalate-budget", type=int, default=0,
+                   help="second sound BaB pass with this node budget on each chunk's UNKNOWN residue")
+    v.add_argument("--concurrency", type=int, default=0,
+                   help="chunks verified at once per rank, one HIP stream each (default 4 on GPU, 1 on CPU)")
     v.add_argument("--smt", default="auto", help="host SMT back-end for the residue: auto | z3py | z3bin | none")
     v.add_argument("--no-accuracy", action="store_true")
     v.add_argument("--device", default=None)

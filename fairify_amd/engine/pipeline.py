@@ -402,6 +402,57 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
         cex_x=cex_x, cex_xp=cex_xp), orig_acc)
 
 
+class StreamPool:
+    """Host threads, each driving its own HIP stream, that verify several chunks of one model
+    concurrently (the native BaB level loop releases the GIL, so one chunk's host phases and
+    synchronisations overlap the other chunks' kernels).  ``workers == 1`` runs inline."""
+
+    def __init__(self, device: torch.device, workers: int):
+        import threading
+        from concurrent.futures import ThreadPoolExecutor
+
+        self.device = torch.device(device)
+        self.workers = max(1, int(workers))
+        self._tls = threading.local()
+        self._pool = ThreadPoolExecutor(max_workers=self.workers) if self.workers > 1 else None
+
+    def _stream_ctx(self):
+        import contextlib
+
+        if self.device.type != "cuda":
+            return contextlib.nullcontext()
+        if getattr(self._tls, "stream", None) is None:
+            self._tls.stream = torch.cuda.Stream(self.device)
+        return torch.cuda.stream(self._tls.stream)
+
+    def run(self, fn: Callable, items: Sequence) -> List:
+        """``[fn(item) for item in items]``, concurrently, results in item order."""
+        def one(it):
+            with self._stream_ctx():
+                out = fn(it)
+                if self.device.type == "cuda":
+                    torch.cuda.current_stream(self.device).synchronize()
+            return out
+
+        if self._pool is None or len(items) <= 1:
+            return [one(it) for it in items]
+        return [f.result() for f in [self._pool.submit(one, it) for it in items]]
+
+    def close(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+
+
+def concat_records(parts: Sequence["ChunkRecords"]) -> "ChunkRecords":
+    parts = [p for p in parts if len(p)]
+    if not parts:
+        raise ValueError("no records")
+    if len(parts) == 1:
+        return parts[0]
+    cols = {k: np.concatenate([p.cols[k] for p in parts]) for k in parts[0].cols}
+    return ChunkRecords(cols, parts[0].orig_acc)
+
+
 class ChunkRecords(Sequence):
     """Per-partition results of one chunk, stored column-wise (numpy arrays).
 

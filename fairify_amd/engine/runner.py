@@ -30,7 +30,7 @@ from ..presets import Preset
 from ..report.csv_report import PartitionCSV, format_table, table_v_row, write_summary
 from ..utils import faults
 from ..utils.timer import StageTimer
-from .pipeline import PartitionRecord, VerifyConfig, verify_chunk
+from .pipeline import PartitionRecord, StreamPool, VerifyConfig, concat_records, verify_chunk
 
 VCODE = {"sat": 1, "unsat": 2, "unknown": 0}
 VNAME = {v: k for k, v in VCODE.items()}
@@ -127,9 +127,12 @@ def _residual_pass(be, mlp, q, grid, order, gathered: np.ndarray, cfg: VerifyCon
 def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str = "zoo", out_dir: str = "results",
                cfg: Optional[VerifyConfig] = None, info: Optional[D.DistInfo] = None,
                max_partitions: Optional[int] = None, resume: bool = False, seed: int = 0,
-               accuracy: bool = True, verbose: bool = True, escalate: int = 1) -> List[Dict]:
+               accuracy: bool = True, verbose: bool = True, escalate: int = 1,
+               concurrency: int = 1) -> List[Dict]:
     """``escalate`` > 1: every round's UNKNOWN partitions are re-distributed over all ranks and
-    retried with ``escalate`` x the node budget (residual work stealing)."""
+    retried with ``escalate`` x the node budget (residual work stealing).  ``concurrency`` > 1:
+    each rank verifies that many chunks of a round at once, one host thread + HIP stream each
+    (a round is then ``chunk x concurrency`` partitions per rank)."""
     info = info or D.DistInfo()
     grid = preset.grid(seed=seed)
     q = preset.resolved()
@@ -139,6 +142,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                               hard_timeout=preset.hard_timeout, heuristic_p=preset.heuristic_p, seed=seed)
     n0 = q.n
     rows_out: List[Dict] = []
+    streams = StreamPool(info.device, concurrency)
     pa_name = ",".join(a for a in preset.query.pa if preset.domain().has(a))
     for name in (models or list(preset.models)):
         mlp = get_model(name, weights=weights, seed=seed)
@@ -155,17 +159,20 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         all_records: List[PartitionRecord] = []
         timer = StageTimer(info.device)
         t0 = time.time()
-        rounds = int(np.ceil(len(todo) / max(1, cfg.chunk * info.world))) if len(todo) else 0
+        per_round = cfg.chunk * streams.workers
+        rounds = int(np.ceil(len(todo) / max(1, per_round * info.world))) if len(todo) else 0
         stopped = False
         for r in range(rounds):
             elapsed = D.all_reduce_max(info, time.time() - t0)
             if elapsed > cfg.hard_timeout:
                 stopped = True
                 break
-            pos = mine[r * cfg.chunk:(r + 1) * cfg.chunk]
+            pos = mine[r * per_round:(r + 1) * per_round]
             if len(pos):
-                recs = verify_chunk(be, mlp, q, grid, order[pos], cfg, orig_acc=acc,
-                                    time_budget=cfg.hard_timeout - elapsed, timer=timer)
+                subs = [pos[s:s + cfg.chunk] for s in range(0, len(pos), cfg.chunk)]
+                recs = concat_records(streams.run(
+                    lambda sp: verify_chunk(be, mlp, q, grid, order[sp], cfg, orig_acc=acc,
+                                            time_budget=cfg.hard_timeout - elapsed, timer=timer), subs))
                 packed = pack(recs, pos, n0)
             else:
                 packed = np.zeros((0, 4 + len(_SCALARS) + 1 + 2 * n0))
@@ -192,6 +199,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                 print(f"[{preset.name}] {name}: {row['SAT']} sat / {row['UNSAT']} unsat / {row['UNK']} unknown "
                       f"of {row['#P']} (grid {len(grid)}, cov {row['Cov%']}%) in {wall:.2f}s "
                       f"= {row['partitions_per_s']} partitions/s", flush=True)
+    streams.close()
     if info.is_main:
         write_summary(os.path.join(out_dir, "summary.json"), rows_out,
                       {"preset": preset.name, "weights": weights, "n_ranks": info.world, "seed": seed,
