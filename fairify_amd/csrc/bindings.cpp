@@ -73,6 +73,7 @@ struct Net {
 
 const NetDesc& fa_net_desc(py::handle h) { return h.cast<const Net&>().d; }
 void register_bab(py::module& m);
+void register_csv(py::module& m);
 
 static void check(int rc, const char* what) {
   if (rc != 0) throw std::runtime_error(std::string(what) + " launch failed, code " + std::to_string(rc));
@@ -209,4 +210,5 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("arch", []() { return std::string("gfx950"); });
   register_bab(m);
+  register_csv(m);
 }

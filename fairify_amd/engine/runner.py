@@ -17,6 +17,7 @@ from __future__ import annotations
 import json
 import os
 import time
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import asdict, replace
 from typing import Dict, List, Optional
 
@@ -27,7 +28,7 @@ from ..ops.backend import Backend
 from ..parallel import dist as D
 from ..partition import processing_order
 from ..presets import Preset
-from ..report.csv_report import PartitionCSV, format_table, table_v_row, write_summary
+from ..report.csv_report import PartitionCSV, format_table, table_v_row_columns, write_summary
 from ..utils import faults
 from ..utils.timer import StageTimer
 from .pipeline import PartitionRecord, StreamPool, VerifyConfig, concat_records, verify_chunk
@@ -82,6 +83,57 @@ def unpack(rows: np.ndarray, n0: int, orig_acc: Optional[float]) -> List[Partiti
         recs.append(PartitionRecord(partition_id=int(row[0]) + 1, grid_id=int(row[1]), verdict=VNAME[int(row[2])],
                                     stage=STAGES[int(row[3])], c1=c1, c2=c2, orig_acc=orig_acc, **kw))
     return recs
+
+
+def columns(rows: np.ndarray, n0: int) -> Dict[str, np.ndarray]:
+    """Packed rows -> the per-partition columns of :meth:`PartitionCSV.write_columns`."""
+    c = {name: rows[:, 4 + k] for k, name in enumerate(_SCALARS)}
+    c["partition_id"] = rows[:, 0].astype(np.int64) + 1
+    c["grid_id"] = rows[:, 1].astype(np.int64)
+    c["verdict"] = rows[:, 2].astype(np.int64)
+    c["stage"] = rows[:, 3].astype(np.int64)
+    c["has_cex"] = rows[:, 4 + len(_SCALARS)] > 0
+    c["c1"] = rows[:, 5 + len(_SCALARS):5 + len(_SCALARS) + n0].astype(np.float32)
+    c["c2"] = rows[:, 5 + len(_SCALARS) + n0:].astype(np.float32)
+    return c
+
+
+def csv_layout(n0: int) -> List[int]:
+    """Column indices of the packed rows for PartitionCSV.write_packed."""
+    ix = {name: 4 + k for k, name in enumerate(_SCALARS)}
+    return [0, 2, ix["h_attempt"], ix["h_success"], ix["b_comp"], ix["s_comp"], ix["st_comp"], ix["h_comp"],
+            ix["t_comp"], ix["sv_time"], ix["s_time"], ix["hv_time"], ix["h_time"], ix["total_time"],
+            ix["c_check"], ix["v_accurate"], ix["pruned_acc"], 4 + len(_SCALARS), 5 + len(_SCALARS),
+            5 + len(_SCALARS) + n0]
+
+
+def _save_done(path: str, done: np.ndarray) -> None:
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    tmp = path + ".tmp.npz"
+    np.savez(tmp, done_bits=np.packbits(done), total=np.int64(len(done)))
+    os.replace(tmp, path)
+
+
+def _load_done(path: str, total: int) -> np.ndarray:
+    z = np.load(path)
+    done = np.zeros(total, dtype=bool)
+    if "done_bits" in z:
+        bits = np.unpackbits(z["done_bits"])[:int(z["total"])].astype(bool)
+        done[:min(total, len(bits))] = bits[:total]
+    else:                                           # older checkpoints: list of positions
+        pos = z["done"].astype(np.int64)
+        done[pos[pos < total]] = True
+    return done
+
+
+def _write_round(writer: PartitionCSV, rows: np.ndarray, n0: int, acc, done: np.ndarray, state_path: str) -> None:
+    """CSV rows of one round, then the checkpoint that covers them (so resume never duplicates)."""
+    writer.write_packed(rows, csv_layout(n0), n0, acc)
+    done[rows[:, 0].astype(np.int64)] = True
+    _save_done(state_path, done)
+
+
+_TABLE_COLS = ("verdict", "h_attempt", "h_success", "st_comp", "h_comp", "sv_time", "hv_time", "total_time")
 
 
 def model_accuracy(mlp, suite: str, seed: int = 0) -> Optional[float]:
@@ -150,13 +202,17 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         acc = model_accuracy(mlp, preset.suite, seed) if accuracy else None
         state_path = os.path.join(out_dir, "state", f"{name}.npz")
         csv_path = os.path.join(out_dir, f"{name}.csv")
-        done = np.zeros(0, dtype=np.int64)
+        done = np.zeros(total, dtype=bool)            # checkpoint: finished processing positions
         if resume and os.path.exists(state_path):
-            done = np.load(state_path)["done"]
-        todo = np.setdiff1d(np.arange(total), done)
+            done = _load_done(state_path, total)
+        todo = np.nonzero(~done)[0]
         mine = todo[info.rank::info.world]
         writer = PartitionCSV(csv_path, resume=resume) if info.is_main else None
-        all_records: List[PartitionRecord] = []
+        # rank 0 formats/writes round r (native formatter, GIL released) and checkpoints it on a
+        # background thread while round r+1's chunks drive the GPU; one worker keeps the order
+        io = ThreadPoolExecutor(max_workers=1) if info.is_main else None
+        pending = []
+        table_cols: Dict[str, List[np.ndarray]] = {k: [] for k in _TABLE_COLS}
         timer = StageTimer(info.device)
         t0 = time.time()
         per_round = cfg.chunk * streams.workers
@@ -182,16 +238,25 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                                           cfg.hard_timeout - elapsed)
             if info.is_main:
                 gathered = gathered[np.argsort(gathered[:, 0], kind="stable")]
-                recs_all = unpack(gathered, n0, acc)
-                writer.write(recs_all)
-                all_records.extend(recs_all)
-                done = np.union1d(done, gathered[:, 0].astype(np.int64))
-                os.makedirs(os.path.dirname(state_path), exist_ok=True)
-                np.savez(state_path, done=done)
+                cols = columns(gathered, n0)
+                for k in _TABLE_COLS:
+                    table_cols[k].append(cols[k])
+                pending.append(io.submit(_write_round, writer, gathered, n0, acc, done, state_path))
+                if len(pending) > 2:
+                    pending.pop(0).result()
+            if faults.crash_after() >= 0:          # fault injection: crash only after a checkpoint
+                for f in pending:
+                    f.result()
+                pending.clear()
             faults.maybe_crash(r + 1, info.rank)
+        for f in pending:
+            f.result()
+        if io is not None:
+            io.shutdown(wait=True)
         wall = D.all_reduce_max(info, time.time() - t0)
         if info.is_main:
-            row = table_v_row(name, pa_name, all_records, len(grid), wall=wall)
+            tc = {k: (np.concatenate(v) if v else np.zeros(0)) for k, v in table_cols.items()}
+            row = table_v_row_columns(name, pa_name, grid_size=len(grid), wall=wall, **tc)
             row["stopped_by_hard_timeout"] = stopped
             row["original_acc"] = acc
             rows_out.append(row)

@@ -74,3 +74,39 @@ def test_capped_partitioner_reference_semantics():
     assert [a.index for a in g.attrs] == [1]          # only AGE is split (LIMIT_BAL too large)
     lo, hi = g.decode(np.arange(8))
     assert lo[:, 1].min() == 21 and hi[:, 1].max() == 79
+
+
+def test_columnar_csv_matches_record_writer(tmp_path):
+    """The runner's columnar CSV path writes exactly the bytes of the per-record writer."""
+    import numpy as np
+
+    from fairify_amd.engine.runner import _SCALARS, columns, csv_layout, unpack
+    from fairify_amd.report.csv_report import PartitionCSV
+
+    rng = np.random.default_rng(3)
+    n0, R = 13, 400
+    rows = np.zeros((R, 4 + len(_SCALARS) + 1 + 2 * n0))
+    rows[:, 0] = np.arange(R)
+    rows[:, 1] = rng.integers(0, 10 ** 6, R)
+    rows[:, 2] = rng.integers(0, 3, R)
+    rows[:, 4:4 + len(_SCALARS)] = rng.random((R, len(_SCALARS)))
+    rows[:, 4] = rng.integers(0, 2, R)
+    rows[:, 5] = rng.integers(0, 2, R)
+    sat = rows[:, 2] == 1
+    rows[sat, 4 + len(_SCALARS)] = 1
+    rows[sat, 5 + len(_SCALARS):] = rng.integers(0, 100, (int(sat.sum()), 2 * n0))
+    rows[sat, 5 + len(_SCALARS) + 3] = 20000.0        # exponent-notation array on some rows
+    rows[::7, 5 + len(_SCALARS) + 1] = -3.0
+    rows[::5, 4 + 7] = 1e-7                          # repr in exponent notation
+    rows[::6, 4 + 8] = 123456.0                      # integral float -> "123456.0"
+    rows[::13, 4 + 2] = -0.0
+    for acc in (None, 0.8123456):
+        a, b, c, d = (tmp_path / f"{k}{acc}.csv" for k in "abcd")
+        wa, wb, wc, wd = PartitionCSV(str(a)), PartitionCSV(str(b)), PartitionCSV(str(c)), PartitionCSV(str(d))
+        for half in (rows[:150], rows[150:]):
+            wa.write(unpack(half, n0, acc))
+            wb.write_columns(columns(half, n0), acc)
+            wc.write_packed(half, csv_layout(n0), n0, acc)                 # native formatter
+            wd.write_packed(half, csv_layout(n0), n0, acc, native=False)
+        assert a.read_bytes() == b.read_bytes() == c.read_bytes() == d.read_bytes()
+        assert wa.counts == wb.counts == wc.counts == wd.counts
