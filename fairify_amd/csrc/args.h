@@ -124,6 +124,8 @@ struct SplitArgs {
   const uint8_t* shared;
   int8_t* status;                         // [P]
   int* part_nodes;                        // [P]
+  int* part_open;                         // [P] open nodes left unexpanded when the partition
+                                          //     stopped (budget / capacity), or nullptr
   int budget;
   int m;                                  // requested split dims (children = 2^m)
   float *oxlo, *oxhi, *oxplo, *oxphi;     // output pool

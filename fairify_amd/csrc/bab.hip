@@ -28,12 +28,23 @@ __device__ __forceinline__ void fa_tighten(const SplitArgs& a, float* lo, float*
   }
 }
 
+// budget / capacity exhausted: the partition ends UNKNOWN with this node left open
+__device__ __forceinline__ void fa_stop(const SplitArgs& a, int p) {
+  a.status[p] = ST_UNKNOWN;
+  if (a.part_open) atomicAdd(&a.part_open[p], 1);
+}
+
 #define FA_SPLIT_THREADS 64
 __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a) {
   const int n = blockIdx.x * FA_SPLIT_THREADS + threadIdx.x;
   if (n >= a.Nn) return;
   const int p = a.part[n];
-  if (a.status[p] != ST_RUNNING || !a.open[n]) return;
+  if (!a.open[n]) return;
+  if (a.status[p] != ST_RUNNING) {
+    // open node of a partition that already ran out of budget: part of the frontier it left
+    if (a.part_open && a.status[p] == ST_UNKNOWN && !a.leaf[n]) atomicAdd(&a.part_open[p], 1);
+    return;
+  }
   const int n0 = a.n0;
   const float* xl = a.xlo + (size_t)n * n0;
   const float* xh = a.xhi + (size_t)n * n0;
@@ -101,9 +112,9 @@ __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a)
   const int k = 1 << m;
   if (!a.relaxed) {  // fast path: every child feasible, boxes written on the fly
     const int old = atomicAdd(&a.part_nodes[p], k);
-    if (old + k > a.budget) { a.status[p] = ST_UNKNOWN; return; }
+    if (old + k > a.budget) { fa_stop(a, p); return; }
     const int off = atomicAdd(a.count_out, k);
-    if (off + k > a.cap) { a.status[p] = ST_UNKNOWN; return; }
+    if (off + k > a.cap) { fa_stop(a, p); return; }
     for (int c = 0; c < k; ++c) {
       float* ol = a.oxlo + (size_t)(off + c) * n0;
       float* oh = a.oxhi + (size_t)(off + c) * n0;
@@ -150,9 +161,9 @@ __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a)
   }
   if (feasible == 0) return;
   const int old = atomicAdd(&a.part_nodes[p], feasible);
-  if (old + feasible > a.budget) { a.status[p] = ST_UNKNOWN; return; }
+  if (old + feasible > a.budget) { fa_stop(a, p); return; }
   const int off = atomicAdd(a.count_out, feasible);
-  if (off + feasible > a.cap) { a.status[p] = ST_UNKNOWN; return; }
+  if (off + feasible > a.cap) { fa_stop(a, p); return; }
   int w = off;
   for (int c = 0; c < k; ++c) {
     if (!((fmask >> c) & 1ull)) continue;

@@ -143,9 +143,11 @@ class BabRuntime {
       throw std::invalid_argument("solve: shape mismatch");
     status_.ensure(P);
     nodes_.ensure(P);
+    open_left_.ensure(P);
     std::vector<int8_t> hstatus(status0.data(), status0.data() + P);
     ck(hipMemcpyAsync(status_.p, hstatus.data(), P, hipMemcpyHostToDevice, st), "cp status");
     ck(hipMemsetAsync(nodes_.p, 0, P * sizeof(int), st), "memset nodes");
+    ck(hipMemsetAsync(open_left_.p, 0, P * sizeof(int), st), "memset open_left");
     // initial pool: running partitions
     std::vector<int> run;
     for (int p = 0; p < P; ++p)
@@ -252,7 +254,7 @@ class BabRuntime {
         sa.pairs = pairs_.p; sa.values = vals_i_.p; sa.npa = npa_;
         for (int k = 0; k < npa_; ++k) sa.pa_idx[k] = pa_[k];
         sa.shared = shared_.p;
-        sa.status = status_.p; sa.part_nodes = nodes_.p; sa.budget = budget; sa.m = m;
+        sa.status = status_.p; sa.part_nodes = nodes_.p; sa.part_open = open_left_.p; sa.budget = budget; sa.m = m;
         sa.oxlo = lo_[nxt].p; sa.oxhi = hi_[nxt].p;
         sa.oxplo = relaxed_ ? plo_[nxt].p : nullptr; sa.oxphi = relaxed_ ? phi_[nxt].p : nullptr;
         sa.opart = part_[nxt].p; sa.count_out = counters_.p; sa.cap = pool_[nxt];
@@ -273,18 +275,20 @@ class BabRuntime {
     }
     }
     std::vector<int8_t> sout(P);
-    std::vector<int> nout(P);
+    std::vector<int> nout(P), oout(P);
     ck(hipMemcpyAsync(sout.data(), status_.p, P, hipMemcpyDeviceToHost, st), "cp");
     ck(hipMemcpyAsync(nout.data(), nodes_.p, P * sizeof(int), hipMemcpyDeviceToHost, st), "cp");
+    ck(hipMemcpyAsync(oout.data(), open_left_.p, P * sizeof(int), hipMemcpyDeviceToHost, st), "cp");
     ck(hipStreamSynchronize(st), "sync");
     py::array_t<int8_t> status_out(P);
-    py::array_t<int64_t> nodes_out(P);
+    py::array_t<int64_t> nodes_out(P), open_out(P);
     for (int p = 0; p < P; ++p) {
       int8_t v = sout[p];
       if (got[p]) v = 1;
       else if (v == 3) v = timed_out ? 0 : 2;   // all nodes closed => UNSAT
       status_out.mutable_data()[p] = v;
       nodes_out.mutable_data()[p] = nout[p];
+      open_out.mutable_data()[p] = (v == 0) ? oout[p] : 0;
     }
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     py::dict stats;
@@ -296,6 +300,7 @@ class BabRuntime {
     py::array_t<int64_t> ax({P, n0_}), axp({P, n0_});
     std::memcpy(ax.mutable_data(), cex_x.data(), sizeof(int64_t) * cex_x.size());
     std::memcpy(axp.mutable_data(), cex_xp.data(), sizeof(int64_t) * cex_xp.size());
+    stats["open_left"] = open_out;
     return py::make_tuple(status_out, ax, axp, nodes_out, stats);
   }
 
@@ -397,7 +402,7 @@ class BabRuntime {
   DevBuf<float> gmin_, tstar_, score_, cand_, scores_, pe_lb_, pe_ub_, cand_buf_;
   DevBuf<uint8_t> open_, leaf_;
   DevBuf<int64_t> split_, cv_, co_;
-  DevBuf<int> pe_part_, cand_part_, counters_, nodes_, idx_;
+  DevBuf<int> pe_part_, cand_part_, counters_, nodes_, idx_, open_left_;
   DevBuf<int8_t> status_;
   int* hcount_ = nullptr;
 };

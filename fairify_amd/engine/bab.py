@@ -55,6 +55,8 @@ class BaBResult:
     nodes: np.ndarray                # [P] int64 nodes expanded
     iters: int = 0
     time: float = 0.0
+    open_left: Optional[np.ndarray] = None   # [P] open nodes left when an UNKNOWN partition stopped
+                                             # (native runtime; the escalation filter's predictor)
 
 
 def _pa_table(q: ResolvedQuery, lo: np.ndarray, hi: np.ndarray):
@@ -340,7 +342,7 @@ class BaBSolver:
                                                   confirm, stream)
         self.stats = dict(stats)
         return BaBResult(np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes),
-                         int(stats["levels"]), time.time() - t0)
+                         int(stats["levels"]), time.time() - t0, open_left=np.asarray(stats["open_left"]))
 
     # --------------------------------------------------------------------------------------
     def _confirm(self, rows, cx, cxp, bpart, status, status_t, cex_x, cex_xp, mlp_exact, exact_models,

@@ -218,6 +218,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         per_round = cfg.chunk * streams.workers
         rounds = int(np.ceil(len(todo) / max(1, per_round * info.world))) if len(todo) else 0
         stopped = False
+        last_note = time.time()
         for r in range(rounds):
             elapsed = D.all_reduce_max(info, time.time() - t0)
             if elapsed > cfg.hard_timeout:
@@ -249,6 +250,11 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                     f.result()
                 pending.clear()
             faults.maybe_crash(r + 1, info.rank)
+            if verbose and info.is_main and time.time() - last_note > 20.0:
+                last_note = time.time()
+                print(f"[{preset.name}] {name}: round {r + 1}/{rounds}, "
+                      f"{min(len(todo), (r + 1) * per_round * info.world)}/{len(todo)} partitions, "
+                      f"{time.time() - t0:.0f}s", flush=True)
         for f in pending:
             f.result()
         if io is not None:
