@@ -52,6 +52,8 @@ def main() -> None:
     ap.add_argument("--node-budget", type=int, default=2048)
     ap.add_argument("--escalate-budget", type=int, default=8192,
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
+    ap.add_argument("--escalate-max-open", type=int, default=0,
+                    help="escalate only partitions that left <= this many open BaB nodes (0 = all)")
     ap.add_argument("--residual-samples", type=int, default=None, help="residual falsifier samples (0 = off)")
     ap.add_argument("--residual-iters", type=int, default=None)
     ap.add_argument("--bisect-steps", type=int, default=None, help="boundary-walk bisection steps (0 = off)")
@@ -92,7 +94,8 @@ def main() -> None:
     cfg = VerifyConfig(sim_size=args.sim_size or pre.sim_size, seed=args.seed, chunk=args.chunk,
                        soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
                        node_budget=args.node_budget, heuristic=True, heuristic_p=pre.heuristic_p,
-                       heuristic_node_budget=args.node_budget, escalate_budget=args.escalate_budget)
+                       heuristic_node_budget=args.node_budget, escalate_budget=args.escalate_budget,
+                       escalate_max_open=args.escalate_max_open)
     if args.residual_samples is not None:
         cfg.residual_samples = args.residual_samples
     if args.residual_iters is not None:
@@ -177,7 +180,8 @@ def main() -> None:
         "config": {"model": f"AC suite ({','.join(names)})", "global_batch": int(per_step), "seq_len": None,
                    "parallelism": f"dp{info.world}", "preset": args.preset, "grid_per_model": len(grid),
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
-                   "escalate_budget": cfg.escalate_budget, "chunk": args.chunk},
+                   "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
+                   "chunk": args.chunk},
         "pct_verified": round(100.0 * dec / max(1.0, att), 3),
         "partitions_per_s": round(att / dt_max, 3) if dt_max > 0 else 0.0,
         "sat": int(sat), "unsat": int(uns), "unknown": int(att - dec),

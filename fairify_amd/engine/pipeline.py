@@ -44,6 +44,8 @@ class VerifyConfig:
     node_budget: int = 4096              # BaB expansions per partition
     escalate_budget: int = 0             # second sound BaB pass on the residue with this node
                                          # budget (0 = off); runs after the residual falsifier
+    escalate_max_open: int = 0           # only escalate partitions that left at most this many
+                                         # open nodes in the first pass (0 = all; native BaB only)
     batch_nodes: int = 32768
     heuristic: bool = True               # reference behaviour: heuristic retry on unknown
     heuristic_p: float = 5.0             # HEURISTIC_PRUNE_THRESHOLD
@@ -221,6 +223,7 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     cex_xp[newly_sat] = res.cex_xp[newly_sat]
     status = res.status.copy()
     nodes = res.nodes.copy()
+    open_left = res.open_left
     forced = faults.forced_unknown(ids) & (stage == "bab")      # fault injection: solver "timeouts"
     if forced.any():
         status[forced] = UNKNOWN
@@ -259,7 +262,10 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     # ---------------- stage 3b: escalated sound BaB on what is still UNKNOWN (the cheap first
     # pass decides the bulk; only the residue pays for the deep budget)
     if cfg.escalate_budget > cfg.node_budget:
-        unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+        want = (status == UNKNOWN) & ~forced
+        if cfg.escalate_max_open > 0 and open_left is not None:
+            want &= open_left <= cfg.escalate_max_open
+        unk = np.nonzero(want)[0]
         if unk.size:
             t0 = time.time()
             el = time.time() - t_start
