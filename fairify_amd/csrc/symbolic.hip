@@ -472,18 +472,31 @@ SymKernel sym_ptr() {
   return fa_sym_kernel<NT, TM>;
 }
 
+// widest layer (in 16-neuron tiles) served by the register-resident kernel; FAIRIFY_SYM_MAX_TM
+// lowers it for A/B runs against the LDS-tiled kernel
+int max_tm() {
+  static const int v = [] {
+    const char* e = getenv("FAIRIFY_SYM_MAX_TM");
+    return (e && *e) ? atoi(e) : 10;
+  }();
+  return v;
+}
+
 SymKernel select_kernel(int NT, int TM) {
+  if (TM > max_tm()) return nullptr;
   switch (NT) {
     case 1:
       if (TM <= 1) return sym_ptr<1, 1>();
       if (TM <= 2) return sym_ptr<1, 2>();
       if (TM <= 4) return sym_ptr<1, 4>();
       if (TM <= 7) return sym_ptr<1, 7>();
+      if (TM <= 10) return sym_ptr<1, 10>();   // e.g. BM-4's 150-wide layer (scratch-backed operands)
       return nullptr;
     case 2:
       if (TM <= 1) return sym_ptr<2, 1>();
       if (TM <= 2) return sym_ptr<2, 2>();
       if (TM <= 4) return sym_ptr<2, 4>();
+      if (TM <= 10) return sym_ptr<2, 10>();
       return nullptr;
     case 3:
       if (TM <= 1) return sym_ptr<3, 1>();
