@@ -50,9 +50,9 @@ def main() -> None:
                     help="partitions per work item (big chunks win even for small per-rank shards: a 1/8 "
                          "shard takes 1.02 s per step at 4096 vs 1.76 s at 667, profiles/scaling_emulation.md)")
     ap.add_argument("--node-budget", type=int, default=2048)
-    ap.add_argument("--escalate-budget", type=int, default=8192,
+    ap.add_argument("--escalate-budget", type=int, default=16384,
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
-    ap.add_argument("--escalate-max-open", type=int, default=0,
+    ap.add_argument("--escalate-max-open", type=int, default=768,
                     help="escalate only partitions that left <= this many open BaB nodes (0 = all)")
     ap.add_argument("--residual-samples", type=int, default=None, help="residual falsifier samples (0 = off)")
     ap.add_argument("--residual-iters", type=int, default=None)
