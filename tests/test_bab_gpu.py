@@ -78,3 +78,19 @@ def test_native_matches_torch_bab_on_adult(cuda):
     decided = (nat.status != 0) & (tor.status != 0)
     assert np.array_equal(nat.status[decided], tor.status[decided])
     assert decided.mean() > 0.9
+
+
+def test_open_left_reported_only_for_unknown(cuda):
+    """The native BaB reports, for partitions it leaves UNKNOWN at the node budget, the open
+    frontier they left (the escalation filter's predictor); decided partitions report 0."""
+    q = Query(pa=("f2",)).resolve(DOM)
+    lo = np.zeros((6, 5), int)
+    hi = np.tile(np.array([3, 4, 2, 4, 5]), (6, 1))
+    for seed in range(4):
+        m = random_mlp(5, [12, 12], seed=700 + seed, bias_scale=0.3)
+        res = BaBSolver(Backend(m, cuda), q, BaBConfig(node_budget=4)).solve(lo, hi, m)
+        assert res.open_left is not None and res.open_left.shape == (6,)
+        assert np.all(res.open_left[res.status != 0] == 0)
+        assert np.all(res.open_left >= 0)
+        if np.any(res.status == 0):
+            assert np.all(res.open_left[res.status == 0] > 0)

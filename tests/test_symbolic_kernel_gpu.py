@@ -1,7 +1,7 @@
 """Register-resident symbolic bound kernel (csrc/symbolic.hip) vs the PyTorch reference.
 
 Covers every template shape the dispatcher can pick (column tiles NT = 1..3, row tiles
-TM = 1..7), folded degenerate input dims (the node-row expansion of the BaB runtime), forced
+TM = 1..10), folded degenerate input dims (the node-row expansion of the BaB runtime), forced
 dead neurons, and soundness against brute-force enumeration.  Run on a real MI355X.
 """
 import itertools
@@ -27,6 +27,8 @@ SHAPES = [
     (30, [16, 16, 16], (20,)),         # DF: NT=3, TM=2
     (6, [16, 8], (3,)),                # CP-1: NT=1, TM=1
     (12, [32, 32], (3, 4)),            # two folded dims
+    (16, [150, 100, 50], (0,)),        # BM-4: NT=2, TM=10 (scratch-backed operand tiles)
+    (13, [150, 20], (8,)),             # NT=1, TM=10
 ]
 
 
