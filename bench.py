@@ -49,11 +49,13 @@ def main() -> None:
     ap.add_argument("--chunk", type=int, default=4096,
                     help="partitions per work item (big chunks win even for small per-rank shards: a 1/8 "
                          "shard takes 1.02 s per step at 4096 vs 1.76 s at 667, profiles/scaling_emulation.md)")
-    ap.add_argument("--node-budget", type=int, default=2048)
+    ap.add_argument("--node-budget", type=int, default=512)
     ap.add_argument("--escalate-budget", type=int, default=16384,
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
-    ap.add_argument("--escalate-max-open", type=int, default=768,
+    ap.add_argument("--escalate-max-open", type=int, default=256,
                     help="escalate only partitions that left <= this many open BaB nodes (0 = all)")
+    ap.add_argument("--stages", default="",
+                    help="further escalation passes 'budget:max_open,...' after --escalate-budget")
     ap.add_argument("--residual-samples", type=int, default=None, help="residual falsifier samples (0 = off)")
     ap.add_argument("--residual-iters", type=int, default=None)
     ap.add_argument("--bisect-steps", type=int, default=None, help="boundary-walk bisection steps (0 = off)")
@@ -95,7 +97,8 @@ def main() -> None:
                        soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
                        node_budget=args.node_budget, heuristic=True, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=args.node_budget, escalate_budget=args.escalate_budget,
-                       escalate_max_open=args.escalate_max_open)
+                       escalate_max_open=args.escalate_max_open,
+                       escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
     if args.residual_samples is not None:
         cfg.residual_samples = args.residual_samples
     if args.residual_iters is not None:
@@ -181,6 +184,7 @@ def main() -> None:
                    "parallelism": f"dp{info.world}", "preset": args.preset, "grid_per_model": len(grid),
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
+                   "stages": [list(st) for st in cfg.escalate_stages],
                    "chunk": args.chunk},
         "pct_verified": round(100.0 * dec / max(1.0, att), 3),
         "partitions_per_s": round(att / dt_max, 3) if dt_max > 0 else 0.0,

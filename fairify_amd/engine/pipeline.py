@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import time
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -46,6 +46,9 @@ class VerifyConfig:
                                          # budget (0 = off); runs after the residual falsifier
     escalate_max_open: int = 0           # only escalate partitions that left at most this many
                                          # open nodes in the first pass (0 = all; native BaB only)
+    escalate_stages: Tuple[Tuple[int, int], ...] = ()
+                                         # further (budget, max_open) passes after the escalated one,
+                                         # each on the residue the previous pass left
     batch_nodes: int = 32768
     heuristic: bool = True               # reference behaviour: heuristic retry on unknown
     heuristic_p: float = 5.0             # HEURISTIC_PRUNE_THRESHOLD
@@ -259,30 +262,43 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
             sync()
             t_bab += time.time() - t0
 
-    # ---------------- stage 3b: escalated sound BaB on what is still UNKNOWN (the cheap first
-    # pass decides the bulk; only the residue pays for the deep budget)
+    # ---------------- stage 3b: escalated sound BaB passes on what is still UNKNOWN (the cheap
+    # first pass decides the bulk; only residue partitions whose open frontier stayed small -- the
+    # ones a deeper search can still close -- pay for the deep budgets)
+    stages = []
     if cfg.escalate_budget > cfg.node_budget:
+        stages.append((cfg.escalate_budget, cfg.escalate_max_open))
+    stages += [tuple(st) for st in cfg.escalate_stages]
+    prev_budget = cfg.node_budget
+    for e_budget, e_open in stages:
+        if e_budget <= prev_budget:
+            continue
+        prev_budget = e_budget
         want = (status == UNKNOWN) & ~forced
-        if cfg.escalate_max_open > 0 and open_left is not None:
-            want &= open_left <= cfg.escalate_max_open
+        if e_open > 0 and open_left is not None:
+            want &= open_left <= e_open
         unk = np.nonzero(want)[0]
-        if unk.size:
-            t0 = time.time()
-            el = time.time() - t_start
-            esolver = BaBSolver(be, q, BaBConfig(node_budget=cfg.escalate_budget, batch_nodes=cfg.batch_nodes,
-                                                 time_budget=max(0.0, budget - el)), timer=tm)
-            with tm("bab.escalate"):
-                eres = esolver.solve(lo_np[unk], hi_np[unk], mlp)
-            dec_e = np.isin(eres.status, (SAT, UNSAT))
-            hit = unk[dec_e]
-            status[hit] = eres.status[dec_e]
-            stage[hit] = "bab"
-            es = eres.status == SAT
-            cex_x[unk[es]] = eres.cex_x[es]
-            cex_xp[unk[es]] = eres.cex_xp[es]
-            nodes[unk] += eres.nodes
-            sync()
-            t_bab += time.time() - t0
+        if not unk.size:
+            continue
+        t0 = time.time()
+        el = time.time() - t_start
+        esolver = BaBSolver(be, q, BaBConfig(node_budget=e_budget, batch_nodes=cfg.batch_nodes,
+                                             time_budget=max(0.0, budget - el)), timer=tm)
+        with tm("bab.escalate"):
+            eres = esolver.solve(lo_np[unk], hi_np[unk], mlp)
+        dec_e = np.isin(eres.status, (SAT, UNSAT))
+        hit = unk[dec_e]
+        status[hit] = eres.status[dec_e]
+        stage[hit] = "bab"
+        es = eres.status == SAT
+        cex_x[unk[es]] = eres.cex_x[es]
+        cex_xp[unk[es]] = eres.cex_xp[es]
+        nodes[unk] += eres.nodes
+        if open_left is not None and eres.open_left is not None:
+            open_left = open_left.copy()
+            open_left[unk] = eres.open_left
+        sync()
+        t_bab += time.time() - t0
 
     # ---------------- stage 3c: host SMT on the sound-pruned subnetworks of the residue
     # (the reference's Z3 check, src/AC/Verify-AC.py:145-158; no-op without a back-end)
