@@ -54,7 +54,7 @@ def cmd_verify(args):
                        node_budget=args.node_budget, heuristic=not args.no_heuristic,
                        heuristic_p=args.heuristic_p if args.heuristic_p is not None else pre.heuristic_p,
                        heuristic_node_budget=args.node_budget, smt_backend=args.smt,
-                       escalate_budget=args.escalate_budget)
+                       escalate_budget=args.escalate_budget, escalate_max_open=args.escalate_max_open)
     models = args.models.split(",") if args.models else None
     run_preset(pre, models=models, weights=args.weights, out_dir=args.out, cfg=cfg, info=info,
                max_partitions=args.max_partitions, resume=args.resume, seed=args.seed,
@@ -162,6 +162,8 @@ def main(argv=None):
                    help="retry each round's UNKNOWN partitions on all ranks with N x the node budget")
     v.add_argument("--escalate-budget", type=int, default=0,
                    help="second sound BaB pass with this node budget on each chunk's UNKNOWN residue")
+    v.add_argument("--escalate-max-open", type=int, default=0,
+                   help="escalate only residue partitions that left <= this many open BaB nodes (0 = all)")
     v.add_argument("--concurrency", type=int, default=0,
                    help="chunks verified at once per rank, one HIP stream each (default 4 on GPU, 1 on CPU)")
     v.add_argument("--smt", default="auto", help="host SMT back-end for the residue: auto | z3py | z3bin | none")

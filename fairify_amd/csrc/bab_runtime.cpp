@@ -34,6 +34,7 @@ extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
 extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream);
 extern "C" int fa_mark_unknown_launch(const int* part, int n, int8_t* status, hipStream_t stream);
 extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_t v, hipStream_t stream);
+extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 
 // defined in bindings.cpp
 const NetDesc& fa_net_desc(py::handle net);
@@ -74,7 +75,7 @@ class BabRuntime {
  public:
   BabRuntime(py::handle net, uintptr_t flat, std::vector<int> pa, std::vector<float> values_f,
              std::vector<int64_t> values_i, std::vector<int64_t> pairs, std::vector<int> ra, float tau,
-             std::vector<uint8_t> shared, int capacity, int batch_nodes, int cand_cap, double unit)
+             std::vector<uint8_t> shared, int capacity, int batch_nodes, int cand_cap, double unit, bool crown)
       : net_(fa_net_desc(net)),
         flat_((const float*)flat),
         pa_(std::move(pa)),
@@ -83,7 +84,8 @@ class BabRuntime {
         cap_(capacity),
         batch_(batch_nodes),
         cand_cap_(cand_cap),
-        unit_(unit) {
+        unit_(unit),
+        crown_(crown) {
     n0_ = net_.dims[0];
     npa_ = (int)pa_.size();
     if (npa_ == 0 || npa_ > FA_CMAX_PA || (int)ra_.size() > FA_MAX_RA) throw std::invalid_argument("bad PA/RA");
@@ -108,6 +110,10 @@ class BabRuntime {
       Uc_[s].ensure(R * n0_);
       L0_[s].ensure(R); Le_[s].ensure(R); U0_[s].ensure(R); Ue_[s].ensure(R);
       olb_[s].ensure(R); oub_[s].ensure(R);
+      if (crown_) {
+        lay_lb_[s].ensure(R * net_.n_neurons);
+        lay_ub_[s].ensure(R * net_.n_neurons);
+      }
     }
     const size_t Q = (size_t)Pp_ * norient_;
     gmin_.ensure(batch_ * Q);
@@ -324,7 +330,13 @@ class BabRuntime {
       b.node_part = part;
       b.dead_part = (const uint8_t*)dead_part;
     }
+    if (crown_) {
+      b.layer_lb = lay_lb_[slot].p;
+      b.layer_ub = lay_ub_[slot].p;
+    }
     ckl(fa_bounds_launch(net_, b, st), "bounds");
+    // backward output bounds: tighter forms / logit bounds for the certificate
+    if (crown_) ckl(fa_crown_launch(net_, b, st), "crown");
   }
 
   // grow pool `i` to hold at least `need` nodes (clamped to cap_; over-capacity children make
@@ -391,6 +403,7 @@ class BabRuntime {
   int cap_, batch_, cand_cap_;
   int pool_[2] = {0, 0};
   double unit_;
+  bool crown_ = false;
   int n0_ = 0, npa_ = 0, V_ = 0, Pp_ = 0, norient_ = 1;
   bool relaxed_ = false;
   DevBuf<float> vals_f_;
@@ -398,7 +411,7 @@ class BabRuntime {
   DevBuf<uint8_t> shared_;
   DevBuf<float> lo_[2], hi_[2], plo_[2], phi_[2];
   DevBuf<int> part_[2];
-  DevBuf<float> Lc_[2], Uc_[2], L0_[2], Le_[2], U0_[2], Ue_[2], olb_[2], oub_[2];
+  DevBuf<float> Lc_[2], Uc_[2], L0_[2], Le_[2], U0_[2], Ue_[2], olb_[2], oub_[2], lay_lb_[2], lay_ub_[2];
   DevBuf<float> gmin_, tstar_, score_, cand_, scores_, pe_lb_, pe_ub_, cand_buf_;
   DevBuf<uint8_t> open_, leaf_;
   DevBuf<int64_t> split_, cv_, co_;
@@ -410,10 +423,10 @@ class BabRuntime {
 void register_bab(py::module& m) {
   py::class_<BabRuntime>(m, "BabRuntime")
       .def(py::init<py::handle, uintptr_t, std::vector<int>, std::vector<float>, std::vector<int64_t>,
-                    std::vector<int64_t>, std::vector<int>, float, std::vector<uint8_t>, int, int, int, double>(),
+                    std::vector<int64_t>, std::vector<int>, float, std::vector<uint8_t>, int, int, int, double, bool>(),
            py::arg("net"), py::arg("flat"), py::arg("pa"), py::arg("values_f"), py::arg("values_i"),
            py::arg("pairs"), py::arg("ra"), py::arg("tau"), py::arg("shared"), py::arg("capacity"),
-           py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"))
+           py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"), py::arg("crown") = true)
       .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"));
 }

@@ -73,6 +73,7 @@ struct Net {
 
 const NetDesc& fa_net_desc(py::handle h) { return h.cast<const Net&>().d; }
 void register_bab(py::module& m);
+extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 void register_csv(py::module& m);
 
 static void check(int rc, const char* what) {
@@ -115,6 +116,25 @@ PYBIND11_MODULE(_C, m) {
      py::arg("symbolic"), py::arg("out_lb"), py::arg("out_ub"), py::arg("Lc"), py::arg("L0"), py::arg("Le"),
      py::arg("Uc"), py::arg("U0"), py::arg("Ue"), py::arg("layer_lb"), py::arg("layer_ub"), py::arg("dead_out"),
      py::arg("G"), py::arg("stream"), py::arg("fold") = 0ull);
+
+  // backward output bounds refining forms/out bounds written by a preceding `bounds` call
+  m.def("crown", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t dead_in, int R,
+                    uintptr_t out_lb, uintptr_t out_ub, uintptr_t Lc, uintptr_t L0, uintptr_t Le, uintptr_t Uc,
+                    uintptr_t U0, uintptr_t Ue, uintptr_t layer_lb, uintptr_t layer_ub, uintptr_t stream) {
+    BoundArgs a{};
+    a.flat = P<const float>(flat);
+    a.lo = P<const float>(lo);
+    a.hi = P<const float>(hi);
+    a.dead_in = P<const uint8_t>(dead_in);
+    a.R = R;
+    a.out_lb = P<float>(out_lb);
+    a.out_ub = P<float>(out_ub);
+    a.Lc = P<float>(Lc); a.L0 = P<float>(L0); a.Le = P<float>(Le);
+    a.Uc = P<float>(Uc); a.U0 = P<float>(U0); a.Ue = P<float>(Ue);
+    a.layer_lb = P<float>(layer_lb);
+    a.layer_ub = P<float>(layer_ub);
+    check(fa_crown_launch(net.d, a, (hipStream_t)stream), "crown");
+  });
 
   m.def("point_bounds", [](const Net& net, uintptr_t flat, uintptr_t x, uintptr_t dead_in, int R, uintptr_t out_lb,
                            uintptr_t out_ub, uintptr_t stream) {

@@ -219,16 +219,17 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
       cl[ierow * S] = gnext * il;
       if (!sym) continue;
       const float* gm = s_m + g * n0;
-      // upper relaxation: identity (stable active) / zero / chord over [aa, bb] of T = U + eU
+      // upper relaxation: identity (stable active, or the upper form T = U + eU >= 0 on the
+      // whole box: relu(z) <= T there) / zero / chord over [aa, bb] of T
       float eUn = 0.f, mgUn = 0.f;
+      const float aa = mnU - gc * mgU + eU;
       if (zero) {
         for (int i = 0; i <= crow; ++i) cu[i * S] = 0.f;
-      } else if (isact) {
+      } else if (isact || aa >= 0.f) {
         cu[crow * S] = cU;
         eUn = eU;
         mgUn = mgU;
       } else {
-        const float aa = mnU - gc * mgU + eU;
         const float bb = mxU + gc * mgU + eU;
         const float s = (bb / (bb - aa)) * (1.f + 4.f * unit);
         const float shift = eU - aa;

@@ -184,13 +184,14 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
     const bool zero = isdead || forced || !jv;
     float s, cnew, en, mgn, ivn;
     if (ob == 0) {
-      // upper: identity (stable active) / zero / chord over [aa, bb] of T = U + eU
+      // upper: identity (stable active, or the upper form T = U + eU >= 0 on the whole box:
+      // relu(z) <= T there, a chord from (aa, 0) would cut below it) / zero / chord over [aa, bb]
       ivn = zero ? 0.f : fmaxf(ub, 0.f);
       s = 1.f; cnew = c0; en = e; mgn = mg;
+      const float aa = mn - gc * mg + e;
       if (zero) {
         s = 0.f; cnew = 0.f; en = 0.f; mgn = 0.f;
-      } else if (!isact) {
-        const float aa = mn - gc * mg + e;
+      } else if (!isact && aa < 0.f) {
         const float bb = mx + gc * mg + e;
         s = (bb / (bb - aa)) * (1.f + 4.f * unit);
         const float shift = e - aa;

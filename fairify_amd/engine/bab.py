@@ -45,6 +45,7 @@ class BaBConfig:
     time_budget: float = 1e9         # wall-clock seconds for the whole call
     mode: str = "symbolic"
     cand_cap: int = 1 << 17          # candidate pairs confirmed per BFS level (native runtime)
+    crown: bool = os.environ.get("FAIRIFY_CROWN", "1") != "0"   # backward output bounds per node
 
 
 @dataclass
@@ -176,10 +177,10 @@ class BaBSolver:
                 dead_rows = self.dead[bpart].repeat_interleave(V, dim=0)
             with self.tm("bab.bounds"):
                 rlo, rhi = self._rows(blo, bhi, values)
-                res_x = self.be.bounds(rlo, rhi, mode=cfg.mode, dead=dead_rows)
+                res_x = self.be.bounds(rlo, rhi, mode=cfg.mode, dead=dead_rows, crown=cfg.crown)
                 if self.relaxed:
                     plo, phi = self._rows(bplo, bphi, values)
-                    res_xp = self.be.bounds(plo, phi, mode=cfg.mode, dead=dead_rows)
+                    res_xp = self.be.bounds(plo, phi, mode=cfg.mode, dead=dead_rows, crown=cfg.crown)
                 else:
                     res_xp = res_x
             with self.tm("bab.certify"):
@@ -293,7 +294,7 @@ class BaBSolver:
         # one runtime per (query, host thread): concurrent chunks of one model on several
         # streams must not share device work buffers
         key = (tuple(self.q.pa_idx), tuple(self.q.ra_idx), self.q.tau, values_np.tobytes(), pairs_np.tobytes(),
-               threading.get_ident())
+               threading.get_ident(), bool(self.cfg.crown))
         cache = self.be.__dict__.setdefault("_bab_rt", {})
         cap = max(self.cfg.max_pool, n_run)
         rt = cache.get(key)
@@ -306,7 +307,7 @@ class BaBSolver:
                                    pairs_np.astype(np.int64).reshape(-1).tolist(),
                                    list(self.q.ra_idx) if self.relaxed else [], float(self.q.tau),
                                    shared.tolist(), int(cap), int(self.cfg.batch_nodes), int(self.cfg.cand_cap),
-                                   float(self.be.unit)), cap)
+                                   float(self.be.unit), bool(self.cfg.crown)), cap)
             cache[key] = rt
         return rt[0]
 

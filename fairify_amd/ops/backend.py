@@ -79,15 +79,21 @@ class Backend:
 
     # ----------------------------------------------------------------------------- bounds
     def bounds(self, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic",
-               dead: Optional[torch.Tensor] = None, keep_layers: bool = False, fold=()) -> ref.BoundResult:
-        """``fold``: dims degenerate (lo == hi) in every row — a HIP-kernel layout hint only."""
+               dead: Optional[torch.Tensor] = None, keep_layers: bool = False, fold=(),
+               crown: bool = False) -> ref.BoundResult:
+        """``fold``: dims degenerate (lo == hi) in every row — a HIP-kernel layout hint only.
+        ``crown``: refine the logit forms/bounds with the backward pass (symbolic mode only)."""
         lo = lo.to(self.dtype)
         hi = hi.to(self.dtype)
+        crown = crown and mode == "symbolic"
         if self.hip:
             from . import hip
 
-            return hip.bounds(self, lo, hi, mode=mode, dead=dead, keep_layers=keep_layers, fold=fold)
-        return ref.bounds(self.ws, self.bs, lo, hi, mode=mode, dead=dead, unit=self.unit, keep_layers=keep_layers)
+            r = hip.bounds(self, lo, hi, mode=mode, dead=dead, keep_layers=keep_layers or crown, fold=fold)
+            return hip.crown(self, lo, hi, r, dead) if crown else r
+        r = ref.bounds(self.ws, self.bs, lo, hi, mode=mode, dead=dead, unit=self.unit,
+                       keep_layers=keep_layers or crown)
+        return ref.crown_output(self.ws, self.bs, lo, hi, r, dead, unit=self.unit) if crown else r
 
     def point_bounds(self, x: torch.Tensor, dead: Optional[torch.Tensor] = None):
         """Rigorous [lb, ub] of the logit at points x [R, n0] (candidate-pair screening)."""

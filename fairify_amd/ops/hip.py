@@ -137,6 +137,33 @@ def bounds(be, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic", dead:
 
 
 # ------------------------------------------------------------------------------------------------
+def crown(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, dead: Optional[torch.Tensor] = None):
+    """Backward output bounds (csrc/crown.hip) refining ``res`` in place: ``res`` must come from
+    :func:`bounds` with mode='symbolic' and keep_layers=True on the same rows."""
+    R, n0 = lo.shape
+    N = be.mlp.n_neurons
+    if res.Lc is None or res.layer_lb is None:
+        raise ValueError("crown needs symbolic bounds with keep_layers=True")
+    lo = _c(lo, torch.float32, (R, n0), "lo")
+    hi = _c(hi, torch.float32, (R, n0), "hi")
+    lay_lb = torch.cat(res.layer_lb, dim=1).contiguous() if isinstance(res.layer_lb, list) else res.layer_lb
+    lay_ub = torch.cat(res.layer_ub, dim=1).contiguous() if isinstance(res.layer_ub, list) else res.layer_ub
+    if lay_lb.shape[1] != N:          # keep_layers splits off the output neuron: append a pad column
+        pad = torch.zeros(R, N - lay_lb.shape[1], dtype=torch.float32, device=lo.device)
+        lay_lb = torch.cat([lay_lb, pad], dim=1).contiguous()
+        lay_ub = torch.cat([lay_ub, pad], dim=1).contiguous()
+    d = None
+    if dead is not None:
+        d = _c(dead, torch.uint8, (R, be.n_hidden), "dead")
+    if R:
+        ext().crown(_net(be), be.flat.data_ptr(), lo.data_ptr(), hi.data_ptr(), _ptr(d), R,
+                    res.out_lb.data_ptr(), res.out_ub.data_ptr(), res.Lc.data_ptr(), res.L0.data_ptr(),
+                    res.Le.data_ptr(), res.Uc.data_ptr(), res.U0.data_ptr(), res.Ue.data_ptr(),
+                    lay_lb.data_ptr(), lay_ub.data_ptr(), _stream(lo.device))
+    return res
+
+
+# ------------------------------------------------------------------------------------------------
 def pair_certify(be, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, shared, relaxed) -> ref.PairDecision:
     Nn, n0 = xlo.shape
     dev = xlo.device

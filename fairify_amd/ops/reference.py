@@ -303,10 +303,12 @@ def bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Ten
         Il = torch.where(zero, torch.zeros_like(lb), lb.clamp(min=0))
         if not sym:
             continue
-        # upper: identity if stable active, zero if dead, else chord over [a, bb] of T = U + eU
+        # upper: identity if stable active -- or if the upper form T = U + eU itself stays >= 0
+        # on the box (then relu(z) <= relu(T) = T; a chord from (a, 0) would cut below T) --
+        # zero if dead, else the chord over [a, bb] of T
         a = lbU - gc * MUn + eUn
         bb = ubU + gc * MUn + eUn
-        identU = is_act & ~zero
+        identU = (is_act | (a >= 0)) & ~zero
         cross = ~(zero | identU)
         denom = torch.where(cross, bb - a, torch.ones_like(bb))
         s = torch.where(cross, (bb / denom) * (1 + 4 * unit), torch.ones_like(bb))
@@ -336,6 +338,96 @@ def bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Ten
     if keep_layers:
         res.layer_lb, res.layer_ub = layer_lb, layer_ub
     return res
+
+
+def crown_output(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Tensor, hi: torch.Tensor,
+                 res: BoundResult, dead: Optional[torch.Tensor] = None, unit: Optional[float] = None) -> BoundResult:
+    """Backward (CROWN-style) linear bounds of the logit, replacing the forward-symbolic output
+    forms of ``res`` where they are tighter (csrc/crown.hip, same arithmetic and error terms).
+
+    The forward pass concretises each layer's forms before relaxing it, so the relaxation
+    slack of every layer is propagated as a fixed interval term; back-substituting from the
+    output instead picks, per neuron, the relaxation that the sign of its output multiplier
+    needs (lower: h >= a z with a in {0, 1}; upper: the chord h <= s (z - l)).  The per-neuron
+    pre-activation bounds ``res.layer_lb/layer_ub`` of the forward pass are the relaxation
+    intervals.  On the deep AC shapes this halves the open BaB frontier (tools/diag_open_nodes.py).
+
+    Rounding: every multiplier mu = lambda * slope, intercept t = -mu l, back-substituted
+    coefficient lambda' = W mu and constant sum carries a gamma-bounded error, accumulated with
+    the magnitudes of the layer's inputs (|x| on the box, max(0, ub) of hidden outputs) into the
+    form's error term, so ``sigma * y >= lambda . x + c - err`` holds for the exact network.
+    """
+    dt = lo.dtype
+    if unit is None:
+        unit = FP64_UNIT if dt == torch.float64 else FP32_UNIT
+    R, n0 = lo.shape
+    L = len(ws)
+    lbs, ubs = res.layer_lb, res.layer_ub
+    offs = [0]
+    for l in range(L - 1):
+        offs.append(offs[-1] + ws[l].shape[1])
+    mx_in = torch.maximum(lo.abs(), hi.abs())
+    out = {}
+    for sg in (1.0, -1.0):
+        lam = (sg * ws[L - 1][:, 0].to(dt))[None].expand(R, -1).clone()
+        c = torch.full((R,), sg * float(bs[L - 1][0]), dtype=dt, device=lo.device)
+        err = torch.zeros(R, dtype=dt, device=lo.device)
+        for l in range(L - 2, -1, -1):
+            W = ws[l].to(dt)
+            b = bs[l].to(dt)
+            n = W.shape[1]
+            lb, ub = lbs[l].to(dt), ubs[l].to(dt)
+            dd = ub <= 0
+            if dead is not None:
+                dd = dd | dead[:, offs[l]:offs[l] + n].bool()
+            act = (lb >= 0) & ~dd
+            unst = ~(dd | act)
+            alpha = (ub > -lb).to(dt)
+            den = torch.where(unst, ub - lb, torch.ones_like(ub))
+            s = torch.where(unst, (ub / den) * (1 + 4 * unit), torch.zeros_like(ub))
+            neg = unst & (lam < 0)
+            slope = torch.where(act, torch.ones_like(ub), torch.where(dd, torch.zeros_like(ub),
+                                torch.where(lam >= 0, alpha, s)))
+            mu = lam * slope
+            t = torch.where(neg, -mu * lb, torch.zeros_like(ub))
+            # only the chord multipliers mu = lambda * s and intercepts t = -mu l are rounded
+            zmax = torch.maximum(lb.abs(), ub.abs())
+            e_rel = torch.where(neg, 3 * unit * (mu.abs() * zmax + t.abs()), torch.zeros_like(ub))
+            g_c = gamma(2 * n + 1, unit)
+            csum = (mu * b[None]).sum(1) + t.sum(1)
+            cmag = c.abs() + (mu * b[None]).abs().sum(1) + t.abs().sum(1)
+            c = c + csum
+            if l > 0:                       # |h| of the layer below: max(0, ub), 0 if forced dead
+                hm = ubs[l - 1].to(dt).clamp(min=0)
+                if dead is not None:
+                    hm = torch.where(dead[:, offs[l - 1]:offs[l - 1] + W.shape[0]].bool(), torch.zeros_like(hm), hm)
+            else:
+                hm = mx_in
+            lam = mu @ W.T
+            eps = gamma(n + 1, unit) * (mu.abs() @ W.abs().T)
+            err = err + e_rel.sum(1) + (eps * hm).sum(1) + g_c * cmag
+        a = lam * lo
+        bb = lam * hi
+        conc = torch.minimum(a, bb).sum(1) + c
+        cmg = (lam.abs() * mx_in).sum(1) + c.abs()
+        err = err * (1 + 2 * gamma(2 * sum(int(w.shape[1]) for w in ws) + 4 * L + 4, unit))
+        low = conc - err - gamma(n0 + 1, unit) * cmg - gamma(1, unit) * conc.abs()
+        out[sg] = (lam, c, err, low)
+    lamL, cL, eL, lowL = out[1.0]
+    lamU, cU, eU, lowU = out[-1.0]
+    r = BoundResult(out_lb=torch.maximum(res.out_lb, lowL.to(res.out_lb.dtype)),
+                    out_ub=torch.minimum(res.out_ub, (-lowU).to(res.out_ub.dtype)))
+    r.layer_lb, r.layer_ub, r.dead, r.active = res.layer_lb, res.layer_ub, res.dead, res.active
+    # per row, keep the forward forms where they concretise tighter (both are sound)
+    useL = (lowL >= res.out_lb.to(dt))[:, None]
+    useU = ((-lowU) <= res.out_ub.to(dt))[:, None]
+    r.Lc = torch.where(useL, lamL, res.Lc.to(dt)).to(res.Lc.dtype)
+    r.L0 = torch.where(useL[:, 0], cL, res.L0.to(dt)).to(res.L0.dtype)
+    r.Le = torch.where(useL[:, 0], eL, res.Le.to(dt)).to(res.Le.dtype)
+    r.Uc = torch.where(useU, -lamU, res.Uc.to(dt)).to(res.Uc.dtype)
+    r.U0 = torch.where(useU[:, 0], -cU, res.U0.to(dt)).to(res.U0.dtype)
+    r.Ue = torch.where(useU[:, 0], eU, res.Ue.to(dt)).to(res.Ue.dtype)
+    return r
 
 
 # ======================================================================================

@@ -99,3 +99,35 @@ def test_point_bounds_contain_exact_logits():
         assert float((ub - lb).max()) < 1e-2 * (1 + float(np.abs(z).max()))
         s = exact.exact_signs(m, x.numpy().astype(np.int64))
         assert np.all(s[lb.numpy() > 0] == 1) and np.all(s[ub.numpy() < 0] == -1)
+
+
+@pytest.mark.parametrize("crown", [False, True])
+def test_output_forms_pointwise_sound(crown):
+    """The logit's linear forms (not only their concretisation) bound every lattice point:
+    L(x) - eL <= N(x) <= U(x) + eU.  Regression: an unstable neuron whose upper form stays >= 0
+    on the box must keep the identity upper relaxation (a chord from the form's minimum cut
+    below relu(z)); the pair certificate evaluates the forms themselves."""
+    import itertools
+
+    from fairify_amd.models.mlp import random_mlp
+    from fairify_amd.ops.backend import Backend
+
+    g = np.random.default_rng(4)
+    for seed in range(24):
+        n0 = 13 if seed % 2 else 6
+        hidden = [[64, 32, 16, 8, 4], [8, 8, 8], [5] * 6, [16, 8]][seed % 4]
+        m = random_mlp(n0, hidden, seed=seed, bias_scale=0.0 if seed % 3 == 0 else 0.4)
+        be = Backend(m, "cpu")
+        lo = g.integers(0, 5, size=(1, n0))
+        hi = lo.copy()
+        dims = g.choice(n0, size=min(n0, 4), replace=False)
+        hi[0, dims] += g.integers(1, 3, size=dims.size)
+        pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[0], hi[0])])))
+        z = m.logits(pts)
+        r = be.bounds(torch.tensor(lo, dtype=torch.float32), torch.tensor(hi, dtype=torch.float32), mode="symbolic",
+                      crown=crown)
+        Lf = pts @ r.Lc[0].double().numpy() + float(r.L0[0]) - float(r.Le[0])
+        Uf = pts @ r.Uc[0].double().numpy() + float(r.U0[0]) + float(r.Ue[0])
+        assert np.all(z >= Lf - 1e-9), (seed, float((z - Lf).min()))
+        assert np.all(z <= Uf + 1e-9), (seed, float((Uf - z).min()))
+        assert z.min() >= float(r.out_lb[0]) and z.max() <= float(r.out_ub[0])

@@ -149,3 +149,46 @@ def test_point_kernel_matches_reference(cuda, n0, hidden):
         if max(hidden) <= 112:      # wider nets fall back to interval propagation (different bound)
             tol = 1e-4 * (1 + float(z.abs().max()))
             assert torch.allclose(lb.cpu(), rl, atol=tol) and torch.allclose(ub.cpu(), ru, atol=tol)
+
+
+CROWN_SHAPES = [(13, [100, 100]), (13, [64, 32, 16, 8, 4]), (13, [5] * 9), (16, [150, 100, 50]), (20, [50]),
+                (30, [16, 16, 16]), (6, [3])]
+
+
+@pytest.mark.parametrize("n0,hidden", CROWN_SHAPES)
+def test_crown_kernel_matches_reference(cuda, n0, hidden):
+    """csrc/crown.hip vs ops/reference.py:crown_output on the same forward-pass layer bounds."""
+    from fairify_amd.ops import reference as ref
+
+    m = random_mlp(n0, hidden, seed=11 + n0 + len(hidden), bias_scale=0.3)
+    lo, hi = _boxes(n0, 257, 9, ())
+    cpu = Backend(m, "cpu")
+    gpu = Backend(m, cuda)
+    rc = cpu.bounds(lo, hi, mode="symbolic", crown=True)
+    rg = gpu.bounds(lo.to(cuda), hi.to(cuda), mode="symbolic", crown=True)
+    scale = float(((rc.out_ub - rc.out_lb).abs() + rc.out_ub.abs()).max() + 1e-3)
+    assert torch.allclose(rg.out_lb.cpu(), rc.out_lb, rtol=1e-3, atol=1e-3 * scale)
+    assert torch.allclose(rg.out_ub.cpu(), rc.out_ub, rtol=1e-3, atol=1e-3 * scale)
+    # the backward bounds never loosen the forward ones
+    rf = gpu.bounds(lo.to(cuda), hi.to(cuda), mode="symbolic")
+    assert bool((rg.out_lb >= rf.out_lb).all()) and bool((rg.out_ub <= rf.out_ub).all())
+
+
+@pytest.mark.parametrize("n0,hidden", CROWN_SHAPES[:3] + [(5, [8, 8, 8])])
+def test_crown_kernel_sound_vs_bruteforce(cuda, n0, hidden):
+    m = random_mlp(n0, hidden, seed=3 + len(hidden), bias_scale=0.0 if len(hidden) > 2 else 0.5)
+    g = np.random.default_rng(4)
+    gpu = Backend(m, cuda)
+    for _ in range(6):
+        lo = g.integers(0, 5, size=(1, n0))
+        hi = lo.copy()
+        dims = g.choice(n0, size=min(n0, 4), replace=False)
+        hi[0, dims] += g.integers(1, 3, size=dims.size)
+        pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[0], hi[0])])))
+        z = m.logits(pts)
+        r = gpu.bounds(torch.tensor(lo, dtype=torch.float32, device=cuda),
+                       torch.tensor(hi, dtype=torch.float32, device=cuda), mode="symbolic", crown=True)
+        Lf = pts @ r.Lc[0].double().cpu().numpy() + float(r.L0[0]) - float(r.Le[0])
+        Uf = pts @ r.Uc[0].double().cpu().numpy() + float(r.U0[0]) + float(r.Ue[0])
+        assert np.all(z >= Lf - 1e-9) and np.all(z <= Uf + 1e-9)
+        assert z.min() >= float(r.out_lb[0]) and z.max() <= float(r.out_ub[0])

@@ -103,6 +103,76 @@ def smear_dims(be, lo, hi, values, pa):
     return sc.argmax(dim=1)
 
 
+def full_crown(be, lo, hi):
+    """CROWN with backward-computed intermediate bounds (fp64 prototype, no rounding terms):
+    every hidden layer's pre-activation bounds come from back-substitution to the input box
+    through the relaxations of the layers below, then the output forms likewise."""
+    from fairify_amd.ops.reference import BoundResult
+    ws = [w.double() for w in be.ws]
+    bs = [b.double() for b in be.bs]
+    lo = lo.double(); hi = hi.double()
+    R = lo.shape[0]
+    L = len(ws)
+    lbs, ubs = [], []
+
+    def backsub(lam, c, upto):
+        # lam [R, n_upto]: coefficients on pre-activations z_upto ... wait: on h_{upto-1}
+        for k in range(upto - 1, -1, -1):
+            l, u = lbs[k], ubs[k]
+            dead = u <= 0
+            act = l >= 0
+            unst = ~(dead | act)
+            s = torch.where(unst, u / torch.where(unst, u - l, torch.ones_like(u)), torch.zeros_like(u))
+            alpha = (u > -l).double()
+            slope = torch.where(act, torch.ones_like(u), torch.where(dead, torch.zeros_like(u),
+                                torch.where(lam >= 0, alpha, s)))
+            c = c + torch.where(unst & (lam < 0), -lam * s * l, torch.zeros_like(u)).sum(1)
+            mu = lam * slope
+            c = c + mu @ bs[k]
+            lam = mu @ ws[k].T
+        return lam, c
+
+    def concretize_lower(lam, c):
+        return (torch.where(lam >= 0, lam * lo, lam * hi)).sum(1) + c
+
+    for k in range(L):
+        n_out = ws[k].shape[1]
+        # bounds of z_k = W_k^T h_{k-1} + b_k for all neurons j: lower via lam = e_j^T W_k^T
+        Wt = ws[k].T                                   # [n_out, n_in]
+        lam = Wt[None].expand(R, n_out, -1).reshape(R * n_out, -1)
+        c = bs[k][None].expand(R, n_out).reshape(-1)
+        # backsub over layers below k (batch rows x neurons)
+        def rep(t):
+            return t.repeat_interleave(n_out, dim=0)
+        saved = (lbs, ubs)
+        lbs_r = [rep(t) for t in lbs]; ubs_r = [rep(t) for t in ubs]
+        lo_r, hi_r = rep(lo), rep(hi)
+        res = []
+        for sign in (1.0, -1.0):
+            lam_s, c_s = sign * lam, sign * c
+            for kk in range(k - 1, -1, -1):
+                l, u = lbs_r[kk], ubs_r[kk]
+                dead = u <= 0; act = l >= 0; unst = ~(dead | act)
+                s = torch.where(unst, u / torch.where(unst, u - l, torch.ones_like(u)), torch.zeros_like(u))
+                alpha = (u > -l).double()
+                slope = torch.where(act, torch.ones_like(u), torch.where(dead, torch.zeros_like(u),
+                                    torch.where(lam_s >= 0, alpha, s)))
+                c_s = c_s + torch.where(unst & (lam_s < 0), -lam_s * s * l, torch.zeros_like(u)).sum(1)
+                mu = lam_s * slope
+                c_s = c_s + mu @ bs[kk]
+                lam_s = mu @ ws[kk].T
+            res.append(((torch.where(lam_s >= 0, lam_s * lo_r, lam_s * hi_r)).sum(1) + c_s, lam_s, c_s))
+        low = res[0][0].view(R, n_out)
+        up = (-res[1][0]).view(R, n_out)
+        if k < L - 1:
+            lbs.append(low); ubs.append(up)
+        else:
+            r = BoundResult(out_lb=low[:, 0].float(), out_ub=up[:, 0].float())
+            r.Lc, r.L0, r.Le = res[0][1].float(), res[0][2].float(), torch.zeros(R)
+            r.Uc, r.U0, r.Ue = (-res[1][1]).float(), (-res[1][2]).float(), torch.zeros(R)
+            return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="src/AC-sex")
@@ -110,7 +180,8 @@ def main():
     ap.add_argument("--partitions", type=int, default=256)
     ap.add_argument("--budget", type=int, default=2048)
     ap.add_argument("--weights", default="random")
-    ap.add_argument("--bound", default="fwd", choices=["fwd", "crown", "both", "zero", "one", "fwd+zero", "fwd+zero+one"])
+    ap.add_argument("--bound", default="fwd", choices=["fwd", "crown", "both", "zero", "one", "fwd+zero", "fwd+zero+one",
+                                                       "fullcrown", "fwd+fullcrown"])
     ap.add_argument("--split", default="cert", choices=["cert", "strong", "smear"])
     args = ap.parse_args()
     from fairify_amd import presets
@@ -167,6 +238,12 @@ def main():
                     dec = dz
                 else:
                     dec.open_ = dec.open_ & dz.open_
+        elif args.bound in ("fullcrown", "fwd+fullcrown"):
+            rf = full_crown(be, rlo.reshape(-1, q.n), rhi.reshape(-1, q.n))
+            dec = be.pair_certify(rf, rf, xlo, xhi, xlo, xhi, pairs, values, pa, shared, False)
+            if args.bound == "fwd+fullcrown":
+                d2 = be.pair_certify(res, res, xlo, xhi, xlo, xhi, pairs, values, pa, shared, False)
+                dec.open_ = dec.open_ & d2.open_
         else:
             rc = crown(be, res, rlo.reshape(-1, q.n), rhi.reshape(-1, q.n))
             dec = be.pair_certify(rc, rc, xlo, xhi, xlo, xhi, pairs, values, pa, shared, False)
