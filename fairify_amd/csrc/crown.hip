@@ -11,9 +11,10 @@
 // open branch-and-bound frontier (tools/diag_open_nodes.py --bound crown).
 //
 // Layout: the row-major weights + biases (the `flat` prefix [W_0|b_0|W_1|b_1|...]) are staged
-// once per workgroup in LDS; each wave owns a slab [lambda(2) | mu(2)] x FA_CROWN_MAXW.  Per
-// layer: lanes over the layer's neurons form mu = lambda * slope (+ chord intercepts), then
-// lanes over the layer's inputs form lambda' = W mu (and |W| |mu| for the rounding term).
+// once per workgroup in LDS; a group of G lanes (G = widest layer rounded up to a power of two,
+// 4..64) owns a row and a slab [lambda(2) | mu(2)] x WP.  Per layer: lanes over the layer's
+// neurons form mu = lambda * slope (+ chord intercepts), then lanes over the layer's inputs
+// form lambda' = W mu (and |W| |mu| for the rounding term).
 // The wave writes the back-substituted forms where they concretise tighter than the forward
 // ones and intersects the logit bounds.
 //
@@ -23,6 +24,7 @@
 // form's error term -- so sigma * y >= lambda . x + c - err holds for the exact network.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "args.h"
@@ -35,30 +37,41 @@ __device__ __forceinline__ float fa_gam(int k, float u) {
   return ku / (1.f - ku) * (1.f + 4.f * u);
 }
 
-__device__ __forceinline__ float fa_wave_sum(float v) {
+// butterfly sum within aligned groups of G lanes (every lane of the group gets the total)
+template <int G>
+__device__ __forceinline__ float fa_group_sum(float v) {
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
 
-__global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc net, BoundArgs a, int nparams) {
+// G lanes per box-row (G >= widest layer, up to 64): tiny networks (AC-8's 5-wide layers) pack
+// 64 / G rows into one wave instead of leaving 59 of 64 lanes idle.  WP = per-row slab stride.
+template <int G>
+__global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc net, BoundArgs a, int nparams, int WP) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int RPW = 64 / G;                                 // rows per wave
   const int tid = threadIdx.x;
   for (int e = tid; e < nparams; e += 64 * FA_CROWN_WAVES) smem[e] = a.flat[e];
   __syncthreads();
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  float* lam = smem + nparams + wave * 4 * FA_CROWN_MAXW;   // [2][MAXW]
-  float* mu = lam + 2 * FA_CROWN_MAXW;                     // [2][MAXW]
+  const int grp = lane / G;
+  const int gl = lane % G;
+  float* lam = smem + nparams + (wave * RPW + grp) * 4 * WP;   // [2][WP]
+  float* mu = lam + 2 * WP;                                    // [2][WP]
   const int L = net.n_layers;
   const int n0 = net.dims[0];
   const int N = net.n_neurons;
   const float u = net.unit;
-  for (int r0 = blockIdx.x * FA_CROWN_WAVES + wave; r0 < a.R; r0 += gridDim.x * FA_CROWN_WAVES) {
-    const int r = __builtin_amdgcn_readfirstlane(r0);
+  const int rows_per_block = FA_CROWN_WAVES * RPW;
+  for (int rb = blockIdx.x * rows_per_block; rb < a.R; rb += gridDim.x * rows_per_block) {
+    const int r0 = rb + wave * RPW + grp;
+    const bool valid = r0 < a.R;
+    const int r = valid ? r0 : a.R - 1;            // idle groups shadow the last row, never write
     const int node = a.V > 0 ? r / a.V : r;
     const int v = a.V > 0 ? r - node * a.V : 0;
-    const uint8_t* dmask = nullptr;             // forced-dead hidden neurons of this row
+    const uint8_t* dmask = nullptr;                // forced-dead hidden neurons of this row
     if (a.dead_in) dmask = a.dead_in + (size_t)r * net.n_hidden;
     else if (a.dead_part) dmask = a.dead_part + (size_t)a.node_part[node] * net.n_hidden;
     const float* lbr = a.layer_lb + (size_t)r * N;
@@ -67,9 +80,9 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
     {
       const int n = net.dims[L - 1];
       const float* W = smem + net.w_off[L - 1];
-      for (int i = lane; i < n; i += 64) {
+      for (int i = gl; i < n; i += G) {
         lam[i] = W[i];
-        lam[FA_CROWN_MAXW + i] = -W[i];
+        lam[WP + i] = -W[i];
       }
     }
     float c[2], err[2];
@@ -84,7 +97,7 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
       const float* W = smem + net.w_off[l];
       const float* b = smem + net.b_off[l];
       float cs[2] = {0.f, 0.f}, cm[2] = {0.f, 0.f}, er[2] = {0.f, 0.f};
-      for (int j = lane; j < n; j += 64) {
+      for (int j = gl; j < n; j += G) {
         const float lb = lbr[off + j], ub = ubr[off + j];
         const bool dd = ub <= 0.f || (dmask && dmask[off + j]);
         const bool act = !dd && lb >= 0.f;
@@ -95,12 +108,12 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
         const float bj = b[j];
 #pragma unroll
         for (int sg = 0; sg < 2; ++sg) {
-          const float lm = lam[sg * FA_CROWN_MAXW + j];
+          const float lm = lam[sg * WP + j];
           const float slope = act ? 1.f : (dd ? 0.f : (lm >= 0.f ? alpha : s));
           const float m = lm * slope;
           const bool neg = unst && lm < 0.f;
           const float t = neg ? -m * lb : 0.f;
-          mu[sg * FA_CROWN_MAXW + j] = m;
+          mu[sg * WP + j] = m;
           cs[sg] += m * bj + t;
           cm[sg] += fabsf(m * bj) + fabsf(t);
           if (neg) er[sg] += 3.f * u * (fabsf(m) * zmax + fabsf(t));
@@ -108,12 +121,12 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
       }
       __builtin_amdgcn_wave_barrier();
       const float gn = fa_gam(n + 1, u);
-      for (int i = lane; i < nin; i += 64) {
+      for (int i = gl; i < nin; i += G) {
         float acc0 = 0.f, acc1 = 0.f, mag0 = 0.f, mag1 = 0.f;
         const float* Wi = W + (size_t)i * n;
         for (int j = 0; j < n; ++j) {
           const float w = Wi[j];
-          const float m0 = mu[j], m1 = mu[FA_CROWN_MAXW + j];
+          const float m0 = mu[j], m1 = mu[WP + j];
           acc0 = fmaf(w, m0, acc0);
           acc1 = fmaf(w, m1, acc1);
           mag0 = fmaf(fabsf(w), fabsf(m0), mag0);
@@ -132,16 +145,16 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
           hm = fmaxf(fabsf(xl), fabsf(xh));
         }
         lam[i] = acc0;
-        lam[FA_CROWN_MAXW + i] = acc1;
+        lam[WP + i] = acc1;
         er[0] += gn * mag0 * hm;
         er[1] += gn * mag1 * hm;
       }
       const float gc = fa_gam(2 * n + 1, u);
 #pragma unroll
       for (int sg = 0; sg < 2; ++sg) {
-        const float csum = fa_wave_sum(cs[sg]);
-        const float cmag = fa_wave_sum(cm[sg]);
-        const float esum = fa_wave_sum(er[sg]);
+        const float csum = fa_group_sum<G>(cs[sg]);
+        const float cmag = fa_group_sum<G>(cm[sg]);
+        const float esum = fa_group_sum<G>(er[sg]);
         const float cold = c[sg];
         c[sg] = cold + csum;
         err[sg] += esum + gc * (fabsf(cold) + cmag);
@@ -158,30 +171,32 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
 #pragma unroll
     for (int sg = 0; sg < 2; ++sg) {
       float cp = 0.f, mp = 0.f;
-      for (int i = lane; i < n0; i += 64) {
+      for (int i = gl; i < n0; i += G) {
         float xl = a.lo[(size_t)node * n0 + i], xh = a.hi[(size_t)node * n0 + i];
         if (a.V > 0)
           for (int k = 0; k < a.npa; ++k)
             if (a.pa_idx[k] == i) xl = xh = a.values[v * a.npa + k];
-        const float lm = lam[sg * FA_CROWN_MAXW + i];
+        const float lm = lam[sg * WP + i];
         cp += fminf(lm * xl, lm * xh);
         mp += fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
       }
-      const float conc = fa_wave_sum(cp) + c[sg];
-      const float cmg = fa_wave_sum(mp) + fabsf(c[sg]);
+      const float conc = fa_group_sum<G>(cp) + c[sg];
+      const float cmg = fa_group_sum<G>(mp) + fabsf(c[sg]);
       err[sg] *= 1.f + 2.f * gK;
       low[sg] = conc - err[sg] - g0 * cmg - g1 * fabsf(conc);
     }
-    const float olb = a.out_lb[r], oub = a.out_ub[r];
-    const bool useL = low[0] >= olb;
-    const bool useU = -low[1] <= oub;
-    for (int i = lane; i < n0; i += 64) {
-      if (useL) a.Lc[(size_t)r * n0 + i] = lam[i];
-      if (useU) a.Uc[(size_t)r * n0 + i] = -lam[FA_CROWN_MAXW + i];
-    }
-    if (lane == 0) {
-      if (useL) { a.L0[r] = c[0]; a.Le[r] = err[0]; a.out_lb[r] = low[0]; }
-      if (useU) { a.U0[r] = -c[1]; a.Ue[r] = err[1]; a.out_ub[r] = -low[1]; }
+    if (valid) {
+      const float olb = a.out_lb[r], oub = a.out_ub[r];
+      const bool useL = low[0] >= olb;
+      const bool useU = -low[1] <= oub;
+      for (int i = gl; i < n0; i += G) {
+        if (useL) a.Lc[(size_t)r * n0 + i] = lam[i];
+        if (useU) a.Uc[(size_t)r * n0 + i] = -lam[WP + i];
+      }
+      if (gl == 0) {
+        if (useL) { a.L0[r] = c[0]; a.Le[r] = err[0]; a.out_lb[r] = low[0]; }
+        if (useU) { a.U0[r] = -c[1]; a.Ue[r] = err[1]; a.out_ub[r] = -low[1]; }
+      }
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -192,24 +207,35 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream) {
   if (a.R <= 0) return 0;
   if (!a.layer_lb || !a.layer_ub || !a.Lc || !a.Uc) return -2;
-  for (int l = 0; l <= net.n_layers; ++l)
+  int wmax = 1;
+  for (int l = 0; l <= net.n_layers; ++l) {
     if (net.dims[l] > FA_CROWN_MAXW) return -1;
+    if (l > 0) wmax = std::max(wmax, net.dims[l]);
+  }
+  // group size: smallest power of two >= the widest hidden/output layer (>= 4, <= 64)
+  int G = 4;
+  while (G < wmax && G < 64) G *= 2;
+  const int WP = (std::max(wmax, net.dims[0]) + 3) & ~3;
   int nparams = 0;
   for (int l = 0; l < net.n_layers; ++l) nparams = net.b_off[l] + net.dims[l + 1];
-  const size_t bytes = ((size_t)nparams + (size_t)FA_CROWN_WAVES * 4 * FA_CROWN_MAXW) * sizeof(float);
+  const int rows_per_block = FA_CROWN_WAVES * (64 / G);
+  const size_t bytes = ((size_t)nparams + (size_t)rows_per_block * 4 * WP) * sizeof(float);
   if (bytes > 160 * 1024) return -1;
+  typedef void (*K)(NetDesc, BoundArgs, int, int);
+  K k = G == 4 ? fa_crown_kernel<4> : G == 8 ? fa_crown_kernel<8> : G == 16 ? fa_crown_kernel<16>
+      : G == 32 ? fa_crown_kernel<32> : fa_crown_kernel<64>;
   static std::mutex mu;
-  static size_t raised = 0;
+  static size_t raised[7] = {0, 0, 0, 0, 0, 0, 0};
+  const int gi = G == 4 ? 0 : G == 8 ? 1 : G == 16 ? 2 : G == 32 ? 3 : 4;
   if (bytes > 64 * 1024) {
     std::lock_guard<std::mutex> g(mu);
-    if (bytes > raised) {
-      if (hipFuncSetAttribute((const void*)fa_crown_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) !=
-          hipSuccess)
+    if (bytes > raised[gi]) {
+      if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
         return -3;
-      raised = bytes;
+      raised[gi] = bytes;
     }
   }
-  const int blocks = (int)std::min<long long>(((long long)a.R + FA_CROWN_WAVES - 1) / FA_CROWN_WAVES, 256LL * 8);
-  hipLaunchKernelGGL(fa_crown_kernel, dim3(blocks), dim3(64 * FA_CROWN_WAVES), bytes, stream, net, a, nparams);
+  const int blocks = (int)std::min<long long>(((long long)a.R + rows_per_block - 1) / rows_per_block, 256LL * 8);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * FA_CROWN_WAVES), bytes, stream, net, a, nparams, WP);
   return (int)hipGetLastError();
 }
