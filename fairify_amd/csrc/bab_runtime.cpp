@@ -335,8 +335,14 @@ class BabRuntime {
       b.layer_ub = lay_ub_[slot].p;
     }
     ckl(fa_bounds_launch(net_, b, st), "bounds");
-    // backward output bounds: tighter forms / logit bounds for the certificate
-    if (crown_) ckl(fa_crown_launch(net_, b, st), "crown");
+    // backward output bounds: tighter forms / logit bounds for the certificate.  A network the
+    // kernel cannot hold (layer > 256 wide or weights beyond the LDS budget: -1) keeps the
+    // forward forms, which are sound on their own.
+    if (crown_) {
+      const int rc = fa_crown_launch(net_, b, st);
+      if (rc == -1) crown_ = false;
+      else ckl(rc, "crown");
+    }
   }
 
   // grow pool `i` to hold at least `need` nodes (clamped to cap_; over-capacity children make
