@@ -49,10 +49,10 @@ def main() -> None:
     ap.add_argument("--chunk", type=int, default=4096,
                     help="partitions per work item (big chunks win even for small per-rank shards: a 1/8 "
                          "shard takes 1.02 s per step at 4096 vs 1.76 s at 667, profiles/scaling_emulation.md)")
-    ap.add_argument("--node-budget", type=int, default=384)
+    ap.add_argument("--node-budget", type=int, default=512)
     ap.add_argument("--escalate-budget", type=int, default=8192,
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
-    ap.add_argument("--escalate-max-open", type=int, default=192,
+    ap.add_argument("--escalate-max-open", type=int, default=384,
                     help="escalate only partitions that left <= this many open BaB nodes (0 = all)")
     ap.add_argument("--stages", default="",
                     help="further escalation passes 'budget:max_open,...' after --escalate-budget")

@@ -126,6 +126,8 @@ struct SplitArgs {
   int* part_nodes;                        // [P]
   int* part_open;                         // [P] open nodes left unexpanded when the partition
                                           //     stopped (budget / capacity), or nullptr
+  int* lvl_open;                          // [P] open inner nodes of this level (reset per level)
+  const int* nodes_start;                 // [P] part_nodes at the start of this level
   int budget;
   int m;                                  // requested split dims (children = 2^m)
   float *oxlo, *oxhi, *oxplo, *oxphi;     // output pool

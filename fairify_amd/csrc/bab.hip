@@ -9,6 +9,14 @@
 //                      the pool capacity with device atomics (overflow => partition UNKNOWN).
 //                      Relaxed queries keep a separate x' box for the relaxed features and
 //                      tighten the |x_r - x'_r| <= tau coupling per child (empty children dropped).
+//                      Budget (deterministic): a partition keeps splitting while its node count
+//                      at the START of the level is below the budget (the last level may
+//                      overshoot it); at the first level that starts at or over the budget its
+//                      open nodes are bounded, their candidates emitted, and it goes to
+//                      ST_STOPPING; fa_settle turns it UNKNOWN with open_left = its open inner
+//                      nodes of that level.  No decision depends on the order in which device
+//                      atomics were served (concurrent streams, other GPUs, rank counts).
+// fa_settle            level end: STOPPING -> UNKNOWN (+ open_left), reset the level counters.
 // fa_mark_unknown      time budget hit: every RUNNING partition with live nodes -> UNKNOWN.
 // fa_set_status        host-confirmed SAT partitions -> SAT.
 #include "args.h"
@@ -17,6 +25,7 @@
 #define ST_SAT 1
 #define ST_UNSAT 2
 #define ST_RUNNING 3
+#define ST_STOPPING 4   // out of budget during the current level
 
 __device__ __forceinline__ void fa_tighten(const SplitArgs& a, float* lo, float* hi, float* plo, float* phi) {
   for (int k = 0; k < a.nra; ++k) {
@@ -29,10 +38,7 @@ __device__ __forceinline__ void fa_tighten(const SplitArgs& a, float* lo, float*
 }
 
 // budget / capacity exhausted: the partition ends UNKNOWN with this node left open
-__device__ __forceinline__ void fa_stop(const SplitArgs& a, int p) {
-  a.status[p] = ST_UNKNOWN;
-  if (a.part_open) atomicAdd(&a.part_open[p], 1);
-}
+__device__ __forceinline__ void fa_stop(const SplitArgs& a, int p) { a.status[p] = ST_STOPPING; }
 
 #define FA_SPLIT_THREADS 64
 __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a) {
@@ -40,11 +46,10 @@ __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a)
   if (n >= a.Nn) return;
   const int p = a.part[n];
   if (!a.open[n]) return;
-  if (a.status[p] != ST_RUNNING) {
-    // open node of a partition that already ran out of budget: part of the frontier it left
-    if (a.part_open && a.status[p] == ST_UNKNOWN && !a.leaf[n]) atomicAdd(&a.part_open[p], 1);
-    return;
-  }
+  // RUNNING or STOPPING (budget ran out earlier in this same level): both still active this level
+  const int8_t s0 = a.status[p];
+  if (s0 != ST_RUNNING && s0 != ST_STOPPING) return;
+  if (!a.leaf[n] && a.lvl_open) atomicAdd(&a.lvl_open[p], 1);
   const int n0 = a.n0;
   const float* xl = a.xlo + (size_t)n * n0;
   const float* xh = a.xhi + (size_t)n * n0;
@@ -60,7 +65,7 @@ __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a)
         if (!poss) continue;
         const int slot = atomicAdd(a.cand_count, 1);
         if (slot >= a.cand_cap) {      // cannot confirm this leaf: stay sound
-          a.status[p] = ST_UNKNOWN;
+          fa_stop(a, p);
           return;
         }
         float* cb = a.cand_buf + (size_t)slot * 2 * n0;
@@ -110,9 +115,9 @@ __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a)
   }
   if (m == 0) return;  // no splittable dimension: treated as leaf by the certificate
   const int k = 1 << m;
+  if (a.nodes_start[p] >= a.budget) { fa_stop(a, p); return; }
   if (!a.relaxed) {  // fast path: every child feasible, boxes written on the fly
-    const int old = atomicAdd(&a.part_nodes[p], k);
-    if (old + k > a.budget) { fa_stop(a, p); return; }
+    atomicAdd(&a.part_nodes[p], k);
     const int off = atomicAdd(a.count_out, k);
     if (off + k > a.cap) { fa_stop(a, p); return; }
     for (int c = 0; c < k; ++c) {
@@ -134,7 +139,7 @@ __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a)
   }
   // children feasibility (relaxed coupling can empty a child)
   float clo[64], chi[64], cplo[64], cphi[64];
-  if (n0 > 64) { a.status[p] = ST_UNKNOWN; return; }
+  if (n0 > 64) { fa_stop(a, p); return; }
   int feasible = 0;
   unsigned long long fmask = 0ull;
   for (int c = 0; c < k; ++c) {
@@ -160,8 +165,7 @@ __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a)
     if (ok) { fmask |= (1ull << c); ++feasible; }
   }
   if (feasible == 0) return;
-  const int old = atomicAdd(&a.part_nodes[p], feasible);
-  if (old + feasible > a.budget) { fa_stop(a, p); return; }
+  atomicAdd(&a.part_nodes[p], feasible);
   const int off = atomicAdd(a.count_out, feasible);
   if (off + feasible > a.cap) { fa_stop(a, p); return; }
   int w = off;
@@ -199,7 +203,17 @@ __global__ void fa_mark_unknown_kernel(const int* part, int n, int8_t* status) {
   const int i = blockIdx.x * FA_THREADS + threadIdx.x;
   if (i >= n) return;
   const int p = part[i];
-  if (status[p] == ST_RUNNING) status[p] = ST_UNKNOWN;
+  if (status[p] == ST_RUNNING || status[p] == ST_STOPPING) status[p] = ST_UNKNOWN;
+}
+
+__global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part_open) {
+  const int p = blockIdx.x * FA_THREADS + threadIdx.x;
+  if (p >= P) return;
+  if (status[p] == ST_STOPPING) {
+    status[p] = ST_UNKNOWN;
+    if (part_open) part_open[p] = lvl_open[p];
+  }
+  lvl_open[p] = 0;
 }
 
 __global__ void fa_set_status_kernel(const int* idx, int n, int8_t* status, int8_t v) {
@@ -226,5 +240,12 @@ extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_
   if (n <= 0) return 0;
   hipLaunchKernelGGL(fa_set_status_kernel, dim3((n + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, idx,
                      n, status, v);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, hipStream_t stream) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(fa_settle_kernel, dim3((P + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, P,
+                     status, lvl_open, part_open);
   return (int)hipGetLastError();
 }

@@ -34,6 +34,7 @@ extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
 extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream);
 extern "C" int fa_mark_unknown_launch(const int* part, int n, int8_t* status, hipStream_t stream);
 extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_t v, hipStream_t stream);
+extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, hipStream_t stream);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 
 // defined in bindings.cpp
@@ -150,10 +151,13 @@ class BabRuntime {
     status_.ensure(P);
     nodes_.ensure(P);
     open_left_.ensure(P);
+    lvl_open_.ensure(P);
+    nodes_start_.ensure(P);
     std::vector<int8_t> hstatus(status0.data(), status0.data() + P);
     ck(hipMemcpyAsync(status_.p, hstatus.data(), P, hipMemcpyHostToDevice, st), "cp status");
     ck(hipMemsetAsync(nodes_.p, 0, P * sizeof(int), st), "memset nodes");
     ck(hipMemsetAsync(open_left_.p, 0, P * sizeof(int), st), "memset open_left");
+    ck(hipMemsetAsync(lvl_open_.p, 0, P * sizeof(int), st), "memset lvl_open");
     // initial pool: running partitions
     std::vector<int> run;
     for (int p = 0; p < P; ++p)
@@ -206,6 +210,7 @@ class BabRuntime {
       // every kernel of the previous level has finished (level-end sync), so the next pool
       // can be re-allocated safely: children <= n_in * 2^m
       ensure_pool(nxt, (long long)n_in << m);
+      ck(hipMemcpyAsync(nodes_start_.p, nodes_.p, P * sizeof(int), hipMemcpyDeviceToDevice, st), "cp nodes");
       for (int s = 0; s < n_in; s += batch_) {
         const int nb = std::min(batch_, n_in - s);
         const float* blo = lo_[cur].p + (size_t)s * n0_;
@@ -260,7 +265,9 @@ class BabRuntime {
         sa.pairs = pairs_.p; sa.values = vals_i_.p; sa.npa = npa_;
         for (int k = 0; k < npa_; ++k) sa.pa_idx[k] = pa_[k];
         sa.shared = shared_.p;
-        sa.status = status_.p; sa.part_nodes = nodes_.p; sa.part_open = open_left_.p; sa.budget = budget; sa.m = m;
+        sa.status = status_.p; sa.part_nodes = nodes_.p; sa.part_open = open_left_.p; sa.lvl_open = lvl_open_.p;
+        sa.nodes_start = nodes_start_.p;
+        sa.budget = budget; sa.m = m;
         sa.oxlo = lo_[nxt].p; sa.oxhi = hi_[nxt].p;
         sa.oxplo = relaxed_ ? plo_[nxt].p : nullptr; sa.oxphi = relaxed_ ? phi_[nxt].p : nullptr;
         sa.opart = part_[nxt].p; sa.count_out = counters_.p; sa.cap = pool_[nxt];
@@ -269,6 +276,7 @@ class BabRuntime {
         ckl(fa_split_launch(sa, st), "split");
         launches += relaxed_ ? 6 : 5;
       }
+      ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, st), "settle");
       ck(hipMemcpyAsync(hcount_, counters_.p, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "cp counters");
       ck(hipStreamSynchronize(st), "sync");
       total_nodes += n_in;
@@ -382,9 +390,19 @@ class BabRuntime {
       py::array_t<bool> res = confirm(aparts, abuf).cast<py::array_t<bool>>();
       for (int i = 0; i < n_cand; ++i) ok[i] = res.data()[i] ? 1 : 0;
     }
+    // the device appended candidates in atomic order: pick each partition's witness by a fixed
+    // order (partition, then the pair lexicographically) so the reported pair does not depend
+    // on scheduling
     std::vector<int> newly;
     const float* B = buf.data();
-    for (int i = 0; i < n_cand; ++i) {
+    const size_t w2 = (size_t)2 * n0_;
+    std::vector<int> order(n_cand);
+    for (int i = 0; i < n_cand; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int x, int y) {
+      if (parts[x] != parts[y]) return parts[x] < parts[y];
+      return std::lexicographical_compare(B + x * w2, B + (x + 1) * w2, B + y * w2, B + (y + 1) * w2);
+    });
+    for (int i : order) {
       const int p = parts[i];
       if (!ok[i] || got[p]) continue;
       got[p] = 1;
@@ -421,7 +439,7 @@ class BabRuntime {
   DevBuf<float> gmin_, tstar_, score_, cand_, scores_, pe_lb_, pe_ub_, cand_buf_;
   DevBuf<uint8_t> open_, leaf_;
   DevBuf<int64_t> split_, cv_, co_;
-  DevBuf<int> pe_part_, cand_part_, counters_, nodes_, idx_, open_left_;
+  DevBuf<int> pe_part_, cand_part_, counters_, nodes_, idx_, open_left_, lvl_open_, nodes_start_;
   DevBuf<int8_t> status_;
   int* hcount_ = nullptr;
 };

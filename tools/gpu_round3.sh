@@ -1,0 +1,14 @@
+#!/bin/bash
+# Full GPU test pass (no -x, to see every failure), smoke and the default bench.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r3
+mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?
+tail -15 $O/pytest_gpu.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 3
+tail -1 $O/smoke.log
+timeout -k 10 300 python bench.py --json-out $O/bench.json > $O/bench.log 2>&1 || exit 4
+cat $O/bench.json
