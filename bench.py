@@ -132,21 +132,28 @@ def main() -> None:
 
     pool = ThreadPoolExecutor(max_workers=conc) if conc > 1 else None
 
-    def one_item(k: int, ids: np.ndarray):
+    # measured wall time per (model, chunk slot) from the previous step: the next step schedules
+    # the longest items first (LPT), so the slowest model's chain starts at t=0 instead of after
+    # a wave of cheap items (prior before any measurement: model size)
+    item_cost = {}
+
+    def one_item(k: int, j: int, ids: np.ndarray):
         m, be = models[k], backends[k]
+        t_item = time.time()
         with thread_stream():
             recs = verify_chunk(be, m, q, grid, ids, cfg, timer=timer)
             if info.device.type == "cuda":
                 torch.cuda.current_stream(info.device).synchronize()
+        item_cost[(k, j)] = time.time() - t_item
         c = recs.counts()
         return np.array([len(recs), c["sat"] + c["unsat"], c["sat"], c["unsat"]], dtype=np.float64)
 
     def run_step(step: int):
-        order_k = sorted(range(len(models)), key=lambda k: -models[k].n_neurons)
-        items = [(k, ids) for k in order_k for ids in chunks_for_step(step)]
+        items = [(k, j, ids) for k in range(len(models)) for j, ids in enumerate(chunks_for_step(step))]
+        items.sort(key=lambda it: (-item_cost.get((it[0], it[1]), 0.0), -models[it[0]].n_neurons))
         if pool is None:
-            return sum(one_item(k, ids) for k, ids in items)
-        return sum(f.result() for f in [pool.submit(one_item, k, ids) for k, ids in items])
+            return sum(one_item(k, j, ids) for k, j, ids in items)
+        return sum(f.result() for f in [pool.submit(one_item, k, j, ids) for k, j, ids in items])
 
     sync = (lambda: torch.cuda.synchronize(info.device)) if info.device.type == "cuda" else (lambda: None)
     for w in range(args.warmup):
