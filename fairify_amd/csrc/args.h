@@ -47,6 +47,29 @@ struct FwdArgs {
   int S;
 };
 
+// Lattice coordinate ascent of the residual falsifier (engine/falsify.py), one workgroup per
+// partition: K starts, +-1 moves on the free (non-protected) dims, every PA assignment.
+struct AscentArgs {
+  const float* flat;
+  const float* lo;          // [P, n0]
+  const float* hi;          // [P, n0]
+  const float* x0;          // [P, K, n0] start points
+  const float* f0;          // [P, K] start margins
+  const int* q0;            // [P, K] start pair index
+  int P, K, iters;
+  int V, npa;
+  int pa_idx[FA_MAX_PA];
+  const int64_t* values;    // [V, npa]
+  int Pp;
+  const int64_t* pairs;     // [Pp, 2]
+  int nfree;
+  int free_idx[64];
+  uint8_t* found;           // [P]
+  float* wit_x;             // [P, n0]
+  float* wit_xp;            // [P, n0]
+  int S;
+};
+
 struct SimArgs {
   const float* flat;
   const float* lo;          // [P, n0]

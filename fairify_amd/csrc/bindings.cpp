@@ -20,6 +20,7 @@ extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t 
 extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_forward_launch(const NetDesc& net, FwdArgs a, hipStream_t stream);
 extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream);
+extern "C" int fa_ascent_launch(const NetDesc& net, AscentArgs a, hipStream_t stream);
 extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
 
 template <typename T>
@@ -190,6 +191,36 @@ PYBIND11_MODULE(_C, m) {
     a.wit_xp = P<float>(wit_xp);
     a.z0 = P<float>(z0);
     check(fa_sim_launch(net.d, a, (hipStream_t)stream), "sim");
+  });
+
+  // returns false if the partition's candidate rows do not fit in LDS (caller keeps PyTorch)
+  m.def("ascent", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t x0, uintptr_t f0,
+                     uintptr_t q0, int Pn, int K, int iters, int V, const std::vector<int>& pa, uintptr_t values,
+                     int Pp, uintptr_t pairs, const std::vector<int>& free_dims, uintptr_t found, uintptr_t wit_x,
+                     uintptr_t wit_xp, uintptr_t stream) {
+    if (pa.size() > FA_MAX_PA || free_dims.size() > 64) throw std::invalid_argument("too many PA/free dims");
+    AscentArgs a{};
+    a.flat = P<const float>(flat);
+    a.lo = P<const float>(lo);
+    a.hi = P<const float>(hi);
+    a.x0 = P<const float>(x0);
+    a.f0 = P<const float>(f0);
+    a.q0 = P<const int>(q0);
+    a.P = Pn; a.K = K; a.iters = iters; a.V = V;
+    a.npa = (int)pa.size();
+    for (size_t i = 0; i < pa.size(); ++i) a.pa_idx[i] = pa[i];
+    a.values = P<const int64_t>(values);
+    a.Pp = Pp;
+    a.pairs = P<const int64_t>(pairs);
+    a.nfree = (int)free_dims.size();
+    for (size_t i = 0; i < free_dims.size(); ++i) a.free_idx[i] = free_dims[i];
+    a.found = P<uint8_t>(found);
+    a.wit_x = P<float>(wit_x);
+    a.wit_xp = P<float>(wit_xp);
+    const int rc = fa_ascent_launch(net.d, a, (hipStream_t)stream);
+    if (rc == -1) return false;
+    check(rc, "ascent");
+    return true;
   });
 
   m.def("certify", [](int Nn, int n0, int V, int Pp, int norient, std::vector<uintptr_t> fx, std::vector<uintptr_t> fxp,

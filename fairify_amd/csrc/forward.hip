@@ -8,6 +8,11 @@
 //                     `candidate_dead_nodes`, utils/prune.py:168-192), re-evaluates each point
 //                     under every protected-attribute value (+ relaxed offsets) and records the
 //                     first strict sign flip (K3 + K8 fused).
+// fa_ascent_kernel  : the residual falsifier's lattice coordinate ascent; one workgroup per
+//                     partition keeps its K start points in LDS and runs every iteration
+//                     (K x moves x PA values candidate rows through the MFMA tile forward,
+//                     pair margins, best improving move per start) without leaving the kernel:
+//                     one launch instead of ~10 launches and 2 host syncs per iteration.
 //
 // A 64-row tile goes through all layers in LDS; each layer is a 64 x n_in x n_out GEMM on
 // v_mfma_f32_16x16x4_f32 with bias / ReLU / mask / activation counting fused into the
@@ -226,5 +231,143 @@ extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) 
   if (bytes > 64 * 1024)
     FA_CHECK(hipFuncSetAttribute((const void*)fa_sim_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
   hipLaunchKernelGGL(fa_sim_kernel, dim3(a.P), dim3(FA_THREADS), bytes, stream, net, a);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// margin of a violation for ordered PA pair (vi, vj): min(-N(x, vi), N(x, vj)) > 0 iff strict flip
+__global__ void __launch_bounds__(FA_THREADS) fa_ascent_kernel(NetDesc net, AscentArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int S = a.S;
+  const int n0 = net.dims[0];
+  const int K = a.K, V = a.V;
+  const int nm = 2 * a.nfree;
+  const int per = nm * V;                   // candidate rows per start
+  const int total = K * per;
+  const int p = blockIdx.x;
+  const int tid = threadIdx.x;
+  float* bufA = smem;
+  float* bufB = bufA + FA_TR * S;
+  float* zt = bufB + FA_TR * S;             // [FA_TR]
+  float* X = zt + FA_TR;                    // [K][n0]
+  float* F = X + K * n0;                    // [K]
+  float* zall = F + K;                      // [K * nm * V]
+  float* marg = zall + total;               // [K * nm]
+  float* s_lo = marg + K * nm;              // [n0]
+  float* s_hi = s_lo + n0;
+  int* Q = (int*)(s_hi + n0);               // [K]
+  int* margq = Q + K;                       // [K * nm]
+  int* flag = margq + K * nm;               // [2]: any hit, any change
+  for (int i = tid; i < n0; i += FA_THREADS) {
+    s_lo[i] = a.lo[(size_t)p * n0 + i];
+    s_hi[i] = a.hi[(size_t)p * n0 + i];
+  }
+  for (int i = tid; i < K * n0; i += FA_THREADS) X[i] = a.x0[(size_t)p * K * n0 + i];
+  for (int i = tid; i < K; i += FA_THREADS) {
+    F[i] = a.f0[(size_t)p * K + i];
+    Q[i] = a.q0[(size_t)p * K + i];
+  }
+  __syncthreads();
+  for (int it = 0; it < a.iters && nm > 0; ++it) {
+    if (tid == 0) {
+      int h = 0;
+      for (int s = 0; s < K; ++s) h |= F[s] > 0.f;
+      flag[0] = h;
+      flag[1] = 0;
+    }
+    __syncthreads();
+    if (flag[0]) break;                     // uniform: every thread reads the same LDS word
+    for (int t0 = 0; t0 < total; t0 += FA_TR) {
+      const int nvalid = min(FA_TR, total - t0);
+      for (int i = tid; i < FA_TR * n0; i += FA_THREADS) {
+        const int r = i / n0, d = i % n0;
+        float val = 0.f;
+        const int idx = t0 + r;
+        if (r < nvalid) {
+          const int v = idx % V;
+          const int mv = (idx / V) % nm;
+          const int s = idx / per;
+          val = X[s * n0 + d];
+          if (d == a.free_idx[mv >> 1]) val = fminf(fmaxf(val + ((mv & 1) ? 1.f : -1.f), s_lo[d]), s_hi[d]);
+          for (int k = 0; k < a.npa; ++k)
+            if (a.pa_idx[k] == d) val = (float)a.values[v * a.npa + k];
+        }
+        bufA[r * S + d] = val;
+      }
+      __syncthreads();
+      fa_tile_forward(net, a.flat, bufA, bufB, S, nvalid, nullptr, 0, nullptr, zt);
+      for (int r = tid; r < nvalid; r += FA_THREADS) zall[t0 + r] = zt[r];
+      __syncthreads();
+    }
+    // best pair per (start, move); first index on ties
+    for (int i = tid; i < K * nm; i += FA_THREADS) {
+      const float* z = zall + (size_t)i * V;
+      float g = -INFINITY;
+      int gq = 0;
+      for (int q = 0; q < a.Pp; ++q) {
+        const float m = fminf(-z[a.pairs[2 * q]], z[a.pairs[2 * q + 1]]);
+        if (m > g) { g = m; gq = q; }
+      }
+      marg[i] = g;
+      margq[i] = gq;
+    }
+    __syncthreads();
+    // best improving move per start
+    for (int s = tid; s < K; s += FA_THREADS) {
+      float g = -INFINITY;
+      int gm = 0;
+      for (int mv = 0; mv < nm; ++mv)
+        if (marg[s * nm + mv] > g) { g = marg[s * nm + mv]; gm = mv; }
+      if (g > F[s]) {
+        const int d = a.free_idx[gm >> 1];
+        X[s * n0 + d] = fminf(fmaxf(X[s * n0 + d] + ((gm & 1) ? 1.f : -1.f), s_lo[d]), s_hi[d]);
+        F[s] = g;
+        Q[s] = margq[s * nm + gm];
+        flag[1] = 1;
+      }
+    }
+    __syncthreads();
+    if (!flag[1]) break;
+    __syncthreads();
+  }
+  // witness: the first start with a strictly positive margin
+  __syncthreads();
+  int sh = -1;
+  for (int s = 0; s < K; ++s)
+    if (F[s] > 0.f) { sh = s; break; }
+  if (tid == 0) a.found[p] = sh >= 0;
+  if (sh >= 0) {
+    const int q = Q[sh];
+    const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+    for (int d = tid; d < n0; d += FA_THREADS) {
+      float x = X[sh * n0 + d], xp = x;
+      for (int k = 0; k < a.npa; ++k)
+        if (a.pa_idx[k] == d) {
+          x = (float)a.values[vi * a.npa + k];
+          xp = (float)a.values[vj * a.npa + k];
+        }
+      a.wit_x[(size_t)p * n0 + d] = x;
+      a.wit_xp[(size_t)p * n0 + d] = xp;
+    }
+  }
+}
+
+// 0 on success, -1 if the candidate rows of one partition do not fit in LDS (callers keep the
+// PyTorch path), -3 on bad arguments
+extern "C" int fa_ascent_launch(const NetDesc& net, AscentArgs a, hipStream_t stream) {
+  if (a.P <= 0) return 0;
+  if (a.npa > FA_MAX_PA || a.nfree > 64 || a.K <= 0 || a.V <= 0 || a.Pp <= 0) return -3;
+  a.S = net.max_width | 1;
+  const int n0 = net.dims[0];
+  const size_t nm = 2 * (size_t)a.nfree;
+  const size_t floats = 2 * (size_t)FA_TR * a.S + FA_TR + (size_t)a.K * n0 + a.K + (size_t)a.K * nm * a.V +
+                        (size_t)a.K * nm + 2 * (size_t)n0;
+  size_t bytes = floats * sizeof(float) + ((size_t)a.K + (size_t)a.K * nm + 2) * sizeof(int);
+  bytes = (bytes + 15) & ~(size_t)15;
+  if (bytes > 160 * 1024) return -1;
+  if (bytes > 64 * 1024)
+    FA_CHECK(hipFuncSetAttribute((const void*)fa_ascent_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)bytes));
+  hipLaunchKernelGGL(fa_ascent_kernel, dim3(a.P), dim3(FA_THREADS), bytes, stream, net, a);
   return (int)hipGetLastError();
 }

@@ -14,6 +14,8 @@ the LP-optimal vertex candidates of the BaB miss them.  For those partitions onl
 3. from the ``k_starts`` best points, coordinate ascent on the integer lattice: every ±1 move
    of a non-protected feature (and of the relaxed offset x'_r - x_r within [-tau, tau]) is
    evaluated in one batched forward, the best improving move is taken, ``iters`` rounds.
+   On the HIP path (non-relaxed queries) all rounds run inside one ``fa_ascent_kernel``
+   launch per sub-batch (``csrc/forward.hip``); each partition stops at its first hit.
 
 Hits are only *candidates*: the pipeline confirms them with the exact checker
 (:mod:`fairify_amd.engine.exact`) before a partition becomes SAT.
@@ -133,6 +135,17 @@ def _local_search(be: Backend, q: ResolvedQuery, lo: torch.Tensor, hi: torch.Ten
         cd = D[ar, top]                                                               # [p, k, nra]
         cf = fbest[ar, top]
         cp = pbest[ar, top]
+        if be.hip and not relaxed and nm:
+            from ..ops import hip
+
+            out = hip.ascent(be, q, plo, phi, cx, cf, cp, iters, values, pairs, fdims.tolist())
+            if out is not None:
+                g = torch.nonzero(out[0]).flatten()
+                idx = torch.arange(s0, s0 + p_, device=dev)[g]
+                found[idx] = True
+                wx[idx] = out[1][g]
+                wxp[idx] = out[2][g]
+                continue
         for _ in range(iters if nm else 0):
             if bool((cf > 0).any(dim=1).all()):
                 break

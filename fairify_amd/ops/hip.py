@@ -236,3 +236,34 @@ def simulate(be, q, lo, hi, pids, n_samples, seed, values, pairs, bisect_pairs, 
         boundary_walk(be, q, lo_c, hi_c, pids_c, n_samples, seed, values_c, pairs_c, res, z0, bisect_pairs,
                       bisect_steps)
     return res
+
+
+def ascent(be, q, lo, hi, x0, f0, q0, iters, values, pairs, free_dims):
+    """Lattice coordinate ascent of the residual falsifier in one launch (``fa_ascent_kernel``).
+
+    ``x0`` [P, K, n0] start points, ``f0`` [P, K] their margins, ``q0`` [P, K] pair indices.
+    Returns ``(found [P] bool, wit_x [P, n0], wit_xp [P, n0])``, or ``None`` when one partition's
+    candidate rows do not fit in LDS (the caller then runs the PyTorch loop)."""
+    P, K, n0 = x0.shape
+    dev = x0.device
+    lo_c = _c(lo, torch.float32, (P, n0), "lo")
+    hi_c = _c(hi, torch.float32, (P, n0), "hi")
+    x0_c = _c(x0, torch.float32, (P, K, n0), "x0")
+    f0_c = _c(f0, torch.float32, (P, K), "f0")
+    q0_c = _c(q0, torch.int32, (P, K), "q0")
+    V = values.shape[0]
+    Pp = pairs.shape[0]
+    values_c = _c(values, torch.int64, None, "values")
+    pairs_c = _c(pairs, torch.int64, (Pp, 2), "pairs")
+    found = torch.zeros(P, dtype=torch.uint8, device=dev)
+    wx = torch.zeros(P, n0, dtype=torch.float32, device=dev)
+    wxp = torch.zeros(P, n0, dtype=torch.float32, device=dev)
+    if P == 0:
+        return found.bool(), wx, wxp
+    ok = ext().ascent(_net(be), be.flat.data_ptr(), lo_c.data_ptr(), hi_c.data_ptr(), x0_c.data_ptr(),
+                      f0_c.data_ptr(), q0_c.data_ptr(), P, K, int(iters), V, list(q.pa_idx), values_c.data_ptr(),
+                      Pp, pairs_c.data_ptr(), [int(d) for d in free_dims], found.data_ptr(), wx.data_ptr(),
+                      wxp.data_ptr(), _stream(dev))
+    if not ok:
+        return None
+    return found.bool(), wx, wxp
