@@ -10,8 +10,8 @@
 // bounds are two multiplier vectors processed together.  On the deep AC shapes this halves the
 // open branch-and-bound frontier (tools/diag_open_nodes.py --bound crown).
 //
-// Layout: the row-major weights + biases (the `flat` prefix [W_0|b_0|W_1|b_1|...]) are staged
-// once per workgroup in LDS; a group of G lanes (G = widest layer rounded up to a power of two,
+// Layout: the weights + biases (the `flat` prefix [W_0|b_0|W_1|b_1|...], each W_l transposed to
+// [n_out][n_in]) are staged once per workgroup in LDS; a group of G lanes (G = widest layer rounded up to a power of two,
 // 4..64) owns a row and a slab [lambda(2) | mu(2)] x WP.  Per layer: lanes over the layer's
 // neurons form mu = lambda * slope (+ chord intercepts), then lanes over the layer's inputs
 // form lambda' = W mu (and |W| |mu| for the rounding term).
@@ -52,13 +52,28 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int RPW = 64 / G;                                 // rows per wave
   const int tid = threadIdx.x;
-  for (int e = tid; e < nparams; e += 64 * FA_CROWN_WAVES) smem[e] = a.flat[e];
+  // stage W_l TRANSPOSED ([n_out][n_in]) so the lambda' = W mu loop (lanes over inputs i, loop
+  // over outputs j) reads consecutive LDS words across lanes: the row-major copy made lanes
+  // stride by n_out words (8-way bank conflicts for 100-wide layers, ~1/3 of the kernel's cycles
+  // waiting on LDS, profiles/pmc/)
+  for (int l = 0; l < net.n_layers; ++l) {
+    const int nin = net.dims[l], nout = net.dims[l + 1];
+    const float* src = a.flat + net.w_off[l];
+    float* dst = smem + net.w_off[l];
+    for (int e = tid; e < nin * nout; e += 64 * FA_CROWN_WAVES) {
+      const int j = e / nin, i = e - j * nin;
+      dst[e] = src[(size_t)i * nout + j];
+    }
+    for (int e = tid; e < nout; e += 64 * FA_CROWN_WAVES) smem[net.b_off[l] + e] = a.flat[net.b_off[l] + e];
+  }
   __syncthreads();
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int grp = lane / G;
   const int gl = lane % G;
-  float* lam = smem + nparams + (wave * RPW + grp) * 4 * WP;   // [2][WP]
+  // per-row slabs at an odd stride: groups of one wave reading lam/mu[j] at the same j hit
+  // different banks
+  float* lam = smem + nparams + (wave * RPW + grp) * (4 * WP + 1);   // [2][WP]
   float* mu = lam + 2 * WP;                                    // [2][WP]
   const int L = net.n_layers;
   const int n0 = net.dims[0];
@@ -123,9 +138,8 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
       const float gn = fa_gam(n + 1, u);
       for (int i = gl; i < nin; i += G) {
         float acc0 = 0.f, acc1 = 0.f, mag0 = 0.f, mag1 = 0.f;
-        const float* Wi = W + (size_t)i * n;
         for (int j = 0; j < n; ++j) {
-          const float w = Wi[j];
+          const float w = W[(size_t)j * nin + i];   // W^T in LDS
           const float m0 = mu[j], m1 = mu[WP + j];
           acc0 = fmaf(w, m0, acc0);
           acc1 = fmaf(w, m1, acc1);
@@ -219,7 +233,7 @@ extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stre
   int nparams = 0;
   for (int l = 0; l < net.n_layers; ++l) nparams = net.b_off[l] + net.dims[l + 1];
   const int rows_per_block = FA_CROWN_WAVES * (64 / G);
-  const size_t bytes = ((size_t)nparams + (size_t)rows_per_block * 4 * WP) * sizeof(float);
+  const size_t bytes = ((size_t)nparams + (size_t)rows_per_block * (4 * WP + 1)) * sizeof(float);
   if (bytes > 160 * 1024) return -1;
   typedef void (*K)(NetDesc, BoundArgs, int, int);
   K k = G == 4 ? fa_crown_kernel<4> : G == 8 ? fa_crown_kernel<8> : G == 16 ? fa_crown_kernel<16>
