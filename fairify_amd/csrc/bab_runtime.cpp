@@ -134,6 +134,17 @@ class BabRuntime {
     cand_part_.ensure(cand_cap_);
     counters_.ensure(2);
     ck(hipHostMalloc((void**)&hcount_, 2 * sizeof(int)), "hipHostMalloc");
+    // host fp64 copy of [W_0|b_0|W_1|b_1|...] for the native exact confirmation
+    int np_ = 0;
+    for (int l = 0; l < net_.n_layers; ++l) np_ = std::max(np_, net_.b_off[l] + net_.dims[l + 1]);
+    std::vector<float> hf(np_);
+    ck(hipMemcpy(hf.data(), flat_, np_ * sizeof(float), hipMemcpyDeviceToHost), "cp weights");
+    hw_.assign(hf.begin(), hf.end());
+    is_pa_.assign(n0_, 0);
+    is_ra_.assign(n0_, 0);
+    for (int k : pa_) is_pa_[k] = 1;
+    if (relaxed_)
+      for (int k : ra_) is_ra_[k] = 1;
   }
   ~BabRuntime() {
     if (hcount_) hipHostFree(hcount_);
@@ -142,8 +153,12 @@ class BabRuntime {
   py::tuple solve(py::array_t<float, py::array::c_style | py::array::forcecast> lo,
                   py::array_t<float, py::array::c_style | py::array::forcecast> hi,
                   py::array_t<int8_t, py::array::c_style | py::array::forcecast> status0, int budget,
-                  double time_budget, uintptr_t dead_part, py::object confirm, uintptr_t stream_i) {
+                  double time_budget, uintptr_t dead_part, py::object confirm, uintptr_t stream_i,
+                  bool native_exact) {
     hipStream_t st = (hipStream_t)stream_i;
+    native_exact_ = native_exact;
+    box_lo_ = lo.data();
+    box_hi_ = hi.data();
     const auto t0 = std::chrono::steady_clock::now();
     const int P = (int)lo.shape(0);
     if (lo.ndim() != 2 || lo.shape(1) != n0_ || hi.shape(0) != P || status0.shape(0) != P)
@@ -381,14 +396,32 @@ class BabRuntime {
     ck(hipMemcpyAsync(parts.data(), cand_part_.p, sizeof(int) * n_cand, hipMemcpyDeviceToHost, st), "cp");
     ck(hipStreamSynchronize(st), "sync");
     std::vector<char> ok(n_cand, 0);
-    {
+    // native exact check (no GIL): pair constraints + fp64 logits with a rigorous rounding
+    // bound; only pairs whose sign the bound cannot settle go to the Python callback
+    // (exact rational arithmetic), as do all pairs of per-partition (masked) networks
+    std::vector<int> ask;
+    if (native_exact_) {
+      for (int i = 0; i < n_cand; ++i) {
+        const int r = exact_check(buf.data() + (size_t)i * 2 * n0_, parts[i]);
+        if (r < 0) ask.push_back(i);
+        else ok[i] = (char)r;
+      }
+    } else {
+      ask.resize(n_cand);
+      for (int i = 0; i < n_cand; ++i) ask[i] = i;
+    }
+    if (!ask.empty()) {
       py::gil_scoped_acquire gil;
-      py::array_t<float> abuf({n_cand, 2 * n0_});
-      py::array_t<int> aparts(n_cand);
-      std::memcpy(abuf.mutable_data(), buf.data(), sizeof(float) * buf.size());
-      std::memcpy(aparts.mutable_data(), parts.data(), sizeof(int) * parts.size());
+      const int na = (int)ask.size();
+      py::array_t<float> abuf({na, 2 * n0_});
+      py::array_t<int> aparts(na);
+      for (int k = 0; k < na; ++k) {
+        std::memcpy(abuf.mutable_data() + (size_t)k * 2 * n0_, buf.data() + (size_t)ask[k] * 2 * n0_,
+                    sizeof(float) * 2 * n0_);
+        aparts.mutable_data()[k] = parts[ask[k]];
+      }
       py::array_t<bool> res = confirm(aparts, abuf).cast<py::array_t<bool>>();
-      for (int i = 0; i < n_cand; ++i) ok[i] = res.data()[i] ? 1 : 0;
+      for (int k = 0; k < na; ++k) ok[ask[k]] = res.data()[k] ? 1 : 0;
     }
     // the device appended candidates in atomic order: pick each partition's witness by a fixed
     // order (partition, then the pair lexicographically) so the reported pair does not depend
@@ -420,8 +453,69 @@ class BabRuntime {
     }
   }
 
+  // sign of the exact logit at integer point x: +1 / -1, 0 for exactly zero is never returned
+  // (an ambiguous |z| <= err gives 2 = "ask the exact rational check")
+  int exact_sign(const double* x) const {
+    const int L = net_.n_layers;
+    std::vector<double> h(x, x + n0_), m(n0_), e(n0_, 0.0), hn, mn, en;
+    for (int i = 0; i < n0_; ++i) m[i] = std::fabs(h[i]);
+    const double u = std::ldexp(1.0, -53);
+    for (int l = 0; l < L; ++l) {
+      const int nin = net_.dims[l], nout = net_.dims[l + 1];
+      const double* W = hw_.data() + net_.w_off[l];
+      const double* b = hw_.data() + net_.b_off[l];
+      const double ku = (nin + 3) * u;
+      const double g = ku / (1.0 - ku);
+      hn.assign(nout, 0.0); mn.assign(nout, 0.0); en.assign(nout, 0.0);
+      for (int j = 0; j < nout; ++j) {
+        double z = b[j], mm = std::fabs(b[j]), ee = g * std::fabs(b[j]);
+        for (int i = 0; i < nin; ++i) {
+          const double w = W[(size_t)i * nout + j];
+          z += h[i] * w;
+          mm += m[i] * std::fabs(w);
+          ee += (e[i] + g * m[i]) * std::fabs(w);
+        }
+        if (l < L - 1) { z = std::max(z, 0.0); mm = std::max(mm, 0.0); }
+        hn[j] = z; mn[j] = mm; en[j] = ee;
+      }
+      h.swap(hn); m.swap(mn); e.swap(en);
+    }
+    const double err = e[0] * 1.0001 + 1e-300;
+    if (std::fabs(h[0]) <= err) return 2;
+    return h[0] > 0 ? 1 : -1;
+  }
+
+  // 1 violation, 0 not a violation, -1 undecided here (Python exact check)
+  int exact_check(const float* pair, int p) const {
+    std::vector<double> x(n0_), xp(n0_);
+    const float* lo = box_lo_ + (size_t)p * n0_;
+    const float* hi = box_hi_ + (size_t)p * n0_;
+    for (int d = 0; d < n0_; ++d) {
+      x[d] = std::nearbyint((double)pair[d]);
+      xp[d] = std::nearbyint((double)pair[n0_ + d]);
+      if (x[d] < lo[d] || x[d] > hi[d]) return 0;
+      if (is_pa_[d]) {
+        if (x[d] == xp[d] || xp[d] < lo[d] || xp[d] > hi[d]) return 0;
+      } else if (is_ra_[d]) {
+        if (std::fabs(x[d] - xp[d]) > tau_) return 0;
+      } else if (x[d] != xp[d]) {
+        return 0;
+      }
+    }
+    const int sx = exact_sign(x.data());
+    if (sx == 2) return -1;
+    const int sp = exact_sign(xp.data());
+    if (sp == 2) return -1;
+    return sx * sp < 0 ? 1 : 0;
+  }
+
   NetDesc net_;
   const float* flat_;
+  std::vector<double> hw_;
+  std::vector<char> is_pa_, is_ra_;
+  bool native_exact_ = false;
+  const float* box_lo_ = nullptr;
+  const float* box_hi_ = nullptr;
   std::vector<int> pa_, ra_;
   float tau_;
   int cap_, batch_, cand_cap_;
@@ -452,5 +546,6 @@ void register_bab(py::module& m) {
            py::arg("pairs"), py::arg("ra"), py::arg("tau"), py::arg("shared"), py::arg("capacity"),
            py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"), py::arg("crown") = true)
       .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
-           py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"));
+           py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"),
+           py::arg("native_exact") = false);
 }

@@ -340,7 +340,7 @@ class BaBSolver:
         with self.tm("bab.native"):
             st, cx, cxp, nodes, stats = rt.solve(lo_np.astype(np.float32), hi_np.astype(np.float32), status,
                                                   int(self.cfg.node_budget), float(self.cfg.time_budget), dead_ptr,
-                                                  confirm, stream)
+                                                  confirm, stream, exact_models is None)
         self.stats = dict(stats)
         return BaBResult(np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes),
                          int(stats["levels"]), time.time() - t0, open_left=np.asarray(stats["open_left"]))

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Native exact confirmation in the BaB runtime: GPU suite, bench, 1/8 shard.
+set -eo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/nexact
+mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+run() {
+  tag=$1; shift
+  timeout -k 10 300 python bench.py "$@" --json-out $O/$tag.json > $O/$tag.log 2>&1
+  python -c "import json; d=json.load(open('$O/$tag.json')); print('$tag', '$*', d['ms_per_step'], d['value'], d['pct_verified'])"
+}
+run full --steps 2
+run full_b --steps 2
+run s8 --emulate-shard 0/8 --steps 3
+run s8b --emulate-shard 7/8 --steps 3
