@@ -66,24 +66,25 @@ struct SymBox {
   }
 };
 
-// per-wave LDS slab: tile staging T[2 blocks][16 neurons][TS] + box values [3][48]
+// per-wave LDS slab: tile staging T[2 blocks][16 neurons][TS] + box values [2 boxes][3][48]
 template <int NT>
 struct SymSlab {
   static constexpr int TS = 16 * NT + 4;                 // padded row stride (floats)
   static constexpr int TILE1 = 2 * 16 * TS;             // one 16-neuron tile, U and L blocks
   static constexpr int TILE = 2 * TILE1;                 // two tiles per epilogue pass
   static constexpr int BOX = 3 * FA_SYM_MAXC;
-  static constexpr int FLOATS = (TILE + BOX + 3) & ~3;
+  static constexpr int FLOATS = (TILE + 2 * BOX + 3) & ~3;    // two boxes (paired-row variant)
 };
 
 // Epilogue of one 16-neuron output tile (accumulators U, Lq of tile jt): spill to the wave's
 // LDS slab, one lane per (neuron, block) computes the rigorous bounds and the ReLU relaxation
 // once, the new form rows are reloaded in MFMA operand layout into (nu, nlo).  Returns false on
 // the last layer (outputs written, nothing to reload).
-template <int NT>
+template <int NT, bool PAIR>
 __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
-                                                const float* smem, float* T, const float* bxv, const int* cdim_s,
-                                                int l, int r, int node, int lane, int jt0, const f32x4 (&U)[2][NT],
+                                                const float* smem, float* T, const float* bxv_in, const int* cdim_s,
+                                                int l, int r_in, int node_in, int r2, int node2, bool v2, int lane,
+                                                int jt0, const f32x4 (&U)[2][NT],
                                                 const f32x4 (&Lq)[2][NT], float (&nu)[2][NT][4],
                                                 float (&nlo)[2][NT][4]) {
   constexpr int TS = SymSlab<NT>::TS;
@@ -100,11 +101,16 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
   const int nc = cfg.nc;
   const int n0 = net.dims[0];
   // neuron lane role in the epilogue: tile jt0 + (lane >> 5); within it lanes 0-15 = U block,
-  // 16-31 = L block of neuron (lane & 15) -- all 64 lanes busy for two output tiles
+  // 16-31 = L block of neuron (lane & 15) -- all 64 lanes busy for two output tiles.  PAIR: the
+  // two tiles are the same neurons of two box rows (r_in, r2), each with its own box values
   const int tsub = lane >> 5;
-  const int jt = jt0 + tsub;
+  const bool second = PAIR && tsub;
+  const int r = second ? r2 : r_in;
+  const int node = second ? node2 : node_in;
+  const float* bxv = bxv_in + (second ? SymSlab<NT>::BOX : 0);
+  const int jt = PAIR ? jt0 : jt0 + tsub;
   const int n_out_t = net.dims[l + 1];
-  const bool nl_act = 16 * jt < n_out_t;
+  const bool nl_act = 16 * jt < n_out_t && (!second || v2);
   const int ob = (lane >> 4) & 1;
   float* Trow = T + tsub * SymSlab<NT>::TILE1 + (ob * 16 + col) * TS;
     // ---------------- spill both tiles: T[tile][block][neuron][column]
@@ -237,12 +243,15 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
     return true;
 }
 
-template <int NT, int TM>
+// PAIR (TM == 1 only): the wave carries two box rows; operand/accumulator slot u (the "tile"
+// index) is the box, both use output tile 0 of W.
+template <int NT, int TM, bool PAIR>
 __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
                                              const float* smem, float* T, const float* bxv, const int* cdim_s,
-                                             int l, int r,
-                                             int node, int lane, const float (&B)[NT][TM][2][4],
-                                             float (&A)[NT][TM][2][4]) {
+                                             int l, int r, int node, int r2, int node2, bool v2, int lane,
+                                             const float (&B)[NT][PAIR ? 2 : TM][2][4],
+                                             float (&A)[NT][PAIR ? 2 : TM][2][4]) {
+  constexpr int TMS = PAIR ? 2 : TM;
   constexpr int TS = SymSlab<NT>::TS;
   const int col = lane & 15, grp = lane >> 4;
   const int n_in = net.dims[l], n_out = net.dims[l + 1];
@@ -268,9 +277,12 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
     // 15 rows are padding.  Lane (grp, col) sums its 4*tin neurons k = 16t + 4 grp + i for its
     // form column; two cross-group butterflies finish the sum (any summation order stays within
     // the layer's gamma_{2 n_in + 1} bound).  W[k][0] is lane (grp*16) of the permuted block.
-    float su[NT], sl[NT];
+    constexpr int NB = PAIR ? 2 : 1;   // boxes carried by the wave
+    float su[NB][NT], sl[NB][NT];
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct) su[ct] = sl[ct] = 0.f;
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) su[bi][ct] = sl[bi][ct] = 0.f;
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
       if (t >= tin) break;
@@ -280,25 +292,33 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
       for (int i = 0; i < 4; ++i) {
         const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
-          su[ct] = fmaf(wp, B[ct][t][0][i], fmaf(wn, B[ct][t][1][i], su[ct]));
-          sl[ct] = fmaf(wp, B[ct][t][1][i], fmaf(wn, B[ct][t][0][i], sl[ct]));
-        }
+        for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+          for (int ct = 0; ct < NT; ++ct) {
+            const int bt = PAIR ? bi : t;
+            su[bi][ct] = fmaf(wp, B[ct][bt][0][i], fmaf(wn, B[ct][bt][1][i], su[bi][ct]));
+            sl[bi][ct] = fmaf(wp, B[ct][bt][1][i], fmaf(wn, B[ct][bt][0][i], sl[bi][ct]));
+          }
       }
     }
     f32x4 U[2][NT], Lq[2][NT];
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct) {
-      su[ct] += __shfl_xor(su[ct], 16, 64);
-      sl[ct] += __shfl_xor(sl[ct], 16, 64);
-      su[ct] += __shfl_xor(su[ct], 32, 64);
-      sl[ct] += __shfl_xor(sl[ct], 32, 64);
-      U[0][ct] = f32x4{grp == 0 ? su[ct] : 0.f, 0.f, 0.f, 0.f};     // row 0 of tile 0 = neuron 0
-      Lq[0][ct] = f32x4{grp == 0 ? sl[ct] : 0.f, 0.f, 0.f, 0.f};
-      U[1][ct] = Lq[1][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int ct = 0; ct < NT; ++ct) U[1][ct] = Lq[1][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        float xu = su[bi][ct], xl = sl[bi][ct];
+        xu += __shfl_xor(xu, 16, 64);
+        xl += __shfl_xor(xl, 16, 64);
+        xu += __shfl_xor(xu, 32, 64);
+        xl += __shfl_xor(xl, 32, 64);
+        U[bi][ct] = f32x4{grp == 0 ? xu : 0.f, 0.f, 0.f, 0.f};     // row 0 of tile bi = neuron 0
+        Lq[bi][ct] = f32x4{grp == 0 ? xl : 0.f, 0.f, 0.f, 0.f};
+      }
     float nu[2][NT][4], nlo[2][NT][4];
-    fa_sym_epilogue<NT>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, lane, 0, U, Lq, nu, nlo);
+    fa_sym_epilogue<NT, PAIR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq, nu,
+                              nlo);
     return;
   }
 #endif
@@ -314,8 +334,8 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
         U[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
         Lq[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if (jt >= tout || jt >= TM) continue;
-      const float4* wq = reinterpret_cast<const float4*>(sw) + (size_t)jt * tin * 64 + lane;
+      if (PAIR ? (jt0 > 0) : (jt >= tout || jt >= TM)) continue;
+      const float4* wq = reinterpret_cast<const float4*>(sw) + (size_t)(PAIR ? 0 : jt) * tin * 64 + lane;
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
         if (t >= tin) break;
@@ -326,7 +346,8 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
           const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
 #pragma unroll
           for (int ct = 0; ct < NT; ++ct) {
-            const float bu = B[ct][t][0][i], bl = B[ct][t][1][i];
+            const int bt = PAIR ? u : t;
+            const float bu = B[ct][bt][0][i], bl = B[ct][bt][1][i];
             U[u][ct] = fa_mfma4(wp, bu, U[u][ct]);
             Lq[u][ct] = fa_mfma4(wp, bl, Lq[u][ct]);
             U[u][ct] = fa_mfma4(wn, bl, U[u][ct]);
@@ -352,11 +373,13 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
       continue;
     }
 #else
-    if (!fa_sym_epilogue<NT>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, lane, jt0, U, Lq, nu, nlo)) continue;
+    if (!fa_sym_epilogue<NT, PAIR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, jt0, U, Lq,
+                                   nu, nlo))
+      continue;
 #endif
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      if (jt0 + u >= TM) break;
+      if (jt0 + u >= TMS) break;
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
@@ -368,8 +391,9 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
   }
 }
 
-template <int NT, int TM>
+template <int NT, int TM, bool PAIR>
 __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
+  constexpr int TMS = PAIR ? 2 : TM;   // operand slots: K tiles, or (PAIR) the wave's two boxes
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   // ---- stage the MFMA-operand-order weights + biases (pre-permuted in `flat`) into LDS
@@ -399,34 +423,45 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundAr
     role[ct] = c == 0 ? 1 : c == 1 ? 2 : c == 2 ? 3 : c == 3 ? 4 : (c - 4 < nc ? 0 : 5);
     cdm[ct] = (role[ct] == 0) ? cdim_s[c - 4] : -1;
   }
-  for (int r0 = blockIdx.x * nw + wave; r0 < a.R; r0 += gridDim.x * nw) {
+  constexpr int RPW = PAIR ? 2 : 1;   // box rows per wave and pass
+  for (int r0 = (blockIdx.x * nw + wave) * RPW; r0 < a.R; r0 += gridDim.x * nw * RPW) {
     const int r = __builtin_amdgcn_readfirstlane(r0);
-    SymBox bx;
-    bx.a = &a;
-    bx.n0 = n0;
-    bx.node = a.V > 0 ? r / a.V : r;
-    bx.v = a.V > 0 ? r - bx.node * a.V : 0;
-    if (lane < FA_SYM_MAXC) {   // box values per column (0 on non-coefficient columns)
-      const int d = (lane >= 4 && lane - 4 < nc) ? cdim_s[lane - 4] : -1;
-      const float l0 = d >= 0 ? bx.lo(d) : 0.f, h0 = d >= 0 ? bx.hi(d) : 0.f;
-      bxv[lane] = l0;
-      bxv[FA_SYM_MAXC + lane] = h0;
-      bxv[2 * FA_SYM_MAXC + lane] = fmaxf(fabsf(l0), fabsf(h0));
+    const bool v2 = PAIR && r + 1 < a.R;           // second row valid (else it shadows r, no writes)
+    const int rb = v2 ? r + 1 : r;
+    SymBox bxs[2];
+#pragma unroll
+    for (int bi = 0; bi < RPW; ++bi) {
+      SymBox& bx = bxs[bi];
+      const int rr = bi ? rb : r;
+      bx.a = &a;
+      bx.n0 = n0;
+      bx.node = a.V > 0 ? rr / a.V : rr;
+      bx.v = a.V > 0 ? rr - bx.node * a.V : 0;
+      if (lane < FA_SYM_MAXC) {   // box values per column (0 on non-coefficient columns)
+        float* bv = bxv + bi * SymSlab<NT>::BOX;
+        const int d = (lane >= 4 && lane - 4 < nc) ? cdim_s[lane - 4] : -1;
+        const float l0 = d >= 0 ? bx.lo(d) : 0.f, h0 = d >= 0 ? bx.hi(d) : 0.f;
+        bv[lane] = l0;
+        bv[FA_SYM_MAXC + lane] = h0;
+        bv[2 * FA_SYM_MAXC + lane] = fmaxf(fabsf(l0), fabsf(h0));
+      }
     }
-    float XA[NT][TM][2][4], XB[NT][TM][2][4];
+    const SymBox& bx = bxs[0];
+    float XA[NT][TMS][2][4], XB[NT][TMS][2][4];
     // ---- layer-0 operands: identity forms (folded dims -> constant) + [hi | lo] interval rows;
     //      L-block error columns negated
 #pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      if (t >= tin0) break;
+    for (int t = 0; t < TMS; ++t) {
+      if (!PAIR && t >= tin0) break;
+      const SymBox& bt = bxs[PAIR ? t : 0];   // PAIR: slot t = box t (n0 <= 16: one K tile)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int k = 16 * t + 4 * grp + i;
+        const int k = (PAIR ? 0 : 16 * t) + 4 * grp + i;
         float xl = 0.f, xh = 0.f;
         const bool kv = k < n0;
         if (kv) {
-          xl = bx.lo(k);
-          xh = bx.hi(k);
+          xl = bt.lo(k);
+          xh = bt.hi(k);
         }
         const bool folded = kv && ((cfg.fold >> k) & 1ull);
         const float m = fmaxf(fabsf(xl), fabsf(xh));
@@ -451,9 +486,11 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundAr
     __builtin_amdgcn_wave_barrier();
     for (int l = 0; l < net.n_layers; ++l) {
       if (l & 1)
-        fa_sym_layer<NT, TM>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, lane, XB, XA);
+        fa_sym_layer<NT, TM, PAIR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
+                                   lane, XB, XA);
       else
-        fa_sym_layer<NT, TM>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, lane, XA, XB);
+        fa_sym_layer<NT, TM, PAIR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
+                                   lane, XA, XB);
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -468,9 +505,18 @@ namespace {
 
 typedef void (*SymKernel)(NetDesc, BoundArgs, SymCfg);
 
-template <int NT, int TM>
+template <int NT, int TM, bool PAIR = false>
 SymKernel sym_ptr() {
-  return fa_sym_kernel<NT, TM>;
+  return fa_sym_kernel<NT, TM, PAIR>;
+}
+
+// two box rows per wave for single-tile networks (FAIRIFY_SYM_PAIR=0 turns it off for A/B runs)
+bool use_pair() {
+  static const bool v = [] {
+    const char* e = getenv("FAIRIFY_SYM_PAIR");
+    return !(e && *e == '0');
+  }();
+  return v;
 }
 
 // widest layer (in 16-neuron tiles) served by the register-resident kernel; FAIRIFY_SYM_MAX_TM
@@ -487,7 +533,7 @@ SymKernel select_kernel(int NT, int TM) {
   if (TM > max_tm()) return nullptr;
   switch (NT) {
     case 1:
-      if (TM <= 1) return sym_ptr<1, 1>();
+      if (TM <= 1) return use_pair() ? sym_ptr<1, 1, true>() : sym_ptr<1, 1>();
       if (TM <= 2) return sym_ptr<1, 2>();
       if (TM <= 4) return sym_ptr<1, 4>();
       if (TM <= 7) return sym_ptr<1, 7>();
@@ -565,7 +611,8 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
     case 2: slab = SymSlab<2>::FLOATS; break;
     default: slab = SymSlab<3>::FLOATS; break;
   }
-  const int threads = FA_THREADS, rows_per_block = FA_THREADS / 64;
+  const bool pair = k == sym_ptr<1, 1, true>();   // two box rows per wave
+  const int threads = FA_THREADS, rows_per_block = (FA_THREADS / 64) * (pair ? 2 : 1);
   const size_t bytes = (size_t)(off + (FA_THREADS / 64) * slab) * sizeof(float);
   if (bytes > 160 * 1024) return 0;
   // per (kernel, LDS bytes): raise the dynamic-LDS limit once and cache the occupancy
