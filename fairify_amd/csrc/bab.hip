@@ -16,7 +16,8 @@
 //                      ST_STOPPING; fa_settle turns it UNKNOWN with open_left = its open inner
 //                      nodes of that level.  No decision depends on the order in which device
 //                      atomics were served (concurrent streams, other GPUs, rank counts).
-// fa_settle            level end: STOPPING -> UNKNOWN (+ open_left), reset the level counters.
+// fa_settle            level end: STOPPING -> UNKNOWN (+ open_left), next level's budget reference,
+//                      level counters to pinned host memory, next counter slot cleared.
 // fa_mark_unknown      time budget hit: every RUNNING partition with live nodes -> UNKNOWN.
 // fa_set_status        host-confirmed SAT partitions -> SAT.
 #include "args.h"
@@ -206,14 +207,23 @@ __global__ void fa_mark_unknown_kernel(const int* part, int n, int8_t* status) {
   if (status[p] == ST_RUNNING || status[p] == ST_STOPPING) status[p] = ST_UNKNOWN;
 }
 
-__global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part_open) {
+__global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
+                                 int* nodes_start, const int* counters_cur, int* counters_next, int* host_counts) {
   const int p = blockIdx.x * FA_THREADS + threadIdx.x;
+  if (p == 0) {
+    // level counters straight into pinned host memory (no blit per level), next slot cleared
+    __hip_atomic_store(&host_counts[0], counters_cur[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host_counts[1], counters_cur[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    counters_next[0] = 0;
+    counters_next[1] = 0;
+  }
   if (p >= P) return;
   if (status[p] == ST_STOPPING) {
     status[p] = ST_UNKNOWN;
     if (part_open) part_open[p] = lvl_open[p];
   }
   lvl_open[p] = 0;
+  nodes_start[p] = part_nodes[p];     // the next level's budget reference
 }
 
 __global__ void fa_set_status_kernel(const int* idx, int n, int8_t* status, int8_t v) {
@@ -243,9 +253,11 @@ extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_
   return (int)hipGetLastError();
 }
 
-extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, hipStream_t stream) {
-  if (P <= 0) return 0;
-  hipLaunchKernelGGL(fa_settle_kernel, dim3((P + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, P,
-                     status, lvl_open, part_open);
+extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
+                                int* nodes_start, const int* counters_cur, int* counters_next, int* host_counts,
+                                hipStream_t stream) {
+  const int n = P > 0 ? P : 1;
+  hipLaunchKernelGGL(fa_settle_kernel, dim3((n + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, P,
+                     status, lvl_open, part_open, part_nodes, nodes_start, counters_cur, counters_next, host_counts);
   return (int)hipGetLastError();
 }

@@ -34,7 +34,9 @@ extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
 extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream);
 extern "C" int fa_mark_unknown_launch(const int* part, int n, int8_t* status, hipStream_t stream);
 extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_t v, hipStream_t stream);
-extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, hipStream_t stream);
+extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
+                                int* nodes_start, const int* counters_cur, int* counters_next, int* host_counts,
+                                hipStream_t stream);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 
 // defined in bindings.cpp
@@ -132,8 +134,9 @@ class BabRuntime {
     pe_part_.ensure(2 * (size_t)batch_);
     cand_buf_.ensure((size_t)cand_cap_ * 2 * n0_);
     cand_part_.ensure(cand_cap_);
-    counters_.ensure(2);
-    ck(hipHostMalloc((void**)&hcount_, 2 * sizeof(int)), "hipHostMalloc");
+    counters_.ensure(4);   // two slots of (children, candidates), alternating per level
+    // fine-grained (coherent) pinned words: the settle kernel writes the level counters here
+    ck(hipHostMalloc((void**)&hcount_, 2 * sizeof(int), hipHostMallocCoherent), "hipHostMalloc");
     // host fp64 copy of [W_0|b_0|W_1|b_1|...] for the native exact confirmation
     int np_ = 0;
     for (int l = 0; l < net_.n_layers; ++l) np_ = std::max(np_, net_.b_off[l] + net_.dims[l + 1]);
@@ -173,6 +176,9 @@ class BabRuntime {
     ck(hipMemsetAsync(nodes_.p, 0, P * sizeof(int), st), "memset nodes");
     ck(hipMemsetAsync(open_left_.p, 0, P * sizeof(int), st), "memset open_left");
     ck(hipMemsetAsync(lvl_open_.p, 0, P * sizeof(int), st), "memset lvl_open");
+    ck(hipMemsetAsync(nodes_start_.p, 0, P * sizeof(int), st), "memset nodes_start");
+    ck(hipMemsetAsync(counters_.p, 0, 4 * sizeof(int), st), "memset counters");
+    int slot = 0;
     // initial pool: running partitions
     std::vector<int> run;
     for (int p = 0; p < P; ++p)
@@ -220,12 +226,11 @@ class BabRuntime {
       }
       int m = 1;
       while (m < FA_MAX_SPLIT && (long long)n_in << (m + 1) <= (long long)target) ++m;
-      ck(hipMemsetAsync(counters_.p, 0, 2 * sizeof(int), st), "memset counters");
+      int* cnt = counters_.p + 2 * slot;
       const int nxt = cur ^ 1;
       // every kernel of the previous level has finished (level-end sync), so the next pool
       // can be re-allocated safely: children <= n_in * 2^m
       ensure_pool(nxt, (long long)n_in << m);
-      ck(hipMemcpyAsync(nodes_start_.p, nodes_.p, P * sizeof(int), hipMemcpyDeviceToDevice, st), "cp nodes");
       for (int s = 0; s < n_in; s += batch_) {
         const int nb = std::min(batch_, n_in - s);
         const float* blo = lo_[cur].p + (size_t)s * n0_;
@@ -285,18 +290,19 @@ class BabRuntime {
         sa.budget = budget; sa.m = m;
         sa.oxlo = lo_[nxt].p; sa.oxhi = hi_[nxt].p;
         sa.oxplo = relaxed_ ? plo_[nxt].p : nullptr; sa.oxphi = relaxed_ ? phi_[nxt].p : nullptr;
-        sa.opart = part_[nxt].p; sa.count_out = counters_.p; sa.cap = pool_[nxt];
-        sa.cand_buf = cand_buf_.p; sa.cand_part = cand_part_.p; sa.cand_count = counters_.p + 1;
+        sa.opart = part_[nxt].p; sa.count_out = cnt; sa.cap = pool_[nxt];
+        sa.cand_buf = cand_buf_.p; sa.cand_part = cand_part_.p; sa.cand_count = cnt + 1;
         sa.cand_cap = cand_cap_;
         ckl(fa_split_launch(sa, st), "split");
         launches += relaxed_ ? 6 : 5;
       }
-      ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, st), "settle");
-      ck(hipMemcpyAsync(hcount_, counters_.p, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "cp counters");
+      ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, nodes_.p, nodes_start_.p, cnt,
+                           counters_.p + 2 * (slot ^ 1), hcount_, st), "settle");
       ck(hipStreamSynchronize(st), "sync");
+      slot ^= 1;
       total_nodes += n_in;
-      const int n_out = std::min(hcount_[0], pool_[nxt]);
-      const int n_cand = std::min(hcount_[1], cand_cap_);
+      const int n_out = std::min((int)((volatile int*)hcount_)[0], pool_[nxt]);
+      const int n_cand = std::min((int)((volatile int*)hcount_)[1], cand_cap_);
       ++levels;
       if (n_cand > 0) confirm_candidates(n_cand, confirm, got, cex_x, cex_xp, st);
       cur = nxt;

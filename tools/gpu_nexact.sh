@@ -2,7 +2,7 @@
 # Native exact confirmation in the BaB runtime: GPU suite, bench, 1/8 shard.
 set -eo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/nexact
+O=gpurun_out/${OUT:-nexact}
 mkdir -p $O
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
