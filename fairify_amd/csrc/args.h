@@ -92,6 +92,8 @@ struct SimArgs {
   float* wit_x;             // [P, n0]
   float* wit_xp;            // [P, n0]
   float* z0;                // [P, n_samples] logit at PA value 0 (boundary walk) or nullptr
+  int* keys;                // [P] first-flip key scratch (INT_MAX-initialised) when split > 1
+  int split;                // workgroups per partition (sample tiles strided over them)
   int S;
 };
 

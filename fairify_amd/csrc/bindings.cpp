@@ -166,8 +166,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("sim", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t pids, int Pn, int n_samples,
                   uint32_t seed, int V, const std::vector<int>& pa, uintptr_t values, int Pp, uintptr_t pairs,
                   const std::vector<int>& ra, int tau, uintptr_t counts, uintptr_t found, uintptr_t wit_x,
-                  uintptr_t wit_xp, uintptr_t z0, uintptr_t stream) {
+                  uintptr_t wit_xp, uintptr_t z0, uintptr_t keys, int split, uintptr_t stream) {
     if (pa.size() > FA_MAX_PA || ra.size() > FA_MAX_RA) throw std::invalid_argument("too many PA/RA dims");
+    if (split < 1 || (split > 1 && !keys)) throw std::invalid_argument("sim: split > 1 needs a keys buffer");
     SimArgs a{};
     a.flat = P<const float>(flat);
     a.lo = P<const float>(lo);
@@ -190,6 +191,8 @@ PYBIND11_MODULE(_C, m) {
     a.wit_x = P<float>(wit_x);
     a.wit_xp = P<float>(wit_xp);
     a.z0 = P<float>(z0);
+    a.keys = P<int>(keys);
+    a.split = split;
     check(fa_sim_launch(net.d, a, (hipStream_t)stream), "sim");
   });
 

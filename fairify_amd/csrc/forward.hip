@@ -122,11 +122,41 @@ __device__ __forceinline__ float fa_sample_coord(uint32_t seed, int64_t pid, int
   return lo + (float)(h % w);
 }
 
+// Witness of the first strict flip `key` = sample * Pp + pair of partition p (threads of one block).
+__device__ void fa_sim_witness(const SimArgs& a, int n0, int p, int64_t pid, int key, const float* lo,
+                               const float* hi) {
+  const uint32_t seed_ra = a.seed ^ 0x2545F491u;
+  const int s = key / a.Pp, q = key % a.Pp;
+  const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+  for (int d = threadIdx.x; d < n0; d += FA_THREADS) {
+    const float base = fa_sample_coord(a.seed, pid, s, d, lo[d], hi[d]);
+    float x = base, xp = base;
+    for (int k = 0; k < a.npa; ++k)
+      if (a.pa_idx[k] == d) {
+        x = (float)a.values[vi * a.npa + k];
+        xp = (float)a.values[vj * a.npa + k];
+      }
+    for (int k = 0; k < a.nra; ++k)
+      if (a.ra_idx[k] == d) {
+        const uint32_t h = fa_rng(seed_ra, pid, s, d);
+        xp += (float)(h % (uint32_t)(2 * a.tau + 1)) - (float)a.tau;
+      }
+    a.wit_x[(size_t)p * n0 + d] = x;
+    a.wit_xp[(size_t)p * n0 + d] = xp;
+  }
+}
+
+// split > 1: `split` workgroups share one partition's sample tiles (tile t goes to group
+// t % split), so a short residue list with a large sample budget still fills the 256 CUs.  The
+// groups merge through global integer atomics (activation counts, min flip key), so the result
+// is identical to split == 1; fa_sim_finalize_kernel then writes found / witness.
 __global__ void __launch_bounds__(FA_THREADS) fa_sim_kernel(NetDesc net, SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int S = a.S;
   const int n0 = net.dims[0];
-  const int p = blockIdx.x;
+  const int G = a.split;
+  const int p = blockIdx.x / G;
+  const int g = blockIdx.x - p * G;
   const int tid = threadIdx.x;
   float* bufA = smem;
   float* bufB = bufA + FA_TR * S;
@@ -147,7 +177,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_kernel(NetDesc net, SimArgs
   if (tid == 0) best[0] = 0x7FFFFFFF;
   __syncthreads();
   const uint32_t seed_ra = a.seed ^ 0x2545F491u;
-  for (int s0 = 0; s0 < a.n_samples; s0 += FA_TR) {
+  for (int s0 = g * FA_TR; s0 < a.n_samples; s0 += G * FA_TR) {
     const int nvalid = min(FA_TR, a.n_samples - s0);
     for (int i = tid; i < FA_TR * n0; i += FA_THREADS) {
       const int r = i / n0, d = i % n0;
@@ -194,29 +224,25 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_kernel(NetDesc net, SimArgs
     }
     __syncthreads();
   }
-  for (int i = tid; i < net.n_neurons; i += FA_THREADS) a.counts[(size_t)p * net.n_neurons + i] = cnt[i];
   const int key = best[0];
-  if (tid == 0) a.found[p] = key != 0x7FFFFFFF;
-  if (key != 0x7FFFFFFF) {
-    const int s = key / a.Pp, q = key % a.Pp;
-    const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
-    for (int d = tid; d < n0; d += FA_THREADS) {
-      const float base = fa_sample_coord(a.seed, pid, s, d, s_lo[d], s_hi[d]);
-      float x = base, xp = base;
-      for (int k = 0; k < a.npa; ++k)
-        if (a.pa_idx[k] == d) {
-          x = (float)a.values[vi * a.npa + k];
-          xp = (float)a.values[vj * a.npa + k];
-        }
-      for (int k = 0; k < a.nra; ++k)
-        if (a.ra_idx[k] == d) {
-          const uint32_t h = fa_rng(seed_ra, pid, s, d);
-          xp += (float)(h % (uint32_t)(2 * a.tau + 1)) - (float)a.tau;
-        }
-      a.wit_x[(size_t)p * n0 + d] = x;
-      a.wit_xp[(size_t)p * n0 + d] = xp;
-    }
+  if (G > 1) {
+    for (int i = tid; i < net.n_neurons; i += FA_THREADS)
+      if (cnt[i]) atomicAdd(&a.counts[(size_t)p * net.n_neurons + i], cnt[i]);
+    if (tid == 0 && key != 0x7FFFFFFF) atomicMin(&a.keys[p], key);
+    return;
   }
+  for (int i = tid; i < net.n_neurons; i += FA_THREADS) a.counts[(size_t)p * net.n_neurons + i] = cnt[i];
+  if (tid == 0) a.found[p] = key != 0x7FFFFFFF;
+  if (key != 0x7FFFFFFF) fa_sim_witness(a, n0, p, pid, key, s_lo, s_hi);
+}
+
+__global__ void __launch_bounds__(FA_THREADS) fa_sim_finalize_kernel(NetDesc net, SimArgs a) {
+  const int n0 = net.dims[0];
+  const int p = blockIdx.x;
+  const int key = a.keys[p];
+  if (threadIdx.x == 0) a.found[p] = key != 0x7FFFFFFF;
+  if (key != 0x7FFFFFFF)
+    fa_sim_witness(a, n0, p, a.pids[p], key, a.lo + (size_t)p * n0, a.hi + (size_t)p * n0);
 }
 
 extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) {
@@ -230,7 +256,10 @@ extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) 
   if (bytes > 160 * 1024) return -1;
   if (bytes > 64 * 1024)
     FA_CHECK(hipFuncSetAttribute((const void*)fa_sim_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-  hipLaunchKernelGGL(fa_sim_kernel, dim3(a.P), dim3(FA_THREADS), bytes, stream, net, a);
+  const int tiles = (a.n_samples + FA_TR - 1) / FA_TR;
+  if (a.split < 1 || (a.split > 1 && (!a.keys || a.split > tiles))) return -2;
+  hipLaunchKernelGGL(fa_sim_kernel, dim3((unsigned)a.P * (unsigned)a.split), dim3(FA_THREADS), bytes, stream, net, a);
+  if (a.split > 1) hipLaunchKernelGGL(fa_sim_finalize_kernel, dim3(a.P), dim3(FA_THREADS), 0, stream, net, a);
   return (int)hipGetLastError();
 }
 

@@ -6,6 +6,7 @@ GPU), and passes raw pointers + ``torch.cuda.current_stream().cuda_stream``.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -209,6 +210,20 @@ def pair_certify(be, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, sha
 
 
 # ------------------------------------------------------------------------------------------------
+def _sim_split(P: int, n_samples: int) -> int:
+    """Workgroups per partition for ``fa_sim_kernel``: with ``FAIRIFY_SIM_BLOCKS=B`` a short list
+    of partitions with a large sample budget (the residual falsifier on a per-rank residue) is
+    spread over about B workgroups instead of one per partition walking its 64-sample tiles
+    serially.  Results are bit-identical either way (tests/test_kernels_gpu.py).  Off by default:
+    with 8 concurrent host streams the extra blocks only contend with the other streams' bound
+    kernels (A/B in profiles/r1_sim_split_ab.md)."""
+    target = int(os.environ.get("FAIRIFY_SIM_BLOCKS", "0") or 0)
+    if not P or target <= P:
+        return 1
+    tiles = (n_samples + 63) // 64
+    return max(1, min(tiles, -(-target // P)))
+
+
 def simulate(be, q, lo, hi, pids, n_samples, seed, values, pairs, bisect_pairs, bisect_steps, return_z0=False):
     from ..engine.sim import SimResult, boundary_walk
 
@@ -221,7 +236,9 @@ def simulate(be, q, lo, hi, pids, n_samples, seed, values, pairs, bisect_pairs, 
     Pp = pairs.shape[0]
     values_c = _c(values, torch.int64, None, "values")
     pairs_c = _c(pairs, torch.int64, (Pp, 2), "pairs")
-    counts = torch.empty(P, be.mlp.n_neurons, dtype=torch.int32, device=dev)
+    split = _sim_split(P, n_samples)
+    counts = (torch.zeros if split > 1 else torch.empty)(P, be.mlp.n_neurons, dtype=torch.int32, device=dev)
+    keys = torch.full((P,), 0x7FFFFFFF, dtype=torch.int32, device=dev) if split > 1 else None
     found = torch.zeros(P, dtype=torch.uint8, device=dev)
     wx = torch.zeros(P, n0, dtype=torch.float32, device=dev)
     wxp = torch.zeros(P, n0, dtype=torch.float32, device=dev)
@@ -230,7 +247,7 @@ def simulate(be, q, lo, hi, pids, n_samples, seed, values, pairs, bisect_pairs, 
         ext().sim(_net(be), be.flat.data_ptr(), lo_c.data_ptr(), hi_c.data_ptr(), pids_c.data_ptr(), P, n_samples,
                   int(seed) & 0xFFFFFFFF, V, list(q.pa_idx), values_c.data_ptr(), Pp, pairs_c.data_ptr(),
                   list(q.ra_idx) if q.relaxed else [], int(q.tau), counts.data_ptr(), found.data_ptr(),
-                  wx.data_ptr(), wxp.data_ptr(), _ptr(z0), _stream(dev))
+                  wx.data_ptr(), wxp.data_ptr(), _ptr(z0), _ptr(keys), split, _stream(dev))
     res = SimResult(counts=counts, found=found.bool(), wit_x=wx, wit_xp=wxp)
     if z0 is not None:
         boundary_walk(be, q, lo_c, hi_c, pids_c, n_samples, seed, values_c, pairs_c, res, z0, bisect_pairs,

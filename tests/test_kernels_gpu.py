@@ -105,6 +105,36 @@ def test_sim_kernel_matches_reference(cuda):
     assert torch.equal(a.wit_x[both], b.wit_x.cpu()[both])
 
 
+@pytest.mark.parametrize("relaxed", [False, True])
+def test_sim_split_identical(cuda, monkeypatch, relaxed):
+    """Sample tiles spread over several workgroups per partition (``fa_sim_kernel`` split +
+    ``fa_sim_finalize_kernel``) give bit-identical counts, flags and witnesses."""
+    from fairify_amd.engine.sim import simulate
+    from fairify_amd.ops import hip
+    from fairify_amd.partition import Grid
+
+    q = (Query(("sex",), ("age",), 2) if relaxed else Query(("race",))).resolve(ADULT)
+    grid = Grid.reference(ADULT, 10)
+    ids = np.arange(0, 16000, 401)[:37]
+    lo, hi = grid.decode(ids)
+    values = torch.from_numpy(q.pa_values(lo[0], hi[0])).to(cuda)
+    pairs = torch.from_numpy(q.pa_pairs(values.cpu().numpy())).to(cuda)
+    gpu = Backend(get_model("AC-3"), cuda)
+    lo_t, hi_t = torch.from_numpy(lo).float().to(cuda), torch.from_numpy(hi).float().to(cuda)
+    pid = torch.from_numpy(ids).to(cuda)
+    monkeypatch.setenv("FAIRIFY_SIM_BLOCKS", "2048")
+    assert hip._sim_split(37, 4000) > 1
+    out = []
+    for flag in ("0", "2048"):
+        monkeypatch.setenv("FAIRIFY_SIM_BLOCKS", flag)
+        out.append(simulate(gpu, q, lo_t, hi_t, pid, 4000, 9, values, pairs, 0, 0))
+    a, b = out
+    assert torch.equal(a.counts, b.counts)
+    assert torch.equal(a.found, b.found)
+    assert torch.equal(a.wit_x[a.found], b.wit_x[b.found])
+    assert torch.equal(a.wit_xp[a.found], b.wit_xp[b.found])
+
+
 def test_certify_matches_reference(cuda):
     from fairify_amd.engine.bab import BaBSolver, BaBConfig
 
