@@ -10,11 +10,22 @@ ranks (strong scaling: total work fixed).  Weights are random-init (glorot-unifo
 seed) per BASELINE.json; ``--weights zoo`` uses the reference's trained weights instead.
 
 value  = decided partitions (SAT + UNSAT, every SAT confirmed exactly) per second, whole job.
+         Heuristic-retry UNSAT (the reference's unsound retry, src/AC/Verify-AC.py:173-212) is
+         counted like the reference counts it; the JSON splits it out (``unsat_sound``,
+         ``unsat_heuristic``, ``sat_by_stage``) and ``--no-heuristic`` measures the sound-only
+         rate.
 vs_baseline = value / 0.02497 decided partitions/s, the reference's AC/sex aggregate from
 Table V (553 decided in sum(#P x Total) = 22 144 s).
 
+Multi-GPU: one process per GPU, ``torch.distributed`` backend ``nccl`` (= RCCL over xGMI).
+
     python bench.py --gpus 1 --steps 1 --warmup 1
+    python bench.py --gpus 8                      # self-launches 8 ranks (no torchrun needed)
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --steps 1 --warmup 1
+
+Self-launch: with ``--gpus N > 1`` and no ``WORLD_SIZE`` in the environment, this process
+starts N child processes of itself (rank env vars set, rendezvous on 127.0.0.1) BEFORE any GPU
+call, waits for them and exits with their worst return code; rank 0 prints the JSON line.
 """
 from __future__ import annotations
 
@@ -22,6 +33,8 @@ import argparse
 import contextlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -33,9 +46,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_DECIDED_PER_S = 553.0 / 22143.5
 METRIC = "% partitions verified + partitions/sec on AC suite at 1/2/4/8 MI355X"
+STAGES = ("sim", "bab", "falsify", "smt", "heuristic")
 
 
-def main() -> None:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
@@ -49,6 +63,8 @@ def main() -> None:
     ap.add_argument("--chunk", type=int, default=4096,
                     help="partitions per work item (big chunks win even for small per-rank shards: a 1/8 "
                          "shard takes 1.02 s per step at 4096 vs 1.76 s at 667, profiles/scaling_emulation.md)")
+    ap.add_argument("--limit", type=int, default=0,
+                    help="verify only the first LIMIT partitions of the seeded order per model (tests)")
     ap.add_argument("--node-budget", type=int, default=512)
     ap.add_argument("--escalate-budget", type=int, default=8192,
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
@@ -56,6 +72,8 @@ def main() -> None:
                     help="escalate only partitions that left <= this many open BaB nodes (0 = all)")
     ap.add_argument("--stages", default="",
                     help="further escalation passes 'budget:max_open,...' after --escalate-budget")
+    ap.add_argument("--no-heuristic", action="store_true",
+                    help="skip the reference's unsound heuristic retry (sound verdicts only)")
     ap.add_argument("--residual-samples", type=int, default=None, help="residual falsifier samples (0 = off)")
     ap.add_argument("--residual-iters", type=int, default=None)
     ap.add_argument("--bisect-steps", type=int, default=None, help="boundary-walk bisection steps (0 = off)")
@@ -68,7 +86,40 @@ def main() -> None:
     ap.add_argument("--profile", action="store_true", help="per-stage timing breakdown on stderr (syncs)")
     ap.add_argument("--concurrency", type=int, default=0,
                     help="host threads / HIP streams verifying (model, chunk) items concurrently (default 8 on GPU)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args) -> int:
+    """Start ``--gpus`` ranks of this script (one per GPU) and wait for them.
+
+    This process never touches the GPU (no torch import at all), so its children start from a
+    clean HIP state; each child binds ``cuda:LOCAL_RANK`` and joins the RCCL group."""
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FAIRIFY_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def main() -> None:
+    args = parse_args()
+    if os.environ.get("FAIRIFY_FORCE_REFERENCE") == "1":
+        raise SystemExit("bench.py refuses FAIRIFY_FORCE_REFERENCE=1: the benchmark must run the HIP kernels")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.emulate_shard:
+        raise SystemExit(launch(args))
 
     import torch
 
@@ -80,12 +131,22 @@ def main() -> None:
     from fairify_amd.partition import processing_order
     from fairify_amd.utils.timer import StageTimer
 
-    dev_type = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    dev_type = args.device or ("cuda" if torch.cuda.device_count() > 0 else "cpu")
     info = D.init(dev_type)
+    if dev_type == "cpu" and info.world > 1:      # CPU rehearsal ranks share the host's cores
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // info.world))
+    if not args.emulate_shard and info.world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={info.world}: launch one rank per GPU")
+    if dev_type == "cuda" and info.world > torch.cuda.device_count() and \
+            os.environ.get("FAIRIFY_DIST_BACKEND", "nccl") == "nccl":
+        raise SystemExit(f"{info.world} ranks but only {torch.cuda.device_count()} GPUs visible")
+    backend_name = D.backend_name(info)
     pre = presets.get(args.preset)
     grid = pre.grid()
     q = pre.resolved()
     order = processing_order(grid, seed=args.seed)
+    if args.limit:
+        order = order[:args.limit]
     shard = order[info.rank::info.world]
     if args.emulate_shard:
         er, en = (int(v) for v in args.emulate_shard.split("/"))
@@ -93,9 +154,11 @@ def main() -> None:
     names = args.models.split(",") if args.models else list(pre.models)
     models = [get_model(n, weights=args.weights, seed=args.seed) for n in names]
     backends = [Backend(m, device=info.device) for m in models]
+    if info.device.type == "cuda" and not all(be.hip for be in backends):
+        raise SystemExit("HIP extension inactive on a GPU run")
     cfg = VerifyConfig(sim_size=args.sim_size or pre.sim_size, seed=args.seed, chunk=args.chunk,
                        soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
-                       node_budget=args.node_budget, heuristic=True, heuristic_p=pre.heuristic_p,
+                       node_budget=args.node_budget, heuristic=not args.no_heuristic, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=args.node_budget, escalate_budget=args.escalate_budget,
                        escalate_max_open=args.escalate_max_open,
                        escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
@@ -136,6 +199,8 @@ def main() -> None:
     # the longest items first (LPT), so the slowest model's chain starts at t=0 instead of after
     # a wave of cheap items (prior before any measurement: model size)
     item_cost = {}
+    # counters: attempted, decided, sat, unsat, unsat_heuristic, sat per stage (STAGES order)
+    NC = 5 + len(STAGES)
 
     def one_item(k: int, j: int, ids: np.ndarray):
         m, be = models[k], backends[k]
@@ -145,12 +210,19 @@ def main() -> None:
             if info.device.type == "cuda":
                 torch.cuda.current_stream(info.device).synchronize()
         item_cost[(k, j)] = time.time() - t_item
-        c = recs.counts()
-        return np.array([len(recs), c["sat"] + c["unsat"], c["sat"], c["unsat"]], dtype=np.float64)
+        v, st = recs.cols["verdict"], recs.cols["stage"]
+        sat, uns = v == "sat", v == "unsat"
+        out = np.zeros(NC, dtype=np.float64)
+        out[:5] = [len(recs), sat.sum() + uns.sum(), sat.sum(), uns.sum(), (uns & (st == "heuristic")).sum()]
+        for i, name in enumerate(STAGES):
+            out[5 + i] = (sat & (st == name)).sum()
+        return out
 
     def run_step(step: int):
-        items = [(k, j, ids) for k in range(len(models)) for j, ids in enumerate(chunks_for_step(step))]
+        items = [(k, j, ids) for k in range(len(models)) for j, ids in enumerate(chunks_for_step(step)) if len(ids)]
         items.sort(key=lambda it: (-item_cost.get((it[0], it[1]), 0.0), -models[it[0]].n_neurons))
+        if not items:
+            return np.zeros(NC)
         if pool is None:
             return sum(one_item(k, j, ids) for k, j, ids in items)
         return sum(f.result() for f in [pool.submit(one_item, k, j, ids) for k, j, ids in items])
@@ -162,16 +234,19 @@ def main() -> None:
     D.barrier(info)
     sync()
     t0 = time.time()
-    tot = np.zeros(4)
+    tot = np.zeros(NC)
     for s in range(args.steps):
         tot += run_step(args.warmup + s)
     sync()
+    t_local = time.time() - t0          # this rank's own work, before waiting for the others
     D.barrier(info)
     sync()
     dt = time.time() - t0
     dt_max = D.all_reduce_max(info, dt)
+    rank_ms = D.all_gather_floats(info, 1000.0 * t_local / max(1, args.steps))
     tot = D.all_reduce_sum(info, tot)
-    att, dec, sat, uns = tot.tolist()
+    att, dec, sat, uns, uns_h = tot[:5].tolist()
+    sat_stage = {name: int(tot[5 + i]) for i, name in enumerate(STAGES)}
     value = dec / dt_max if dt_max > 0 else 0.0
     per_step = att / max(1, args.steps)
     out = {
@@ -188,14 +263,19 @@ def main() -> None:
         "dtype": "fp32",
         "data": f"synthetic: reference src/AC integer domain, {args.weights}-init AC-1..12 weights",
         "config": {"model": f"AC suite ({','.join(names)})", "global_batch": int(per_step), "seq_len": None,
-                   "parallelism": f"dp{info.world}", "preset": args.preset, "grid_per_model": len(grid),
+                   "parallelism": f"dp{info.world}", "preset": args.preset, "grid_per_model": len(order),
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
-                   "stages": [list(st) for st in cfg.escalate_stages],
-                   "chunk": args.chunk},
+                   "stages": [list(st) for st in cfg.escalate_stages], "heuristic": cfg.heuristic,
+                   "chunk": args.chunk, "concurrency": conc},
         "pct_verified": round(100.0 * dec / max(1.0, att), 3),
+        "pct_verified_sound": round(100.0 * (dec - uns_h - sat_stage["heuristic"]) / max(1.0, att), 3),
         "partitions_per_s": round(att / dt_max, 3) if dt_max > 0 else 0.0,
         "sat": int(sat), "unsat": int(uns), "unknown": int(att - dec),
+        "unsat_sound": int(uns - uns_h), "unsat_heuristic": int(uns_h), "sat_by_stage": sat_stage,
+        "dist": {"world": info.world, "backend": backend_name,
+                 "rank_ms_per_step": [round(x, 1) for x in rank_ms],
+                 "skew_ms": round(max(rank_ms) - min(rank_ms), 1) if rank_ms else 0.0},
         "baseline": {"decided_per_s": round(BASELINE_DECIDED_PER_S, 5), "pct_verified_of_attempted": 89.0,
                      "coverage_of_grid_pct": 0.29},
     }
@@ -207,6 +287,8 @@ def main() -> None:
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    if pool is not None:
+        pool.shutdown(wait=True)
     D.destroy(info)
 
 

@@ -100,6 +100,21 @@ def all_reduce_sum(info: DistInfo, arr: np.ndarray) -> np.ndarray:
     return t.cpu().numpy()
 
 
+def backend_name(info: DistInfo) -> str:
+    """``nccl`` (RCCL on ROCm), ``gloo`` or ``none`` for a single process."""
+    return dist.get_backend() if info.initialized and dist.is_initialized() else "none"
+
+
+def all_gather_floats(info: DistInfo, x: float) -> List[float]:
+    """One float per rank, in rank order (e.g. per-rank step times for the skew report)."""
+    if not info.initialized:
+        return [float(x)]
+    t = torch.tensor([x], dtype=torch.float64, device=_dev(info))
+    out = [torch.zeros_like(t) for _ in range(info.world)]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
+
+
 def all_gather_rows(info: DistInfo, arr: np.ndarray, chunk_bytes: int = 64 << 20) -> np.ndarray:
     """Gather variable-length row blocks [n_i, ...] from every rank -> concatenated in rank order.
 

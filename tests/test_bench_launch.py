@@ -1,0 +1,51 @@
+"""bench.py self-launch: ``--gpus N`` starts N ranks itself (gloo on CPU here, RCCL on GPUs) and
+the verdict totals of the strong-scaling step do not depend on N."""
+import json
+import os
+import subprocess
+import sys
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(gpus: int, extra=()):
+    env = dict(os.environ, FAIRIFY_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--device", "cpu",
+           "--models", "AC-8,AC-9", "--limit", "48", "--chunk", "16", "--steps", "1", "--warmup", "0", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout          # only rank 0 prints
+    return json.loads(lines[0])
+
+
+def test_self_launch_totals_match_one_rank():
+    one = _bench(1)
+    assert one["n_gpus"] == 1 and one["dist"]["backend"] == "none"
+    for n in (2, 4):
+        d = _bench(n)
+        assert d["n_gpus"] == n and d["dist"]["world"] == n and d["dist"]["backend"] == "gloo"
+        assert len(d["dist"]["rank_ms_per_step"]) == n
+        assert d["config"]["parallelism"] == f"dp{n}"
+        for k in ("sat", "unsat", "unknown", "unsat_sound", "unsat_heuristic"):
+            assert d[k] == one[k], (n, k)
+        assert d["sat_by_stage"] == one["sat_by_stage"]
+    # honest accounting fields add up
+    assert one["unsat_sound"] + one["unsat_heuristic"] == one["unsat"]
+    assert sum(one["sat_by_stage"].values()) == one["sat"]
+
+
+def test_bench_refuses_reference_fallback():
+    env = dict(os.environ, FAIRIFY_FORCE_REFERENCE="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=120, cwd=ROOT)
+    assert r.returncode != 0 and "FAIRIFY_FORCE_REFERENCE" in r.stderr
+
+
+def test_world_size_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+                        "--steps", "1"], capture_output=True, text=True, env=env, timeout=120, cwd=ROOT)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
