@@ -145,12 +145,42 @@ def _amortize(total: float, work: np.ndarray) -> np.ndarray:
 
 def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.ndarray, cfg: VerifyConfig,
                  orig_acc: Optional[float] = None, time_budget: Optional[float] = None,
-                 timer: Optional[StageTimer] = None) -> List[dict]:
-    """Decide one chunk of partitions; returns per-partition dicts (no cumulative columns)."""
+                 timer: Optional[StageTimer] = None) -> "ChunkRecords":
+    """Decide one chunk of partitions; returns its per-partition records (no cumulative columns).
+
+    The kernels share one table of protected-attribute assignments per launch, so a chunk whose
+    partitions split the PA range differently (a PA wider than the partition size, e.g. Adult
+    age with P=10) is verified as one group per distinct PA range; the records come back in
+    ``ids`` order with the chunk's stage times apportioned over all of its partitions."""
+    lo_np, hi_np = grid.decode(ids)
+    pa = list(q.pa_idx)
+    key = np.concatenate([lo_np[:, pa], hi_np[:, pa]], axis=1)
+    uniq, inv = np.unique(key, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    if len(uniq) <= 1:
+        core, seg = _verify_group(be, mlp, q, ids, lo_np, hi_np, cfg, time_budget, timer)
+    else:
+        t0 = time.time()
+        core, seg = None, np.zeros(5)
+        for g in range(len(uniq)):
+            sel = np.nonzero(inv == g)[0]
+            left = None if time_budget is None else time_budget - (time.time() - t0)
+            gcore, gseg = _verify_group(be, mlp, q, ids[sel], lo_np[sel], hi_np[sel], cfg, left, timer)
+            if core is None:
+                core = {k: np.zeros((len(ids),) + v.shape[1:], dtype=v.dtype) for k, v in gcore.items()}
+            for k, v in gcore.items():
+                core[k][sel] = v
+            seg += np.asarray(gseg, dtype=np.float64)
+        seg = (len(ids),) + tuple(seg[1:].tolist())
+    return ChunkRecords(core, orig_acc, segments=[seg], n_neurons=mlp.n_neurons, sim_size=cfg.sim_size)
+
+
+def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_np: np.ndarray, hi_np: np.ndarray,
+                  cfg: VerifyConfig, time_budget: Optional[float], timer: Optional[StageTimer]):
+    """One group of partitions sharing their protected-attribute range: (core columns, segment)."""
     tm = timer if timer is not None else StageTimer()
     t_start = time.time()
     dev = be.device
-    lo_np, hi_np = grid.decode(ids)
     Pn, n = lo_np.shape
     widths = mlp.widths
     Nh = int(sum(mlp.hidden))
@@ -388,7 +418,7 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
             c1 = (zp[:sat_idx.size] > 0).astype(np.int64)
             c2 = (zp[sat_idx.size:] > 0).astype(np.int64)
             c_check[sat_idx] = ((c1 == xo) & (c2 == xpo)).astype(np.int64)
-        pruned_acc = np.ones(Pn)
+        agree = np.full(Pn, cfg.sim_size, dtype=np.int64)     # Pruned-acc numerator
         if masked:
             from ..ops.reference import sample_points
 
@@ -397,31 +427,21 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
             dm = torch.from_numpy(np.stack([masked[p][:Nh] for p in hp])).to(dev)
             z0 = be.forward(X)
             z1 = be.forward(X, dm[:, None, :].expand(-1, X.shape[1], -1))
-            pruned_acc[hp] = ((z0 > 0) == (z1 > 0)).float().mean(dim=1).cpu().numpy()
+            agree[hp] = ((z0 > 0) == (z1 > 0)).sum(dim=1).cpu().numpy()
     t_replay = time.time() - t0
 
-    # ---------------- records (timings apportioned by work)
-    work = nodes
-    s_share = _amortize(t_sim + t_prune + t_bab, work)
-    sv_share = _amortize(t_bab, work)
-    h_work = np.where(h_attempt > 0, nodes, 0)
-    hv_share = _amortize(t_heur, h_work) if t_heur > 0 else np.zeros(Pn)
-    rp_share = _amortize(t_replay, np.zeros(Pn))
-    b_c = P_.compression(b_dead).cpu().numpy()
-    s_c = P_.compression(s_dead).cpu().numpy()
-    st_c = P_.compression(st_dead).cpu().numpy()
-    h_c = h_dead_np.mean(axis=1)
-    t_c = t_dead_np.mean(axis=1)
+    # ---------------- records: dead-neuron counts, work, per-chunk stage times (the per-partition
+    # time columns are apportioned from these by derive_columns, here and after a gather)
     verdict = np.where(status == SAT, "sat", np.where(status == UNSAT, "unsat", "unknown"))
     stage_f = np.where(stage == "", np.where(verdict != "unknown", "bab", ""), stage)
-    return ChunkRecords(dict(
-        grid_id=np.asarray(ids, dtype=np.int64), verdict=verdict, h_attempt=h_attempt, h_success=h_success,
-        b_comp=b_c.astype(np.float64), s_comp=s_c.astype(np.float64), st_comp=st_c.astype(np.float64),
-        h_comp=np.where(h_attempt > 0, h_c, 0.0), t_comp=np.where(h_attempt > 0, t_c, st_c).astype(np.float64),
-        sv_time=sv_share, s_time=s_share, hv_time=hv_share, h_time=hv_share,
-        total_time=s_share + hv_share + rp_share, c_check=c_check, v_accurate=v_acc,
-        pruned_acc=pruned_acc.astype(np.float64), nodes=nodes.astype(np.int64), stage=stage_f.astype(object),
-        cex_x=cex_x, cex_xp=cex_xp), orig_acc)
+    core = dict(
+        grid_id=np.asarray(ids, dtype=np.int64), verdict=verdict, stage=stage_f.astype(object),
+        h_attempt=h_attempt, h_success=h_success,
+        b_cnt=b_dead.sum(dim=1).cpu().numpy().astype(np.int64), s_cnt=s_dead.sum(dim=1).cpu().numpy().astype(np.int64),
+        st_cnt=st_dead.sum(dim=1).cpu().numpy().astype(np.int64), h_cnt=h_dead_np.sum(axis=1).astype(np.int64),
+        t_cnt=t_dead_np.sum(axis=1).astype(np.int64), agree=agree, nodes=nodes.astype(np.int64),
+        c_check=c_check, v_accurate=v_acc, cex_x=cex_x, cex_xp=cex_xp)
+    return core, (Pn, t_sim + t_prune + t_bab, t_bab, t_heur, t_replay)
 
 
 class StreamPool:
@@ -471,21 +491,71 @@ def concat_records(parts: Sequence["ChunkRecords"]) -> "ChunkRecords":
         raise ValueError("no records")
     if len(parts) == 1:
         return parts[0]
-    cols = {k: np.concatenate([p.cols[k] for p in parts]) for k in parts[0].cols}
-    return ChunkRecords(cols, parts[0].orig_acc)
+    core = {k: np.concatenate([p.core[k] for p in parts]) for k in parts[0].core}
+    segs = [sg for p in parts for sg in p.segments]
+    return ChunkRecords(core, parts[0].orig_acc, segments=segs, n_neurons=parts[0].n_neurons,
+                        sim_size=parts[0].sim_size)
+
+
+CORE_COLUMNS = ("grid_id", "verdict", "stage", "h_attempt", "h_success", "b_cnt", "s_cnt", "st_cnt", "h_cnt",
+                "t_cnt", "agree", "nodes", "c_check", "v_accurate", "cex_x", "cex_xp")
+
+
+def derive_columns(core: Dict[str, np.ndarray], segments, n_neurons: int, sim_size: int) -> Dict[str, np.ndarray]:
+    """The 24-column CSV quantities from the per-partition core columns.
+
+    Compressions = dead counts / N (output neuron included, utils/prune.py:194-203); Pruned-acc
+    = agreeing simulation points / sim_size; the stage times of every chunk segment
+    ``(n, t_sim+prune+bab, t_bab, t_heur, t_replay)`` are apportioned over its partitions by
+    work (BaB node expansions).  Pure function of its inputs, so rank 0 reproduces exactly what
+    the producing rank would have written."""
+    N = float(max(1, n_neurons))
+    h = core["h_attempt"] > 0
+    out = dict(core)
+    out["b_comp"] = core["b_cnt"] / N
+    out["s_comp"] = core["s_cnt"] / N
+    out["st_comp"] = core["st_cnt"] / N
+    out["h_comp"] = np.where(h, core["h_cnt"] / N, 0.0)
+    out["t_comp"] = core["t_cnt"] / N
+    out["pruned_acc"] = core["agree"] / float(max(1, sim_size))
+    n = len(core["verdict"])
+    s_t, sv_t, hv_t, rp_t = (np.zeros(n) for _ in range(4))
+    off = 0
+    for cnt, t_spb, t_bab, t_heur, t_rep in segments:
+        cnt = int(cnt)
+        sl = slice(off, off + cnt)
+        work = core["nodes"][sl]
+        s_t[sl] = _amortize(t_spb, work)
+        sv_t[sl] = _amortize(t_bab, work)
+        if t_heur > 0:
+            hv_t[sl] = _amortize(t_heur, np.where(h[sl], work, 0))
+        rp_t[sl] = _amortize(t_rep, np.zeros(cnt))
+        off += cnt
+    if off != n:
+        raise ValueError(f"segments cover {off} partitions, records hold {n}")
+    out["sv_time"], out["s_time"], out["hv_time"], out["h_time"] = sv_t, s_t, hv_t, hv_t
+    out["total_time"] = s_t + hv_t + rp_t
+    return out
 
 
 class ChunkRecords(Sequence):
-    """Per-partition results of one chunk, stored column-wise (numpy arrays).
+    """Per-partition results of one or more chunks, stored column-wise (numpy arrays).
 
-    Behaves like a list of per-partition dicts (the CSV/runner view, built lazily per row) and
-    exposes the columns for vectorised consumers (bench counters, packing for collectives)."""
+    ``core`` holds what a rank ships (verdicts, stages, dead counts, work, counterexamples),
+    ``segments`` the per-chunk stage times; ``cols`` adds the derived CSV quantities.  Behaves
+    like a list of per-partition dicts (the CSV/runner view, built lazily per row)."""
 
     _INT = ("grid_id", "h_attempt", "h_success", "c_check", "v_accurate", "nodes")
+    _HIDE = ("cex_x", "cex_xp", "b_cnt", "s_cnt", "st_cnt", "h_cnt", "t_cnt", "agree")
 
-    def __init__(self, cols: Dict[str, np.ndarray], orig_acc: Optional[float] = None):
-        self.cols = cols
+    def __init__(self, core: Dict[str, np.ndarray], orig_acc: Optional[float] = None, segments=None,
+                 n_neurons: int = 1, sim_size: int = 1):
+        self.core = core
         self.orig_acc = orig_acc
+        self.segments = list(segments) if segments is not None else [(len(core["verdict"]), 0.0, 0.0, 0.0, 0.0)]
+        self.n_neurons = n_neurons
+        self.sim_size = sim_size
+        self.cols = derive_columns(core, self.segments, n_neurons, sim_size)
 
     def __len__(self) -> int:
         return len(self.cols["verdict"])
@@ -496,7 +566,7 @@ class ChunkRecords(Sequence):
         c = self.cols
         sat = c["verdict"][i] == "sat"
         d = {k: (int(v[i]) if k in self._INT else (str(v[i]) if v.dtype.kind in "OU" else float(v[i])))
-             for k, v in c.items() if k not in ("cex_x", "cex_xp")}
+             for k, v in c.items() if k not in self._HIDE}
         d["orig_acc"] = self.orig_acc
         d["c1"] = c["cex_x"][i].astype(np.float32) if sat else None
         d["c2"] = c["cex_xp"][i].astype(np.float32) if sat else None

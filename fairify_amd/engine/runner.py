@@ -26,6 +26,7 @@ import numpy as np
 from ..models.zoo import get_model
 from ..ops.backend import Backend
 from ..parallel import dist as D
+from ..parallel import wire
 from ..partition import processing_order
 from ..presets import Preset
 from ..report.csv_report import PartitionCSV, format_table, table_v_row_columns, write_summary
@@ -40,38 +41,28 @@ _SCALARS = ["h_attempt", "h_success", "b_comp", "s_comp", "st_comp", "h_comp", "
             "hv_time", "h_time", "total_time", "c_check", "v_accurate", "pruned_acc", "nodes"]
 
 
-def pack(records: List[dict], positions: np.ndarray, n0: int) -> np.ndarray:
-    """Fixed-width float64 rows: [pos, grid_id, verdict, stage, scalars..., has_cex, c1[n0], c2[n0]]."""
+def pack(records, positions: np.ndarray, n0: int) -> np.ndarray:
+    """Fixed-width float64 rows [pos, grid_id, verdict, stage, scalars..., has_cex, c1[n0], c2[n0]]:
+    the input of the native CSV formatter on rank 0 (never sent over the wire; ranks ship
+    :mod:`parallel.wire` buffers)."""
     w = 4 + len(_SCALARS) + 1 + 2 * n0
     out = np.zeros((len(records), w), dtype=np.float64)
-    cols = getattr(records, "cols", None)
-    if cols is not None:            # columnar chunk result: vectorised packing
-        out[:, 0] = positions
-        out[:, 1] = cols["grid_id"]
-        out[:, 2] = np.select([cols["verdict"] == "sat", cols["verdict"] == "unsat"], [1, 2], 0)
-        out[:, 3] = [STAGES.index(x) if x in STAGES else 0 for x in cols["stage"]]
-        for k, name in enumerate(_SCALARS):
-            out[:, 4 + k] = cols[name]
-        sat = cols["verdict"] == "sat"
-        out[:, 4 + len(_SCALARS)] = sat
-        out[sat, 5 + len(_SCALARS):5 + len(_SCALARS) + n0] = cols["cex_x"][sat]
-        out[sat, 5 + len(_SCALARS) + n0:] = cols["cex_xp"][sat]
-        return out
-    for i, (r, pos) in enumerate(zip(records, positions)):
-        out[i, 0] = pos
-        out[i, 1] = r["grid_id"]
-        out[i, 2] = VCODE[r["verdict"]]
-        out[i, 3] = STAGES.index(r.get("stage", "")) if r.get("stage", "") in STAGES else 0
-        for k, name in enumerate(_SCALARS):
-            out[i, 4 + k] = float(r[name])
-        if r["c1"] is not None:
-            out[i, 4 + len(_SCALARS)] = 1
-            out[i, 5 + len(_SCALARS):5 + len(_SCALARS) + n0] = r["c1"]
-            out[i, 5 + len(_SCALARS) + n0:] = r["c2"]
+    cols = records.cols
+    out[:, 0] = positions
+    out[:, 1] = cols["grid_id"]
+    out[:, 2] = np.select([cols["verdict"] == "sat", cols["verdict"] == "unsat"], [1, 2], 0)
+    out[:, 3] = [STAGES.index(x) if x in STAGES else 0 for x in cols["stage"]]
+    for k, name in enumerate(_SCALARS):
+        out[:, 4 + k] = cols[name]
+    sat = cols["verdict"] == "sat"
+    out[:, 4 + len(_SCALARS)] = sat
+    out[sat, 5 + len(_SCALARS):5 + len(_SCALARS) + n0] = cols["cex_x"][sat]
+    out[sat, 5 + len(_SCALARS) + n0:] = cols["cex_xp"][sat]
     return out
 
 
 def unpack(rows: np.ndarray, n0: int, orig_acc: Optional[float]) -> List[PartitionRecord]:
+    """Packed rows -> per-partition record objects (the per-record CSV writer's input)."""
     recs = []
     for row in rows:
         kw = {name: row[4 + k] for k, name in enumerate(_SCALARS)}
@@ -149,31 +140,42 @@ def model_accuracy(mlp, suite: str, seed: int = 0) -> Optional[float]:
     return float(np.mean(mlp.predict(ds.X_test) == ds.y_test))
 
 
-def _residual_pass(be, mlp, q, grid, order, gathered: np.ndarray, cfg: VerifyConfig, escalate: int, acc,
-                   info: D.DistInfo, timer, budget: float) -> np.ndarray:
+def _round_positions(todo: np.ndarray, r: int, per_round: int, world: int) -> List[np.ndarray]:
+    """Every rank's positions of round ``r`` (rank k verifies ``todo[k::world]`` in rounds of
+    ``per_round``); rank 0 uses this instead of receiving positions over the wire."""
+    return [todo[k::world][r * per_round:(r + 1) * per_round] for k in range(world)]
+
+
+def _residual_pass(be, mlp, q, grid, order, round_pos: np.ndarray, codes: np.ndarray, cfg: VerifyConfig,
+                   escalate: int, acc, info: D.DistInfo, timer, budget: float):
     """Residual re-distribution ("work stealing"): the UNKNOWN partitions of the
-    round — wherever they fell — are re-sharded evenly over the ranks and retried with an
-    escalated node budget; every rank sees the same gathered rows, so the split needs no
-    extra coordination.  Returns the round's rows with the retried ones replaced."""
-    n0 = q.n
-    unk = np.nonzero(gathered[:, 2] == VCODE["unknown"])[0] if len(gathered) else np.zeros(0, np.int64)
+    round -- wherever they fell -- are re-sharded evenly over the ranks and retried with an
+    escalated node budget.  Every rank holds the round's int8 verdicts (``codes``, aligned with
+    ``round_pos``), so the split needs no extra coordination.  Returns (positions, records) of
+    the retried partitions on rank 0 (``None`` elsewhere)."""
+    unk = round_pos[codes == VCODE["unknown"]] if len(round_pos) else np.zeros(0, np.int64)
     if unk.size == 0 or budget <= 0:
-        return gathered
-    pos_all = gathered[unk, 0].astype(np.int64)
-    share = pos_all[info.rank::info.world]
+        return None
+    shares = wire.split_positions(unk, info.world)
+    share = shares[info.rank]
     c2 = replace(cfg, node_budget=cfg.node_budget * escalate,
                  heuristic_node_budget=cfg.heuristic_node_budget * escalate)
+    buf = wire.empty(q)
     if len(share):
         recs = verify_chunk(be, mlp, q, grid, order[share], c2, orig_acc=acc, time_budget=budget, timer=timer)
-        packed = pack(recs, share, n0)
-    else:
-        packed = np.zeros((0, gathered.shape[1]))
-    retried = D.all_gather_rows(info, packed)
-    if len(retried):
-        idx = {int(p): k for k, p in enumerate(gathered[:, 0].astype(np.int64))}
-        for row in retried:
-            gathered[idx[int(row[0])]] = row
-    return gathered
+        buf = wire.encode(recs, q)
+    bufs = D.gather_bytes(info, buf)
+    if not info.is_main:
+        return None
+    parts = [(sh, wire.decode(b, order[sh], acc, mlp.n_neurons, cfg.sim_size, q)) for sh, b in zip(shares, bufs)]
+    return wire.merge_rounds(parts)
+
+
+def _replace(pos: np.ndarray, recs, new_pos: np.ndarray, new_recs) -> None:
+    """Overwrite the rows of ``recs`` (sorted by ``pos``) at ``new_pos`` with ``new_recs``."""
+    idx = np.searchsorted(pos, new_pos)
+    for k, v in new_recs.cols.items():
+        recs.cols[k][idx] = v
 
 
 def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str = "zoo", out_dir: str = "results",
@@ -212,6 +214,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         # background thread while round r+1's chunks drive the GPU; one worker keeps the order
         io = ThreadPoolExecutor(max_workers=1) if info.is_main else None
         pending = []
+        wire_bytes = [0, 0]
         table_cols: Dict[str, List[np.ndarray]] = {k: [] for k in _TABLE_COLS}
         timer = StageTimer(info.device)
         t0 = time.time()
@@ -219,33 +222,58 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         rounds = int(np.ceil(len(todo) / max(1, per_round * info.world))) if len(todo) else 0
         stopped = False
         last_note = time.time()
+        inflight = None      # (async gather handle, per-rank positions) of the previous round
+
+        def flush(item):
+            handle, rpos, retried = item
+            bufs = handle.wait()
+            if not info.is_main:
+                return
+            parts = [(p, wire.decode(b, order[p], acc, mlp.n_neurons, cfg.sim_size, q)) for p, b in zip(rpos, bufs)]
+            gpos, grecs = wire.merge_rounds(parts)
+            if grecs is None:
+                return
+            if retried is not None and retried[1] is not None:
+                _replace(gpos, grecs, *retried)
+            rows = pack(grecs, gpos, n0)
+            cols = columns(rows, n0)
+            for k in _TABLE_COLS:
+                table_cols[k].append(cols[k])
+            wire_bytes[0] += sum(len(b) for b in bufs)
+            wire_bytes[1] += len(gpos)
+            pending.append(io.submit(_write_round, writer, rows, n0, acc, done, state_path))
+            if len(pending) > 2:
+                pending.pop(0).result()
+
         for r in range(rounds):
             elapsed = D.all_reduce_max(info, time.time() - t0)
             if elapsed > cfg.hard_timeout:
                 stopped = True
                 break
-            pos = mine[r * per_round:(r + 1) * per_round]
+            rpos = _round_positions(todo, r, per_round, info.world)
+            pos = rpos[info.rank]
+            buf = wire.empty(q)
+            codes = np.zeros(0, np.int8)
             if len(pos):
                 subs = [pos[s:s + cfg.chunk] for s in range(0, len(pos), cfg.chunk)]
                 recs = concat_records(streams.run(
                     lambda sp: verify_chunk(be, mlp, q, grid, order[sp], cfg, orig_acc=acc,
                                             time_budget=cfg.hard_timeout - elapsed, timer=timer), subs))
-                packed = pack(recs, pos, n0)
-            else:
-                packed = np.zeros((0, 4 + len(_SCALARS) + 1 + 2 * n0))
-            gathered = D.all_gather_rows(info, packed)
+                buf = wire.encode(recs, q)
+                codes = wire.verdict_codes(recs)
+            retried = None
             if escalate > 1:
-                gathered = _residual_pass(be, mlp, q, grid, order, gathered, cfg, escalate, acc, info, timer,
-                                          cfg.hard_timeout - elapsed)
-            if info.is_main:
-                gathered = gathered[np.argsort(gathered[:, 0], kind="stable")]
-                cols = columns(gathered, n0)
-                for k in _TABLE_COLS:
-                    table_cols[k].append(cols[k])
-                pending.append(io.submit(_write_round, writer, gathered, n0, acc, done, state_path))
-                if len(pending) > 2:
-                    pending.pop(0).result()
+                all_codes = D.all_gather_int8(info, codes)
+                retried = _residual_pass(be, mlp, q, grid, order, np.concatenate(rpos), all_codes, cfg, escalate,
+                                         acc, info, timer, cfg.hard_timeout - elapsed)
+            # this round's results travel to rank 0 while the next round computes
+            handle = D.gather_bytes(info, buf, async_op=True)
+            if inflight is not None:
+                flush(inflight)
+            inflight = (handle, rpos, retried)
             if faults.crash_after() >= 0:          # fault injection: crash only after a checkpoint
+                flush(inflight)
+                inflight = None
                 for f in pending:
                     f.result()
                 pending.clear()
@@ -255,6 +283,8 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                 print(f"[{preset.name}] {name}: round {r + 1}/{rounds}, "
                       f"{min(len(todo), (r + 1) * per_round * info.world)}/{len(todo)} partitions, "
                       f"{time.time() - t0:.0f}s", flush=True)
+        if inflight is not None:
+            flush(inflight)
         for f in pending:
             f.result()
         if io is not None:
@@ -265,6 +295,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             row = table_v_row_columns(name, pa_name, grid_size=len(grid), wall=wall, **tc)
             row["stopped_by_hard_timeout"] = stopped
             row["original_acc"] = acc
+            row["wire_bytes_per_partition"] = round(wire_bytes[0] / max(1, wire_bytes[1]), 2)
             rows_out.append(row)
             if verbose:
                 print(f"[{preset.name}] {name}: {row['SAT']} sat / {row['UNSAT']} unsat / {row['UNK']} unknown "

@@ -52,7 +52,10 @@ def init(device_type: Optional[str] = None) -> DistInfo:
     else:
         dev = torch.device("cpu")
     info = DistInfo(rank=rank, world=world, local_rank=local, device=dev)
-    if world > 1 and not dist.is_initialized():
+    # FAIRIFY_DIST_INIT=1: form the process group even for a single rank (exercises the RCCL
+    # communicator and collectives on a one-GPU box, where RCCL refuses two ranks per device)
+    force = os.environ.get("FAIRIFY_DIST_INIT") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         backend = "nccl" if device_type == "cuda" else "gloo"
@@ -148,6 +151,60 @@ def all_gather_rows(info: DistInfo, arr: np.ndarray, chunk_bytes: int = 64 << 20
             out[r, s:e] = bufs[r].cpu().numpy()
     parts = [out[r, :ns[r]].copy().view(arr.dtype).reshape((ns[r],) + row_shape) for r in range(info.world)]
     return np.concatenate(parts, axis=0) if parts else arr
+
+
+class _Pending:
+    """An in-flight :func:`gather_bytes`: ``wait()`` -> list of per-rank buffers on ``dst``
+    (``None`` elsewhere)."""
+
+    def __init__(self, work, bufs, sizes, is_dst, value=None):
+        self.work, self.bufs, self.sizes, self.is_dst, self.value = work, bufs, sizes, is_dst, value
+
+    def wait(self) -> Optional[List[np.ndarray]]:
+        if self.value is not None or self.work is None:
+            return self.value
+        self.work.wait()
+        self.work = None
+        if not self.is_dst:
+            return None
+        self.value = [b[:n].cpu().numpy() for b, n in zip(self.bufs, self.sizes)]
+        return self.value
+
+
+def gather_bytes(info: DistInfo, buf: np.ndarray, dst: int = 0, async_op: bool = False):
+    """Gather one variable-length uint8 buffer per rank to ``dst`` only (not an all-gather: the
+    other ranks never need the results).  Sizes travel first (one int64 all-gather), payloads
+    are padded to the largest.  ``async_op=True`` returns a handle whose ``wait()`` yields the
+    list: the gather runs on the communicator's own stream (RCCL) / thread (gloo) while the
+    caller's next round computes."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    if not info.initialized:
+        p = _Pending(None, None, None, True, [buf])
+        return p if async_op else p.wait()
+    dev = _dev(info)
+    n = torch.tensor([buf.size], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(info.world)]
+    dist.all_gather(ns, n)
+    sizes = [int(v.item()) for v in ns]
+    nmax = max(1, max(sizes))
+    src = torch.zeros(nmax, dtype=torch.uint8)
+    src[:buf.size] = torch.from_numpy(buf)
+    src = src.to(dev)
+    is_dst = info.rank == dst
+    bufs = [torch.empty(nmax, dtype=torch.uint8, device=dev) for _ in range(info.world)] if is_dst else None
+    work = dist.gather(src, gather_list=bufs, dst=dst, async_op=True)
+    p = _Pending(work, bufs, sizes, is_dst)
+    p.src = src                     # keep the send buffer alive until the gather completes
+    return p if async_op else p.wait()
+
+
+def all_gather_int8(info: DistInfo, arr: np.ndarray) -> np.ndarray:
+    """Variable-length int8 vectors (e.g. verdict codes) from every rank, concatenated in rank
+    order on every rank."""
+    arr = np.ascontiguousarray(arr, dtype=np.int8)
+    if not info.initialized:
+        return arr
+    return all_gather_rows(info, arr.reshape(-1, 1)).reshape(-1)
 
 
 def broadcast_array(info: DistInfo, arr: Optional[np.ndarray], src: int = 0) -> np.ndarray:
