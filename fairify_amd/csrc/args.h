@@ -153,8 +153,12 @@ struct SplitArgs {
                                           //     stopped (budget / capacity), or nullptr
   int* lvl_open;                          // [P] open inner nodes of this level (reset per level)
   const int* nodes_start;                 // [P] part_nodes at the start of this level
+  const int* prev_start;                  // [P] part_nodes at the start of the previous level
+                                          //     (nodes_start - prev_start = the partition's nodes
+                                          //     in this level; -1 before the first level)
   int budget;
-  int m;                                  // requested split dims (children = 2^m)
+  int m;                                  // largest split-dim count (children = 2^m per node)
+  int target;                             // per-partition frontier target of the branching rule
   float *oxlo, *oxhi, *oxplo, *oxphi;     // output pool
   int* opart;
   int* count_out;

@@ -4,9 +4,12 @@
 //                      partitions; flag possible violations for exact host confirmation (every
 //                      possible PA pair of a leaf = single lattice point; the LP-optimal vertex
 //                      pair of an inner node); split open inner nodes along their top-m scored
-//                      dimensions into 2^m children (m adapts to the frontier size so small
-//                      frontiers still fill the GPU), enforcing the per-partition node budget and
+//                      dimensions into 2^m children, enforcing the per-partition node budget and
 //                      the pool capacity with device atomics (overflow => partition UNKNOWN).
+//                      Branching rule (per partition, so a partition's search tree does not depend
+//                      on which other partitions share its chunk): a partition with w nodes in
+//                      this level splits each along m = clamp(floor(log2(target / w)), 1, m_max)
+//                      dimensions -- wide first levels, binary once its frontier reaches target.
 //                      Relaxed queries keep a separate x' box for the relaxed features and
 //                      tighten the |x_r - x'_r| <= tau coupling per child (empty children dropped).
 //                      Budget (deterministic): a partition keeps splitting while its node count
@@ -102,7 +105,12 @@ __global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a)
   const float* sc = a.scores + (size_t)n * 2 * n0;
   int dims[FA_MAX_SPLIT];
   int m = 0;
-  const int mreq = a.m < FA_MAX_SPLIT ? a.m : FA_MAX_SPLIT;
+  int mreq = 1;
+  {
+    const int mmax = a.m < FA_MAX_SPLIT ? a.m : FA_MAX_SPLIT;
+    const int w = a.nodes_start[p] - a.prev_start[p];      // this partition's nodes in the level
+    while (mreq < mmax && ((long long)w << (mreq + 1)) <= (long long)a.target) ++mreq;
+  }
   for (int j = 0; j < mreq; ++j) {
     float best = -0.5f;
     int bd = -1;
@@ -208,7 +216,8 @@ __global__ void fa_mark_unknown_kernel(const int* part, int n, int8_t* status) {
 }
 
 __global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
-                                 int* nodes_start, const int* counters_cur, int* counters_next, int* host_counts) {
+                                 int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
+                                 int* host_counts) {
   const int p = blockIdx.x * FA_THREADS + threadIdx.x;
   if (p == 0) {
     // level counters straight into pinned host memory (no blit per level), next slot cleared
@@ -223,6 +232,7 @@ __global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part
     if (part_open) part_open[p] = lvl_open[p];
   }
   lvl_open[p] = 0;
+  prev_start[p] = nodes_start[p];
   nodes_start[p] = part_nodes[p];     // the next level's budget reference
 }
 
@@ -254,10 +264,11 @@ extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_
 }
 
 extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
-                                int* nodes_start, const int* counters_cur, int* counters_next, int* host_counts,
-                                hipStream_t stream) {
+                                int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
+                                int* host_counts, hipStream_t stream) {
   const int n = P > 0 ? P : 1;
   hipLaunchKernelGGL(fa_settle_kernel, dim3((n + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, P,
-                     status, lvl_open, part_open, part_nodes, nodes_start, counters_cur, counters_next, host_counts);
+                     status, lvl_open, part_open, part_nodes, nodes_start, prev_start, counters_cur, counters_next,
+                     host_counts);
   return (int)hipGetLastError();
 }

@@ -28,6 +28,8 @@
 
 namespace py = pybind11;
 
+#define FA_CAND_MAX (1LL << 24)   // candidates confirmable per BFS level
+
 extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream);
 extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
@@ -35,8 +37,8 @@ extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream);
 extern "C" int fa_mark_unknown_launch(const int* part, int n, int8_t* status, hipStream_t stream);
 extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_t v, hipStream_t stream);
 extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
-                                int* nodes_start, const int* counters_cur, int* counters_next, int* host_counts,
-                                hipStream_t stream);
+                                int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
+                                int* host_counts, hipStream_t stream);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 
 // defined in bindings.cpp
@@ -78,7 +80,8 @@ class BabRuntime {
  public:
   BabRuntime(py::handle net, uintptr_t flat, std::vector<int> pa, std::vector<float> values_f,
              std::vector<int64_t> values_i, std::vector<int64_t> pairs, std::vector<int> ra, float tau,
-             std::vector<uint8_t> shared, int capacity, int batch_nodes, int cand_cap, double unit, bool crown)
+             std::vector<uint8_t> shared, int capacity, int batch_nodes, int cand_cap, double unit, bool crown,
+             int split_target)
       : net_(fa_net_desc(net)),
         flat_((const float*)flat),
         pa_(std::move(pa)),
@@ -88,7 +91,8 @@ class BabRuntime {
         batch_(batch_nodes),
         cand_cap_(cand_cap),
         unit_(unit),
-        crown_(crown) {
+        crown_(crown),
+        split_target_(std::max(2, split_target)) {
     n0_ = net_.dims[0];
     npa_ = (int)pa_.size();
     if (npa_ == 0 || npa_ > FA_CMAX_PA || (int)ra_.size() > FA_MAX_RA) throw std::invalid_argument("bad PA/RA");
@@ -132,8 +136,7 @@ class BabRuntime {
     pe_lb_.ensure(2 * (size_t)batch_);
     pe_ub_.ensure(2 * (size_t)batch_);
     pe_part_.ensure(2 * (size_t)batch_);
-    cand_buf_.ensure((size_t)cand_cap_ * 2 * n0_);
-    cand_part_.ensure(cand_cap_);
+    ensure_cand(cand_cap_);
     counters_.ensure(4);   // two slots of (children, candidates), alternating per level
     // fine-grained (coherent) pinned words: the settle kernel writes the level counters here
     ck(hipHostMalloc((void**)&hcount_, 2 * sizeof(int), hipHostMallocCoherent), "hipHostMalloc");
@@ -171,12 +174,14 @@ class BabRuntime {
     open_left_.ensure(P);
     lvl_open_.ensure(P);
     nodes_start_.ensure(P);
+    prev_start_.ensure(P);
     std::vector<int8_t> hstatus(status0.data(), status0.data() + P);
     ck(hipMemcpyAsync(status_.p, hstatus.data(), P, hipMemcpyHostToDevice, st), "cp status");
     ck(hipMemsetAsync(nodes_.p, 0, P * sizeof(int), st), "memset nodes");
     ck(hipMemsetAsync(open_left_.p, 0, P * sizeof(int), st), "memset open_left");
     ck(hipMemsetAsync(lvl_open_.p, 0, P * sizeof(int), st), "memset lvl_open");
     ck(hipMemsetAsync(nodes_start_.p, 0, P * sizeof(int), st), "memset nodes_start");
+    ck(hipMemsetAsync(prev_start_.p, 0xFF, P * sizeof(int), st), "memset prev_start");   // -1: one root node
     ck(hipMemsetAsync(counters_.p, 0, 4 * sizeof(int), st), "memset counters");
     int slot = 0;
     // initial pool: running partitions
@@ -210,10 +215,9 @@ class BabRuntime {
     // host result buffers
     std::vector<int64_t> cex_x((size_t)P * n0_, 0), cex_xp((size_t)P * n0_, 0);
     std::vector<char> got(P, 0);
-    int levels = 0, launches = 0;
+    int levels = 0, launches = 0, cand_overflow = 0;
     long long total_nodes = 0;
     bool timed_out = false;
-    const int target = std::max(batch_, 1);
     {
     // the level loop runs without the GIL: several models/streams can be driven from Python threads
     py::gil_scoped_release nogil;
@@ -224,13 +228,15 @@ class BabRuntime {
         timed_out = true;
         break;
       }
-      int m = 1;
-      while (m < FA_MAX_SPLIT && (long long)n_in << (m + 1) <= (long long)target) ++m;
       int* cnt = counters_.p + 2 * slot;
       const int nxt = cur ^ 1;
       // every kernel of the previous level has finished (level-end sync), so the next pool
-      // can be re-allocated safely: children <= n_in * 2^m
-      ensure_pool(nxt, (long long)n_in << m);
+      // can be re-allocated safely.  Per partition with w nodes in the level the branching rule
+      // makes at most max(split_target, 2 w) children: <= 2 n_in + split_target * min(P, n_in)
+      ensure_pool(nxt, 2LL * n_in + (long long)split_target_ * std::min(P, n_in));
+      // candidate buffer for the whole level (one per inner node, every PA pair of a leaf): a
+      // capped buffer would drop candidates depending on which partitions share the chunk
+      ensure_cand(std::min<long long>((long long)n_in * std::max(1, Pp_ * norient_), FA_CAND_MAX));
       for (int s = 0; s < n_in; s += batch_) {
         const int nb = std::min(batch_, n_in - s);
         const float* blo = lo_[cur].p + (size_t)s * n0_;
@@ -287,22 +293,25 @@ class BabRuntime {
         sa.shared = shared_.p;
         sa.status = status_.p; sa.part_nodes = nodes_.p; sa.part_open = open_left_.p; sa.lvl_open = lvl_open_.p;
         sa.nodes_start = nodes_start_.p;
-        sa.budget = budget; sa.m = m;
+        sa.prev_start = prev_start_.p;
+        sa.budget = budget; sa.m = FA_MAX_SPLIT; sa.target = split_target_;
         sa.oxlo = lo_[nxt].p; sa.oxhi = hi_[nxt].p;
         sa.oxplo = relaxed_ ? plo_[nxt].p : nullptr; sa.oxphi = relaxed_ ? phi_[nxt].p : nullptr;
         sa.opart = part_[nxt].p; sa.count_out = cnt; sa.cap = pool_[nxt];
         sa.cand_buf = cand_buf_.p; sa.cand_part = cand_part_.p; sa.cand_count = cnt + 1;
-        sa.cand_cap = cand_cap_;
+        sa.cand_cap = cand_alloc_;
         ckl(fa_split_launch(sa, st), "split");
         launches += relaxed_ ? 6 : 5;
       }
-      ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, nodes_.p, nodes_start_.p, cnt,
+      ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, nodes_.p, nodes_start_.p, prev_start_.p, cnt,
                            counters_.p + 2 * (slot ^ 1), hcount_, st), "settle");
       ck(hipStreamSynchronize(st), "sync");
       slot ^= 1;
       total_nodes += n_in;
       const int n_out = std::min((int)((volatile int*)hcount_)[0], pool_[nxt]);
-      const int n_cand = std::min((int)((volatile int*)hcount_)[1], cand_cap_);
+      const int n_cand_all = ((volatile int*)hcount_)[1];
+      const int n_cand = std::min(n_cand_all, cand_alloc_);
+      if (n_cand_all > cand_alloc_) ++cand_overflow;
       ++levels;
       if (n_cand > 0) confirm_candidates(n_cand, confirm, got, cex_x, cex_xp, st);
       cur = nxt;
@@ -329,6 +338,7 @@ class BabRuntime {
     py::dict stats;
     stats["levels"] = levels;
     stats["launches"] = launches;
+    stats["cand_overflow_levels"] = cand_overflow;
     stats["nodes"] = total_nodes;
     stats["time"] = el;
     stats["timed_out"] = timed_out;
@@ -391,6 +401,16 @@ class BabRuntime {
       phi_[i].ensure(cn);
     }
     pool_[i] = n;
+  }
+
+  void ensure_cand(long long need) {
+    if (need <= cand_alloc_) return;
+    long long n = std::max<long long>(cand_alloc_, 1 << 16);
+    while (n < need) n *= 2;
+    n = std::min<long long>(n, FA_CAND_MAX);
+    cand_buf_.ensure((size_t)n * 2 * n0_);
+    cand_part_.ensure((size_t)n);
+    cand_alloc_ = (int)n;
   }
 
   // called WITHOUT the GIL; takes it only around the Python confirmation callback
@@ -525,9 +545,11 @@ class BabRuntime {
   std::vector<int> pa_, ra_;
   float tau_;
   int cap_, batch_, cand_cap_;
+  int cand_alloc_ = 0;
   int pool_[2] = {0, 0};
   double unit_;
   bool crown_ = false;
+  int split_target_ = 256;
   int n0_ = 0, npa_ = 0, V_ = 0, Pp_ = 0, norient_ = 1;
   bool relaxed_ = false;
   DevBuf<float> vals_f_;
@@ -539,7 +561,7 @@ class BabRuntime {
   DevBuf<float> gmin_, tstar_, score_, cand_, scores_, pe_lb_, pe_ub_, cand_buf_;
   DevBuf<uint8_t> open_, leaf_;
   DevBuf<int64_t> split_, cv_, co_;
-  DevBuf<int> pe_part_, cand_part_, counters_, nodes_, idx_, open_left_, lvl_open_, nodes_start_;
+  DevBuf<int> pe_part_, cand_part_, counters_, nodes_, idx_, open_left_, lvl_open_, nodes_start_, prev_start_;
   DevBuf<int8_t> status_;
   int* hcount_ = nullptr;
 };
@@ -547,10 +569,12 @@ class BabRuntime {
 void register_bab(py::module& m) {
   py::class_<BabRuntime>(m, "BabRuntime")
       .def(py::init<py::handle, uintptr_t, std::vector<int>, std::vector<float>, std::vector<int64_t>,
-                    std::vector<int64_t>, std::vector<int>, float, std::vector<uint8_t>, int, int, int, double, bool>(),
+                    std::vector<int64_t>, std::vector<int>, float, std::vector<uint8_t>, int, int, int, double, bool,
+                    int>(),
            py::arg("net"), py::arg("flat"), py::arg("pa"), py::arg("values_f"), py::arg("values_i"),
            py::arg("pairs"), py::arg("ra"), py::arg("tau"), py::arg("shared"), py::arg("capacity"),
-           py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"), py::arg("crown") = true)
+           py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"), py::arg("crown") = true,
+           py::arg("split_target") = 256)
       .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"),
            py::arg("native_exact") = false);

@@ -34,6 +34,10 @@ from ..utils.timer import NULL, StageTimer
 from . import exact
 
 UNKNOWN, SAT, UNSAT, RUNNING = 0, 1, 2, 3
+
+# process-wide native-runtime counters (diagnostics: tools/diag_shard_diff.py, bench --profile)
+STATS: Dict[str, int] = {"levels": 0, "launches": 0, "cand_overflow_levels": 0}
+_STATS_LOCK = threading.Lock()
 VERDICT_NAMES = {UNKNOWN: "unknown", SAT: "sat", UNSAT: "unsat", RUNNING: "running"}
 
 
@@ -46,6 +50,10 @@ class BaBConfig:
     mode: str = "symbolic"
     cand_cap: int = 1 << 17          # candidate pairs confirmed per BFS level (native runtime)
     crown: bool = os.environ.get("FAIRIFY_CROWN", "1") != "0"   # backward output bounds per node
+    # native runtime branching rule: a partition with w nodes in a BFS level splits each along
+    # clamp(log2(split_target / w), 1, 6) dims (per partition: verdicts do not depend on which
+    # partitions share a chunk)
+    split_target: int = int(os.environ.get("FAIRIFY_SPLIT_TARGET", "256"))
 
 
 @dataclass
@@ -294,7 +302,7 @@ class BaBSolver:
         # one runtime per (query, host thread): concurrent chunks of one model on several
         # streams must not share device work buffers
         key = (tuple(self.q.pa_idx), tuple(self.q.ra_idx), self.q.tau, values_np.tobytes(), pairs_np.tobytes(),
-               threading.get_ident(), bool(self.cfg.crown))
+               threading.get_ident(), bool(self.cfg.crown), int(self.cfg.split_target))
         cache = self.be.__dict__.setdefault("_bab_rt", {})
         cap = max(self.cfg.max_pool, n_run)
         rt = cache.get(key)
@@ -307,7 +315,7 @@ class BaBSolver:
                                    pairs_np.astype(np.int64).reshape(-1).tolist(),
                                    list(self.q.ra_idx) if self.relaxed else [], float(self.q.tau),
                                    shared.tolist(), int(cap), int(self.cfg.batch_nodes), int(self.cfg.cand_cap),
-                                   float(self.be.unit), bool(self.cfg.crown)), cap)
+                                   float(self.be.unit), bool(self.cfg.crown), int(self.cfg.split_target)), cap)
             cache[key] = rt
         return rt[0]
 
@@ -342,6 +350,9 @@ class BaBSolver:
                                                   int(self.cfg.node_budget), float(self.cfg.time_budget), dead_ptr,
                                                   confirm, stream, exact_models is None)
         self.stats = dict(stats)
+        with _STATS_LOCK:
+            for k in STATS:
+                STATS[k] += int(self.stats.get(k, 0))
         return BaBResult(np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes),
                          int(stats["levels"]), time.time() - t0, open_left=np.asarray(stats["open_left"]))
 
