@@ -70,6 +70,33 @@ struct AscentArgs {
   int S;
 };
 
+// Fused residual falsifier (engine/falsify.py), non-relaxed queries, one workgroup per partition:
+// heavy sampling (first strict flip), boundary walk between extreme samples, lattice coordinate
+// ascent from the best samples.
+struct FalsifyArgs {
+  const float* flat;
+  const float* lo;          // [P, n0]
+  const float* hi;          // [P, n0]
+  const int64_t* pids;      // [P]
+  int P;
+  int n_samples;            // heavy-sampling points per partition
+  int n_local;              // the first n_local samples seed the local search
+  uint32_t seed;
+  int V, npa;
+  int pa_idx[FA_MAX_PA];
+  const int64_t* values;    // [V, npa]
+  int Pp;
+  const int64_t* pairs;     // [Pp, 2]
+  int walk_k, walk_steps;   // boundary walk: k extreme pairs, bisection steps (0 = off)
+  int K, iters;             // local search: starts, coordinate-ascent rounds
+  int nfree;
+  int free_idx[64];
+  uint8_t* found;           // [P]
+  float* wit_x;             // [P, n0]
+  float* wit_xp;            // [P, n0]
+  int8_t* how;              // [P] 0 none, 1 sampling, 2 boundary walk, 3 local search
+};
+
 struct SimArgs {
   const float* flat;
   const float* lo;          // [P, n0]

@@ -1,6 +1,6 @@
 // Branch-and-bound level kernels (K9): close / flag / split nodes into the next BFS level.
 //
-// fa_split_kernel      one thread per node of a sub-batch: drop closed nodes and nodes of decided
+// fa_split_kernel      one wave64 per node of a sub-batch: drop closed nodes and nodes of decided
 //                      partitions; flag possible violations for exact host confirmation (every
 //                      possible PA pair of a leaf = single lattice point; the LP-optimal vertex
 //                      pair of an inner node); split open inner nodes along their top-m scored
@@ -31,180 +31,273 @@
 #define ST_RUNNING 3
 #define ST_STOPPING 4   // out of budget during the current level
 
-__device__ __forceinline__ void fa_tighten(const SplitArgs& a, float* lo, float* hi, float* plo, float* phi) {
-  for (int k = 0; k < a.nra; ++k) {
-    const int r = a.ra_idx[k];
-    plo[r] = fmaxf(plo[r], lo[r] - a.tau);
-    phi[r] = fminf(phi[r], hi[r] + a.tau);
-    lo[r] = fmaxf(lo[r], plo[r] - a.tau);
-    hi[r] = fminf(hi[r], phi[r] + a.tau);
-  }
-}
-
 // budget / capacity exhausted: the partition ends UNKNOWN with this node left open
 __device__ __forceinline__ void fa_stop(const SplitArgs& a, int p) { a.status[p] = ST_STOPPING; }
 
-#define FA_SPLIT_THREADS 64
-__global__ void __launch_bounds__(FA_SPLIT_THREADS) fa_split_kernel(SplitArgs a) {
-  const int n = blockIdx.x * FA_SPLIT_THREADS + threadIdx.x;
-  if (n >= a.Nn) return;
-  const int p = a.part[n];
-  if (!a.open[n]) return;
-  // RUNNING or STOPPING (budget ran out earlier in this same level): both still active this level
-  const int8_t s0 = a.status[p];
-  if (s0 != ST_RUNNING && s0 != ST_STOPPING) return;
-  if (!a.leaf[n] && a.lvl_open) atomicAdd(&a.lvl_open[p], 1);
+// Dimension d of child c (bit j of c = upper half along dims[j]): x box [lo, hi], x' box [plo, phi].
+// Every dimension of a child is a function of that dimension alone (the relaxed |x_r - x'_r| <= tau
+// tightening included), so lanes can build (child, dim) entries independently.
+__device__ __forceinline__ void fa_child_dim(const SplitArgs& a, const float* xl, const float* xh, const float* pl,
+                                             const float* ph, const int* dims, int m, int c, int d, float& lo,
+                                             float& hi, float& plo, float& phi) {
+  lo = xl[d]; hi = xh[d]; plo = pl[d]; phi = ph[d];
+  for (int j = 0; j < m; ++j) {
+    const int dd = dims[j];
+    const bool up = (c >> j) & 1;
+    if (dd == d) {
+      const float mid = floorf(0.5f * (xl[d] + xh[d]));
+      if (up) lo = mid + 1.f; else hi = mid;
+      if (a.relaxed && a.shared[d]) { plo = lo; phi = hi; }
+    } else if (dd == a.n0 + d) {
+      const float mid = floorf(0.5f * (pl[d] + ph[d]));
+      if (up) plo = mid + 1.f; else phi = mid;
+    }
+  }
+  if (a.relaxed)
+    for (int k = 0; k < a.nra; ++k)
+      if (a.ra_idx[k] == d) {
+        plo = fmaxf(plo, lo - a.tau);
+        phi = fminf(phi, hi + a.tau);
+        lo = fmaxf(lo, plo - a.tau);
+        hi = fminf(hi, phi + a.tau);
+      }
+}
+
+// (score, dim) arg-max over the wave: larger score wins, ties go to the lower dimension (the
+// sequential scan's first strict maximum)
+__device__ __forceinline__ void fa_wave_argmax(float& s, int& d) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float s2 = __shfl_xor(s, o);
+    const int d2 = __shfl_xor(d, o);
+    if (s2 > s || (s2 == s && d2 < d)) { s = s2; d = d2; }
+  }
+}
+
+// Per-node plan of the split kernel (phase A -> phase C through LDS).
+struct FaSplitPlan {
+  unsigned long long fmask;   // feasible children (bit c = child c)
+  unsigned long long dims;    // split dims, 7 bits each
+  int m;                      // split dim count (children = 2^m before feasibility)
+  int nchild;                 // feasible children to write
+  int ncand;                  // candidate pairs to write
+  int leaf;
+};
+
+// Possible-violation test of (orientation, pair) t at a leaf node (rows of the node's PA values).
+__device__ __forceinline__ bool fa_leaf_poss(const SplitArgs& a, int n, int t) {
+  const int o = t / a.Pp, q = t - o * a.Pp;
+  const size_t ri = (size_t)n * a.V + (int)a.pairs[2 * q], rj = (size_t)n * a.V + (int)a.pairs[2 * q + 1];
+  return (o == 0) ? (a.olb[ri] < 0.f && a.oubp[rj] > 0.f) : (a.oub[ri] > 0.f && a.olbp[rj] < 0.f);
+}
+
+// Inclusive wave64 prefix sum.
+__device__ __forceinline__ int fa_wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// One wave64 per node, FA_SPLIT_NPW nodes per wave, FA_SPLIT_NB nodes per workgroup, three phases:
+//   A  each wave plans its nodes: split dims by wave arg-max reductions, feasible children by a
+//      ballot (lane c = child c), candidate counts by ballots over the leaf's PA pairs;
+//   B  wave 0 scans the block's child / candidate counts and reserves both ranges with ONE
+//      atomic each (a per-node atomic on the level counter serialised ~32 K same-address atomics
+//      per sub-batch in L2: ~135 us of the kernel's time in the round-2 baseline);
+//   C  each wave writes its children lane-parallel over (child, dim) entries (consecutive lanes
+//      store consecutive floats of the pool) and its candidate pairs.
+#define FA_SPLIT_WAVES 8
+#define FA_SPLIT_NPW 8
+#define FA_SPLIT_NB (FA_SPLIT_WAVES * FA_SPLIT_NPW)
+__global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs a) {
+  __shared__ FaSplitPlan plan[FA_SPLIT_NB];
+  __shared__ int child_off[FA_SPLIT_NB], cand_off[FA_SPLIT_NB];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   const int n0 = a.n0;
-  const float* xl = a.xlo + (size_t)n * n0;
-  const float* xh = a.xhi + (size_t)n * n0;
-  const float* pl = a.relaxed ? a.xplo + (size_t)n * n0 : xl;
-  const float* ph = a.relaxed ? a.xphi + (size_t)n * n0 : xh;
-  // ---------------- candidates for exact confirmation
-  if (a.leaf[n]) {
-    for (int o = 0; o < a.norient; ++o)
-      for (int q = 0; q < a.Pp; ++q) {
-        const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
-        const size_t ri = (size_t)n * a.V + vi, rj = (size_t)n * a.V + vj;
-        const bool poss = (o == 0) ? (a.olb[ri] < 0.f && a.oubp[rj] > 0.f) : (a.oub[ri] > 0.f && a.olbp[rj] < 0.f);
-        if (!poss) continue;
-        const int slot = atomicAdd(a.cand_count, 1);
-        if (slot >= a.cand_cap) {      // cannot confirm this leaf: stay sound
-          fa_stop(a, p);
-          return;
-        }
-        float* cb = a.cand_buf + (size_t)slot * 2 * n0;
-        for (int d = 0; d < n0; ++d) {
-          cb[d] = xl[d];
-          cb[n0 + d] = pl[d];
-        }
-        for (int k = 0; k < a.npa; ++k) {
-          cb[a.pa_idx[k]] = (float)a.values[vi * a.npa + k];
-          cb[n0 + a.pa_idx[k]] = (float)a.values[vj * a.npa + k];
-        }
-        a.cand_part[slot] = p;
+  const int npair = a.norient * a.Pp;
+  // ---------------- phase A: plan
+  for (int i = 0; i < FA_SPLIT_NPW; ++i) {
+    const int loc = wave * FA_SPLIT_NPW + i;
+    const int n = blockIdx.x * FA_SPLIT_NB + loc;
+    FaSplitPlan pl{0ull, 0ull, 0, 0, 0, 0};
+    do {
+      if (n >= a.Nn || !a.open[n]) break;                  // wave-uniform
+      const int p = a.part[n];
+      // RUNNING or STOPPING (budget ran out earlier in this same level): both still active
+      const int8_t s0 = a.status[p];
+      if (s0 != ST_RUNNING && s0 != ST_STOPPING) break;
+      if (a.leaf[n]) {   // every possible PA pair of the single lattice point goes to the host check
+        pl.leaf = 1;
+        for (int t0 = 0; t0 < npair; t0 += 64)
+          pl.ncand += __popcll(__ballot(t0 + lane < npair && fa_leaf_poss(a, n, t0 + lane)));
+        break;
       }
-    return;  // a leaf is decided by the host check
-  }
-  {
-    const float lbx = a.pe_lb[n], ubx = a.pe_ub[n];
-    const float lbp = a.pe_lb[a.Nn + n], ubp = a.pe_ub[a.Nn + n];
-    const bool poss = (lbx < 0.f && ubp > 0.f) || (ubx > 0.f && lbp < 0.f);
-    if (poss) {
-      const int slot = atomicAdd(a.cand_count, 1);
-      if (slot < a.cand_cap) {
-        float* cb = a.cand_buf + (size_t)slot * 2 * n0;
-        for (int d = 0; d < n0; ++d) {
-          cb[d] = a.cand_x[(size_t)n * n0 + d];
-          cb[n0 + d] = a.cand_xp[(size_t)n * n0 + d];
-        }
-        a.cand_part[slot] = p;
+      if (lane == 0 && a.lvl_open) atomicAdd(&a.lvl_open[p], 1);
+      {
+        const float lbx = a.pe_lb[n], ubx = a.pe_ub[n];
+        const float lbp = a.pe_lb[a.Nn + n], ubp = a.pe_ub[a.Nn + n];
+        pl.ncand = ((lbx < 0.f && ubp > 0.f) || (ubx > 0.f && lbp < 0.f)) ? 1 : 0;
       }
+      // split along the top-m scored dimensions (2 n0 <= 128 scores: two per lane)
+      const float* sc = a.scores + (size_t)n * 2 * n0;
+      int mreq = 1;
+      {
+        const int mmax = a.m < FA_MAX_SPLIT ? a.m : FA_MAX_SPLIT;
+        const int w = a.nodes_start[p] - a.prev_start[p];  // this partition's nodes in the level
+        while (mreq < mmax && ((long long)w << (mreq + 1)) <= (long long)a.target) ++mreq;
+      }
+      const int d0 = lane, d1 = lane + 64;
+      float s0v = (d0 < 2 * n0) ? sc[d0] : -1.f;
+      float s1v = (d1 < 2 * n0) ? sc[d1] : -1.f;
+      if (!(s0v > -0.5f)) s0v = -1.f;                      // NaN / below the threshold: never picked
+      if (!(s1v > -0.5f)) s1v = -1.f;
+      int dims[FA_MAX_SPLIT];
+      int m = 0;
+      for (int j = 0; j < mreq; ++j) {
+        float sv = s0v >= s1v ? s0v : s1v;                 // ties: d0 < d1
+        int d = s0v >= s1v ? d0 : d1;
+        if (sv <= -0.5f) d = 0x7fffffff;
+        fa_wave_argmax(sv, d);
+        if (sv <= -0.5f) break;                            // wave-uniform after the reduction
+        dims[m++] = d;
+        if (d == d0) s0v = -1.f;
+        if (d == d1) s1v = -1.f;
+      }
+      if (m == 0) break;   // no splittable dimension: treated as leaf by the certificate
+      if (a.nodes_start[p] >= a.budget) {
+        if (lane == 0) fa_stop(a, p);
+        break;
+      }
+      const int k = 1 << m;
+      const float* xl = a.xlo + (size_t)n * n0;
+      const float* xh = a.xhi + (size_t)n * n0;
+      const float* xpl = a.relaxed ? a.xplo + (size_t)n * n0 : xl;
+      const float* xph = a.relaxed ? a.xphi + (size_t)n * n0 : xh;
+      bool ok = lane < k;   // children feasibility (the relaxed coupling can empty a child)
+      if (a.relaxed && ok)
+        for (int d = 0; d < n0; ++d) {
+          float lo, hi, plo, phi;
+          fa_child_dim(a, xl, xh, xpl, xph, dims, m, lane, d, lo, hi, plo, phi);
+          ok = ok && lo <= hi && plo <= phi;
+        }
+      pl.fmask = __ballot(ok);
+      pl.nchild = __popcll(pl.fmask);
+      pl.m = m;
+      for (int j = 0; j < m; ++j) pl.dims |= (unsigned long long)dims[j] << (7 * j);
+      if (lane == 0 && pl.nchild) atomicAdd(&a.part_nodes[p], pl.nchild);
+    } while (false);
+    if (lane == 0) plan[loc] = pl;
+  }
+  __syncthreads();
+  // ---------------- phase B: one reservation per workgroup for children and candidates
+  if (wave == 0) {
+    const int c = plan[lane].nchild, q = plan[lane].ncand;
+    const int ci = fa_wave_incl_scan(c, lane), qi = fa_wave_incl_scan(q, lane);
+    int cb = 0, qb = 0;
+    if (lane == 63) {
+      if (ci) cb = atomicAdd(a.count_out, ci);
+      if (qi) qb = atomicAdd(a.cand_count, qi);
     }
+    cb = __shfl(cb, 63);
+    qb = __shfl(qb, 63);
+    child_off[lane] = cb + ci - c;
+    cand_off[lane] = qb + qi - q;
   }
-  // ---------------- split along the top-m scored dimensions
-  const float* sc = a.scores + (size_t)n * 2 * n0;
-  int dims[FA_MAX_SPLIT];
-  int m = 0;
-  int mreq = 1;
-  {
-    const int mmax = a.m < FA_MAX_SPLIT ? a.m : FA_MAX_SPLIT;
-    const int w = a.nodes_start[p] - a.prev_start[p];      // this partition's nodes in the level
-    while (mreq < mmax && ((long long)w << (mreq + 1)) <= (long long)a.target) ++mreq;
-  }
-  for (int j = 0; j < mreq; ++j) {
-    float best = -0.5f;
-    int bd = -1;
-    for (int d = 0; d < 2 * n0; ++d) {
-      bool used = false;
-      for (int u = 0; u < m; ++u) used |= (dims[u] == d);
-      if (!used && sc[d] > best) { best = sc[d]; bd = d; }
-    }
-    if (bd < 0) break;
-    dims[m++] = bd;
-  }
-  if (m == 0) return;  // no splittable dimension: treated as leaf by the certificate
-  const int k = 1 << m;
-  if (a.nodes_start[p] >= a.budget) { fa_stop(a, p); return; }
-  if (!a.relaxed) {  // fast path: every child feasible, boxes written on the fly
-    atomicAdd(&a.part_nodes[p], k);
-    const int off = atomicAdd(a.count_out, k);
-    if (off + k > a.cap) { fa_stop(a, p); return; }
-    for (int c = 0; c < k; ++c) {
-      float* ol = a.oxlo + (size_t)(off + c) * n0;
-      float* oh = a.oxhi + (size_t)(off + c) * n0;
-      for (int d = 0; d < n0; ++d) {
-        float lo = xl[d], hi = xh[d];
-        for (int j = 0; j < m; ++j)
-          if (dims[j] == d) {
-            const float mid = floorf(0.5f * (lo + hi));
-            if ((c >> j) & 1) lo = mid + 1.f; else hi = mid;
+  __syncthreads();
+  // ---------------- phase C: write candidates and children
+  for (int i = 0; i < FA_SPLIT_NPW; ++i) {
+    const int loc = wave * FA_SPLIT_NPW + i;
+    const int n = blockIdx.x * FA_SPLIT_NB + loc;
+    const FaSplitPlan pl = plan[loc];
+    if (pl.ncand == 0 && pl.nchild == 0) continue;         // wave-uniform (LDS broadcast)
+    const int p = a.part[n];
+    const float* xl = a.xlo + (size_t)n * n0;
+    const float* xh = a.xhi + (size_t)n * n0;
+    const float* xpl = a.relaxed ? a.xplo + (size_t)n * n0 : xl;
+    const float* xph = a.relaxed ? a.xphi + (size_t)n * n0 : xh;
+    if (pl.leaf) {
+      int slot0 = cand_off[loc];
+      for (int t0 = 0; t0 < npair; t0 += 64) {
+        const int t = t0 + lane;
+        const bool poss = t < npair && fa_leaf_poss(a, n, t);
+        const unsigned long long bm = __ballot(poss);
+        if (poss) {
+          const int slot = slot0 + __popcll(bm & ((1ull << lane) - 1ull));
+          if (slot >= a.cand_cap) {
+            fa_stop(a, p);        // cannot confirm this leaf: stay sound
+          } else {
+            const int o = t / a.Pp, q = t - o * a.Pp;
+            const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
+            float* cbuf = a.cand_buf + (size_t)slot * 2 * n0;
+            for (int d = 0; d < n0; ++d) {
+              cbuf[d] = xl[d];
+              cbuf[n0 + d] = xpl[d];
+            }
+            for (int k = 0; k < a.npa; ++k) {
+              cbuf[a.pa_idx[k]] = (float)a.values[vi * a.npa + k];
+              cbuf[n0 + a.pa_idx[k]] = (float)a.values[vj * a.npa + k];
+            }
+            a.cand_part[slot] = p;
           }
-        ol[d] = lo;
-        oh[d] = hi;
+        }
+        slot0 += __popcll(bm);
       }
-      a.opart[off + c] = p;
+      continue;
     }
-    return;
-  }
-  // children feasibility (relaxed coupling can empty a child)
-  float clo[64], chi[64], cplo[64], cphi[64];
-  if (n0 > 64) { fa_stop(a, p); return; }
-  int feasible = 0;
-  unsigned long long fmask = 0ull;
-  for (int c = 0; c < k; ++c) {
-    for (int d = 0; d < n0; ++d) { clo[d] = xl[d]; chi[d] = xh[d]; cplo[d] = pl[d]; cphi[d] = ph[d]; }
-    for (int j = 0; j < m; ++j) {
-      const int d = dims[j];
-      const int bit = (c >> j) & 1;
-      if (d < n0) {
-        const float mid = floorf(0.5f * (xl[d] + xh[d]));
-        if (bit) clo[d] = mid + 1.f; else chi[d] = mid;
-        if (a.relaxed && a.shared[d]) { cplo[d] = clo[d]; cphi[d] = chi[d]; }
-      } else {
-        const int e = d - n0;
-        const float mid = floorf(0.5f * (pl[e] + ph[e]));
-        if (bit) cplo[e] = mid + 1.f; else cphi[e] = mid;
+    if (pl.ncand) {
+      const int slot = cand_off[loc];
+      if (slot < a.cand_cap) {
+        float* cbuf = a.cand_buf + (size_t)slot * 2 * n0;
+        for (int d = lane; d < 2 * n0; d += 64)
+          cbuf[d] = d < n0 ? a.cand_x[(size_t)n * n0 + d] : a.cand_xp[(size_t)n * n0 + d - n0];
+        if (lane == 0) a.cand_part[slot] = p;
       }
     }
-    bool ok = true;
-    if (a.relaxed) {
-      fa_tighten(a, clo, chi, cplo, cphi);
-      for (int d = 0; d < n0; ++d) ok &= (clo[d] <= chi[d]) && (cplo[d] <= cphi[d]);
+    if (pl.nchild == 0) continue;
+    const int off = child_off[loc];
+    if (off + pl.nchild > a.cap) {
+      // pool full: the partition stops UNKNOWN.  Slots of this reservation below the capacity
+      // are counted in the next level, so they get a copy of the parent (a sub-box of its own
+      // partition: re-bounding it is redundant but sound) instead of stale or unset entries.
+      if (lane == 0) fa_stop(a, p);
+      const int lim = a.cap - off;
+      for (int e = lane; e < lim * n0; e += 64) {
+        const int r = e / n0, d = e - r * n0;
+        const size_t o = (size_t)(off + r) * n0 + d;
+        a.oxlo[o] = xl[d];
+        a.oxhi[o] = xh[d];
+        if (a.relaxed) { a.oxplo[o] = xpl[d]; a.oxphi[o] = xph[d]; }
+      }
+      for (int r = lane; r < lim; r += 64) a.opart[off + r] = p;
+      continue;
     }
-    if (ok) { fmask |= (1ull << c); ++feasible; }
-  }
-  if (feasible == 0) return;
-  atomicAdd(&a.part_nodes[p], feasible);
-  const int off = atomicAdd(a.count_out, feasible);
-  if (off + feasible > a.cap) { fa_stop(a, p); return; }
-  int w = off;
-  for (int c = 0; c < k; ++c) {
-    if (!((fmask >> c) & 1ull)) continue;
-    for (int d = 0; d < n0; ++d) { clo[d] = xl[d]; chi[d] = xh[d]; cplo[d] = pl[d]; cphi[d] = ph[d]; }
-    for (int j = 0; j < m; ++j) {
-      const int d = dims[j];
-      const int bit = (c >> j) & 1;
-      if (d < n0) {
-        const float mid = floorf(0.5f * (xl[d] + xh[d]));
-        if (bit) clo[d] = mid + 1.f; else chi[d] = mid;
-        if (a.relaxed && a.shared[d]) { cplo[d] = clo[d]; cphi[d] = chi[d]; }
-      } else {
-        const int e = d - n0;
-        const float mid = floorf(0.5f * (pl[e] + ph[e]));
-        if (bit) cplo[e] = mid + 1.f; else cphi[e] = mid;
+    int dims[FA_MAX_SPLIT];
+    for (int j = 0; j < pl.m; ++j) dims[j] = (int)((pl.dims >> (7 * j)) & 127ull);
+    // output slot of feasible child c = off + (feasible children before c)
+    if ((pl.fmask >> lane) & 1ull) a.opart[off + __popcll(pl.fmask & ((1ull << lane) - 1ull))] = p;
+    const int dense = (pl.fmask & (pl.fmask + 1ull)) == 0ull;   // feasible children = 0 .. nchild-1
+    for (int e = lane; e < pl.nchild * n0; e += 64) {
+      const int r = e / n0, d = e - r * n0;      // r-th feasible child
+      int c = r;
+      if (!dense) {                              // relaxed: the r-th set bit of fmask
+        unsigned long long mm = pl.fmask;
+        for (int t = 0; t < r; ++t) mm &= mm - 1ull;
+        c = __ffsll((long long)mm) - 1;
+      }
+      float lo, hi, plo, phi;
+      fa_child_dim(a, xl, xh, xpl, xph, dims, pl.m, c, d, lo, hi, plo, phi);
+      const size_t o = (size_t)(off + r) * n0 + d;
+      a.oxlo[o] = lo;
+      a.oxhi[o] = hi;
+      if (a.relaxed) {
+        a.oxplo[o] = plo;
+        a.oxphi[o] = phi;
       }
     }
-    if (a.relaxed) fa_tighten(a, clo, chi, cplo, cphi);
-    float* ol = a.oxlo + (size_t)w * n0;
-    float* oh = a.oxhi + (size_t)w * n0;
-    for (int d = 0; d < n0; ++d) { ol[d] = clo[d]; oh[d] = chi[d]; }
-    if (a.relaxed) {
-      float* opl = a.oxplo + (size_t)w * n0;
-      float* oph = a.oxphi + (size_t)w * n0;
-      for (int d = 0; d < n0; ++d) { opl[d] = cplo[d]; oph[d] = cphi[d]; }
-    }
-    a.opart[w] = p;
-    ++w;
   }
 }
 
@@ -244,7 +337,7 @@ __global__ void fa_set_status_kernel(const int* idx, int n, int8_t* status, int8
 extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream) {
   if (a.Nn <= 0) return 0;
   if (a.nra > FA_MAX_RA || a.npa > FA_CMAX_PA || a.n0 > 64) return -3;
-  hipLaunchKernelGGL(fa_split_kernel, dim3((a.Nn + FA_SPLIT_THREADS - 1) / FA_SPLIT_THREADS), dim3(FA_SPLIT_THREADS),
+  hipLaunchKernelGGL(fa_split_kernel, dim3((a.Nn + FA_SPLIT_NB - 1) / FA_SPLIT_NB), dim3(64 * FA_SPLIT_WAVES),
                      0, stream, a);
   return (int)hipGetLastError();
 }

@@ -22,6 +22,7 @@ extern "C" int fa_forward_launch(const NetDesc& net, FwdArgs a, hipStream_t stre
 extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream);
 extern "C" int fa_ascent_launch(const NetDesc& net, AscentArgs a, hipStream_t stream);
 extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
+extern "C" int fa_falsify_launch(const NetDesc& net, FalsifyArgs a, hipStream_t stream);
 
 template <typename T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
@@ -223,6 +224,39 @@ PYBIND11_MODULE(_C, m) {
     const int rc = fa_ascent_launch(net.d, a, (hipStream_t)stream);
     if (rc == -1) return false;
     check(rc, "ascent");
+    return true;
+  });
+
+  // fused residual falsifier; returns false when the network shape is not supported (caller
+  // keeps the PyTorch path)
+  m.def("falsify", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t pids, int Pn,
+                      int n_samples, int n_local, uint32_t seed, int V, const std::vector<int>& pa, uintptr_t values,
+                      int Pp, uintptr_t pairs, int walk_k, int walk_steps, int K, int iters,
+                      const std::vector<int>& free_dims, uintptr_t found, uintptr_t wit_x, uintptr_t wit_xp,
+                      uintptr_t how, uintptr_t stream) {
+    if (pa.size() > FA_MAX_PA || free_dims.size() > 64) throw std::invalid_argument("too many PA/free dims");
+    FalsifyArgs a{};
+    a.flat = P<const float>(flat);
+    a.lo = P<const float>(lo);
+    a.hi = P<const float>(hi);
+    a.pids = P<const int64_t>(pids);
+    a.P = Pn; a.n_samples = n_samples; a.n_local = n_local; a.seed = seed;
+    a.V = V;
+    a.npa = (int)pa.size();
+    for (size_t i = 0; i < pa.size(); ++i) a.pa_idx[i] = pa[i];
+    a.values = P<const int64_t>(values);
+    a.Pp = Pp;
+    a.pairs = P<const int64_t>(pairs);
+    a.walk_k = walk_k; a.walk_steps = walk_steps; a.K = K; a.iters = iters;
+    a.nfree = (int)free_dims.size();
+    for (size_t i = 0; i < free_dims.size(); ++i) a.free_idx[i] = free_dims[i];
+    a.found = P<uint8_t>(found);
+    a.wit_x = P<float>(wit_x);
+    a.wit_xp = P<float>(wit_xp);
+    a.how = P<int8_t>(how);
+    const int rc = fa_falsify_launch(net.d, a, (hipStream_t)stream);
+    if (rc == 0) return false;
+    if (rc < 0) check(-rc, "falsify");
     return true;
   });
 

@@ -248,6 +248,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_finalize_kernel(NetDesc net
 extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) {
   if (a.P <= 0) return 0;
   if (a.npa > FA_MAX_PA || a.nra > FA_MAX_RA) return -3;
+  if ((long long)a.n_samples * a.Pp >= 0x7FFFFFFFLL) return -3;   // flip keys sample * Pp + pair are int
   a.S = net.max_width | 1;
   const int n0 = net.dims[0];
   size_t floats = 2 * (size_t)FA_TR * a.S + (size_t)FA_TR * n0 + 2 * (size_t)FA_TR * a.V + FA_TR + 2 * n0;

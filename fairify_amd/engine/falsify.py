@@ -14,15 +14,20 @@ the LP-optimal vertex candidates of the BaB miss them.  For those partitions onl
 3. from the ``k_starts`` best points, coordinate ascent on the integer lattice: every ±1 move
    of a non-protected feature (and of the relaxed offset x'_r - x_r within [-tau, tau]) is
    evaluated in one batched forward, the best improving move is taken, ``iters`` rounds.
-   On the HIP path (non-relaxed queries) all rounds run inside one ``fa_ascent_kernel``
-   launch per sub-batch (``csrc/forward.hip``); each partition stops at its first hit.
+   On the HIP path (non-relaxed queries) all three steps -- heavy sampling, the boundary walk of
+   :func:`engine.sim.boundary_walk` and the ascent -- run in ONE ``fa_falsify_kernel`` launch
+   (``csrc/falsify.hip``, register-resident MFMA forward); each partition stops at its first hit.
+   Relaxed queries keep the simulation kernel + PyTorch walk + ``fa_ascent_kernel`` path.
 
 Hits are only *candidates*: the pipeline confirms them with the exact checker
 (:mod:`fairify_amd.engine.exact`) before a partition becomes SAT.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
+from typing import Optional
+
 import torch
 
 from ..ops import reference as ref
@@ -35,6 +40,7 @@ class FalsifyResult:
     found: torch.Tensor       # [P] bool
     wit_x: torch.Tensor       # [P, n0] float (integral values)
     wit_xp: torch.Tensor
+    how: Optional[torch.Tensor] = None   # [P] int8 (fused kernel): 1 sampling, 2 boundary walk, 3 local search
 
 
 def _margins(be: Backend, X: torch.Tensor, D: torch.Tensor, pa: torch.Tensor, ra: torch.Tensor,
@@ -67,6 +73,14 @@ def residual_falsify(be: Backend, q: ResolvedQuery, lo: torch.Tensor, hi: torch.
     ``n_local`` materialised samples of the partitions still without a witness."""
     P, n = lo.shape
     dev = lo.device
+    if be.hip and P and not q.relaxed and os.environ.get("FAIRIFY_FUSED_FALSIFY", "1") != "0":
+        from ..ops import hip
+
+        free = [d for d in range(n) if d not in set(q.pa_idx)]
+        out = hip.falsify(be, q, lo, hi, pids, values, pairs, (seed ^ 0x6A09E667) & 0xFFFFFFFF, n_samples, n_local,
+                          16, 12, k_starts, iters, free)
+        if out is not None:
+            return FalsifyResult(out[0], out[1], out[2], how=out[3])
     if be.hip and P:
         from ..ops import hip
 

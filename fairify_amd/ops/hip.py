@@ -284,3 +284,38 @@ def ascent(be, q, lo, hi, x0, f0, q0, iters, values, pairs, free_dims):
     if not ok:
         return None
     return found.bool(), wx, wxp
+
+
+def falsify(be, q, lo, hi, pids, values, pairs, seed, n_samples, n_local, walk_k, walk_steps, k_starts, iters,
+            free_dims):
+    """Fused residual falsifier (``csrc/falsify.hip``), non-relaxed queries: heavy sampling,
+    boundary walk, lattice coordinate ascent in one launch.  Returns ``(found [P] bool,
+    wit_x [P, n0], wit_xp [P, n0], how [P] int8)`` or ``None`` when the network shape is not
+    supported by the kernel (the caller keeps the PyTorch path)."""
+    P, n0 = lo.shape
+    dev = lo.device
+    if q.relaxed:
+        raise ValueError("fused falsifier: non-relaxed queries only")
+    lo_c = _c(lo, torch.float32, (P, n0), "lo")
+    hi_c = _c(hi, torch.float32, (P, n0), "hi")
+    pids_c = _c(pids, torch.int64, (P,), "pids")
+    V = values.shape[0]
+    Pp = pairs.shape[0]
+    values_c = _c(values, torch.int64, None, "values")
+    pairs_c = _c(pairs, torch.int64, (Pp, 2), "pairs")
+    if values_c.numel() != V * len(q.pa_idx):
+        raise ValueError("values: expected [V, n_pa]")
+    found = torch.zeros(P, dtype=torch.uint8, device=dev)
+    wx = torch.zeros(P, n0, dtype=torch.float32, device=dev)
+    wxp = torch.zeros(P, n0, dtype=torch.float32, device=dev)
+    how = torch.zeros(P, dtype=torch.int8, device=dev)
+    if P == 0 or Pp == 0 or n_samples <= 0:
+        return found.bool(), wx, wxp, how
+    ok = ext().falsify(_net(be), be.flat.data_ptr(), lo_c.data_ptr(), hi_c.data_ptr(), pids_c.data_ptr(), P,
+                       int(n_samples), int(n_local), int(seed) & 0xFFFFFFFF, V, list(q.pa_idx), values_c.data_ptr(),
+                       Pp, pairs_c.data_ptr(), int(walk_k), int(walk_steps), int(k_starts), int(iters),
+                       [int(d) for d in free_dims], found.data_ptr(), wx.data_ptr(), wxp.data_ptr(), how.data_ptr(),
+                       _stream(dev))
+    if not ok:
+        return None
+    return found.bool(), wx, wxp, how

@@ -96,3 +96,55 @@ def test_ascent_kernel_matches_torch_loop(cuda, monkeypatch):
             assert exact.check_pair_constraints(X, XP, lo_n, hi_n, q.pa_idx, q.ra_idx, 0).all()
             assert exact.is_violation(m, X, XP).all()
     assert calls["n"] >= 4   # the kernel path ran
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["AC-1", "AC-4", "AC-7"])
+def test_fused_falsifier_matches_sim_and_is_sound(cuda, monkeypatch, model):
+    """fa_falsify_kernel (sampling + boundary walk + ascent in one launch) against the unfused
+    path it replaces (simulation kernel + PyTorch boundary walk + fa_ascent_kernel):
+    * every witness is an exact violation inside its box;
+    * the sampling phase reports the simulation kernel's first flip with the identical witness,
+      except where one of the two witnesses has a logit whose rigorous fp32 bound straddles 0
+      (the two kernels sum the MFMA products in different orders);
+    * it decides at least 98 % of what the unfused path decides."""
+    from fairify_amd import presets
+    from fairify_amd.engine import falsify as F
+    from fairify_amd.engine.bab import _pa_table
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.ops import hip
+    from fairify_amd.partition import processing_order
+
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, seed=0)[:768]
+    lo_np, hi_np = grid.decode(ids)
+    m = get_model(model, weights="random", seed=0)
+    be = Backend(m, cuda)
+    v_np, p_np = _pa_table(q, lo_np, hi_np)
+    values, pairs = torch.from_numpy(v_np).to(cuda), torch.from_numpy(p_np).to(cuda)
+    lo, hi = torch.from_numpy(lo_np).to(cuda).float(), torch.from_numpy(hi_np).to(cuda).float()
+    pids = torch.from_numpy(ids).to(cuda)
+    fused = F.residual_falsify(be, q, lo, hi, pids, values, pairs, 0, n_samples=2048, k_starts=16, iters=12)
+    assert fused.how is not None, "fused kernel did not run"
+    monkeypatch.setenv("FAIRIFY_FUSED_FALSIFY", "0")
+    legacy = F.residual_falsify(be, q, lo, hi, pids, values, pairs, 0, n_samples=2048, k_starts=16, iters=12)
+    sim = hip.simulate(be, q, lo, hi, pids, 2048, (0 ^ 0x6A09E667) & 0xFFFFFFFF, values, pairs, 0, 0)
+    f = fused.found.cpu().numpy()
+    how = fused.how.cpu().numpy()
+    idx = np.nonzero(f)[0]
+    X = fused.wit_x.cpu().numpy()[idx].round().astype(np.int64)
+    XP = fused.wit_xp.cpu().numpy()[idx].round().astype(np.int64)
+    assert exact.check_pair_constraints(X, XP, lo_np[idx], hi_np[idx], q.pa_idx, q.ra_idx, 0).all()
+    assert exact.is_violation(m, X, XP).all()
+    s_found = sim.found.cpu().numpy()
+    sx, sxp = sim.wit_x.cpu().numpy(), sim.wit_xp.cpu().numpy()
+    fx, fxp = fused.wit_x.cpu().numpy(), fused.wit_xp.cpu().numpy()
+    bad = [i for i in range(len(ids)) if s_found[i] != (how[i] == 1) or
+           (s_found[i] and not (np.array_equal(sx[i], fx[i]) and np.array_equal(sxp[i], fxp[i])))]
+    if bad:
+        pts = torch.from_numpy(np.concatenate([sx[bad], sxp[bad], fx[bad], fxp[bad]])).to(cuda)
+        lb, ub = be.point_bounds(pts)
+        amb = ((lb <= 0) & (ub >= 0)).view(4, len(bad)).any(dim=0).cpu().numpy()
+        assert amb.all(), f"{int((~amb).sum())} sampling-phase mismatches outside the rounding margin"
+    assert f.sum() >= 0.98 * legacy.found.cpu().numpy().sum()
