@@ -23,6 +23,14 @@ extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream);
 extern "C" int fa_ascent_launch(const NetDesc& net, AscentArgs a, hipStream_t stream);
 extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
 extern "C" int fa_falsify_launch(const NetDesc& net, FalsifyArgs a, hipStream_t stream);
+extern "C" int fa_prune_masks_launch(const NetDesc& net, int P, const int* counts, const float* ub, int ub_stride,
+                                     const uint8_t* sym_dead, uint8_t* code, int* cnt, hipStream_t stream);
+extern "C" int fa_heuristic_launch(const NetDesc& net, int Pu, const int64_t* rows, const float* lb, const float* ub,
+                                   int stride, const uint8_t* code, double q50, double qlo, double qhi, uint8_t* hnew,
+                                   uint8_t* hmerged, int* hcnt, hipStream_t stream);
+extern "C" int fa_agree_launch(const NetDesc& net, const float* flat, int Pm, const int64_t* rows, const float* lo,
+                               const float* hi, const int64_t* pids, const uint8_t* dead, int S, uint32_t seed,
+                               int* agree, hipStream_t stream);
 
 template <typename T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
@@ -257,6 +265,33 @@ PYBIND11_MODULE(_C, m) {
     const int rc = fa_falsify_launch(net.d, a, (hipStream_t)stream);
     if (rc == 0) return false;
     if (rc < 0) check(-rc, "falsify");
+    return true;
+  });
+
+  m.def("prune_masks", [](const Net& net, int Pn, uintptr_t counts, uintptr_t ub, int ub_stride, uintptr_t sym_dead,
+                          uintptr_t code, uintptr_t cnt, uintptr_t stream) {
+    check(fa_prune_masks_launch(net.d, Pn, P<const int>(counts), P<const float>(ub), ub_stride,
+                                P<const uint8_t>(sym_dead), P<uint8_t>(code), P<int>(cnt), (hipStream_t)stream),
+          "prune_masks");
+  });
+
+  m.def("heuristic", [](const Net& net, int Pu, uintptr_t rows, uintptr_t lb, uintptr_t ub, int stride, uintptr_t code,
+                        double q50, double qlo, double qhi, uintptr_t hnew, uintptr_t hmerged, uintptr_t hcnt,
+                        uintptr_t stream) {
+    check(fa_heuristic_launch(net.d, Pu, P<const int64_t>(rows), P<const float>(lb), P<const float>(ub), stride,
+                              P<const uint8_t>(code), q50, qlo, qhi, P<uint8_t>(hnew), P<uint8_t>(hmerged),
+                              P<int>(hcnt), (hipStream_t)stream),
+          "heuristic");
+  });
+
+  // returns false when the network shape is not supported (caller keeps the PyTorch path)
+  m.def("agree", [](const Net& net, uintptr_t flat, int Pm, uintptr_t rows, uintptr_t lo, uintptr_t hi, uintptr_t pids,
+                    uintptr_t dead, int S, uint32_t seed, uintptr_t agree, uintptr_t stream) {
+    const int rc = fa_agree_launch(net.d, P<const float>(flat), Pm, P<const int64_t>(rows), P<const float>(lo),
+                                   P<const float>(hi), P<const int64_t>(pids), P<const uint8_t>(dead), S, seed,
+                                   P<int>(agree), (hipStream_t)stream);
+    if (rc == 0) return false;
+    if (rc < 0) check(-rc, "agree");
     return true;
   });
 

@@ -48,9 +48,11 @@ __device__ __forceinline__ void fa_stage_wperm(const NetDesc& net, const float* 
 
 // One layer: H (inputs of layer l) -> H2 (ReLU outputs; padded neurons 0).  On the last layer
 // returns the logit of point lane&15 in lanes 0..15 (other lanes: unspecified).
+// ``dead`` (optional, LDS or global): per hidden neuron (all-neuron numbering) forced-zero flags.
 template <int TM>
 __device__ __forceinline__ float fa_reg_layer(const NetDesc& net, const RegNetCfg& cfg, const float* sw_all, int l,
-                                              int lane, const float (&H)[TM][4], float (&H2)[TM][4]) {
+                                              int lane, const float (&H)[TM][4], float (&H2)[TM][4],
+                                              const uint8_t* dead = nullptr) {
   const int grp = lane >> 4;
   const int n_in = net.dims[l], n_out = net.dims[l + 1];
   const int tin = (n_in + 15) >> 4, tout = (n_out + 15) >> 4;
@@ -79,7 +81,8 @@ __device__ __forceinline__ float fa_reg_layer(const NetDesc& net, const RegNetCf
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int j = 16 * jt + 4 * grp + i;
-      H2[jt][i] = j < n_out ? fmaxf(Z[i] + sb[j], 0.f) : 0.f;
+      const bool zero = j >= n_out || (dead && dead[net.neuron_off[l] + j]);
+      H2[jt][i] = zero ? 0.f : fmaxf(Z[i] + sb[j], 0.f);
     }
   }
   return logit;
@@ -89,11 +92,12 @@ __device__ __forceinline__ float fa_reg_layer(const NetDesc& net, const RegNetCf
 // zero beyond n0).  HA and HB are clobbered.  Logit of point lane&15 in lanes 0..15.
 template <int TM>
 __device__ __forceinline__ float fa_reg_forward(const NetDesc& net, const RegNetCfg& cfg, const float* sw_all,
-                                                int lane, float (&HA)[TM][4], float (&HB)[TM][4]) {
+                                                int lane, float (&HA)[TM][4], float (&HB)[TM][4],
+                                                const uint8_t* dead = nullptr) {
   float z = 0.f;
   for (int l = 0; l < net.n_layers; ++l) {
-    if (l & 1) z = fa_reg_layer<TM>(net, cfg, sw_all, l, lane, HB, HA);
-    else z = fa_reg_layer<TM>(net, cfg, sw_all, l, lane, HA, HB);
+    if (l & 1) z = fa_reg_layer<TM>(net, cfg, sw_all, l, lane, HB, HA, dead);
+    else z = fa_reg_layer<TM>(net, cfg, sw_all, l, lane, HA, HB, dead);
   }
   return z;
 }

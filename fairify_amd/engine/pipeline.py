@@ -14,6 +14,7 @@ the work (BaB node expansions), so the 24 CSV columns keep their meaning.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -198,7 +199,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     with tm("sim"):
         sim = simulate(be, q, lo, hi, pids, cfg.sim_size, cfg.seed, values, pairs, cfg.bisect_pairs,
                        cfg.bisect_steps)
-        cand, pos_prob = P_.candidates_from_counts(sim.counts, cfg.sim_size)
+    # stage 2 / 4 mask algebra in HIP kernels (FAIRIFY_FUSED_PRUNE=0: the PyTorch path, for A/B tests)
+    fused = be.hip and cfg.sound_prune_stats and os.environ.get("FAIRIFY_FUSED_PRUNE", "1") != "0"
     status = np.full(Pn, RUNNING, dtype=np.int8)
     cex_x = np.zeros((Pn, n), dtype=np.int64)
     cex_xp = np.zeros((Pn, n), dtype=np.int64)
@@ -220,25 +222,40 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
 
     # ---------------- stage 2: sound pruning statistics (IBP + symbolic on the partition box)
     t0 = time.time()
-    b_dead = torch.zeros(Pn, mlp.n_neurons, dtype=torch.bool, device=dev)
-    s_dead = torch.zeros_like(b_dead)
-    st_dead = torch.zeros_like(b_dead)
-    s_cand = cand.clone()
-    ibp_lb = ibp_ub = None
-    if cfg.sound_prune_stats:
+    ibp_lb = ibp_ub = code = None
+    if fused:
+        from ..ops import hip as H
+
         with tm("prune.bounds"):
             ibp = be.bounds(lo, hi, mode="ibp", keep_layers=True)
-            ibp_lb = torch.cat(ibp.layer_lb, dim=1)
-            ibp_ub = torch.cat(ibp.layer_ub, dim=1)
-            b_dead, b_rem = P_.bound_dead(cand, ibp_ub[:, :Nh], widths)
-            b_dead = P_.ensure_one_alive(b_dead, widths)
+            ibp_lb, ibp_ub = ibp.lay_lb_full, ibp.lay_ub_full
             sym = be.bounds(lo, hi, mode="symbolic")
-            s_hid = b_rem[:, :Nh] & sym.dead
-            s_dead = torch.zeros_like(b_dead)
-            s_dead[:, :Nh] = s_hid
-            s_cand = b_rem.clone()
-            s_cand[:, :Nh] = b_rem[:, :Nh] & ~s_hid
-            st_dead = P_.ensure_one_alive(P_.merge(b_dead, s_dead), widths)
+            code, pcnt = H.prune_masks(be, sim.counts, ibp_ub, sym.dead_u8)
+            pcnt_np = pcnt.cpu().numpy().astype(np.int64)
+        b_cnt, s_cnt, st_cnt = pcnt_np[:, 0], pcnt_np[:, 1], pcnt_np[:, 2]
+    else:
+        cand, _ = P_.candidates_from_counts(sim.counts, cfg.sim_size)
+        b_dead = torch.zeros(Pn, mlp.n_neurons, dtype=torch.bool, device=dev)
+        s_dead = torch.zeros_like(b_dead)
+        st_dead = torch.zeros_like(b_dead)
+        s_cand = cand.clone()
+        if cfg.sound_prune_stats:
+            with tm("prune.bounds"):
+                ibp = be.bounds(lo, hi, mode="ibp", keep_layers=True)
+                ibp_lb = torch.cat(ibp.layer_lb, dim=1)
+                ibp_ub = torch.cat(ibp.layer_ub, dim=1)
+                b_dead, b_rem = P_.bound_dead(cand, ibp_ub[:, :Nh], widths)
+                b_dead = P_.ensure_one_alive(b_dead, widths)
+                sym = be.bounds(lo, hi, mode="symbolic")
+                s_hid = b_rem[:, :Nh] & sym.dead
+                s_dead = torch.zeros_like(b_dead)
+                s_dead[:, :Nh] = s_hid
+                s_cand = b_rem.clone()
+                s_cand[:, :Nh] = b_rem[:, :Nh] & ~s_hid
+                st_dead = P_.ensure_one_alive(P_.merge(b_dead, s_dead), widths)
+        b_cnt = b_dead.sum(dim=1).cpu().numpy().astype(np.int64)
+        s_cnt = s_dead.sum(dim=1).cpu().numpy().astype(np.int64)
+        st_cnt = st_dead.sum(dim=1).cpu().numpy().astype(np.int64)
     sync()
     t_prune = time.time() - t0
 
@@ -340,7 +357,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             t0 = time.time()
             with tm("smt"):
                 ut = torch.from_numpy(unk).to(dev)
-                futs = hs.submit(mlp, q, lo_np[unk], hi_np[unk], st_dead[ut][:, :Nh])
+                st_mask = ((code[ut][:, :Nh] & H.PM_ST) != 0) if fused else st_dead[ut][:, :Nh]
+                futs = hs.submit(mlp, q, lo_np[unk], hi_np[unk], st_mask)
                 for k, f in zip(unk, futs):
                     verdict, pair = f.result()
                     if verdict == "unsat":
@@ -359,8 +377,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     # ---------------- stage 4: heuristic retry for UNKNOWN partitions (unsound, flagged)
     h_attempt = np.zeros(Pn, dtype=np.int64)
     h_success = np.zeros(Pn, dtype=np.int64)
-    h_dead_np = np.zeros((Pn, mlp.n_neurons), dtype=bool)
-    t_dead_np = st_dead.cpu().numpy()
+    h_cnt = np.zeros(Pn, dtype=np.int64)
+    t_cnt = st_cnt.copy()
     masked: Dict[int, np.ndarray] = {}
     t_heur = 0.0
     unk = np.nonzero(status == UNKNOWN)[0]
@@ -369,18 +387,23 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         h_attempt[unk] = 1
         with tm("heuristic.masks"):
             ut = torch.from_numpy(unk).to(dev)
-            hd_t, md_t = P_.heuristic_prune_batch(ibp_lb[ut], ibp_ub[ut], cand[ut], s_cand[ut], st_dead[ut],
-                                                  widths, cfg.heuristic_p)
-            hd_np = hd_t.cpu().numpy()
-            md_np = md_t.cpu().numpy()
-            h_dead_np[unk] = hd_np
-            t_dead_np[unk] = md_np
-            masks = md_np[:, :Nh]
+            if fused:
+                _, hm_t, hc_t = H.heuristic(be, ut, ibp_lb, ibp_ub, code, cfg.heuristic_p)
+                md_np = hm_t.cpu().numpy().astype(bool)
+                hc_np = hc_t.cpu().numpy().astype(np.int64)
+                h_cnt[unk], t_cnt[unk] = hc_np[:, 0], hc_np[:, 1]
+                dead_t = hm_t[:, :Nh].contiguous()
+            else:
+                hd_t, md_t = P_.heuristic_prune_batch(ibp_lb[ut], ibp_ub[ut], cand[ut], s_cand[ut], st_dead[ut],
+                                                      widths, cfg.heuristic_p)
+                md_np = md_t.cpu().numpy()
+                h_cnt[unk] = hd_t.sum(dim=1).cpu().numpy()
+                t_cnt[unk] = md_np.sum(axis=1)
+                dead_t = torch.from_numpy(md_np[:, :Nh]).to(dev)
             for k, p in enumerate(unk):
                 masked[p] = md_np[k]
         # partitions whose heuristic mask equals the sound mask would re-run the same query
         sub_lo, sub_hi = lo_np[unk], hi_np[unk]
-        dead_t = torch.from_numpy(masks).to(dev)
         exact_models = _LazyMasked(mlp, [masked[p] for p in unk], widths)
         hsolver = BaBSolver(be, q, BaBConfig(node_budget=cfg.heuristic_node_budget, batch_nodes=cfg.batch_nodes,
                                              time_budget=budget), dead=dead_t, timer=tm)
@@ -420,14 +443,22 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             c_check[sat_idx] = ((c1 == xo) & (c2 == xpo)).astype(np.int64)
         agree = np.full(Pn, cfg.sim_size, dtype=np.int64)     # Pruned-acc numerator
         if masked:
-            from ..ops.reference import sample_points
-
             hp = np.array(sorted(masked))
-            X = sample_points(lo[hp], hi[hp], pids[hp], cfg.sim_size, cfg.seed)
-            dm = torch.from_numpy(np.stack([masked[p][:Nh] for p in hp])).to(dev)
-            z0 = be.forward(X)
-            z1 = be.forward(X, dm[:, None, :].expand(-1, X.shape[1], -1))
-            agree[hp] = ((z0 > 0) == (z1 > 0)).sum(dim=1).cpu().numpy()
+            dm = torch.from_numpy(np.stack([masked[p][:Nh] for p in hp]).astype(np.uint8)).to(dev)
+            ag = None
+            if be.hip and os.environ.get("FAIRIFY_FUSED_PRUNE", "1") != "0":
+                from ..ops import hip as H
+
+                ag = H.agree(be, torch.from_numpy(hp).to(dev), lo, hi, pids, dm, cfg.sim_size, cfg.seed)
+            if ag is not None:
+                agree[hp] = ag.cpu().numpy()
+            else:
+                from ..ops.reference import sample_points
+
+                X = sample_points(lo[hp], hi[hp], pids[hp], cfg.sim_size, cfg.seed)
+                z0 = be.forward(X)
+                z1 = be.forward(X, dm.bool()[:, None, :].expand(-1, X.shape[1], -1))
+                agree[hp] = ((z0 > 0) == (z1 > 0)).sum(dim=1).cpu().numpy()
     t_replay = time.time() - t0
 
     # ---------------- records: dead-neuron counts, work, per-chunk stage times (the per-partition
@@ -437,9 +468,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     core = dict(
         grid_id=np.asarray(ids, dtype=np.int64), verdict=verdict, stage=stage_f.astype(object),
         h_attempt=h_attempt, h_success=h_success,
-        b_cnt=b_dead.sum(dim=1).cpu().numpy().astype(np.int64), s_cnt=s_dead.sum(dim=1).cpu().numpy().astype(np.int64),
-        st_cnt=st_dead.sum(dim=1).cpu().numpy().astype(np.int64), h_cnt=h_dead_np.sum(axis=1).astype(np.int64),
-        t_cnt=t_dead_np.sum(axis=1).astype(np.int64), agree=agree, nodes=nodes.astype(np.int64),
+        b_cnt=b_cnt, s_cnt=s_cnt, st_cnt=st_cnt, h_cnt=h_cnt, t_cnt=t_cnt, agree=agree, nodes=nodes.astype(np.int64),
         c_check=c_check, v_accurate=v_acc, cex_x=cex_x, cex_xp=cex_xp)
     return core, (Pn, t_sim + t_prune + t_bab, t_bab, t_heur, t_replay)
 

@@ -132,8 +132,10 @@ def bounds(be, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic", dead:
             offs.append(offs[-1] + w)
         res.layer_lb = [lay_lb[:, offs[i]:offs[i + 1]] for i in range(len(widths))]
         res.layer_ub = [lay_ub[:, offs[i]:offs[i + 1]] for i in range(len(widths))]
+        res.lay_lb_full, res.lay_ub_full = lay_lb, lay_ub
     if dead_out is not None:
-        res.dead = dead_out.bool()
+        res.dead_u8 = dead_out
+        res.dead = dead_out.view(torch.bool)
     return res
 
 
@@ -319,3 +321,73 @@ def falsify(be, q, lo, hi, pids, values, pairs, seed, n_samples, n_local, walk_k
     if not ok:
         return None
     return found.bool(), wx, wxp, how
+
+
+# ------------------------------------------------------------------------------------------------
+def prune_masks(be, counts: torch.Tensor, lay_ub: torch.Tensor, sym_dead: Optional[torch.Tensor]):
+    """Sound-prune mask algebra of the pipeline's stage 2 in one launch (``csrc/prune.hip``).
+
+    ``counts`` [P, N] int32 simulation activation counts, ``lay_ub`` [P, N] IBP upper bounds,
+    ``sym_dead`` [P, N_hidden] uint8 symbolic stable-inactive flags (or None).  Returns
+    ``(code [P, N] uint8, cnt [P, 3] int32)``: per neuron bit 0 candidate, 1 bound-dead, 2
+    symbolic-dead, 3 merged sound dead, 4 symbolic candidate; per partition the B/S/ST dead
+    counts."""
+    P, N = counts.shape
+    dev = counts.device
+    counts_c = _c(counts, torch.int32, (P, be.mlp.n_neurons), "counts")
+    ub_c = _c(lay_ub, torch.float32, (P, N), "lay_ub")
+    sd = None
+    if sym_dead is not None:
+        sd = _c(sym_dead, torch.uint8, (P, be.n_hidden), "sym_dead")
+    code = torch.empty(P, N, dtype=torch.uint8, device=dev)
+    cnt = torch.empty(P, 3, dtype=torch.int32, device=dev)
+    if P:
+        ext().prune_masks(_net(be), P, counts_c.data_ptr(), ub_c.data_ptr(), N, _ptr(sd), code.data_ptr(),
+                          cnt.data_ptr(), _stream(dev))
+    return code, cnt
+
+
+PM_CAND, PM_B, PM_S, PM_ST, PM_SCAND = 1, 2, 4, 8, 16
+
+
+def heuristic(be, rows: torch.Tensor, lay_lb: torch.Tensor, lay_ub: torch.Tensor, code: torch.Tensor, perc: float):
+    """The reference's heuristic pruning (utils/prune.py:862-939) for partitions ``rows`` of the
+    stage-2 arrays, one wave per partition (K5).  Returns ``(new [Pu, N] uint8, merged [Pu, N]
+    uint8, cnt [Pu, 2] int32 = (#new, #merged))``."""
+    Pu = rows.shape[0]
+    P, N = lay_ub.shape
+    dev = lay_ub.device
+    rows_c = _c(rows, torch.int64, (Pu,), "rows")
+    lb_c = _c(lay_lb, torch.float32, (P, N), "lay_lb")
+    ub_c = _c(lay_ub, torch.float32, (P, N), "lay_ub")
+    code_c = _c(code, torch.uint8, (P, N), "code")
+    hnew = torch.empty(Pu, N, dtype=torch.uint8, device=dev)
+    hmerged = torch.empty(Pu, N, dtype=torch.uint8, device=dev)
+    cnt = torch.empty(Pu, 2, dtype=torch.int32, device=dev)
+    if Pu:
+        ext().heuristic(_net(be), Pu, rows_c.data_ptr(), lb_c.data_ptr(), ub_c.data_ptr(), N, code_c.data_ptr(),
+                        50.0 / 100.0, float(perc) / 100.0, (100.0 - float(perc)) / 100.0, hnew.data_ptr(),
+                        hmerged.data_ptr(), cnt.data_ptr(), _stream(dev))
+    return hnew, hmerged, cnt
+
+
+def agree(be, rows: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor, pids: torch.Tensor, dead: torch.Tensor,
+          n_samples: int, seed: int):
+    """Pruned-acc numerators: per partition ``rows[k]``, how many of its ``n_samples`` simulation
+    points get the same sign from the full network and the network with ``dead[k]`` [N_hidden]
+    forced to zero.  Returns int32 [Pm] or ``None`` (shape unsupported: caller keeps PyTorch)."""
+    Pm = rows.shape[0]
+    P, n0 = lo.shape
+    dev = lo.device
+    rows_c = _c(rows, torch.int64, (Pm,), "rows")
+    lo_c = _c(lo, torch.float32, (P, n0), "lo")
+    hi_c = _c(hi, torch.float32, (P, n0), "hi")
+    pids_c = _c(pids, torch.int64, (P,), "pids")
+    dead_c = _c(dead, torch.uint8, (Pm, be.n_hidden), "dead")
+    out = torch.zeros(Pm, dtype=torch.int32, device=dev)
+    if Pm == 0:
+        return out
+    ok = ext().agree(_net(be), be.flat.data_ptr(), Pm, rows_c.data_ptr(), lo_c.data_ptr(), hi_c.data_ptr(),
+                     pids_c.data_ptr(), dead_c.data_ptr(), int(n_samples), int(seed) & 0xFFFFFFFF, out.data_ptr(),
+                     _stream(dev))
+    return out if ok else None

@@ -195,6 +195,11 @@ class BoundResult:
     layer_ub: Optional[List[torch.Tensor]] = None
     dead: Optional[torch.Tensor] = None             # [R, N_hidden] stable-inactive (ub <= 0)
     active: Optional[torch.Tensor] = None           # [R, N_hidden] stable-active  (lb >= 0)
+    # HIP path: the per-neuron bounds as one [R, N] tensor each (layer_lb/ub are views into it)
+    # and the stable-inactive flags as the kernel's uint8 [R, N_hidden]
+    lay_lb_full: Optional[torch.Tensor] = None
+    lay_ub_full: Optional[torch.Tensor] = None
+    dead_u8: Optional[torch.Tensor] = None
 
 
 def _concretize(E: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor):
