@@ -72,6 +72,8 @@ def parse_args(argv=None):
                     help="escalate only partitions that left <= this many open BaB nodes (0 = all)")
     ap.add_argument("--stages", default="",
                     help="further escalation passes 'budget:max_open,...' after --escalate-budget")
+    ap.add_argument("--batch-nodes", type=int, default=65536,
+                    help="BaB nodes bounded per sub-batch launch (memory per runtime scales with it)")
     ap.add_argument("--no-heuristic", action="store_true",
                     help="skip the reference's unsound heuristic retry (sound verdicts only)")
     ap.add_argument("--residual-samples", type=int, default=None, help="residual falsifier samples (0 = off)")
@@ -160,7 +162,7 @@ def main() -> None:
                        soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
                        node_budget=args.node_budget, heuristic=not args.no_heuristic, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=args.node_budget, escalate_budget=args.escalate_budget,
-                       escalate_max_open=args.escalate_max_open,
+                       escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
                        escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
     if args.residual_samples is not None:
         cfg.residual_samples = args.residual_samples
@@ -267,6 +269,7 @@ def main() -> None:
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
                    "stages": [list(st) for st in cfg.escalate_stages], "heuristic": cfg.heuristic,
+                   "batch_nodes": cfg.batch_nodes,
                    "chunk": args.chunk, "concurrency": conc},
         "pct_verified": round(100.0 * dec / max(1.0, att), 3),
         "pct_verified_sound": round(100.0 * (dec - uns_h - sat_stage["heuristic"]) / max(1.0, att), 3),

@@ -33,6 +33,8 @@ struct BoundArgs {
   // per-partition forced-dead masks (heuristic nets): dead = dead_part[node_part[node]]
   const int* node_part;     // [R / max(V,1)]
   const uint8_t* dead_part; // [P, n_hidden]
+  int part_mod;             // > 0: node k uses node_part[k % part_mod] (x rows then x' rows of one
+                            //      node list share one part array, no copy)
   // input dims degenerate (lo == hi) in EVERY row: folded into the constant by the
   // register-resident symbolic kernel (PA dims are added automatically when V > 0)
   unsigned long long fold;
@@ -190,8 +192,22 @@ struct SplitArgs {
   int* opart;
   int* count_out;
   int cap;
-  float* cand_buf;                        // [cand_cap, 2*n0] candidate (x, x') pairs
-  int* cand_part;                         // [cand_cap]
+  float* cand_buf;                        // [cand_cap, 2*n0+1] candidate records: x, x', then the
+                                          //   partition id (int bits), one D2H per level
   int* cand_count;
   int cand_cap;
+};
+
+// BaB solve start (fa_bab_init_kernel): staged host block -> per-partition state + root pool.
+struct BabInitArgs {
+  int P, n_run, n0;
+  const unsigned char* stage;             // device copy of the staged block
+  int8_t* status;
+  int *nodes, *open_left, *lvl_open, *nodes_start, *prev_start;
+  int* part;                              // root pool [n_run]
+  float *xlo, *xhi, *xplo, *xphi;         // root pool boxes [n_run, n0] (x' only when relaxed)
+  int nra;
+  int ra_idx[FA_MAX_RA];
+  float tau;
+  int* counters;                          // [4]
 };

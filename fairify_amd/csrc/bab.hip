@@ -23,6 +23,8 @@
 //                      level counters to pinned host memory, next counter slot cleared.
 // fa_mark_unknown      time budget hit: every RUNNING partition with live nodes -> UNKNOWN.
 // fa_set_status        host-confirmed SAT partitions -> SAT.
+#include <algorithm>
+
 #include "args.h"
 
 #define ST_UNKNOWN 0
@@ -232,7 +234,7 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
           } else {
             const int o = t / a.Pp, q = t - o * a.Pp;
             const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
-            float* cbuf = a.cand_buf + (size_t)slot * 2 * n0;
+            float* cbuf = a.cand_buf + (size_t)slot * (2 * n0 + 1);
             for (int d = 0; d < n0; ++d) {
               cbuf[d] = xl[d];
               cbuf[n0 + d] = xpl[d];
@@ -241,7 +243,7 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
               cbuf[a.pa_idx[k]] = (float)a.values[vi * a.npa + k];
               cbuf[n0 + a.pa_idx[k]] = (float)a.values[vj * a.npa + k];
             }
-            a.cand_part[slot] = p;
+            cbuf[2 * n0] = __int_as_float(p);
           }
         }
         slot0 += __popcll(bm);
@@ -251,10 +253,10 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
     if (pl.ncand) {
       const int slot = cand_off[loc];
       if (slot < a.cand_cap) {
-        float* cbuf = a.cand_buf + (size_t)slot * 2 * n0;
-        for (int d = lane; d < 2 * n0; d += 64)
-          cbuf[d] = d < n0 ? a.cand_x[(size_t)n * n0 + d] : a.cand_xp[(size_t)n * n0 + d - n0];
-        if (lane == 0) a.cand_part[slot] = p;
+        float* cbuf = a.cand_buf + (size_t)slot * (2 * n0 + 1);
+        for (int d = lane; d < 2 * n0 + 1; d += 64)
+          cbuf[d] = d < n0 ? a.cand_x[(size_t)n * n0 + d]
+                           : (d < 2 * n0 ? a.cand_xp[(size_t)n * n0 + d - n0] : __int_as_float(p));
       }
     }
     if (pl.nchild == 0) continue;
@@ -299,6 +301,49 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
       }
     }
   }
+}
+
+// Solve start, one launch: per-partition state from the staged host block [status int8 x P,
+// padded to 4 B | running partition ids x n_run | lo x n_run*n0 | hi x n_run*n0] (one H2D copy),
+// the root node pool (x' boxes widened by tau on the relaxed dims), the level counters.
+__global__ void fa_bab_init_kernel(BabInitArgs a) {
+  const int tid = blockIdx.x * FA_THREADS + threadIdx.x;
+  const int nth = gridDim.x * FA_THREADS;
+  const int8_t* st = reinterpret_cast<const int8_t*>(a.stage);
+  const int* run = reinterpret_cast<const int*>(a.stage + ((a.P + 3) & ~3));
+  const float* lo = reinterpret_cast<const float*>(run + a.n_run);
+  const float* hi = lo + (size_t)a.n_run * a.n0;
+  for (int p = tid; p < a.P; p += nth) {
+    a.status[p] = st[p];
+    a.nodes[p] = 0;
+    a.open_left[p] = 0;
+    a.lvl_open[p] = 0;
+    a.nodes_start[p] = 0;
+    a.prev_start[p] = -1;      // one root node in the first level
+  }
+  for (int i = tid; i < a.n_run; i += nth) a.part[i] = run[i];
+  const size_t ne = (size_t)a.n_run * a.n0;
+  for (size_t e = tid; e < ne; e += nth) {
+    a.xlo[e] = lo[e];
+    a.xhi[e] = hi[e];
+    if (a.xplo) {
+      const int d = (int)(e % a.n0);
+      bool r = false;
+      for (int k = 0; k < a.nra; ++k) r |= a.ra_idx[k] == d;
+      a.xplo[e] = r ? lo[e] - a.tau : lo[e];
+      a.xphi[e] = r ? hi[e] + a.tau : hi[e];
+    }
+  }
+  if (tid < 4) a.counters[tid] = 0;
+}
+
+// Solve end, one launch: status / nodes / open_left packed into one int block (one D2H copy).
+__global__ void fa_bab_finish_kernel(int P, const int8_t* status, const int* nodes, const int* open_left, int* out) {
+  const int p = blockIdx.x * FA_THREADS + threadIdx.x;
+  if (p >= P) return;
+  out[p] = status[p];
+  out[P + p] = nodes[p];
+  out[2 * P + p] = open_left[p];
 }
 
 __global__ void fa_mark_unknown_kernel(const int* part, int n, int8_t* status) {
@@ -363,5 +408,21 @@ extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_
   hipLaunchKernelGGL(fa_settle_kernel, dim3((n + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, P,
                      status, lvl_open, part_open, part_nodes, nodes_start, prev_start, counters_cur, counters_next,
                      host_counts);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fa_bab_init_launch(BabInitArgs a, hipStream_t stream) {
+  if (a.nra > FA_MAX_RA) return -3;
+  const long long work = std::max<long long>(std::max(a.P, a.n_run), (long long)a.n_run * a.n0);
+  const int blocks = (int)std::min<long long>((work + FA_THREADS - 1) / FA_THREADS + 1, 4096);
+  hipLaunchKernelGGL(fa_bab_init_kernel, dim3(blocks), dim3(FA_THREADS), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fa_bab_finish_launch(int P, const int8_t* status, const int* nodes, const int* open_left, int* out,
+                                    hipStream_t stream) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(fa_bab_finish_kernel, dim3((P + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, P,
+                     status, nodes, open_left, out);
   return (int)hipGetLastError();
 }

@@ -40,6 +40,9 @@ extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_
                                 int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
                                 int* host_counts, hipStream_t stream);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
+extern "C" int fa_bab_init_launch(BabInitArgs a, hipStream_t stream);
+extern "C" int fa_bab_finish_launch(int P, const int8_t* status, const int* nodes, const int* open_left, int* out,
+                                    hipStream_t stream);
 
 // defined in bindings.cpp
 const NetDesc& fa_net_desc(py::handle net);
@@ -135,7 +138,6 @@ class BabRuntime {
     scores_.ensure((size_t)batch_ * 2 * n0_);
     pe_lb_.ensure(2 * (size_t)batch_);
     pe_ub_.ensure(2 * (size_t)batch_);
-    pe_part_.ensure(2 * (size_t)batch_);
     ensure_cand(cand_cap_);
     counters_.ensure(4);   // two slots of (children, candidates), alternating per level
     // fine-grained (coherent) pinned words: the settle kernel writes the level counters here
@@ -154,6 +156,9 @@ class BabRuntime {
   }
   ~BabRuntime() {
     if (hcount_) hipHostFree(hcount_);
+    if (hstage_) hipHostFree(hstage_);
+    if (hout_) hipHostFree(hout_);
+    if (hcand_) hipHostFree(hcand_);
   }
 
   py::tuple solve(py::array_t<float, py::array::c_style | py::array::forcecast> lo,
@@ -175,43 +180,50 @@ class BabRuntime {
     lvl_open_.ensure(P);
     nodes_start_.ensure(P);
     prev_start_.ensure(P);
-    std::vector<int8_t> hstatus(status0.data(), status0.data() + P);
-    ck(hipMemcpyAsync(status_.p, hstatus.data(), P, hipMemcpyHostToDevice, st), "cp status");
-    ck(hipMemsetAsync(nodes_.p, 0, P * sizeof(int), st), "memset nodes");
-    ck(hipMemsetAsync(open_left_.p, 0, P * sizeof(int), st), "memset open_left");
-    ck(hipMemsetAsync(lvl_open_.p, 0, P * sizeof(int), st), "memset lvl_open");
-    ck(hipMemsetAsync(nodes_start_.p, 0, P * sizeof(int), st), "memset nodes_start");
-    ck(hipMemsetAsync(prev_start_.p, 0xFF, P * sizeof(int), st), "memset prev_start");   // -1: one root node
-    ck(hipMemsetAsync(counters_.p, 0, 4 * sizeof(int), st), "memset counters");
     int slot = 0;
-    // initial pool: running partitions
+    // initial pool: running partitions.  Everything the device needs at the start goes through
+    // ONE pinned staging block + one H2D copy + one init kernel (status, per-partition state,
+    // root boxes, counters) instead of four copies and six memsets.
+    const int8_t* hstatus = status0.data();
     std::vector<int> run;
     for (int p = 0; p < P; ++p)
       if (hstatus[p] == 3) run.push_back(p);
     if ((int)run.size() > cap_) throw std::invalid_argument("more partitions than pool capacity");
     ensure_pool(0, std::max<long long>((long long)run.size(), 1));
-    std::vector<float> hl((size_t)run.size() * n0_), hh((size_t)run.size() * n0_);
-    for (size_t i = 0; i < run.size(); ++i)
-      for (int d = 0; d < n0_; ++d) {
-        hl[i * n0_ + d] = lo.data()[(size_t)run[i] * n0_ + d];
-        hh[i * n0_ + d] = hi.data()[(size_t)run[i] * n0_ + d];
-      }
-    int cur = 0;
-    int n_in = (int)run.size();
-    if (n_in) {
-      ck(hipMemcpyAsync(lo_[0].p, hl.data(), hl.size() * sizeof(float), hipMemcpyHostToDevice, st), "cp lo");
-      ck(hipMemcpyAsync(hi_[0].p, hh.data(), hh.size() * sizeof(float), hipMemcpyHostToDevice, st), "cp hi");
-      ck(hipMemcpyAsync(part_[0].p, run.data(), run.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp part");
-      if (relaxed_) {
-        for (size_t i = 0; i < run.size(); ++i)
-          for (int r : ra_) {
-            hl[i * n0_ + r] -= tau_;
-            hh[i * n0_ + r] += tau_;
-          }
-        ck(hipMemcpyAsync(plo_[0].p, hl.data(), hl.size() * sizeof(float), hipMemcpyHostToDevice, st), "cp");
-        ck(hipMemcpyAsync(phi_[0].p, hh.data(), hh.size() * sizeof(float), hipMemcpyHostToDevice, st), "cp");
-      }
+    const size_t nrun = run.size();
+    const size_t st_bytes = (size_t)((P + 3) & ~3) + nrun * sizeof(int) + 2 * nrun * n0_ * sizeof(float);
+    ensure_host(hstage_, hstage_n_, st_bytes);
+    stage_.ensure(st_bytes);
+    {
+      unsigned char* h = hstage_;
+      std::memcpy(h, hstatus, P);
+      int* hr = reinterpret_cast<int*>(h + ((P + 3) & ~3));
+      std::memcpy(hr, run.data(), nrun * sizeof(int));
+      float* hl = reinterpret_cast<float*>(hr + nrun);
+      float* hh = hl + nrun * n0_;
+      for (size_t i = 0; i < nrun; ++i)
+        for (int d = 0; d < n0_; ++d) {
+          hl[i * n0_ + d] = lo.data()[(size_t)run[i] * n0_ + d];
+          hh[i * n0_ + d] = hi.data()[(size_t)run[i] * n0_ + d];
+        }
     }
+    ck(hipMemcpyAsync(stage_.p, hstage_, st_bytes, hipMemcpyHostToDevice, st), "cp stage");
+    {
+      BabInitArgs ia{};
+      ia.P = P; ia.n_run = (int)nrun; ia.n0 = n0_;
+      ia.stage = stage_.p;
+      ia.status = status_.p; ia.nodes = nodes_.p; ia.open_left = open_left_.p; ia.lvl_open = lvl_open_.p;
+      ia.nodes_start = nodes_start_.p; ia.prev_start = prev_start_.p;
+      ia.part = part_[0].p; ia.xlo = lo_[0].p; ia.xhi = hi_[0].p;
+      ia.xplo = relaxed_ ? plo_[0].p : nullptr; ia.xphi = relaxed_ ? phi_[0].p : nullptr;
+      ia.nra = relaxed_ ? (int)ra_.size() : 0;
+      for (int k = 0; k < ia.nra; ++k) ia.ra_idx[k] = ra_[k];
+      ia.tau = tau_;
+      ia.counters = counters_.p;
+      ckl(fa_bab_init_launch(ia, st), "bab_init");
+    }
+    int cur = 0;
+    int n_in = (int)nrun;
     // host result buffers
     std::vector<int64_t> cex_x((size_t)P * n0_, 0), cex_xp((size_t)P * n0_, 0);
     std::vector<char> got(P, 0);
@@ -269,14 +281,12 @@ class BabRuntime {
         c.scores = scores_.p; c.leaf = leaf_.p;
         ckl(fa_certify_launch(c, st), "certify");
         // rigorous interval evaluation of the candidate pairs (rows: x then x')
-        if (dead_part) {   // per-point partition ids only matter for the heuristic (masked) nets
-          ck(hipMemcpyAsync(pe_part_.p, bpart, nb * sizeof(int), hipMemcpyDeviceToDevice, st), "cp");
-          ck(hipMemcpyAsync(pe_part_.p + nb, bpart, nb * sizeof(int), hipMemcpyDeviceToDevice, st), "cp");
-        }
         BoundArgs b{};
         b.flat = flat_; b.lo = cand_.p; b.hi = cand_.p; b.R = 2 * nb; b.symbolic = 0;
         b.out_lb = pe_lb_.p; b.out_ub = pe_ub_.p;
-        if (dead_part) { b.node_part = pe_part_.p; b.dead_part = (const uint8_t*)dead_part; }
+        // per-point partition ids only matter for the heuristic (masked) nets: points k and
+        // nb + k (x and x' of node k) both read bpart[k]
+        if (dead_part) { b.node_part = bpart; b.part_mod = nb; b.dead_part = (const uint8_t*)dead_part; }
         const int prc = fa_point_try_launch(net_, b, st);
         if (prc < 0) ckl(-prc, "points");
         if (prc == 0) ckl(fa_bounds_launch(net_, b, st), "bounds(points)");
@@ -298,7 +308,7 @@ class BabRuntime {
         sa.oxlo = lo_[nxt].p; sa.oxhi = hi_[nxt].p;
         sa.oxplo = relaxed_ ? plo_[nxt].p : nullptr; sa.oxphi = relaxed_ ? phi_[nxt].p : nullptr;
         sa.opart = part_[nxt].p; sa.count_out = cnt; sa.cap = pool_[nxt];
-        sa.cand_buf = cand_buf_.p; sa.cand_part = cand_part_.p; sa.cand_count = cnt + 1;
+        sa.cand_buf = cand_buf_.p; sa.cand_count = cnt + 1;
         sa.cand_cap = cand_alloc_;
         ckl(fa_split_launch(sa, st), "split");
         launches += relaxed_ ? 6 : 5;
@@ -318,21 +328,22 @@ class BabRuntime {
       n_in = n_out;
     }
     }
-    std::vector<int8_t> sout(P);
-    std::vector<int> nout(P), oout(P);
-    ck(hipMemcpyAsync(sout.data(), status_.p, P, hipMemcpyDeviceToHost, st), "cp");
-    ck(hipMemcpyAsync(nout.data(), nodes_.p, P * sizeof(int), hipMemcpyDeviceToHost, st), "cp");
-    ck(hipMemcpyAsync(oout.data(), open_left_.p, P * sizeof(int), hipMemcpyDeviceToHost, st), "cp");
+    // results: one pack kernel + one D2H copy into pinned memory
+    out_.ensure((size_t)3 * P);
+    ensure_host(hout_, hout_n_, (size_t)3 * P * sizeof(int));
+    ckl(fa_bab_finish_launch(P, status_.p, nodes_.p, open_left_.p, out_.p, st), "bab_finish");
+    ck(hipMemcpyAsync(hout_, out_.p, (size_t)3 * P * sizeof(int), hipMemcpyDeviceToHost, st), "cp out");
     ck(hipStreamSynchronize(st), "sync");
+    const int* hres = reinterpret_cast<const int*>(hout_);
     py::array_t<int8_t> status_out(P);
     py::array_t<int64_t> nodes_out(P), open_out(P);
     for (int p = 0; p < P; ++p) {
-      int8_t v = sout[p];
+      int8_t v = (int8_t)hres[p];
       if (got[p]) v = 1;
       else if (v == 3) v = timed_out ? 0 : 2;   // all nodes closed => UNSAT
       status_out.mutable_data()[p] = v;
-      nodes_out.mutable_data()[p] = nout[p];
-      open_out.mutable_data()[p] = (v == 0) ? oout[p] : 0;
+      nodes_out.mutable_data()[p] = hres[P + p];
+      open_out.mutable_data()[p] = (v == 0) ? hres[2 * P + p] : 0;
     }
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     py::dict stats;
@@ -408,19 +419,27 @@ class BabRuntime {
     long long n = std::max<long long>(cand_alloc_, 1 << 16);
     while (n < need) n *= 2;
     n = std::min<long long>(n, FA_CAND_MAX);
-    cand_buf_.ensure((size_t)n * 2 * n0_);
-    cand_part_.ensure((size_t)n);
+    cand_buf_.ensure((size_t)n * (2 * n0_ + 1));
     cand_alloc_ = (int)n;
   }
 
   // called WITHOUT the GIL; takes it only around the Python confirmation callback
   void confirm_candidates(int n_cand, py::object& confirm, std::vector<char>& got, std::vector<int64_t>& cex_x,
                           std::vector<int64_t>& cex_xp, hipStream_t st) {
+    const size_t rec = (size_t)2 * n0_ + 1;             // x, x', partition id (int bits)
+    ensure_host(hcand_, hcand_n_, (size_t)n_cand * rec * sizeof(float));
+    ck(hipMemcpyAsync(hcand_, cand_buf_.p, (size_t)n_cand * rec * sizeof(float), hipMemcpyDeviceToHost, st),
+       "cp cand");
+    ck(hipStreamSynchronize(st), "sync");
     std::vector<float> buf((size_t)n_cand * 2 * n0_);
     std::vector<int> parts(n_cand);
-    ck(hipMemcpyAsync(buf.data(), cand_buf_.p, sizeof(float) * buf.size(), hipMemcpyDeviceToHost, st), "cp cand");
-    ck(hipMemcpyAsync(parts.data(), cand_part_.p, sizeof(int) * n_cand, hipMemcpyDeviceToHost, st), "cp");
-    ck(hipStreamSynchronize(st), "sync");
+    {
+      const float* hc = reinterpret_cast<const float*>(hcand_);
+      for (int i = 0; i < n_cand; ++i) {
+        std::memcpy(buf.data() + (size_t)i * 2 * n0_, hc + (size_t)i * rec, sizeof(float) * 2 * n0_);
+        std::memcpy(&parts[i], hc + (size_t)i * rec + 2 * n0_, sizeof(int));
+      }
+    }
     std::vector<char> ok(n_cand, 0);
     // native exact check (no GIL): pair constraints + fp64 logits with a rigorous rounding
     // bound; only pairs whose sign the bound cannot settle go to the Python callback
@@ -561,9 +580,29 @@ class BabRuntime {
   DevBuf<float> gmin_, tstar_, score_, cand_, scores_, pe_lb_, pe_ub_, cand_buf_;
   DevBuf<uint8_t> open_, leaf_;
   DevBuf<int64_t> split_, cv_, co_;
-  DevBuf<int> pe_part_, cand_part_, counters_, nodes_, idx_, open_left_, lvl_open_, nodes_start_, prev_start_;
+  DevBuf<int> counters_, nodes_, idx_, open_left_, lvl_open_, nodes_start_, prev_start_, out_;
   DevBuf<int8_t> status_;
+  DevBuf<unsigned char> stage_;
   int* hcount_ = nullptr;
+  // pinned host staging (solve start, solve end, per-level candidate records)
+  unsigned char* hstage_ = nullptr;
+  size_t hstage_n_ = 0;
+  unsigned char* hout_ = nullptr;
+  size_t hout_n_ = 0;
+  unsigned char* hcand_ = nullptr;
+  size_t hcand_n_ = 0;
+
+  // grow a pinned host buffer; only called between solves / after a stream sync, so no copy can
+  // still be reading the old one
+  static void ensure_host(unsigned char*& p, size_t& n, size_t need) {
+    if (need <= n) return;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    size_t m = std::max<size_t>(need, 4096);
+    m = std::max(m, n * 2);
+    ck(hipHostMalloc((void**)&p, m, hipHostMallocDefault), "hipHostMalloc");
+    n = m;
+  }
 };
 
 void register_bab(py::module& m) {

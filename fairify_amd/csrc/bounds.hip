@@ -204,7 +204,8 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
       bool forced = false;
       if (a.dead_in && rv) forced = a.dead_in[(size_t)rglob * net.n_hidden + noff + j] != 0;
       else if (a.dead_part && rv) {
-        const int node = a.V > 0 ? rglob / a.V : rglob;
+        int node = a.V > 0 ? rglob / a.V : rglob;
+        if (a.part_mod) node %= a.part_mod;
         forced = a.dead_part[(size_t)a.node_part[node] * net.n_hidden + noff + j] != 0;
       }
       const bool isdead = ub <= 0.f;

@@ -4,6 +4,9 @@
 //                       piecewise-linear certificate g(t) at t in {0, 1} and at every breakpoint
 //                       of the shared-feature coefficients and keeps min_t g(t) and its argmin;
 //                       pairs already excluded by the rows' rigorous sign bounds get g = -1.
+// fa_pair_fused_kernel: eval + pick in one launch when a node has at most FA_CERT_FUSE_Q
+//                       (pair, orientation) entries (the common single-binary-PA case): one lane
+//                       per entry, shuffle arg-max per node, the node's first lane picks.
 // fa_pair_pick_kernel : one thread per node picks the most violating pair/orientation, and for
 //                       it emits the per-dimension split scores (|coef| x width at t*), the best
 //                       split dimension, the leaf flag and the candidate vertex pair (x, x') that
@@ -95,21 +98,17 @@ __device__ void fa_mags(const CertArgs& a, int n, const Form& A, const Form& B, 
 // (NM >= n0, compile-time), then g(t) is evaluated at t in {0, 1} and at every breakpoint of a
 // shared feature without touching memory again.  Same arithmetic as fa_g_at / fa_mags.
 #define FA_CERT_THREADS 64
+// min_t g(t) of pair qq (orientation-major) of node n -> (gmin, tstar)
 template <int NM>
-__global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_eval_kernel(CertArgs a) {
-  const int Q = a.Pp * a.norient;
-  const int64_t idx = (int64_t)blockIdx.x * FA_CERT_THREADS + threadIdx.x;
-  if (idx >= (int64_t)a.Nn * Q) return;
-  const int n = (int)(idx / Q);
-  const int qq = (int)(idx % Q);
+__device__ __forceinline__ void fa_pair_eval_one(const CertArgs& a, int n, int qq, float& gmin, float& tstar) {
   const int o = qq / a.Pp, q = qq % a.Pp;
   const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
   {  // exact-sign shortcut from the rigorous per-row bounds
     const size_t ri = (size_t)n * a.V + vi, rj = (size_t)n * a.V + vj;
     const bool imp = (o == 0) ? (a.olb[ri] >= 0.f || a.oubp[rj] <= 0.f) : (a.oub[ri] <= 0.f || a.olbp[rj] >= 0.f);
     if (imp) {
-      a.gmin[idx] = -1.f;
-      a.tstar[idx] = 0.f;
+      gmin = -1.f;
+      tstar = 0.f;
       return;
     }
   }
@@ -173,9 +172,23 @@ __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_eval_kernel(CertArgs 
     const float g = g_at(t);
     if (g < best) { best = g; bt = t; }
   }
-  a.gmin[idx] = best;
-  a.tstar[idx] = bt;
+  gmin = best;
+  tstar = bt;
 }
+
+template <int NM>
+__global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_eval_kernel(CertArgs a) {
+  const int Q = a.Pp * a.norient;
+  const int64_t idx = (int64_t)blockIdx.x * FA_CERT_THREADS + threadIdx.x;
+  if (idx >= (int64_t)a.Nn * Q) return;
+  float g, t;
+  fa_pair_eval_one<NM>(a, (int)(idx / Q), (int)(idx % Q), g, t);
+  a.gmin[idx] = g;
+  a.tstar[idx] = t;
+}
+
+// most violating pair (bq, its g = bg, its t*) of node n -> open flag, split scores, candidate
+__device__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t);
 
 __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_pick_kernel(CertArgs a) {
   const int n = blockIdx.x * FA_CERT_THREADS + threadIdx.x;
@@ -187,8 +200,33 @@ __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_pick_kernel(CertArgs 
     const float g = a.gmin[(size_t)n * Q + qq];
     if (g > bg) { bg = g; bq = qq; }
   }
+  fa_pick_node(a, n, bg, bq, a.tstar[(size_t)n * Q + bq]);
+}
+
+// Eval + pick fused for nodes with at most FA_CERT_FUSE_Q (pair, orientation) entries: a group
+// of QG = next_pow2(Q) consecutive lanes per node evaluates one entry each, a shuffle arg-max
+// inside the group keeps the first maximum (the two-kernel path's rule), and the group's first
+// lane runs the pick.  One launch instead of two per BaB sub-batch, no gmin / tstar round trip.
+template <int NM>
+__global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_fused_kernel(CertArgs a, int QG) {
+  const int Q = a.Pp * a.norient;
+  const int gidx = blockIdx.x * FA_CERT_THREADS + threadIdx.x;
+  const int n = gidx / QG, qq = gidx - n * QG;
+  const bool live = n < a.Nn && qq < Q;
+  float g = -INFINITY, t = 0.f;
+  if (live) fa_pair_eval_one<NM>(a, n, qq, g, t);
+  int bq = live ? qq : 0x7fffffff;
+  for (int o = 1; o < QG; o <<= 1) {     // groups are aligned to QG lanes (QG divides 64)
+    const float g2 = __shfl_xor(g, o);
+    const float t2 = __shfl_xor(t, o);
+    const int q2 = __shfl_xor(bq, o);
+    if (g2 > g || (g2 == g && q2 < bq)) { g = g2; t = t2; bq = q2; }
+  }
+  if (n < a.Nn && qq == 0) fa_pick_node(a, n, g, bq == 0x7fffffff ? 0 : bq, t);
+}
+
+__device__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t) {
   const int o = bq / a.Pp, q = bq % a.Pp;
-  const float t = a.tstar[(size_t)n * Q + bq];
   Form A, B;
   float sA, sB;
   fa_pair_forms(a, n, q, o, A, sA, B, sB);
@@ -259,10 +297,24 @@ __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_pick_kernel(CertArgs 
   if (a.leaf) a.leaf[n] = leaf ? 1 : 0;
 }
 
+// pairs x orientations up to which eval and pick run fused (one thread per node); more pairs
+// keep one thread per (node, pair) so wide PA tables still fill the chip
+#ifndef FA_CERT_FUSE_Q
+#define FA_CERT_FUSE_Q 4
+#endif
+
 extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream) {
   if (a.Nn <= 0) return 0;
   if (a.npa > FA_CMAX_PA || a.nra > FA_MAX_RA) return -3;
   const int64_t tot = (int64_t)a.Nn * a.Pp * a.norient;
+  if (a.Pp * a.norient <= FA_CERT_FUSE_Q && a.n0 <= 32) {
+    int QG = 1;
+    while (QG < a.Pp * a.norient) QG <<= 1;
+    const dim3 gn((unsigned)(((int64_t)a.Nn * QG + FA_CERT_THREADS - 1) / FA_CERT_THREADS));
+    if (a.n0 <= 16) hipLaunchKernelGGL(fa_pair_fused_kernel<16>, gn, dim3(FA_CERT_THREADS), 0, stream, a, QG);
+    else hipLaunchKernelGGL(fa_pair_fused_kernel<32>, gn, dim3(FA_CERT_THREADS), 0, stream, a, QG);
+    return (int)hipGetLastError();
+  }
   const dim3 ge((unsigned)((tot + FA_CERT_THREADS - 1) / FA_CERT_THREADS));
   if (a.n0 <= 16) hipLaunchKernelGGL(fa_pair_eval_kernel<16>, ge, dim3(FA_CERT_THREADS), 0, stream, a);
   else if (a.n0 <= 32) hipLaunchKernelGGL(fa_pair_eval_kernel<32>, ge, dim3(FA_CERT_THREADS), 0, stream, a);

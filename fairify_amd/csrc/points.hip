@@ -80,7 +80,8 @@ __device__ __forceinline__ void fa_point_layer(const NetDesc& net, const BoundAr
       bool forced = false;
       if (jv && pv) {
         if (a.dead_in) forced = a.dead_in[(size_t)p * net.n_hidden + noff + j] != 0;
-        else if (a.dead_part) forced = a.dead_part[(size_t)a.node_part[p] * net.n_hidden + noff + j] != 0;
+        else if (a.dead_part)
+          forced = a.dead_part[(size_t)a.node_part[a.part_mod ? p % a.part_mod : p] * net.n_hidden + noff + j] != 0;
       }
       const bool zero = !jv || forced || (z + d <= 0.f);
       const float h = zero ? 0.f : fmaxf(z, 0.f);

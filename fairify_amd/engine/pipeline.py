@@ -50,7 +50,7 @@ class VerifyConfig:
     escalate_stages: Tuple[Tuple[int, int], ...] = ()
                                          # further (budget, max_open) passes after the escalated one,
                                          # each on the residue the previous pass left
-    batch_nodes: int = 32768
+    batch_nodes: int = 65536             # BaB nodes per sub-batch launch
     heuristic: bool = True               # reference behaviour: heuristic retry on unknown
     heuristic_p: float = 5.0             # HEURISTIC_PRUNE_THRESHOLD
     heuristic_node_budget: int = 4096

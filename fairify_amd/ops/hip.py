@@ -212,6 +212,24 @@ def pair_certify(be, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, sha
 
 
 # ------------------------------------------------------------------------------------------------
+def _parse_sim_blocks(v: Optional[str]) -> int:
+    if v is None or v.strip() == "":
+        return 0
+    try:
+        n = int(v)
+    except ValueError:
+        raise ValueError(f"FAIRIFY_SIM_BLOCKS={v!r}: expected a non-negative integer") from None
+    if n < 0:
+        raise ValueError(f"FAIRIFY_SIM_BLOCKS={v!r}: expected a non-negative integer")
+    return n
+
+
+# parsed once at import (a bad value fails here, not inside a worker thread mid-run); tests that
+# change the variable at run time set _SIM_BLOCKS_ENV = "dynamic" to re-read it per call
+_SIM_BLOCKS = _parse_sim_blocks(os.environ.get("FAIRIFY_SIM_BLOCKS"))
+_SIM_BLOCKS_ENV: Optional[str] = None
+
+
 def _sim_split(P: int, n_samples: int) -> int:
     """Workgroups per partition for ``fa_sim_kernel``: with ``FAIRIFY_SIM_BLOCKS=B`` a short list
     of partitions with a large sample budget (the residual falsifier on a per-rank residue) is
@@ -219,7 +237,7 @@ def _sim_split(P: int, n_samples: int) -> int:
     serially.  Results are bit-identical either way (tests/test_kernels_gpu.py).  Off by default:
     with 8 concurrent host streams the extra blocks only contend with the other streams' bound
     kernels (A/B in profiles/r1_sim_split_ab.md)."""
-    target = int(os.environ.get("FAIRIFY_SIM_BLOCKS", "0") or 0)
+    target = _SIM_BLOCKS if _SIM_BLOCKS_ENV is None else _parse_sim_blocks(os.environ.get("FAIRIFY_SIM_BLOCKS"))
     if not P or target <= P:
         return 1
     tiles = (n_samples + 63) // 64

@@ -80,6 +80,11 @@ def test_forward_matches(cuda):
 
 
 def test_sim_kernel_matches_reference(cuda):
+    """fa_sim_kernel against exact (fp64) evaluation of the same counter-hash samples.
+
+    Activation counts may differ from the exact counts only by the number of samples whose
+    pre-activation has a rigorous fp32 interval containing 0; the first flip (found + witness)
+    must be the exact first flip unless a sample at or before it has an ambiguous logit sign."""
     from fairify_amd.engine.sim import simulate
     from fairify_amd.partition import Grid
 
@@ -87,28 +92,60 @@ def test_sim_kernel_matches_reference(cuda):
     grid = Grid.reference(ADULT, 10)
     ids = np.arange(0, 16000, 97)[:128]
     lo, hi = grid.decode(ids)
-    values = torch.from_numpy(q.pa_values(lo[0], hi[0]))
-    pairs = torch.from_numpy(q.pa_pairs(values.numpy()))
+    values = q.pa_values(lo[0], hi[0])
+    pairs = q.pa_pairs(values)
     m = get_model("AC-3")
-    cpu = Backend(m, "cpu")
     gpu = Backend(m, cuda)
-    lo_t = torch.from_numpy(lo).float()
-    hi_t = torch.from_numpy(hi).float()
-    pid = torch.from_numpy(ids)
-    a = simulate(cpu, q, lo_t, hi_t, pid, 300, 5, values, pairs, 0, 0)
-    b = simulate(gpu, q, lo_t.to(cuda), hi_t.to(cuda), pid.to(cuda), 300, 5, values.to(cuda), pairs.to(cuda), 0, 0)
-    diff = (a.counts - b.counts.cpu()).abs()
-    assert int(diff.max()) <= 2
-    agree = (a.found == b.found.cpu()).float().mean()
-    assert float(agree) > 0.97
-    both = a.found & b.found.cpu()
-    assert torch.equal(a.wit_x[both], b.wit_x.cpu()[both])
+    S, seed = 300, 5
+    lo_t, hi_t, pid = torch.from_numpy(lo).float(), torch.from_numpy(hi).float(), torch.from_numpy(ids)
+    b = simulate(gpu, q, lo_t.to(cuda), hi_t.to(cuda), pid.to(cuda), S, seed, torch.from_numpy(values).to(cuda),
+                 torch.from_numpy(pairs).to(cuda), 0, 0)
+    X = ref.sample_points(lo_t, hi_t, pid, S, seed)                       # [P, S, n0]
+    P, n0 = lo.shape
+    Xf = X.reshape(-1, n0)
+    # exact activation counts and rigorous per-neuron pre-activation intervals
+    acts = m.layer_outputs(Xf.numpy().astype(np.float64))               # per layer [R, w], post-ReLU, fp64
+    iv = gpu.bounds(Xf.to(cuda), Xf.to(cuda), mode="ibp", keep_layers=True)
+    cnt_b = b.counts.cpu().numpy()
+    off = 0
+    for l, w in enumerate(m.widths[:-1]):
+        exact = (acts[l] > 0).reshape(P, S, w).sum(1)
+        amb = ((iv.layer_lb[l] <= 0) & (iv.layer_ub[l] >= 0)).cpu().numpy().reshape(P, S, w).sum(1)
+        assert (np.abs(cnt_b[:, off:off + w] - exact) <= amb).all()
+        off += w
+    # exact first flip per partition vs the kernel's
+    V = len(values)
+    XV = np.repeat(X.numpy()[:, :, None, :], V, axis=2)
+    XV[:, :, :, list(q.pa_idx)] = values[None, None]
+    XVf = XV.reshape(-1, n0)
+    z = m.logits(XVf.astype(np.float64)).reshape(P, S, V)
+    lb, ub = gpu.point_bounds(torch.from_numpy(XVf).float().to(cuda))
+    amb = ((lb <= 0) & (ub >= 0)).cpu().numpy().reshape(P, S, V).any(axis=2)
+    zi, zj = z[:, :, pairs[:, 0]], z[:, :, pairs[:, 1]]
+    flip = ((zi < 0) & (zj > 0)) | ((zi > 0) & (zj < 0))                 # [P, S, Pp]
+    found_b = b.found.cpu().numpy()
+    wx, wxp = b.wit_x.cpu().numpy(), b.wit_xp.cpu().numpy()
+    checked = 0
+    for p in range(P):
+        fl = np.nonzero(flip[p].reshape(-1))[0]
+        key = int(fl[0]) if fl.size else S * len(pairs)
+        s_key = key // len(pairs)
+        if amb[p, :min(S, s_key + 1)].any():
+            continue                                                    # sign ambiguous before the flip
+        checked += 1
+        assert bool(found_b[p]) == bool(fl.size)
+        if fl.size:
+            s, qi = divmod(key, len(pairs))
+            assert np.array_equal(wx[p], XV[p, s, pairs[qi, 0]]) and np.array_equal(wxp[p], XV[p, s, pairs[qi, 1]])
+    assert checked >= 0.9 * P
 
 
 @pytest.mark.parametrize("relaxed", [False, True])
-def test_sim_split_identical(cuda, monkeypatch, relaxed):
+@pytest.mark.parametrize("bisect", [(0, 0), (16, 12)])
+def test_sim_split_identical(cuda, monkeypatch, relaxed, bisect):
     """Sample tiles spread over several workgroups per partition (``fa_sim_kernel`` split +
-    ``fa_sim_finalize_kernel``) give bit-identical counts, flags and witnesses."""
+    ``fa_sim_finalize_kernel``) give bit-identical counts, flags and witnesses, also with the
+    boundary walk on (every split workgroup writes its own tiles of z0, which the walk reads)."""
     from fairify_amd.engine.sim import simulate
     from fairify_amd.ops import hip
     from fairify_amd.partition import Grid
@@ -122,12 +159,13 @@ def test_sim_split_identical(cuda, monkeypatch, relaxed):
     gpu = Backend(get_model("AC-3"), cuda)
     lo_t, hi_t = torch.from_numpy(lo).float().to(cuda), torch.from_numpy(hi).float().to(cuda)
     pid = torch.from_numpy(ids).to(cuda)
+    monkeypatch.setattr(hip, "_SIM_BLOCKS_ENV", "dynamic")
     monkeypatch.setenv("FAIRIFY_SIM_BLOCKS", "2048")
     assert hip._sim_split(37, 4000) > 1
     out = []
     for flag in ("0", "2048"):
         monkeypatch.setenv("FAIRIFY_SIM_BLOCKS", flag)
-        out.append(simulate(gpu, q, lo_t, hi_t, pid, 4000, 9, values, pairs, 0, 0))
+        out.append(simulate(gpu, q, lo_t, hi_t, pid, 4000, 9, values, pairs, *bisect))
     a, b = out
     assert torch.equal(a.counts, b.counts)
     assert torch.equal(a.found, b.found)
@@ -162,6 +200,9 @@ def test_certify_matches_reference(cuda):
         outs.append(be.pair_certify(rx, rxp, lo.to(dev), hi.to(dev), plo.to(dev), phi.to(dev), pairs.to(dev),
                                     values.to(dev), pa.to(dev), shared.to(dev), True))
     a, b = outs
-    assert (a.open_ == b.open_.cpu()).float().mean() > 0.95
-    close = (a.score - b.score.cpu()).abs() <= 1e-3 * (a.score.abs() + 1)
-    assert close.float().mean() > 0.95
+    # the two sides round the symbolic forms differently (fp32, different summation orders):
+    # scores agree to rounding, and open/closed may differ only where the score is ~0
+    tol = 1e-3 * (a.score.abs() + 1)
+    assert bool(((a.score - b.score.cpu()).abs() <= tol).all())
+    differ = a.open_ != b.open_.cpu()
+    assert bool((a.score[differ].abs() <= tol[differ]).all())

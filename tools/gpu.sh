@@ -6,7 +6,8 @@
 # OUT is a directory under gpurun_out/; each STEP is one of
 #   tests[:PYTEST_K]          GPU test tier (optionally -k filter)
 #   bench[:ARGS]              bench.py with ARGS ("_" separates arguments), JSON to OUT/bench*.json
-#   prof[:ARGS]               rocprofv3 --kernel-trace --stats of bench.py ARGS (trace csv deleted,
+#   prof[:ARGS]               rocprofv3 --kernel-trace --stats of bench.py ARGS (the trace csv is
+#                             reduced to OUT/profN.busy.txt by tools/trace_busy.py, then deleted;
 #                             the stats csv kept), default host concurrency
 #   pmc:COUNTERS[:ARGS]       one rocprofv3 --pmc pass (counters comma-separated)
 #   py:SCRIPT[:ARGS]          python SCRIPT ARGS
@@ -33,6 +34,7 @@ for step in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
         -d $ROOT/$OUT/prof$n -o run -- python3 -u $ROOT/bench.py $args > $ROOT/$OUT/prof$n.out 2> $ROOT/$OUT/prof$n.err)
       rc=$?
+      for t in $(find $OUT/prof$n -name '*kernel_trace.csv'); do python tools/trace_busy.py $t > $OUT/prof$n.busy.txt; done
       find $OUT/prof$n -name '*kernel_trace.csv' -delete
       cat $OUT/prof$n.out; [ $rc -ne 0 ] && tail -30 $OUT/prof$n.err ;;
     pmc)
