@@ -46,7 +46,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_DECIDED_PER_S = 553.0 / 22143.5
 METRIC = "% partitions verified + partitions/sec on AC suite at 1/2/4/8 MI355X"
-STAGES = ("sim", "bab", "falsify", "smt", "heuristic")
+STAGES = ("sim", "bab", "falsify", "smt", "milp", "heuristic")
 
 
 def parse_args(argv=None):
@@ -74,6 +74,9 @@ def parse_args(argv=None):
                     help="further escalation passes 'budget:max_open,...' after --escalate-budget")
     ap.add_argument("--batch-nodes", type=int, default=65536,
                     help="BaB nodes bounded per sub-batch launch (memory per runtime scales with it)")
+    ap.add_argument("--smt", default="none",
+                    help="exact host solver on the residue in the timed steps: none (fixed-budget throughput "
+                         "bench) | auto | milp | z3py | z3bin")
     ap.add_argument("--no-heuristic", action="store_true",
                     help="skip the reference's unsound heuristic retry (sound verdicts only)")
     ap.add_argument("--residual-samples", type=int, default=None, help="residual falsifier samples (0 = off)")
@@ -163,6 +166,7 @@ def main() -> None:
                        node_budget=args.node_budget, heuristic=not args.no_heuristic, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=args.node_budget, escalate_budget=args.escalate_budget,
                        escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
+                       smt_backend=args.smt,
                        escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
     if args.residual_samples is not None:
         cfg.residual_samples = args.residual_samples

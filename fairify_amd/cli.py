@@ -55,11 +55,14 @@ def cmd_verify(args):
                        heuristic_p=args.heuristic_p if args.heuristic_p is not None else pre.heuristic_p,
                        heuristic_node_budget=args.node_budget, smt_backend=args.smt,
                        escalate_budget=args.escalate_budget, escalate_max_open=args.escalate_max_open)
+    if args.residual_samples is not None:
+        cfg.residual_samples = args.residual_samples
     models = args.models.split(",") if args.models else None
     run_preset(pre, models=models, weights=args.weights, out_dir=args.out, cfg=cfg, info=info,
                max_partitions=args.max_partitions, resume=args.resume, seed=args.seed,
                accuracy=not args.no_accuracy, escalate=args.escalate,
-               concurrency=args.concurrency or (4 if info.device.type == "cuda" else 1))
+               concurrency=args.concurrency or (4 if info.device.type == "cuda" else 1),
+               anytime_budget=(args.anytime_budget or cfg.hard_timeout) if args.anytime else None)
     D.destroy(info)
 
 
@@ -167,6 +170,11 @@ def main(argv=None):
     v.add_argument("--concurrency", type=int, default=0,
                    help="chunks verified at once per rank, one HIP stream each (default 4 on GPU, 1 on CPU)")
     v.add_argument("--smt", default="auto", help="host SMT back-end for the residue: auto | z3py | z3bin | none")
+    v.add_argument("--anytime", action="store_true",
+                   help="spend the per-model wall budget (--anytime-budget, default the preset's hard timeout) on "
+                        "growing sound BaB budgets and falsifier rounds over the UNKNOWN residue")
+    v.add_argument("--anytime-budget", type=float, default=None, help="seconds per model for --anytime")
+    v.add_argument("--residual-samples", type=int, default=None)
     v.add_argument("--no-accuracy", action="store_true")
     v.add_argument("--device", default=None)
     v.set_defaults(fn=cmd_verify)

@@ -61,10 +61,21 @@ class VerifyConfig:
     residual_samples: int = 2048         # residual falsifier on BaB-UNKNOWN partitions (0 = off)
     residual_starts: int = 16            # local-search starts per partition
     residual_iters: int = 12             # coordinate-ascent rounds
-    smt_backend: str = "auto"            # host SMT on the BaB residue: auto | z3py | z3bin | none
-    smt_workers: int = 8
+    smt_backend: str = "auto"            # exact host solver on the BaB residue: auto (Z3 if installed,
+                                         # else the HiGHS MILP back-end) | z3py | z3bin | milp | none
+    smt_workers: int = 12                # host solver threads (the GPU box gives a process 16 CPUs)
     smt_timeout: Optional[float] = None  # per query; defaults to soft_timeout
     smt_fork_params: bool = False        # Z3 seed/restart/phase options of the fork's drivers
+    # anytime mode: after the fixed passes, keep growing the node budget (x anytime_growth per
+    # round) and the residual falsifier's sample count on the sound-UNKNOWN residue until it is
+    # empty or this chunk's share of the model's wall budget is spent (the reference spends up to
+    # its hard timeout per model, src/AC/Verify-AC.py:318-320).  0 = off.
+    anytime_seconds: float = 0.0
+    anytime_growth: int = 4
+    anytime_max_budget: int = 1 << 22
+    anytime_pool: int = 1 << 24          # live BaB nodes per group: group size = pool / budget
+    anytime_max_samples: int = 16384
+    anytime_milp_seconds: float = 1.0    # first MILP round's per-partition limit (x growth per round)
 
 
 @dataclass
@@ -127,6 +138,7 @@ class _LazyMasked:
 
 
 _HOST_SMT: Dict[tuple, object] = {}
+_VERBOSE_ANYTIME = os.environ.get("FAIRIFY_VERBOSE_ANYTIME") == "1"
 
 
 def _host_smt(cfg: VerifyConfig):
@@ -142,6 +154,39 @@ def _host_smt(cfg: VerifyConfig):
 def _amortize(total: float, work: np.ndarray) -> np.ndarray:
     w = work.astype(np.float64) + 1.0
     return total * w / w.sum()
+
+
+def _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, limit, workers, status, stage, cex_x, cex_xp,
+                deadline=None):
+    """HiGHS MILP on the partitions ``unk`` (per-partition time limit ``limit``, nothing starts
+    after ``deadline``); UNSAT and exactly confirmed SAT verdicts are written into the stage
+    arrays."""
+    from ..smt import milp
+
+    futs = milp.submit(be, mlp, q, lo_np[unk], hi_np[unk], values_np, pairs_np, limit, workers=workers,
+                       deadline=deadline)
+    cand_k, cand_x, cand_xp = [], [], []
+    t_note = time.time()
+    for i, (k, f) in enumerate(zip(unk, futs)):
+        verdict, pair = f.result()
+        if _VERBOSE_ANYTIME and time.time() - t_note > 30.0:
+            t_note = time.time()
+            print(f"[milp] {mlp.name}: {i + 1}/{len(unk)} partitions, limit {limit:.1f}s", flush=True)
+        if verdict == "unsat":
+            status[k], stage[k] = UNSAT, "milp"
+        elif verdict == "sat" and pair is not None:
+            cand_k.append(k)
+            cand_x.append(pair[0])
+            cand_xp.append(pair[1])
+    if cand_k:
+        ck_ = np.asarray(cand_k)
+        X, XP = np.asarray(cand_x, dtype=np.int64), np.asarray(cand_xp, dtype=np.int64)
+        ok = exact.check_pair_constraints(X, XP, lo_np[ck_], hi_np[ck_], q.pa_idx, q.ra_idx, q.tau)
+        viol = exact.is_violation(mlp, X, XP) & ok
+        hit = ck_[viol]
+        status[hit] = SAT
+        cex_x[hit], cex_xp[hit] = X[viol], XP[viol]
+        stage[hit] = "milp"
 
 
 def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.ndarray, cfg: VerifyConfig,
@@ -347,32 +392,118 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         sync()
         t_bab += time.time() - t0
 
-    # ---------------- stage 3c: host SMT on the sound-pruned subnetworks of the residue
-    # (the reference's Z3 check, src/AC/Verify-AC.py:145-158; no-op without a back-end)
+    # ---------------- stage 3c: exact host solver on the residue (the reference's Z3 check,
+    # src/AC/Verify-AC.py:145-158): Z3 when installed, else the HiGHS MILP back-end fed the
+    # GPU's rigorous layer bounds (smt/milp.py); no-op with "none"
     t_smt = 0.0
     if cfg.smt_backend != "none":
-        hs = _host_smt(cfg)
-        unk = np.nonzero(status == UNKNOWN)[0]
-        if hs.active and unk.size:
+        from ..smt import solver as smt_solver
+
+        backend = smt_solver.resolve(cfg.smt_backend)
+        unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+        if backend == "milp" and unk.size and cfg.anytime_seconds <= 0:   # anytime: MILP rounds inside 3d
             t0 = time.time()
-            with tm("smt"):
-                ut = torch.from_numpy(unk).to(dev)
-                st_mask = ((code[ut][:, :Nh] & H.PM_ST) != 0) if fused else st_dead[ut][:, :Nh]
-                futs = hs.submit(mlp, q, lo_np[unk], hi_np[unk], st_mask)
-                for k, f in zip(unk, futs):
-                    verdict, pair = f.result()
-                    if verdict == "unsat":
-                        status[k], stage[k] = UNSAT, "smt"
-                    elif verdict == "sat" and pair is not None:
-                        X = np.array([pair[0]], dtype=np.int64)
-                        XP = np.array([pair[1]], dtype=np.int64)
-                        ok = exact.check_pair_constraints(X, XP, lo_np[k:k + 1], hi_np[k:k + 1], q.pa_idx,
-                                                          q.ra_idx, q.tau)
-                        if ok[0] and exact.is_violation(mlp, X, XP)[0]:
-                            status[k], stage[k] = SAT, "smt"
-                            cex_x[k], cex_xp[k] = X[0], XP[0]
+            with tm("milp"):
+                _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, cfg.smt_timeout or cfg.soft_timeout,
+                            cfg.smt_workers, status, stage, cex_x, cex_xp)
             t_smt = time.time() - t0
+        elif backend != "milp":
+            hs = _host_smt(cfg)
+            if hs.active and unk.size:
+                t0 = time.time()
+                with tm("smt"):
+                    ut = torch.from_numpy(unk).to(dev)
+                    st_mask = ((code[ut][:, :Nh] & H.PM_ST) != 0) if fused else st_dead[ut][:, :Nh]
+                    futs = hs.submit(mlp, q, lo_np[unk], hi_np[unk], st_mask)
+                    for k, f in zip(unk, futs):
+                        verdict, pair = f.result()
+                        if verdict == "unsat":
+                            status[k], stage[k] = UNSAT, "smt"
+                        elif verdict == "sat" and pair is not None:
+                            X = np.array([pair[0]], dtype=np.int64)
+                            XP = np.array([pair[1]], dtype=np.int64)
+                            ok = exact.check_pair_constraints(X, XP, lo_np[k:k + 1], hi_np[k:k + 1], q.pa_idx,
+                                                              q.ra_idx, q.tau)
+                            if ok[0] and exact.is_violation(mlp, X, XP)[0]:
+                                status[k], stage[k] = SAT, "smt"
+                                cex_x[k], cex_xp[k] = X[0], XP[0]
+                t_smt = time.time() - t0
     t_bab += t_smt
+
+    # ---------------- stage 3d: anytime escalation on the residue (sound; before the heuristic)
+    anytime_rounds = 0
+    if cfg.anytime_seconds > 0:
+        t0 = time.time()
+        deadline = t0 + cfg.anytime_seconds
+        e_budget = max(prev_budget, cfg.node_budget)
+        n_samp = max(cfg.residual_samples, 1)
+        use_milp = False
+        if cfg.smt_backend != "none":
+            from ..smt import solver as smt_solver
+
+            use_milp = smt_solver.resolve(cfg.smt_backend) == "milp"
+        milp_limit = cfg.anytime_milp_seconds
+        with tm("anytime"):
+            while True:
+                unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+                if not unk.size or time.time() >= deadline:
+                    break
+                anytime_rounds += 1
+                # (a) fresh samples + boundary walk + local search, new seed every round
+                n_samp = min(n_samp * cfg.anytime_growth, cfg.anytime_max_samples)
+                ut = torch.from_numpy(unk).to(dev)
+                fr = residual_falsify(be, q, lo[ut], hi[ut], pids[ut], values, pairs,
+                                      cfg.seed + 7919 * anytime_rounds, n_samples=n_samp,
+                                      k_starts=2 * cfg.residual_starts, iters=2 * cfg.residual_iters)
+                fnd = fr.found.cpu().numpy()
+                if fnd.any():
+                    fi = np.nonzero(fnd)[0]
+                    X = fr.wit_x[fi].cpu().numpy().round().astype(np.int64)
+                    XP = fr.wit_xp[fi].cpu().numpy().round().astype(np.int64)
+                    pi = unk[fi]
+                    ok = exact.check_pair_constraints(X, XP, lo_np[pi], hi_np[pi], q.pa_idx, q.ra_idx, q.tau)
+                    viol = exact.is_violation(mlp, X, XP) & ok
+                    hit = pi[viol]
+                    status[hit] = SAT
+                    cex_x[hit], cex_xp[hit] = X[viol], XP[viol]
+                    stage[hit] = "falsify"
+                # (b) exact host MILP with a growing per-partition time limit
+                if use_milp:
+                    unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+                    left = deadline - time.time()
+                    if unk.size and left > 0:
+                        with tm("milp"):
+                            _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, min(milp_limit, left),
+                                        cfg.smt_workers, status, stage, cex_x, cex_xp, deadline=deadline)
+                    milp_limit *= cfg.anytime_growth
+                # (c) deeper sound BaB, in groups that fit the node pool
+                e_budget *= cfg.anytime_growth
+                if e_budget > cfg.anytime_max_budget:
+                    break
+                unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+                if _VERBOSE_ANYTIME:
+                    print(f"[anytime] {mlp.name} round {anytime_rounds}: {unk.size} unknown after falsify "
+                          f"({n_samp} samples), BaB budget {e_budget}, {deadline - time.time():.1f}s left",
+                          flush=True)
+                G = max(1, cfg.anytime_pool // e_budget)
+                for g0 in range(0, unk.size, G):
+                    left = deadline - time.time()
+                    if left <= 0:
+                        break
+                    grp = unk[g0:g0 + G]
+                    asolver = BaBSolver(be, q, BaBConfig(node_budget=e_budget, batch_nodes=cfg.batch_nodes,
+                                                         time_budget=left, max_pool=cfg.anytime_pool), timer=tm)
+                    ares = asolver.solve(lo_np[grp], hi_np[grp], mlp)
+                    dec_a = np.isin(ares.status, (SAT, UNSAT))
+                    hit = grp[dec_a]
+                    status[hit] = ares.status[dec_a]
+                    stage[hit] = "bab"
+                    sa = ares.status == SAT
+                    cex_x[grp[sa]] = ares.cex_x[sa]
+                    cex_xp[grp[sa]] = ares.cex_xp[sa]
+                    nodes[grp] += ares.nodes
+        sync()
+        t_bab += time.time() - t0
 
     # ---------------- stage 4: heuristic retry for UNKNOWN partitions (unsound, flagged)
     h_attempt = np.zeros(Pn, dtype=np.int64)

@@ -36,7 +36,7 @@ from .pipeline import PartitionRecord, StreamPool, VerifyConfig, concat_records,
 
 VCODE = {"sat": 1, "unsat": 2, "unknown": 0}
 VNAME = {v: k for k, v in VCODE.items()}
-STAGES = ["", "sim", "bab", "heuristic", "smt", "falsify"]
+STAGES = ["", "sim", "bab", "heuristic", "smt", "falsify", "milp"]
 _SCALARS = ["h_attempt", "h_success", "b_comp", "s_comp", "st_comp", "h_comp", "t_comp", "sv_time", "s_time",
             "hv_time", "h_time", "total_time", "c_check", "v_accurate", "pruned_acc", "nodes"]
 
@@ -182,11 +182,14 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                cfg: Optional[VerifyConfig] = None, info: Optional[D.DistInfo] = None,
                max_partitions: Optional[int] = None, resume: bool = False, seed: int = 0,
                accuracy: bool = True, verbose: bool = True, escalate: int = 1,
-               concurrency: int = 1) -> List[Dict]:
+               concurrency: int = 1, anytime_budget: Optional[float] = None) -> List[Dict]:
     """``escalate`` > 1: every round's UNKNOWN partitions are re-distributed over all ranks and
     retried with ``escalate`` x the node budget (residual work stealing).  ``concurrency`` > 1:
     each rank verifies that many chunks of a round at once, one host thread + HIP stream each
-    (a round is then ``chunk x concurrency`` partitions per rank)."""
+    (a round is then ``chunk x concurrency`` partitions per rank).  ``anytime_budget`` (seconds
+    per model, e.g. the preset's hard timeout): every round gets the share of the model's
+    remaining budget proportional to its partitions and spends it on deeper sound BaB passes and
+    falsifier rounds over its UNKNOWN residue (VerifyConfig.anytime_seconds)."""
     info = info or D.DistInfo()
     grid = preset.grid(seed=seed)
     q = preset.resolved()
@@ -254,10 +257,18 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             pos = rpos[info.rank]
             buf = wire.empty(q)
             codes = np.zeros(0, np.int8)
+            rcfg = cfg
+            if anytime_budget:
+                # this round's share of the remaining per-model budget (all ranks agree: the
+                # elapsed time is the global max and the round sizes are known everywhere)
+                n_round = sum(len(p) for p in rpos)
+                n_left = len(todo) - r * per_round * info.world
+                share = max(0.0, (min(anytime_budget, cfg.hard_timeout) - elapsed) * n_round / max(1, n_left))
+                rcfg = replace(cfg, anytime_seconds=0.9 * share)
             if len(pos):
                 subs = [pos[s:s + cfg.chunk] for s in range(0, len(pos), cfg.chunk)]
                 recs = concat_records(streams.run(
-                    lambda sp: verify_chunk(be, mlp, q, grid, order[sp], cfg, orig_acc=acc,
+                    lambda sp: verify_chunk(be, mlp, q, grid, order[sp], rcfg, orig_acc=acc,
                                             time_budget=cfg.hard_timeout - elapsed, timer=timer), subs))
                 buf = wire.encode(recs, q)
                 codes = wire.verdict_codes(recs)

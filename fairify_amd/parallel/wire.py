@@ -27,7 +27,7 @@ import numpy as np
 from ..engine.pipeline import ChunkRecords
 
 VERDICTS = ("unknown", "sat", "unsat")
-STAGES = ("", "sim", "bab", "heuristic", "smt", "falsify")
+STAGES = ("", "sim", "bab", "heuristic", "smt", "falsify", "milp")
 REC = np.dtype([("flags", "<u2"), ("b", "<u2"), ("s", "<u2"), ("st", "<u2"), ("h", "<u2"), ("t", "<u2"),
                 ("agree", "<u2"), ("nodes", "<u4")])
 assert REC.itemsize == 18

@@ -33,6 +33,8 @@ from .solver import resolve, solve
 class HostSMT:
     def __init__(self, backend: str = "auto", workers: int = 8, timeout_s: float = 100.0, fork_params: bool = False):
         self.backend = resolve(backend)
+        if self.backend == "milp":          # not an SMT-LIB consumer: the pipeline calls smt.milp itself
+            self.backend = "none"
         self.timeout_s = float(timeout_s)
         self.fork_params = fork_params
         self.pool = ThreadPoolExecutor(max_workers=max(1, workers)) if self.backend != "none" else None

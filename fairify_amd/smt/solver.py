@@ -6,7 +6,9 @@ subnetwork (:mod:`fairify_amd.smt.encode`):
 
 * ``z3py``  — the ``z3`` Python module, if importable (``z3.Solver().from_string``);
 * ``z3bin`` — a ``z3`` (or ``$FAIRIFY_SMT_BIN``) executable on PATH, fed the script on stdin;
-* ``none``  — no solver available: residual partitions stay UNKNOWN.
+* ``milp``  — HiGHS mixed-integer programming through SciPy, fed the GPU's rigorous layer
+  bounds (:mod:`fairify_amd.smt.milp`; not an SMT-LIB consumer, the pipeline calls it directly);
+* ``none``  — no solver: residual partitions stay UNKNOWN.
 
 Neither Z3 flavour exists in this image; :func:`available` reports what was found and the
 pipeline silently keeps ``none``.  Results come back as ``("sat", (x, x'))``,
@@ -39,11 +41,17 @@ def _z3bin() -> Optional[str]:
 
 
 def available() -> List[str]:
+    """Installed back-ends in preference order (Z3 first: exact arithmetic; then the HiGHS MILP
+    back-end of :mod:`fairify_amd.smt.milp`, which SciPy ships)."""
     out = []
     if _z3py() is not None:
         out.append("z3py")
     if _z3bin():
         out.append("z3bin")
+    from . import milp
+
+    if milp.available():
+        out.append("milp")
     return out
 
 

@@ -63,7 +63,7 @@ def test_export_and_repair_roundtrip(tmp_path):
 
     out = str(tmp_path)
     run_preset(presets.get("src/GC-age"), models=["GC-1"], out_dir=out, accuracy=False, verbose=False,
-               cfg=VerifyConfig(sim_size=200, node_budget=256), max_partitions=12, weights="zoo")
+               cfg=VerifyConfig(sim_size=200, node_budget=256, smt_backend="none"), max_partitions=12, weights="zoo")
     path = export_counterexamples("src/GC-age", "GC-1", out, weights="zoo")
     z = np.load(os.path.splitext(path)[0] + ".npz")
     assert z["x"].shape == z["xp"].shape and len(z["x"]) > 0

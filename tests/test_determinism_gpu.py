@@ -46,7 +46,7 @@ def test_concurrent_streams_match_serial(cuda):
     chunks = [order[i * 512:(i + 1) * 512] for i in range(4)]
     m = get_model("AC-5", weights="random", seed=0)
     be = Backend(m, cuda)
-    cfg = VerifyConfig(sim_size=256, node_budget=512)
+    cfg = VerifyConfig(sim_size=256, node_budget=512, smt_backend="none")
     serial = [verify_chunk(be, m, q, grid, ids, cfg) for ids in chunks]
 
     def run(ids):

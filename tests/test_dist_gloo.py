@@ -30,7 +30,7 @@ def _worker(rank, world, port, out):
     from fairify_amd.parallel import dist as D
 
     info = D.init("cpu")
-    cfg = VerifyConfig(sim_size=200, chunk=16, node_budget=512)
+    cfg = VerifyConfig(sim_size=200, chunk=16, node_budget=512, smt_backend="none")
     run_preset(presets.get("src/GC-age"), models=["GC-1", "GC-4"], out_dir=out, cfg=cfg, info=info,
                max_partitions=70, accuracy=False, verbose=False)
     # collective helpers
@@ -77,7 +77,7 @@ def test_resume_skips_finished(tmp_path):
     from fairify_amd.engine.runner import run_preset
 
     out = str(tmp_path / "r")
-    cfg = VerifyConfig(sim_size=100, chunk=8, node_budget=256)
+    cfg = VerifyConfig(sim_size=100, chunk=8, node_budget=256, smt_backend="none")
     pre = presets.get("src/GC-sex")
     run_preset(pre, models=["GC-3"], out_dir=out, cfg=cfg, max_partitions=20, accuracy=False, verbose=False)
     rows = run_preset(pre, models=["GC-3"], out_dir=out, cfg=cfg, max_partitions=40, resume=True,
@@ -100,7 +100,7 @@ def _worker_escalate(rank, world, port, out):
     from fairify_amd.parallel import dist as D
 
     info = D.init("cpu")
-    cfg = VerifyConfig(sim_size=100, chunk=24, node_budget=16, heuristic=False)
+    cfg = VerifyConfig(sim_size=100, chunk=24, node_budget=16, heuristic=False, smt_backend="none")
     run_preset(presets.get("src/AC-sex"), models=["AC-7"], weights="random", out_dir=out, cfg=cfg, info=info,
                max_partitions=48, accuracy=False, verbose=False, escalate=8)
     D.destroy(info)
@@ -128,7 +128,7 @@ def test_injected_crash_then_resume_matches_uninterrupted(tmp_path, monkeypatch)
     from fairify_amd.utils.faults import InjectedFault
 
     pre = presets.get("src/GC-age")
-    cfg = VerifyConfig(sim_size=100, chunk=8, node_budget=256)
+    cfg = VerifyConfig(sim_size=100, chunk=8, node_budget=256, smt_backend="none")
     ref_dir, out = str(tmp_path / "ref"), str(tmp_path / "crash")
     run_preset(pre, models=["GC-4"], out_dir=ref_dir, cfg=cfg, max_partitions=40, accuracy=False, verbose=False)
     monkeypatch.setenv("FAIRIFY_FAULT_CRASH_AFTER", "2")
@@ -158,7 +158,7 @@ def test_forced_unknown_injection(monkeypatch):
     grid, q = pre.grid(), pre.resolved()
     ids = processing_order(grid, 0)[:32]
     m = get_model("GC-4")
-    cfg = VerifyConfig(sim_size=100, node_budget=256, heuristic=False)
+    cfg = VerifyConfig(sim_size=100, node_budget=256, heuristic=False, smt_backend="none")
     base = [r["verdict"] for r in verify_chunk(Backend(m), m, q, grid, ids, cfg)]
     monkeypatch.setenv("FAIRIFY_FAULT_FORCE_UNKNOWN", "0.5")
     mask = forced_unknown(ids)

@@ -23,7 +23,7 @@ def test_mixed_pa_ranges_in_one_chunk():
     assert len(np.unique(lo[:, pa])) > 1            # several PA ranges in the chunk
     m = get_model("AC-8", weights="random", seed=1)
     be = Backend(m)
-    cfg = VerifyConfig(sim_size=128, node_budget=64, heuristic=False, residual_samples=0)
+    cfg = VerifyConfig(sim_size=128, node_budget=64, heuristic=False, residual_samples=0, smt_backend="none")
     recs = verify_chunk(be, m, q, grid, ids, cfg)
     assert list(recs.cols["grid_id"]) == list(ids)
     # same verdicts as verifying each PA group on its own

@@ -22,7 +22,7 @@ DATA = os.path.isdir(os.environ.get("FAIRIFY_DATA", "/root/reference/data"))
 @pytest.mark.parametrize("model,sat,unsat", [("GC-3", 195, 6), ("GC-4", 2, 199)])
 def test_table_v_gc_exact_counts(tmp_path, preset, model, sat, unsat):
     rows = run_preset(presets.get(preset), models=[model], out_dir=str(tmp_path), accuracy=False, verbose=False,
-                      cfg=VerifyConfig(sim_size=1000, node_budget=100000, heuristic=False))
+                      cfg=VerifyConfig(sim_size=1000, node_budget=100000, heuristic=False, smt_backend="none"))
     r = rows[0]
     assert (r["SAT"], r["UNSAT"], r["UNK"]) == (sat, unsat, 0)
 
