@@ -77,6 +77,10 @@ def parse_args(argv=None):
     ap.add_argument("--smt", default="none",
                     help="exact host solver on the residue in the timed steps: none (fixed-budget throughput "
                          "bench) | auto | milp | z3py | z3bin")
+    ap.add_argument("--budget-pass", type=float, default=10.0,
+                    help="after the timed steps, one untimed pass over the same grid in anytime mode with this "
+                         "many seconds per model (growing BaB budgets + falsifier + MILP rounds on the residue): "
+                         "reports pct_verified_at_budget (0 = skip; default 10 s per model adds ~16 s)")
     ap.add_argument("--no-heuristic", action="store_true",
                     help="skip the reference's unsound heuristic retry (sound verdicts only)")
     ap.add_argument("--residual-samples", type=int, default=None, help="residual falsifier samples (0 = off)")
@@ -286,6 +290,52 @@ def main() -> None:
         "baseline": {"decided_per_s": round(BASELINE_DECIDED_PER_S, 5), "pct_verified_of_attempted": 89.0,
                      "coverage_of_grid_pct": 0.29},
     }
+    if args.budget_pass > 0:
+        # per-model wall budget B: every (model, chunk) item gets the chunk's share of B for its
+        # anytime phase; items of all models run concurrently on the host streams, so the pass
+        # takes about B plus the fixed-schedule time of one step
+        from dataclasses import replace as _replace
+
+        chunks = chunks_for_step(0)
+        n_shard = max(1, sum(len(c) for c in chunks))
+        bcfg = {k: _replace(cfg, smt_backend="auto", anytime_seconds=args.budget_pass * len(c) / n_shard)
+                for k, c in enumerate(chunks)}
+        NB = 2 + len(STAGES) + 2
+
+        def budget_item(k: int, j: int, ids: np.ndarray):
+            with thread_stream():
+                recs = verify_chunk(backends[k], models[k], q, grid, ids, bcfg[j], timer=timer)
+                if info.device.type == "cuda":
+                    torch.cuda.current_stream(info.device).synchronize()
+            v, st = recs.cols["verdict"], recs.cols["stage"]
+            sat, uns = v == "sat", v == "unsat"
+            o = np.zeros(NB)
+            o[0], o[1] = len(recs), sat.sum() + uns.sum()
+            for i, name in enumerate(STAGES):
+                o[2 + i] = (uns & (st == name)).sum()
+            o[2 + len(STAGES)] = sat.sum()
+            o[3 + len(STAGES)] = uns.sum()
+            return o
+
+        D.barrier(info)
+        tb = time.time()
+        items = [(k, j, ids) for k in range(len(models)) for j, ids in enumerate(chunks) if len(ids)]
+        items.sort(key=lambda it: -models[it[0]].n_neurons)
+        if pool is None:
+            btot = sum(budget_item(*it) for it in items)
+        else:
+            btot = sum(f.result() for f in [pool.submit(budget_item, *it) for it in items])
+        sync()
+        D.barrier(info)
+        bwall = D.all_reduce_max(info, time.time() - tb)
+        btot = D.all_reduce_sum(info, np.asarray(btot, dtype=np.float64))
+        out["pct_verified_at_budget"] = round(100.0 * btot[1] / max(1.0, btot[0]), 3)
+        out["budget_pass"] = {
+            "seconds_per_model": args.budget_pass, "wall_s": round(bwall, 2), "attempted": int(btot[0]),
+            "decided": int(btot[1]), "sat": int(btot[2 + len(STAGES)]), "unsat": int(btot[3 + len(STAGES)]),
+            "unsat_by_stage": {name: int(btot[2 + i]) for i, name in enumerate(STAGES) if btot[2 + i]},
+            "note": "untimed; anytime mode: BaB budgets x4 per round, falsifier rounds, HiGHS MILP rounds "
+                    "(UNSAT 'milp' = floating-point dual bound), heuristic retry last"}
     if args.profile and info.is_main:
         print(timer.report(), file=sys.stderr, flush=True)
     if info.is_main:

@@ -124,20 +124,26 @@ def _write_round(writer: PartitionCSV, rows: np.ndarray, n0: int, acc, done: np.
     _save_done(state_path, done)
 
 
-_TABLE_COLS = ("verdict", "h_attempt", "h_success", "st_comp", "h_comp", "sv_time", "hv_time", "total_time")
+_TABLE_COLS = ("verdict", "h_attempt", "h_success", "st_comp", "h_comp", "sv_time", "hv_time", "total_time", "stage")
 
 
-def model_accuracy(mlp, suite: str, seed: int = 0) -> Optional[float]:
-    """``Original-acc`` column: test accuracy on the suite's dataset (real when available)."""
+def model_accuracy(mlp, suite: str, seed: int = 0, with_source: bool = False):
+    """``Original-acc`` column: test accuracy on the suite's dataset (real when available).
+    ``with_source``: returns ``(acc, source)``, source "reference-data" or "synthetic" (the
+    reference's CSVs are absent, e.g. on the GPU box: the number is then NOT the paper's
+    column and is labelled as such in summary.json)."""
     from ..data import tabular
 
     try:
         ds = tabular.load(suite, seed=seed)
     except Exception:
-        return None
+        return (None, None) if with_source else None
     if ds.X_test.shape[1] != mlp.n_in:
-        return None
-    return float(np.mean(mlp.predict(ds.X_test) == ds.y_test))
+        return (None, None) if with_source else None
+    acc = float(np.mean(mlp.predict(ds.X_test) == ds.y_test))
+    if with_source:
+        return acc, ("synthetic" if getattr(ds, "synthetic", False) else "reference-data")
+    return acc
 
 
 def _round_positions(todo: np.ndarray, r: int, per_round: int, world: int) -> List[np.ndarray]:
@@ -204,7 +210,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
     for name in (models or list(preset.models)):
         mlp = get_model(name, weights=weights, seed=seed)
         be = Backend(mlp, device=info.device)
-        acc = model_accuracy(mlp, preset.suite, seed) if accuracy else None
+        acc, acc_src = model_accuracy(mlp, preset.suite, seed, with_source=True) if accuracy else (None, None)
         state_path = os.path.join(out_dir, "state", f"{name}.npz")
         csv_path = os.path.join(out_dir, f"{name}.csv")
         done = np.zeros(total, dtype=bool)            # checkpoint: finished processing positions
@@ -303,9 +309,24 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         wall = D.all_reduce_max(info, time.time() - t0)
         if info.is_main:
             tc = {k: (np.concatenate(v) if v else np.zeros(0)) for k, v in table_cols.items()}
+            stage_codes = tc.pop("stage").astype(np.int64)
             row = table_v_row_columns(name, pa_name, grid_size=len(grid), wall=wall, **tc)
             row["stopped_by_hard_timeout"] = stopped
             row["original_acc"] = acc
+            row["original_acc_source"] = acc_src
+            # honest accounting: which stage decided (heuristic verdicts are the reference's
+            # unsound retry; "milp" UNSAT rests on HiGHS's floating-point dual bound)
+            v = tc["verdict"].astype(np.int64)
+            row["sat_by_stage"] = {STAGES[k] or "none": int(((v == 1) & (stage_codes == k)).sum())
+                                   for k in range(len(STAGES)) if ((v == 1) & (stage_codes == k)).any()}
+            row["unsat_by_stage"] = {STAGES[k] or "none": int(((v == 2) & (stage_codes == k)).sum())
+                                     for k in range(len(STAGES)) if ((v == 2) & (stage_codes == k)).any()}
+            row["UNSAT_sound"] = int(((v == 2) & ~np.isin(stage_codes, [STAGES.index("heuristic"),
+                                                                        STAGES.index("milp")])).sum())
+            row["UNSAT_heuristic"] = int(((v == 2) & (stage_codes == STAGES.index("heuristic"))).sum())
+            row["UNSAT_milp"] = int(((v == 2) & (stage_codes == STAGES.index("milp"))).sum())
+            if anytime_budget:
+                row["anytime_budget_s"] = float(anytime_budget)
             row["wire_bytes_per_partition"] = round(wire_bytes[0] / max(1, wire_bytes[1]), 2)
             rows_out.append(row)
             if verbose:
