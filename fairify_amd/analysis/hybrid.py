@@ -60,3 +60,11 @@ def hybrid_predict(X: np.ndarray, table: VerdictTable, predict_orig, predict_fai
     yo = np.asarray(predict_orig(X))
     yf = np.asarray(predict_fair(X))
     return np.where(v == V_SAT, yf, yo)
+
+
+def case_breakdown(X: np.ndarray, table: VerdictTable) -> Dict[str, int]:
+    """The fork's debug counters (src/AC/Verify-AC-experiment-new.py:594-620, 760-805): which
+    branch of the hybrid predictor each test row takes."""
+    v = table.lookup(X)
+    return {"no_partition": int((v == NOT_ATTEMPTED).sum()), "sat_fairer": int((v == V_SAT).sum()),
+            "unsat_original": int((v == V_UNSAT).sum()), "unknown_original": int((v == V_UNKNOWN).sum())}

@@ -18,7 +18,7 @@ from ..data import tabular
 from ..models.zoo import get_model
 from ..ops.backend import Backend
 from .causal import CausalDiscriminationDetector
-from .hybrid import VerdictTable, hybrid_predict
+from .hybrid import VerdictTable, case_breakdown, hybrid_predict
 from .metrics import all_metrics
 
 
@@ -67,6 +67,7 @@ def analyze_model(preset: str, model: str, fairer: Optional[str] = None, results
             yh = hybrid_predict(X, table, p_orig, p_fair)
             res["hybrid"] = all_metrics(X, y, yh, pa, device=device)
             res["verdicts"] = table.counts()
+            res["cases"] = case_breakdown(X, table)
 
             def p_h(Z):
                 return hybrid_predict(Z, table, p_orig, p_fair)
@@ -78,7 +79,40 @@ def analyze_model(preset: str, model: str, fairer: Optional[str] = None, results
         os.makedirs(out_dir, exist_ok=True)
         with open(os.path.join(out_dir, f"{model}-analysis.json"), "w") as f:
             json.dump(res, f, indent=2, default=float)
+        if "hybrid" in res:
+            write_hybrid_csvs(res, model, fairer, out_dir, n_test=len(y))
     return res
+
+
+_MCOLS = ("accuracy", "DI", "SPD", "EOD", "AOD", "ERD", "CNT", "TI")
+
+
+def write_hybrid_csvs(res: Dict, model: str, fairer: str, out_dir: str, n_test: int) -> None:
+    """``hybrid_approach_results.csv`` and ``debug_case_breakdown.csv`` in the fork's layout
+    (src/AC/Verify-AC-experiment-new.py:760-816)."""
+    import csv
+
+    fname = os.path.splitext(os.path.basename(fairer))[0]
+    with open(os.path.join(out_dir, "hybrid_approach_results.csv"), "w", newline="") as fp:
+        wr = csv.writer(fp, dialect="excel")
+        wr.writerow(["Approach", "Accuracy", "DI", "SPD", "EOD", "AOD", "ERD", "CNT", "TI"])
+        for label, key in (("Hybrid", "hybrid"), (f"{model} Original", "original"), (f"{fname} Fairer", "fairer")):
+            wr.writerow([label] + [res[key][c] for c in _MCOLS])
+    c = res["cases"]
+    orig_used = c["no_partition"] + c["unsat_original"] + c["unknown_original"]
+    pct = lambda k: f"{k / max(1, n_test) * 100:.2f}%"
+    rows = [
+        ["Case", "Description", "Model Used", "Count", "Percentage"],
+        ["Case 1", "No partition found", model, c["no_partition"], pct(c["no_partition"])],
+        ["Case 3", "SAT/Unfair partition", fname, c["sat_fairer"], pct(c["sat_fairer"])],
+        ["Case 4", "UNSAT/Fair partition", model, c["unsat_original"], pct(c["unsat_original"])],
+        ["Case 5", "Unknown partition", model, c["unknown_original"], pct(c["unknown_original"])],
+        ["", "", "", "", ""],
+        ["SUMMARY", f"Total {model} used", model, orig_used, pct(orig_used)],
+        ["SUMMARY", f"Total {fname} used", fname, c["sat_fairer"], pct(c["sat_fairer"])],
+    ]
+    with open(os.path.join(out_dir, "debug_case_breakdown.csv"), "w", newline="") as fp:
+        csv.writer(fp, dialect="excel").writerows(rows)
 
 
 def _load(path: str):

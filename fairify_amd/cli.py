@@ -89,6 +89,23 @@ def cmd_analyze(args):
 
 
 def cmd_repair(args):
+    if args.method == "finetune":
+        # GC/BM recipe: fine-tune on a synthetic CSV with early stopping (src/GC/new_model.py:8-58,
+        # src/BM/new_model.py:8-40)
+        from .models.zoo import get_model
+        from .repair.finetune import finetune_csv
+
+        if not args.data or not args.suite:
+            raise SystemExit("--method finetune needs --data CSV and --suite german|bank")
+        m = get_model(args.model, weights=args.weights, seed=args.seed)
+        r = finetune_csv(m, args.data, args.suite, lr=args.lr, epochs=args.max_epochs, seed=args.seed,
+                         device=_device(args.device), name=os.path.splitext(os.path.basename(args.out))[0])
+        os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
+        r.model.save_npz(args.out if args.out.endswith(".npz") else args.out + ".npz")
+        print(json.dumps({"model": args.model, "out": args.out, "epochs_run": r.epochs_run, "best_epoch": r.best_epoch,
+                          "val_acc": r.val_acc, "val_loss": r.val_loss, "train_rows": r.train_rows,
+                          "val_rows": r.val_rows}, indent=2))
+        return
     from .repair.retrain import repair_model
 
     out = repair_model(args.model, counterexamples=args.counterexamples, method=args.method, out=args.out,
@@ -197,8 +214,12 @@ def main(argv=None):
 
     r = sub.add_parser("repair", help="bias localisation + masked fine-tune / counterexample retraining")
     r.add_argument("--model", required=True)
-    r.add_argument("--counterexamples", required=True)
-    r.add_argument("--method", default="masked", choices=["masked", "retrain"])
+    r.add_argument("--counterexamples", default=None)
+    r.add_argument("--method", default="masked", choices=["masked", "retrain", "finetune"])
+    r.add_argument("--data", default=None, help="finetune: synthetic CSV (reference experimentData layout)")
+    r.add_argument("--suite", default=None, choices=["german", "bank"], help="finetune: column spec")
+    r.add_argument("--lr", type=float, default=5e-4)
+    r.add_argument("--max-epochs", type=int, default=100, help="finetune: epochs before early stopping")
     r.add_argument("--out", required=True)
     r.add_argument("--top-k", type=int, default=10)
     r.add_argument("--epochs", type=int, default=5)

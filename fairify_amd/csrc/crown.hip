@@ -24,7 +24,10 @@
 // form's error term -- so sigma * y >= lambda . x + c - err holds for the exact network.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
+#include <map>
 #include <mutex>
 
 #include "args.h"
@@ -216,11 +219,311 @@ __global__ void __launch_bounds__(64 * FA_CROWN_WAVES) fa_crown_kernel(NetDesc n
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// MFMA variant: the back-substitution lambda' = W mu of 16 box-rows at once as GEMMs on
+// v_mfma_f32_16x16x4_f32.  Rows are the 16 MFMA columns; a multiplier vector lives transposed in
+// registers (reg i of tile t = neuron 16t + 4*(lane>>4) + i of row lane&15), so mu is formed
+// elementwise in registers, W is the A operand (staged once per workgroup in LDS in operand order
+// [ot][t][lane][i] = W[16ot + (lane&15)][16t + 4(lane>>4) + i]) and the accumulator tile of
+// layer l IS the lambda of layer l-1 -- no LDS round trip for the vectors and no per-row
+// serial dot products.  Two MFMA chains per sign: W mu and |W| |mu| (the rounding term).  Same
+// relaxation choices and error terms as fa_crown_kernel, with the GEMM error bound taken for
+// 2n+1 terms (the convention of the MFMA symbolic kernel).
+struct CrownCfg {
+  int w_lds[FA_MAX_LAYERS];   // LDS float offset of layer l's operand-order W (backward orientation)
+  int b_lds[FA_MAX_LAYERS];
+  int floats;
+};
+
+template <int TM>
+__global__ void __launch_bounds__(256) fa_crown_mfma_kernel(NetDesc net, BoundArgs a, CrownCfg cfg) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  // ---- stage every layer's W in backward operand order + biases
+  for (int l = 0; l < net.n_layers; ++l) {
+    const int nin = net.dims[l], nout = net.dims[l + 1];
+    const int tin = (nin + 15) >> 4, tout = (nout + 15) >> 4;
+    const float* W = a.flat + net.w_off[l];
+    float* dst = smem + cfg.w_lds[l];
+    const int tot = tin * tout * 256;
+    for (int e = tid; e < tot; e += 256) {
+      const int i4 = e & 3, ln = (e >> 2) & 63, tt = e >> 8;
+      const int t = tt % tout, ot = tt / tout;
+      const int in = 16 * ot + (ln & 15), out = 16 * t + 4 * (ln >> 4) + i4;
+      dst[e] = (in < nin && out < nout) ? W[(size_t)in * nout + out] : 0.f;
+    }
+    for (int e = tid; e < nout; e += 256) smem[cfg.b_lds[l] + e] = a.flat[net.b_off[l] + e];
+  }
+  __syncthreads();
+  const int lane = tid & 63, col = lane & 15, grp = lane >> 4;
+  const int wave = tid >> 6;
+  const int L = net.n_layers;
+  const int n0 = net.dims[0];
+  const int N = net.n_neurons;
+  const float u = net.unit;
+  const int ntile = (a.R + 15) >> 4;
+  for (int tile = blockIdx.x * 4 + wave; tile < ntile; tile += gridDim.x * 4) {
+    const int r0 = tile * 16 + col;
+    const bool valid = r0 < a.R;
+    const int r = valid ? r0 : a.R - 1;
+    const int node = a.V > 0 ? r / a.V : r;
+    const int v = a.V > 0 ? r - node * a.V : 0;
+    const uint8_t* dmask = nullptr;
+    if (a.dead_in) dmask = a.dead_in + (size_t)r * net.n_hidden;
+    else if (a.dead_part) dmask = a.dead_part + (size_t)a.node_part[a.part_mod ? node % a.part_mod : node] * net.n_hidden;
+    const float* lbr = a.layer_lb + (size_t)r * N;
+    const float* ubr = a.layer_ub + (size_t)r * N;
+    float lam[2][TM][4];
+    // ---- init: lambda = +-W_{L-1}[:, 0], c = +-b_{L-1}
+    {
+      const int n = net.dims[L - 1];
+      const float* W = a.flat + net.w_off[L - 1];
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int j = 16 * t + 4 * grp + i;
+          const float w = j < n ? W[j] : 0.f;
+          lam[0][t][i] = w;
+          lam[1][t][i] = -w;
+        }
+    }
+    float c[2], err[2];
+    c[0] = smem[cfg.b_lds[L - 1]];
+    c[1] = -c[0];
+    err[0] = err[1] = 0.f;
+    for (int l = L - 2; l >= 0; --l) {
+      const int n = net.dims[l + 1];
+      const int nin = net.dims[l];
+      const int tout = (n + 15) >> 4, tin = (nin + 15) >> 4;
+      const int off = net.neuron_off[l];
+      const float* b = smem + cfg.b_lds[l];
+      float mu[2][TM][4];
+      float cs[2] = {0.f, 0.f}, cm[2] = {0.f, 0.f}, er[2] = {0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int j = 16 * t + 4 * grp + i;
+          const bool jv = t < tout && j < n;
+          const float lb = jv ? lbr[off + j] : 0.f, ub = jv ? ubr[off + j] : 0.f;
+          const bool dd = !jv || ub <= 0.f || (dmask && dmask[off + j]);
+          const bool act = !dd && lb >= 0.f;
+          const bool unst = !dd && !act;
+          const float alpha = ub > -lb ? 1.f : 0.f;
+          const float sl = unst ? (ub / (ub - lb)) * (1.f + 4.f * u) : 0.f;
+          const float zmax = fmaxf(fabsf(lb), fabsf(ub));
+          const float bj = jv ? b[j] : 0.f;
+#pragma unroll
+          for (int sg = 0; sg < 2; ++sg) {
+            const float lm = lam[sg][t][i];
+            const float slope = act ? 1.f : (dd ? 0.f : (lm >= 0.f ? alpha : sl));
+            const float m = lm * slope;
+            const bool neg = unst && lm < 0.f;
+            const float tt = neg ? -m * lb : 0.f;
+            mu[sg][t][i] = m;
+            cs[sg] += m * bj + tt;
+            cm[sg] += fabsf(m * bj) + fabsf(tt);
+            if (neg) er[sg] += 3.f * u * (fabsf(m) * zmax + fabsf(tt));
+          }
+        }
+      // lambda' = W mu and |W| |mu| (rounding term), both signs
+      const float4* wb = reinterpret_cast<const float4*>(smem + cfg.w_lds[l]);
+      const float gn = fa_gam(2 * n + 1, u);
+#pragma unroll
+      for (int ot = 0; ot < TM; ++ot) {
+        if (ot >= tin) break;
+        f32x4 Z0 = {0.f, 0.f, 0.f, 0.f}, Z1 = Z0, Q0 = Z0, Q1 = Z0;
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+          if (t >= tout) break;
+          const float4 w4 = wb[((size_t)ot * tout + t) * 64 + lane];
+          const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            Z0 = fa_mfma4(wv[i], mu[0][t][i], Z0);
+            Z1 = fa_mfma4(wv[i], mu[1][t][i], Z1);
+            Q0 = fa_mfma4(fabsf(wv[i]), fabsf(mu[0][t][i]), Q0);
+            Q1 = fa_mfma4(fabsf(wv[i]), fabsf(mu[1][t][i]), Q1);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int in = 16 * ot + 4 * grp + i;
+          float hm = 0.f;
+          if (in < nin) {
+            if (l > 0) {
+              const int po = net.neuron_off[l - 1];
+              hm = fmaxf(ubr[po + in], 0.f);
+              if (dmask && dmask[po + in]) hm = 0.f;
+            } else {
+              float xl = a.lo[(size_t)node * n0 + in], xh = a.hi[(size_t)node * n0 + in];
+              if (a.V > 0)
+                for (int k = 0; k < a.npa; ++k)
+                  if (a.pa_idx[k] == in) xl = xh = a.values[v * a.npa + k];
+              hm = fmaxf(fabsf(xl), fabsf(xh));
+            }
+          }
+          lam[0][ot][i] = in < nin ? Z0[i] : 0.f;
+          lam[1][ot][i] = in < nin ? Z1[i] : 0.f;
+          er[0] += gn * Q0[i] * hm;
+          er[1] += gn * Q1[i] * hm;
+        }
+      }
+#pragma unroll
+      for (int ot = 0; ot < TM; ++ot)       // tiles beyond the layer's inputs: zero
+        if (ot >= tin)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lam[0][ot][i] = lam[1][ot][i] = 0.f;
+      const float gc = fa_gam(2 * n + 1, u);
+#pragma unroll
+      for (int sg = 0; sg < 2; ++sg) {
+        // per-row sums over the 4 lane groups holding this row's neurons
+        float csum = cs[sg], cmag = cm[sg], esum = er[sg];
+        csum += __shfl_xor(csum, 16); csum += __shfl_xor(csum, 32);
+        cmag += __shfl_xor(cmag, 16); cmag += __shfl_xor(cmag, 32);
+        esum += __shfl_xor(esum, 16); esum += __shfl_xor(esum, 32);
+        const float cold = c[sg];
+        c[sg] = cold + csum;
+        err[sg] += esum + gc * (fabsf(cold) + cmag);
+      }
+    }
+    // ---- concretise over the input box
+    int K = 4 * L + 4;
+    for (int l = 0; l < L; ++l) K += 2 * net.dims[l + 1];
+    const float gK = fa_gam(K, u);
+    const float g0 = fa_gam(n0 + 1, u);
+    const float g1 = fa_gam(1, u);
+    float low[2];
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) {
+      float cp = 0.f, mp = 0.f;
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int in = 16 * t + 4 * grp + i;
+          if (in >= n0) continue;
+          float xl = a.lo[(size_t)node * n0 + in], xh = a.hi[(size_t)node * n0 + in];
+          if (a.V > 0)
+            for (int k = 0; k < a.npa; ++k)
+              if (a.pa_idx[k] == in) xl = xh = a.values[v * a.npa + k];
+          const float lm = lam[sg][t][i];
+          cp += fminf(lm * xl, lm * xh);
+          mp += fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
+        }
+      cp += __shfl_xor(cp, 16); cp += __shfl_xor(cp, 32);
+      mp += __shfl_xor(mp, 16); mp += __shfl_xor(mp, 32);
+      const float conc = cp + c[sg];
+      const float cmg = mp + fabsf(c[sg]);
+      err[sg] *= 1.f + 2.f * gK;
+      low[sg] = conc - err[sg] - g0 * cmg - g1 * fabsf(conc);
+    }
+    if (valid) {
+      const float olb = a.out_lb[r], oub = a.out_ub[r];
+      const bool useL = low[0] >= olb;
+      const bool useU = -low[1] <= oub;
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int in = 16 * t + 4 * grp + i;
+          if (in >= n0) continue;
+          if (useL) a.Lc[(size_t)r * n0 + in] = lam[0][t][i];
+          if (useU) a.Uc[(size_t)r * n0 + in] = -lam[1][t][i];
+        }
+      if (grp == 0) {
+        if (useL) { a.L0[r] = c[0]; a.Le[r] = err[0]; a.out_lb[r] = low[0]; }
+        if (useU) { a.U0[r] = -c[1]; a.Ue[r] = err[1]; a.out_ub[r] = -low[1]; }
+      }
+    }
+  }
+}
+
+namespace {
+typedef void (*CrownMfmaKernel)(NetDesc, BoundArgs, CrownCfg);
+CrownMfmaKernel select_crown_mfma(int TM) {
+  if (TM <= 1) return fa_crown_mfma_kernel<1>;
+  if (TM <= 2) return fa_crown_mfma_kernel<2>;
+  if (TM <= 4) return fa_crown_mfma_kernel<4>;
+  if (TM <= 7) return fa_crown_mfma_kernel<7>;
+  return nullptr;
+}
+
+int crown_cus() {
+  static int cus = 0;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  });
+  return cus;
+}
+
+// 1 launched, 0 shape not supported by the MFMA variant, < 0 error
+int crown_mfma_try(const NetDesc& net, const BoundArgs& a, hipStream_t stream) {
+  static const bool off = [] {
+    const char* e = getenv("FAIRIFY_CROWN_MFMA");
+    return e && e[0] == '0';
+  }();
+  if (off) return 0;
+  int TM = 1;
+  for (int l = 0; l <= net.n_layers; ++l) TM = std::max(TM, (net.dims[l] + 15) / 16);
+  CrownMfmaKernel k = select_crown_mfma(TM);
+  if (!k) return 0;
+  CrownCfg cfg{};
+  int offs = 0;
+  for (int l = 0; l < net.n_layers; ++l) {
+    cfg.w_lds[l] = offs;
+    offs += ((net.dims[l] + 15) / 16) * ((net.dims[l + 1] + 15) / 16) * 256;
+  }
+  for (int l = 0; l < net.n_layers; ++l) {
+    cfg.b_lds[l] = offs;
+    offs += net.dims[l + 1];
+  }
+  cfg.floats = (offs + 3) & ~3;
+  const size_t bytes = (size_t)cfg.floats * sizeof(float);
+  if (bytes > 150 * 1024) return 0;
+  static std::mutex mu;
+  static std::map<std::pair<const void*, size_t>, int> occ;
+  int per_cu = 0;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    const auto key = std::make_pair((const void*)k, bytes);
+    auto it = occ.find(key);
+    if (it == occ.end()) {
+      if (bytes > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return -(int)e;
+      }
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, bytes) != hipSuccess || per_cu <= 0) per_cu = 1;
+      occ[key] = per_cu;
+    } else {
+      per_cu = it->second;
+    }
+  }
+  const long long tiles = (a.R + 15) / 16;
+  long long blocks = (tiles + 3) / 4;
+  const long long cap = (long long)crown_cus() * per_cu;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), bytes, stream, net, a, cfg);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 1 : -(int)e;
+}
+}  // namespace
+
 // 0 on success; -1 if the network does not fit (a layer wider than FA_CROWN_MAXW or weights
 // beyond the LDS budget) -- callers then keep the forward forms.
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream) {
   if (a.R <= 0) return 0;
   if (!a.layer_lb || !a.layer_ub || !a.Lc || !a.Uc) return -2;
+  {
+    const int rc = crown_mfma_try(net, a, stream);
+    if (rc == 1) return 0;
+    if (rc < 0) return -3;
+  }
   int wmax = 1;
   for (int l = 0; l <= net.n_layers; ++l) {
     if (net.dims[l] > FA_CROWN_MAXW) return -1;

@@ -23,9 +23,56 @@ import torch
 from ..models.mlp import MLP
 
 
-def load_pairs(path: str, n_features: int, pa_index: int) -> Tuple[np.ndarray, np.ndarray]:
-    """Counterexample pairs from a CSV of encoded rows (x, x' consecutive; optional label col)
-    or from a ``*.npz`` with arrays ``x``, ``xp`` (and optional ``y``)."""
+LABEL_COLUMNS = ("decision", "income-per-year", "prediction", "credit", "y")
+
+
+def reencode_decoded(df, suite: str):
+    """Decoded counterexample rows (category strings, any column order; the fork's
+    ``counterexamples-<model>.csv``) -> encoded feature matrix in the domain's order + labels.
+
+    ``src/AC/detect_bias.py:140-167``: drop NaN rows, ``encoders[f].transform`` for every
+    categorical feature (and race), the KBins transform for capital-gain / capital-loss, label
+    column ``decision``.  The reference then feeds the CSV's own (alphabetical) column order to
+    the network; here columns are put into the dataset's feature order (documented difference).
+    Rows whose categories the training encoders do not know are dropped pairwise."""
+    import pandas as pd
+
+    from ..data import tabular
+
+    ds = tabular.load(suite, allow_synthetic=False)
+    enc = ds.encoders
+    names = list(ds.columns)
+    df = df.dropna().reset_index(drop=True)
+    lab = next((c for c in LABEL_COLUMNS if c in df.columns), None)
+    y = df[lab].to_numpy().astype(int) if lab else None
+    X = np.zeros((len(df), len(names)), dtype=np.float64)
+    ok = np.ones(len(df), dtype=bool)
+    for j, name in enumerate(names):
+        col = df[name]
+        e = enc.get(name)
+        if e is not None and hasattr(e, "classes_") and col.dtype == object:
+            known = np.isin(col.to_numpy(), e.classes_)
+            ok &= known
+            vals = np.zeros(len(df))
+            if known.any():
+                vals[known] = e.transform(col[known])
+            X[:, j] = vals
+        elif e is not None and hasattr(e, "bin_edges_"):
+            X[:, j] = e.transform(pd.DataFrame({name: pd.to_numeric(col)}))[:, 0]
+        else:
+            X[:, j] = pd.to_numeric(col, errors="coerce").to_numpy()
+    ok &= ~np.isnan(X).any(axis=1)
+    n2 = len(ok) // 2 * 2
+    pair_ok = np.zeros(len(ok), dtype=bool)
+    pair_ok[:n2] = ok[:n2].reshape(-1, 2).all(axis=1).repeat(2)
+    return X[pair_ok], (y[pair_ok] if y is not None else None)
+
+
+def load_pairs(path: str, n_features: int, pa_index: int, suite: Optional[str] = None
+               ) -> Tuple[np.ndarray, np.ndarray]:
+    """Counterexample pairs from a CSV of encoded rows (x, x' consecutive; optional label col),
+    a CSV of DECODED rows (category strings: re-encoded with the suite's training encoders, see
+    :func:`reencode_decoded`), or a ``*.npz`` with arrays ``x``, ``xp`` (and optional ``y``)."""
     if path.endswith(".npz"):
         z = np.load(path, allow_pickle=False)
         X = np.stack([z["x"], z["xp"]], axis=1).reshape(-1, n_features)
@@ -34,6 +81,8 @@ def load_pairs(path: str, n_features: int, pa_index: int) -> Tuple[np.ndarray, n
     import pandas as pd
 
     df = pd.read_csv(path)
+    if suite is not None and (df.dtypes == object).any():
+        return reencode_decoded(df, suite)
     num = df.select_dtypes(include=[np.number])
     if num.shape[1] >= n_features + 1:
         X = num.iloc[:, :n_features].to_numpy(dtype=np.float64)
@@ -160,7 +209,7 @@ def repair_model(model: str, counterexamples: str, method: str = "masked", out: 
     pre = next(p for p in PRESETS.values() if p.suite == suite and model in p.models)
     q = pre.resolved()
     pa = q.pa_idx[0]
-    X, y = load_pairs(counterexamples, mlp.n_in, pa)
+    X, y = load_pairs(counterexamples, mlp.n_in, pa, suite=suite)
     if y is None:
         y = mlp.predict(X)
     ds = tabular.load(suite, seed=seed, mlp=mlp)

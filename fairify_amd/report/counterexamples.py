@@ -4,7 +4,9 @@ Reference: ``decode_counterexample`` + ``counterexample.csv`` writers of the for
 (src/AC/Verify-AC-experiment-new2.py:344-407, src/GC/...-new2.py:318-467,
 src/BM/...-new2.py:343-404): encoded integers are mapped back to category strings with the
 training LabelEncoders, KBins bins to their midpoints, and each row gets the model output
-(sigmoid) and the predicted class.  Rows that cannot be decoded (codes outside the encoder's
+(sigmoid) and the predicted class; German rows are mapped back to the raw dataset's A-codes
+(sex A91/A92 and the grouped categories, src/GC/Verify-GC-experiment-new2.py:364-414).  Rows
+that cannot be decoded (codes outside the encoder's
 classes) are dropped, like the reference's BM variant.  An ``.npz`` with the raw pairs is
 written next to it (input of ``repair``).
 """
@@ -34,6 +36,29 @@ def _decode_column(vals: np.ndarray, enc) -> Optional[np.ndarray]:
     return vals
 
 
+# German Credit: the fork maps the grouped categories and sex back to the dataset's A-codes
+# (src/GC/Verify-GC-experiment-new2.py:364-414); the class column is called "decision" there
+GC_REVERSE = {
+    "credit_history": {"None/Paid": "A30", "Delay": "A33", "Other": "A34"},
+    "savings": {"<500": "A61", "500+": "A63", "Unknown/None": "A65"},
+    "employment": {"Unemployed": "A71", "1-4 years": "A72", "4+ years": "A74"},
+    "status": {"<200": "A11", "200+": "A13", "None": "A14"},
+}
+
+
+def gc_reverse_map(df: pd.DataFrame) -> pd.DataFrame:
+    """Decoded German rows -> the raw dataset's codes: sex 1 -> A91 (male), 0 -> A92 (female),
+    grouped categories -> one representative A-code each (the reference's choice)."""
+    out = df.copy()
+    if "sex" in out.columns:
+        sx = pd.to_numeric(out["sex"], errors="coerce")
+        out["sex"] = np.where(sx == 1, "A91", np.where(sx == 0, "A92", out["sex"].astype(object)))
+    for col, mp in GC_REVERSE.items():
+        if col in out.columns:
+            out[col] = out[col].map(lambda v, mp=mp: mp.get(v, v))
+    return out
+
+
 def export_counterexamples(preset: str, model: str, results: str, out: Optional[str] = None,
                            weights: str = "zoo") -> str:
     from .. import presets
@@ -59,10 +84,13 @@ def export_counterexamples(preset: str, model: str, results: str, out: Optional[
     z = mlp.logits(pairs)
     out_df = pd.DataFrame({name: _decode_column(pairs[:, i], enc.get(name)) for i, name in enumerate(dom.names)})
     out_df["output"] = 0.5 * (1 + np.tanh(0.5 * z))
-    out_df["prediction"] = (z > 0).astype(int)
+    label_col = "decision" if pre.suite == "german" else "prediction"
+    out_df[label_col] = (z > 0).astype(int)
     keep = ~out_df[dom.names].isna().any(axis=1).to_numpy()
     keep = keep.reshape(-1, 2).all(axis=1).repeat(2)
     out_df = out_df[keep]
+    if pre.suite == "german":
+        out_df = gc_reverse_map(out_df)
     out = out or os.path.join(results, f"{model}-counterexample.csv")
     out_df.to_csv(out, index=False)
     np.savez(os.path.splitext(out)[0] + ".npz", x=X, xp=XP, y=np.maximum(z[0::2] > 0, z[1::2] > 0).astype(int))
