@@ -62,7 +62,8 @@ def cmd_verify(args):
                max_partitions=args.max_partitions, resume=args.resume, seed=args.seed,
                accuracy=not args.no_accuracy, escalate=args.escalate,
                concurrency=args.concurrency or (4 if info.device.type == "cuda" else 1),
-               anytime_budget=(args.anytime_budget or cfg.hard_timeout) if args.anytime else None)
+               anytime_budget=(args.anytime_budget or cfg.hard_timeout) if args.anytime else None,
+               metrics_csv=True if args.metrics_csv else None)
     D.destroy(info)
 
 
@@ -192,6 +193,9 @@ def main(argv=None):
                         "growing sound BaB budgets and falsifier rounds over the UNKNOWN residue")
     v.add_argument("--anytime-budget", type=float, default=None, help="seconds per model for --anytime")
     v.add_argument("--residual-samples", type=int, default=None)
+    v.add_argument("--metrics-csv", action="store_true",
+                   help="also write the per-partition metrics CSV of the experiment drivers "
+                        "(on by default for experiment/* presets)")
     v.add_argument("--no-accuracy", action="store_true")
     v.add_argument("--device", default=None)
     v.set_defaults(fn=cmd_verify)

@@ -13,10 +13,11 @@
 //                        layer, means / NumPy-'linear' percentiles of the candidates' and the
 //                        non-candidates' IBP upper bounds (fp64, ranks by counting in LDS), harsh
 //                        outliers marked dead, merged with the sound masks, one alive per layer.
-// fa_agree_kernel        one workgroup per heuristically pruned partition: Pruned-acc = sign
-//                        agreement of the full and the pruned network on the partition's
-//                        simulation points (same counter-hash stream), register-resident MFMA
-//                        forward (csrc/regfwd.h) with the dead mask staged in LDS.
+// fa_agree_kernel        one workgroup per partition: Pruned-acc = sign agreement of the full and
+//                        the pruned network on the partition's simulation points (same
+//                        counter-hash stream), plus the true / false positives of the pruned
+//                        labels against the original's (Pruned F1 of the experiment drivers),
+//                        register-resident MFMA forward (csrc/regfwd.h), dead mask in LDS.
 #include <hip/hip_runtime.h>
 
 #include "regfwd.h"
@@ -195,7 +196,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_agree_kernel(NetDesc net, RegNe
   for (int i = tid; i < Nh; i += FA_THREADS) dm[i] = dead[(size_t)k * Nh + i];
   if (tid < 4) acc[tid] = 0;
   __syncthreads();
-  int mine = 0;
+  int mine = 0, tp = 0, fp = 0;
   float HA[TM][4], HB[TM][4], X[TM][4];
   for (int s0 = wave * 16; s0 < S; s0 += 64) {
     const int s = s0 + col;
@@ -219,11 +220,17 @@ __global__ void __launch_bounds__(FA_THREADS) fa_agree_kernel(NetDesc net, RegNe
 #pragma unroll
       for (int i = 0; i < 4; ++i) HA[t][i] = X[t][i];
     const float z1 = fa_reg_forward<TM>(net, cfg, smem, lane, HA, HB, dm);
-    if (grp == 0 && sv) mine += ((z0 > 0.f) == (z1 > 0.f)) ? 1 : 0;
+    if (grp == 0 && sv) {
+      mine += ((z0 > 0.f) == (z1 > 0.f)) ? 1 : 0;
+      tp += (z0 > 0.f && z1 > 0.f) ? 1 : 0;       // F1 of the pruned labels against the original's
+      fp += (z0 <= 0.f && z1 > 0.f) ? 1 : 0;
+    }
   }
   atomicAdd(&acc[0], mine);
+  atomicAdd(&acc[1], tp);
+  atomicAdd(&acc[2], fp);
   __syncthreads();
-  if (tid == 0) agree[k] = acc[0];
+  if (tid < 3) agree[3 * k + tid] = acc[tid];
 }
 
 namespace {

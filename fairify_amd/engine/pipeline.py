@@ -71,6 +71,8 @@ class VerifyConfig:
     # empty or this chunk's share of the model's wall budget is spent (the reference spends up to
     # its hard timeout per model, src/AC/Verify-AC.py:318-320).  0 = off.
     anytime_seconds: float = 0.0
+    pruned_metrics: bool = False         # Pruned-F1 counts for every partition (the experiment
+                                         # drivers' per-partition metrics CSV)
     anytime_growth: int = 4
     anytime_max_budget: int = 1 << 22
     anytime_pool: int = 1 << 24          # live BaB nodes per group: group size = pool / budget
@@ -573,16 +575,25 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             c2 = (zp[sat_idx.size:] > 0).astype(np.int64)
             c_check[sat_idx] = ((c1 == xo) & (c2 == xpo)).astype(np.int64)
         agree = np.full(Pn, cfg.sim_size, dtype=np.int64)     # Pruned-acc numerator
-        if masked:
-            hp = np.array(sorted(masked))
-            dm = torch.from_numpy(np.stack([masked[p][:Nh] for p in hp]).astype(np.uint8)).to(dev)
+        tp = np.zeros(Pn, dtype=np.int64)                      # Pruned-F1 counts (pruned_metrics)
+        fp = np.zeros(Pn, dtype=np.int64)
+        if masked or cfg.pruned_metrics:
+            # pruned_metrics: every partition (unmasked ones with their sound-pruned net, which
+            # equals the original on the box: mask of zeros) for the experiment drivers' F1
+            hp = np.arange(Pn) if cfg.pruned_metrics else np.array(sorted(masked))
+            dm_np = np.zeros((hp.size, Nh), dtype=np.uint8)
+            for k, p in enumerate(hp):
+                if p in masked:
+                    dm_np[k] = masked[p][:Nh]
+            dm = torch.from_numpy(dm_np).to(dev)
             ag = None
             if be.hip and os.environ.get("FAIRIFY_FUSED_PRUNE", "1") != "0":
                 from ..ops import hip as H
 
                 ag = H.agree(be, torch.from_numpy(hp).to(dev), lo, hi, pids, dm, cfg.sim_size, cfg.seed)
             if ag is not None:
-                agree[hp] = ag.cpu().numpy()
+                ag_np = ag.cpu().numpy().astype(np.int64)
+                agree[hp], tp[hp], fp[hp] = ag_np[:, 0], ag_np[:, 1], ag_np[:, 2]
             else:
                 from ..ops.reference import sample_points
 
@@ -590,6 +601,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                 z0 = be.forward(X)
                 z1 = be.forward(X, dm.bool()[:, None, :].expand(-1, X.shape[1], -1))
                 agree[hp] = ((z0 > 0) == (z1 > 0)).sum(dim=1).cpu().numpy()
+                tp[hp] = ((z0 > 0) & (z1 > 0)).sum(dim=1).cpu().numpy()
+                fp[hp] = ((z0 <= 0) & (z1 > 0)).sum(dim=1).cpu().numpy()
     t_replay = time.time() - t0
 
     # ---------------- records: dead-neuron counts, work, per-chunk stage times (the per-partition
@@ -599,7 +612,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     core = dict(
         grid_id=np.asarray(ids, dtype=np.int64), verdict=verdict, stage=stage_f.astype(object),
         h_attempt=h_attempt, h_success=h_success,
-        b_cnt=b_cnt, s_cnt=s_cnt, st_cnt=st_cnt, h_cnt=h_cnt, t_cnt=t_cnt, agree=agree, nodes=nodes.astype(np.int64),
+        b_cnt=b_cnt, s_cnt=s_cnt, st_cnt=st_cnt, h_cnt=h_cnt, t_cnt=t_cnt, agree=agree, tp=tp, fp=fp, nodes=nodes.astype(np.int64),
         c_check=c_check, v_accurate=v_acc, cex_x=cex_x, cex_xp=cex_xp)
     return core, (Pn, t_sim + t_prune + t_bab, t_bab, t_heur, t_replay)
 
@@ -658,7 +671,7 @@ def concat_records(parts: Sequence["ChunkRecords"]) -> "ChunkRecords":
 
 
 CORE_COLUMNS = ("grid_id", "verdict", "stage", "h_attempt", "h_success", "b_cnt", "s_cnt", "st_cnt", "h_cnt",
-                "t_cnt", "agree", "nodes", "c_check", "v_accurate", "cex_x", "cex_xp")
+                "t_cnt", "agree", "tp", "fp", "nodes", "c_check", "v_accurate", "cex_x", "cex_xp")
 
 
 def derive_columns(core: Dict[str, np.ndarray], segments, n_neurons: int, sim_size: int) -> Dict[str, np.ndarray]:
@@ -678,6 +691,13 @@ def derive_columns(core: Dict[str, np.ndarray], segments, n_neurons: int, sim_si
     out["h_comp"] = np.where(h, core["h_cnt"] / N, 0.0)
     out["t_comp"] = core["t_cnt"] / N
     out["pruned_acc"] = core["agree"] / float(max(1, sim_size))
+    # F1 of the pruned net's labels against the original's on the simulation points (sklearn
+    # f1_score(sim_y_orig, sim_y), zero_division -> 0): fn = S - agree - fp
+    if "tp" in core:
+        tp_, fp_ = core["tp"].astype(np.float64), core["fp"].astype(np.float64)
+        fn_ = float(sim_size) - core["agree"] - fp_
+        den = 2 * tp_ + fp_ + fn_
+        out["pruned_f1"] = np.where(den > 0, 2 * tp_ / np.maximum(den, 1), 0.0)
     n = len(core["verdict"])
     s_t, sv_t, hv_t, rp_t = (np.zeros(n) for _ in range(4))
     off = 0
@@ -706,7 +726,7 @@ class ChunkRecords(Sequence):
     like a list of per-partition dicts (the CSV/runner view, built lazily per row)."""
 
     _INT = ("grid_id", "h_attempt", "h_success", "c_check", "v_accurate", "nodes")
-    _HIDE = ("cex_x", "cex_xp", "b_cnt", "s_cnt", "st_cnt", "h_cnt", "t_cnt", "agree")
+    _HIDE = ("cex_x", "cex_xp", "b_cnt", "s_cnt", "st_cnt", "h_cnt", "t_cnt", "agree", "tp", "fp", "pruned_f1")
 
     def __init__(self, core: Dict[str, np.ndarray], orig_acc: Optional[float] = None, segments=None,
                  n_neurons: int = 1, sim_size: int = 1):

@@ -184,18 +184,61 @@ def _replace(pos: np.ndarray, recs, new_pos: np.ndarray, new_recs) -> None:
         recs.cols[k][idx] = v
 
 
+class _MetricsCSV:
+    """Per-partition metrics CSV of the fork's experiment drivers: one row per verified
+    partition with the model's test-set accuracy / F1 and AIF360 group metrics (model-level,
+    computed once) and the partition's Pruned accuracy / F1 on its simulation points."""
+
+    COLS = ["Partition ID", "Original Accuracy", "Original F1 Score", "Pruned Accuracy", "Pruned F1", "DI", "SPD",
+            "EOD", "AOD", "ERD", "CNT", "TI"]
+
+    def __init__(self, out_dir: str, preset: Preset, mlp, seed: int, resume: bool):
+        import csv
+
+        from ..analysis.metrics import all_metrics
+        from ..data import tabular
+
+        ds = tabular.load(preset.suite, seed=seed, mlp=mlp)
+        m = all_metrics(ds.X_test, ds.y_test, mlp.predict(ds.X_test), preset.resolved().pa_idx[0])
+        self.model_vals = [m["accuracy"], m["f1"]]
+        self.group_vals = [m[k] for k in ("DI", "SPD", "EOD", "AOD", "ERD", "CNT", "TI")]
+        self.synthetic = bool(getattr(ds, "synthetic", False))
+        family = mlp.name.split("-")[0]
+        self.path = os.path.join(out_dir, f"synthetic-{preset.suite}-predicted-{family}-metrics.csv")
+        os.makedirs(out_dir, exist_ok=True)
+        exists = resume and os.path.exists(self.path)
+        self.fp = open(self.path, "a" if exists else "w", newline="")
+        self.wr = csv.writer(self.fp, dialect="excel")
+        if not exists:
+            self.wr.writerow(self.COLS)
+
+    def write(self, positions: np.ndarray, recs) -> None:
+        c = recs.cols
+        for k, pos in enumerate(positions):
+            self.wr.writerow([int(pos) + 1] + self.model_vals + [float(c["pruned_acc"][k]), float(c["pruned_f1"][k])]
+                             + self.group_vals)
+        self.fp.flush()
+
+    def close(self) -> None:
+        self.fp.close()
+
+
 def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str = "zoo", out_dir: str = "results",
                cfg: Optional[VerifyConfig] = None, info: Optional[D.DistInfo] = None,
                max_partitions: Optional[int] = None, resume: bool = False, seed: int = 0,
                accuracy: bool = True, verbose: bool = True, escalate: int = 1,
-               concurrency: int = 1, anytime_budget: Optional[float] = None) -> List[Dict]:
+               concurrency: int = 1, anytime_budget: Optional[float] = None,
+               metrics_csv: Optional[bool] = None) -> List[Dict]:
     """``escalate`` > 1: every round's UNKNOWN partitions are re-distributed over all ranks and
     retried with ``escalate`` x the node budget (residual work stealing).  ``concurrency`` > 1:
     each rank verifies that many chunks of a round at once, one host thread + HIP stream each
     (a round is then ``chunk x concurrency`` partitions per rank).  ``anytime_budget`` (seconds
     per model, e.g. the preset's hard timeout): every round gets the share of the model's
     remaining budget proportional to its partitions and spends it on deeper sound BaB passes and
-    falsifier rounds over its UNKNOWN residue (VerifyConfig.anytime_seconds)."""
+    falsifier rounds over its UNKNOWN residue (VerifyConfig.anytime_seconds).  ``metrics_csv``
+    (default: on for the fork's ``experiment/*`` presets): rank 0 also writes the per-partition
+    ``synthetic-<dataset>-predicted-<family>-metrics.csv`` of the experiment drivers
+    (src/AC/Verify-AC-experiment-new.py:482-542)."""
     info = info or D.DistInfo()
     grid = preset.grid(seed=seed)
     q = preset.resolved()
@@ -204,6 +247,10 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
     cfg = cfg or VerifyConfig(sim_size=preset.sim_size, soft_timeout=preset.soft_timeout,
                               hard_timeout=preset.hard_timeout, heuristic_p=preset.heuristic_p, seed=seed)
     n0 = q.n
+    if metrics_csv is None:
+        metrics_csv = preset.name.startswith("experiment/")
+    if metrics_csv:
+        cfg = replace(cfg, pruned_metrics=True)
     rows_out: List[Dict] = []
     streams = StreamPool(info.device, concurrency)
     pa_name = ",".join(a for a in preset.query.pa if preset.domain().has(a))
@@ -219,6 +266,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         todo = np.nonzero(~done)[0]
         mine = todo[info.rank::info.world]
         writer = PartitionCSV(csv_path, resume=resume) if info.is_main else None
+        mwriter = _MetricsCSV(out_dir, preset, mlp, seed, resume) if (metrics_csv and info.is_main) else None
         # rank 0 formats/writes round r (native formatter, GIL released) and checkpoints it on a
         # background thread while round r+1's chunks drive the GPU; one worker keeps the order
         io = ThreadPoolExecutor(max_workers=1) if info.is_main else None
@@ -246,6 +294,8 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                 _replace(gpos, grecs, *retried)
             rows = pack(grecs, gpos, n0)
             cols = columns(rows, n0)
+            if mwriter is not None:
+                mwriter.write(gpos, grecs)
             for k in _TABLE_COLS:
                 table_cols[k].append(cols[k])
             wire_bytes[0] += sum(len(b) for b in bufs)
@@ -306,6 +356,8 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             f.result()
         if io is not None:
             io.shutdown(wait=True)
+        if mwriter is not None:
+            mwriter.close()
         wall = D.all_reduce_max(info, time.time() - t0)
         if info.is_main:
             tc = {k: (np.concatenate(v) if v else np.zeros(0)) for k, v in table_cols.items()}

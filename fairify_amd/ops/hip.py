@@ -391,9 +391,11 @@ def heuristic(be, rows: torch.Tensor, lay_lb: torch.Tensor, lay_ub: torch.Tensor
 
 def agree(be, rows: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor, pids: torch.Tensor, dead: torch.Tensor,
           n_samples: int, seed: int):
-    """Pruned-acc numerators: per partition ``rows[k]``, how many of its ``n_samples`` simulation
-    points get the same sign from the full network and the network with ``dead[k]`` [N_hidden]
-    forced to zero.  Returns int32 [Pm] or ``None`` (shape unsupported: caller keeps PyTorch)."""
+    """Pruned-acc / Pruned-F1 counts: per partition ``rows[k]``, over its ``n_samples``
+    simulation points, (points where the full network and the network with ``dead[k]``
+    [N_hidden] forced to zero agree in sign, points positive for both, points positive only for
+    the pruned network).  Returns int32 [Pm, 3] or ``None`` (shape unsupported: caller keeps
+    PyTorch)."""
     Pm = rows.shape[0]
     P, n0 = lo.shape
     dev = lo.device
@@ -402,7 +404,7 @@ def agree(be, rows: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor, pids: torc
     hi_c = _c(hi, torch.float32, (P, n0), "hi")
     pids_c = _c(pids, torch.int64, (P,), "pids")
     dead_c = _c(dead, torch.uint8, (Pm, be.n_hidden), "dead")
-    out = torch.zeros(Pm, dtype=torch.int32, device=dev)
+    out = torch.zeros(Pm, 3, dtype=torch.int32, device=dev)
     if Pm == 0:
         return out
     ok = ext().agree(_net(be), be.flat.data_ptr(), Pm, rows_c.data_ptr(), lo_c.data_ptr(), hi_c.data_ptr(),

@@ -7,9 +7,10 @@ to every rank.  Here a rank ships, per round, one byte buffer:
 * segments      float64 [S, 5]: per verified chunk (count, t_sim+prune+bab, t_bab, t_heur,
                 t_replay) -- the per-partition time columns are apportioned from these on
                 rank 0 by :func:`engine.pipeline.derive_columns`, exactly as the producer would;
-* records       18 B each (``REC``): flags (verdict 2 b | stage 3 b | h_attempt | h_success |
+* records       22 B each (``REC``): flags (verdict 2 b | stage 3 b | h_attempt | h_success |
                 c_check | v_accurate), dead-neuron counts b/s/st/h/t (uint16), Pruned-acc
-                numerator (uint16), BaB node expansions (uint32);
+                numerator and the Pruned-F1 true / false positives (uint16), BaB node
+                expansions (uint32);
 * counterexamples, SAT partitions only: x [n0] and x' on the protected/relaxed dims only (every
                 other dim of a confirmed pair equals x), int16 when the query domain (widened
                 by tau) fits, else int32 -- 28 B per SAT pair for Adult.
@@ -29,8 +30,8 @@ from ..engine.pipeline import ChunkRecords
 VERDICTS = ("unknown", "sat", "unsat")
 STAGES = ("", "sim", "bab", "heuristic", "smt", "falsify", "milp")
 REC = np.dtype([("flags", "<u2"), ("b", "<u2"), ("s", "<u2"), ("st", "<u2"), ("h", "<u2"), ("t", "<u2"),
-                ("agree", "<u2"), ("nodes", "<u4")])
-assert REC.itemsize == 18
+                ("agree", "<u2"), ("tp", "<u2"), ("fp", "<u2"), ("nodes", "<u4")])
+assert REC.itemsize == 22
 
 
 def verdict_codes(recs: ChunkRecords) -> np.ndarray:
@@ -51,7 +52,10 @@ def encode(recs: ChunkRecords, q) -> np.ndarray:
     n0 = q.n
     c = recs.core
     n = len(c["verdict"])
-    for k in ("b_cnt", "s_cnt", "st_cnt", "h_cnt", "t_cnt", "agree"):
+    c = dict(c)
+    for k in ("tp", "fp"):                       # older producers: no Pruned-F1 counts
+        c.setdefault(k, np.zeros(n, dtype=np.int64))
+    for k in ("b_cnt", "s_cnt", "st_cnt", "h_cnt", "t_cnt", "agree", "tp", "fp"):
         if n and int(np.max(c[k])) > 0xFFFF:
             raise OverflowError(f"{k} exceeds 16 bits")
     stage = np.array([STAGES.index(s) if s in STAGES else 0 for s in c["stage"]], dtype=np.uint16)
@@ -62,6 +66,7 @@ def encode(recs: ChunkRecords, q) -> np.ndarray:
     rec["flags"] = flags
     rec["b"], rec["s"], rec["st"] = c["b_cnt"], c["s_cnt"], c["st_cnt"]
     rec["h"], rec["t"], rec["agree"] = c["h_cnt"], c["t_cnt"], c["agree"]
+    rec["tp"], rec["fp"] = c["tp"], c["fp"]
     rec["nodes"] = np.minimum(c["nodes"], 0xFFFFFFFF)
     sat = c["verdict"] == "sat"
     dims, dt = _cex_layout(q)
@@ -100,6 +105,7 @@ def decode(buf: np.ndarray, grid_ids: np.ndarray, orig_acc, n_neurons: int, sim_
                 h_attempt=(f >> 5) & 1, h_success=(f >> 6) & 1,
                 b_cnt=rec["b"].astype(np.int64), s_cnt=rec["s"].astype(np.int64), st_cnt=rec["st"].astype(np.int64),
                 h_cnt=rec["h"].astype(np.int64), t_cnt=rec["t"].astype(np.int64), agree=rec["agree"].astype(np.int64),
+                tp=rec["tp"].astype(np.int64), fp=rec["fp"].astype(np.int64),
                 nodes=rec["nodes"].astype(np.int64), c_check=(f >> 7) & 1, v_accurate=(f >> 8) & 1,
                 cex_x=cx, cex_xp=cxp)
     return ChunkRecords(core, orig_acc, segments=[tuple(s) for s in segs.tolist()], n_neurons=n_neurons,

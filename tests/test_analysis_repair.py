@@ -124,3 +124,21 @@ def test_ac3_group_metrics_pinned_to_reference_log():
         assert round(r[k], 3) == v, (k, r[k])
     assert round(r["CNT"], 4) == 0.8890
     assert round(consistency(ds.X_test, yp, method="gemm"), 4) == 0.8886    # index tie-breaking
+
+
+def test_experiment_metrics_csv(tmp_path):
+    """experiment/* presets write synthetic-<ds>-predicted-<family>-metrics.csv with one row per
+    partition (src/AC/Verify-AC-experiment-new.py:482-542); Pruned F1 from the agreement counts."""
+    import csv
+
+    out = str(tmp_path)
+    run_preset(presets.get("experiment/GC-1"), out_dir=out, accuracy=False, verbose=False,
+               cfg=VerifyConfig(sim_size=200, node_budget=256, smt_backend="none"), max_partitions=16, weights="zoo")
+    rows = list(csv.reader(open(os.path.join(out, "synthetic-german-predicted-GC-metrics.csv"))))
+    assert rows[0] == ["Partition ID", "Original Accuracy", "Original F1 Score", "Pruned Accuracy", "Pruned F1",
+                       "DI", "SPD", "EOD", "AOD", "ERD", "CNT", "TI"]
+    assert len(rows) == 17 and [int(r[0]) for r in rows[1:]] == list(range(1, 17))
+    for r in rows[1:]:
+        acc, f1 = float(r[3]), float(r[4])
+        assert 0.0 <= acc <= 1.0 and 0.0 <= f1 <= 1.0
+        assert r[1] == rows[1][1] and r[5:] == rows[1][5:]          # model-level columns

@@ -189,7 +189,7 @@ def test_wire_roundtrip_and_size():
                 h_attempt=rng.integers(0, 2, n), h_success=rng.integers(0, 2, n),
                 b_cnt=rng.integers(0, N, n), s_cnt=rng.integers(0, N, n), st_cnt=rng.integers(0, N, n),
                 h_cnt=rng.integers(0, N, n), t_cnt=rng.integers(0, N, n), agree=rng.integers(0, S + 1, n),
-                nodes=rng.integers(0, 1 << 20, n), c_check=rng.integers(0, 2, n), v_accurate=rng.integers(0, 2, n),
+                tp=rng.integers(0, S // 2, n), fp=rng.integers(0, S // 4, n), nodes=rng.integers(0, 1 << 20, n), c_check=rng.integers(0, 2, n), v_accurate=rng.integers(0, 2, n),
                 cex_x=cx, cex_xp=cxp)
     recs = ChunkRecords(core, 0.8, segments=[(1000, 1.0, 0.5, 0.1, 0.01), (n - 1000, 2.0, 1.5, 0.0, 0.02)],
                         n_neurons=N, sim_size=S)

@@ -93,6 +93,12 @@ def test_agree_kernel_within_rounding(cuda, hidden):
     sure = (s0 != 0) & (s1 != 0)
     lo_cnt = (sure & (s0 == s1)).sum(1)
     hi_cnt = lo_cnt + (~sure).sum(1)
-    a = ag.long()
+    a = ag[:, 0].long()
     assert bool(((a >= lo_cnt) & (a <= hi_cnt)).all())
+    # true / false positives of the pruned labels, bracketed the same way
+    tp_lo = (sure & (s0 > 0) & (s1 > 0)).sum(1)
+    fp_lo = (sure & (s0 < 0) & (s1 > 0)).sum(1)
+    unsure = (~sure).sum(1)
+    tp, fp = ag[:, 1].long(), ag[:, 2].long()
+    assert bool(((tp >= tp_lo) & (tp <= tp_lo + unsure) & (fp >= fp_lo) & (fp <= fp_lo + unsure)).all())
     assert int((~sure).sum()) < 0.01 * R
