@@ -92,6 +92,9 @@ def parse_args(argv=None):
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--emulate-shard", default=None,
                     help="r/N: run only rank r's shard of an N-rank job on this one process (diagnostics)")
+    ap.add_argument("--priority-items", type=int, default=0,
+                    help="run the N heaviest items of a step (previous step's wall time) on high-priority "
+                         "HIP streams (0 = off)")
     ap.add_argument("--profile", action="store_true", help="per-stage timing breakdown on stderr (syncs)")
     ap.add_argument("--concurrency", type=int, default=0,
                     help="host threads / HIP streams verifying (model, chunk) items concurrently (default 8 on GPU)")
@@ -196,12 +199,20 @@ def main() -> None:
     # host phases overlap other chunks' kernels and big models no longer serialise the tail.
     tls = threading.local()
 
-    def thread_stream():
+    def thread_stream(high: bool = False):
+        """This thread's HIP stream; ``high``: its high-priority twin (the critical-path items)."""
         if info.device.type != "cuda":
             return contextlib.nullcontext()
         if getattr(tls, "stream", None) is None:
             tls.stream = torch.cuda.Stream(info.device)
-        return torch.cuda.stream(tls.stream)
+            lo_pri, hi_pri = torch.cuda.Stream.priority_range()
+            tls.stream_hi = torch.cuda.Stream(info.device, priority=hi_pri) if hi_pri != lo_pri else tls.stream
+        return torch.cuda.stream(tls.stream_hi if high else tls.stream)
+
+    # the heaviest items of a step (longest previous wall time) run on high-priority streams:
+    # with fewer items than host threads per GPU (small shards) their dependent chain of BaB
+    # levels is the step's critical path, the light items fill the gaps (0 = off)
+    n_hi = args.priority_items
 
     pool = ThreadPoolExecutor(max_workers=conc) if conc > 1 else None
 
@@ -212,10 +223,10 @@ def main() -> None:
     # counters: attempted, decided, sat, unsat, unsat_heuristic, sat per stage (STAGES order)
     NC = 5 + len(STAGES)
 
-    def one_item(k: int, j: int, ids: np.ndarray):
+    def one_item(k: int, j: int, ids: np.ndarray, high: bool = False):
         m, be = models[k], backends[k]
         t_item = time.time()
-        with thread_stream():
+        with thread_stream(high):
             recs = verify_chunk(be, m, q, grid, ids, cfg, timer=timer)
             if info.device.type == "cuda":
                 torch.cuda.current_stream(info.device).synchronize()
@@ -235,7 +246,8 @@ def main() -> None:
             return np.zeros(NC)
         if pool is None:
             return sum(one_item(k, j, ids) for k, j, ids in items)
-        return sum(f.result() for f in [pool.submit(one_item, k, j, ids) for k, j, ids in items])
+        return sum(f.result() for f in [pool.submit(one_item, k, j, ids, i < n_hi)
+                                        for i, (k, j, ids) in enumerate(items)])
 
     sync = (lambda: torch.cuda.synchronize(info.device)) if info.device.type == "cuda" else (lambda: None)
     for w in range(args.warmup):
@@ -278,7 +290,7 @@ def main() -> None:
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
                    "stages": [list(st) for st in cfg.escalate_stages], "heuristic": cfg.heuristic,
                    "batch_nodes": cfg.batch_nodes,
-                   "chunk": args.chunk, "concurrency": conc},
+                   "chunk": args.chunk, "concurrency": conc, "priority_items": args.priority_items},
         "pct_verified": round(100.0 * dec / max(1.0, att), 3),
         "pct_verified_sound": round(100.0 * (dec - uns_h - sat_stage["heuristic"]) / max(1.0, att), 3),
         "partitions_per_s": round(att / dt_max, 3) if dt_max > 0 else 0.0,

@@ -327,7 +327,15 @@ __global__ void __launch_bounds__(256) fa_crown_mfma_kernel(NetDesc net, BoundAr
             if (neg) er[sg] += 3.f * u * (fabsf(m) * zmax + fabsf(tt));
           }
         }
-      // lambda' = W mu and |W| |mu| (rounding term), both signs
+      // lambda' = W mu and |W| |mu| (rounding term), both signs; |mu| once per layer
+      float amu[2][TM][4];
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          amu[0][t][i] = fabsf(mu[0][t][i]);
+          amu[1][t][i] = fabsf(mu[1][t][i]);
+        }
       const float4* wb = reinterpret_cast<const float4*>(smem + cfg.w_lds[l]);
       const float gn = fa_gam(2 * n + 1, u);
 #pragma unroll
@@ -337,14 +345,15 @@ __global__ void __launch_bounds__(256) fa_crown_mfma_kernel(NetDesc net, BoundAr
 #pragma unroll
         for (int t = 0; t < TM; ++t) {
           if (t >= tout) break;
-          const float4 w4 = wb[((size_t)ot * tout + t) * 64 + lane];
+          const float4 w4 = wb[(ot * tout + t) * 64 + lane];
           const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
+            const float aw = fabsf(wv[i]);
             Z0 = fa_mfma4(wv[i], mu[0][t][i], Z0);
             Z1 = fa_mfma4(wv[i], mu[1][t][i], Z1);
-            Q0 = fa_mfma4(fabsf(wv[i]), fabsf(mu[0][t][i]), Q0);
-            Q1 = fa_mfma4(fabsf(wv[i]), fabsf(mu[1][t][i]), Q1);
+            Q0 = fa_mfma4(aw, amu[0][t][i], Q0);
+            Q1 = fa_mfma4(aw, amu[1][t][i], Q1);
           }
         }
 #pragma unroll
