@@ -38,6 +38,10 @@ struct BoundArgs {
   // input dims degenerate (lo == hi) in EVERY row: folded into the constant by the
   // register-resident symbolic kernel (PA dims are added automatically when V > 0)
   unsigned long long fold;
+  // BaB status filter: rows of nodes whose partition (skip_part[node]) is no longer RUNNING /
+  // STOPPING are skipped (nothing written; the split kernel ignores those nodes)
+  const int8_t* skip_status;
+  const int* skip_part;
 };
 
 struct FwdArgs {
@@ -186,6 +190,9 @@ struct SplitArgs {
                                           //     (nodes_start - prev_start = the partition's nodes
                                           //     in this level; -1 before the first level)
   int budget;
+  const int* pbudget;                     // [P] per-partition budget (inline escalation) or nullptr
+  uint8_t* prob;                          // [P] probation flags (inline escalation) or nullptr
+  int budget2;                            // inline escalation budget
   int m;                                  // largest split-dim count (children = 2^m per node)
   int target;                             // per-partition frontier target of the branching rule
   float *oxlo, *oxhi, *oxplo, *oxphi;     // output pool
@@ -210,4 +217,7 @@ struct BabInitArgs {
   int ra_idx[FA_MAX_RA];
   float tau;
   int* counters;                          // [4]
+  int* pbudget;                           // [P] per-partition node budget (inline escalation) or nullptr
+  uint8_t* prob;                          // [P] probation flags or nullptr
+  int budget;
 };

@@ -170,9 +170,18 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
         if (d == d1) s1v = -1.f;
       }
       if (m == 0) break;   // no splittable dimension: treated as leaf by the certificate
-      if (a.nodes_start[p] >= a.budget) {
-        if (lane == 0) fa_stop(a, p);
-        break;
+      {
+        const int bud = a.pbudget ? a.pbudget[p] : a.budget;
+        if (a.nodes_start[p] >= bud) {
+          if (a.prob && bud < a.budget2) {
+            // inline escalation: on probation this level (children are made); fa_settle keeps
+            // it going with budget2 if its open frontier of this level is small, else UNKNOWN
+            if (lane == 0) a.prob[p] = 1;
+          } else {
+            if (lane == 0) fa_stop(a, p);
+            break;
+          }
+        }
       }
       const int k = 1 << m;
       const float* xl = a.xlo + (size_t)n * n0;
@@ -320,6 +329,8 @@ __global__ void fa_bab_init_kernel(BabInitArgs a) {
     a.lvl_open[p] = 0;
     a.nodes_start[p] = 0;
     a.prev_start[p] = -1;      // one root node in the first level
+    if (a.pbudget) a.pbudget[p] = a.budget;
+    if (a.prob) a.prob[p] = 0;
   }
   for (int i = tid; i < a.n_run; i += nth) a.part[i] = run[i];
   const size_t ne = (size_t)a.n_run * a.n0;
@@ -353,9 +364,15 @@ __global__ void fa_mark_unknown_kernel(const int* part, int n, int8_t* status) {
   if (status[p] == ST_RUNNING || status[p] == ST_STOPPING) status[p] = ST_UNKNOWN;
 }
 
+// Inline escalation (prob != nullptr): a partition that started this level at its first budget
+// was on probation (its nodes bounded, candidates emitted, children made).  If its open inner
+// nodes of this level are at most max_open it continues with budget2 -- the deeper second pass
+// of the two-pass schedule, same selection rule (profiles/escalate_sweep/), without restarting
+// from the root; otherwise it ends UNKNOWN with open_left = those nodes, exactly like the
+// first pass.  Its surplus children are skipped by the bound kernels (status filter).
 __global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
                                  int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
-                                 int* host_counts) {
+                                 int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open) {
   const int p = blockIdx.x * FA_THREADS + threadIdx.x;
   if (p == 0) {
     // level counters straight into pinned host memory (no blit per level), next slot cleared
@@ -368,7 +385,15 @@ __global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part
   if (status[p] == ST_STOPPING) {
     status[p] = ST_UNKNOWN;
     if (part_open) part_open[p] = lvl_open[p];
+  } else if (prob && prob[p] && status[p] == ST_RUNNING) {
+    if (lvl_open[p] <= max_open) {
+      pbudget[p] = budget2;
+    } else {
+      status[p] = ST_UNKNOWN;
+      if (part_open) part_open[p] = lvl_open[p];
+    }
   }
+  if (prob) prob[p] = 0;
   lvl_open[p] = 0;
   prev_start[p] = nodes_start[p];
   nodes_start[p] = part_nodes[p];     // the next level's budget reference
@@ -403,11 +428,12 @@ extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_
 
 extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
                                 int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
-                                int* host_counts, hipStream_t stream) {
+                                int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open,
+                                hipStream_t stream) {
   const int n = P > 0 ? P : 1;
   hipLaunchKernelGGL(fa_settle_kernel, dim3((n + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, P,
                      status, lvl_open, part_open, part_nodes, nodes_start, prev_start, counters_cur, counters_next,
-                     host_counts);
+                     host_counts, pbudget, prob, budget2, max_open);
   return (int)hipGetLastError();
 }
 

@@ -38,7 +38,8 @@ extern "C" int fa_mark_unknown_launch(const int* part, int n, int8_t* status, hi
 extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_t v, hipStream_t stream);
 extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
                                 int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
-                                int* host_counts, hipStream_t stream);
+                                int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open,
+                                hipStream_t stream);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_bab_init_launch(BabInitArgs a, hipStream_t stream);
 extern "C" int fa_bab_finish_launch(int P, const int8_t* status, const int* nodes, const int* open_left, int* out,
@@ -165,7 +166,8 @@ class BabRuntime {
                   py::array_t<float, py::array::c_style | py::array::forcecast> hi,
                   py::array_t<int8_t, py::array::c_style | py::array::forcecast> status0, int budget,
                   double time_budget, uintptr_t dead_part, py::object confirm, uintptr_t stream_i,
-                  bool native_exact) {
+                  bool native_exact, int budget2, int max_w) {
+    const bool inline_esc = budget2 > budget && max_w > 0;
     hipStream_t st = (hipStream_t)stream_i;
     native_exact_ = native_exact;
     box_lo_ = lo.data();
@@ -180,6 +182,10 @@ class BabRuntime {
     lvl_open_.ensure(P);
     nodes_start_.ensure(P);
     prev_start_.ensure(P);
+    if (inline_esc) {
+      pbudget_.ensure(P);
+      prob_.ensure(P);
+    }
     int slot = 0;
     // initial pool: running partitions.  Everything the device needs at the start goes through
     // ONE pinned staging block + one H2D copy + one init kernel (status, per-partition state,
@@ -220,6 +226,9 @@ class BabRuntime {
       for (int k = 0; k < ia.nra; ++k) ia.ra_idx[k] = ra_[k];
       ia.tau = tau_;
       ia.counters = counters_.p;
+      ia.pbudget = inline_esc ? pbudget_.p : nullptr;
+      ia.prob = inline_esc ? prob_.p : nullptr;
+      ia.budget = budget;
       ckl(fa_bab_init_launch(ia, st), "bab_init");
     }
     int cur = 0;
@@ -305,6 +314,9 @@ class BabRuntime {
         sa.nodes_start = nodes_start_.p;
         sa.prev_start = prev_start_.p;
         sa.budget = budget; sa.m = FA_MAX_SPLIT; sa.target = split_target_;
+        sa.pbudget = inline_esc ? pbudget_.p : nullptr;
+        sa.prob = inline_esc ? prob_.p : nullptr;
+        sa.budget2 = budget2;
         sa.oxlo = lo_[nxt].p; sa.oxhi = hi_[nxt].p;
         sa.oxplo = relaxed_ ? plo_[nxt].p : nullptr; sa.oxphi = relaxed_ ? phi_[nxt].p : nullptr;
         sa.opart = part_[nxt].p; sa.count_out = cnt; sa.cap = pool_[nxt];
@@ -314,7 +326,9 @@ class BabRuntime {
         launches += relaxed_ ? 6 : 5;
       }
       ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, nodes_.p, nodes_start_.p, prev_start_.p, cnt,
-                           counters_.p + 2 * (slot ^ 1), hcount_, st), "settle");
+                           counters_.p + 2 * (slot ^ 1), hcount_, inline_esc ? pbudget_.p : nullptr,
+                           inline_esc ? prob_.p : nullptr, budget2, max_w, st),
+          "settle");
       ck(hipStreamSynchronize(st), "sync");
       slot ^= 1;
       total_nodes += n_in;
@@ -380,6 +394,8 @@ class BabRuntime {
       b.node_part = part;
       b.dead_part = (const uint8_t*)dead_part;
     }
+    b.skip_status = status_.p;     // skip nodes of partitions decided / stopped earlier
+    b.skip_part = part;
     if (crown_) {
       b.layer_lb = lay_lb_[slot].p;
       b.layer_ub = lay_ub_[slot].p;
@@ -580,8 +596,9 @@ class BabRuntime {
   DevBuf<float> gmin_, tstar_, score_, cand_, scores_, pe_lb_, pe_ub_, cand_buf_;
   DevBuf<uint8_t> open_, leaf_;
   DevBuf<int64_t> split_, cv_, co_;
-  DevBuf<int> counters_, nodes_, idx_, open_left_, lvl_open_, nodes_start_, prev_start_, out_;
+  DevBuf<int> counters_, nodes_, idx_, open_left_, lvl_open_, nodes_start_, prev_start_, out_, pbudget_;
   DevBuf<int8_t> status_;
+  DevBuf<uint8_t> prob_;
   DevBuf<unsigned char> stage_;
   int* hcount_ = nullptr;
   // pinned host staging (solve start, solve end, per-level candidate records)
@@ -616,5 +633,5 @@ void register_bab(py::module& m) {
            py::arg("split_target") = 256)
       .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"),
-           py::arg("native_exact") = false);
+           py::arg("native_exact") = false, py::arg("budget2") = 0, py::arg("max_w") = 0);
 }

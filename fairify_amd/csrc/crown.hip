@@ -268,6 +268,10 @@ __global__ void __launch_bounds__(256) fa_crown_mfma_kernel(NetDesc net, BoundAr
     const int r = valid ? r0 : a.R - 1;
     const int node = a.V > 0 ? r / a.V : r;
     const int v = a.V > 0 ? r - node * a.V : 0;
+    if (a.skip_status) {   // BaB: skip tiles whose rows all belong to decided / stopped partitions
+      const int8_t st = a.skip_status[a.skip_part[node]];
+      if (!__any(valid && (st == 3 || st == 4))) continue;   // wave-uniform
+    }
     const uint8_t* dmask = nullptr;
     if (a.dead_in) dmask = a.dead_in + (size_t)r * net.n_hidden;
     else if (a.dead_part) dmask = a.dead_part + (size_t)a.node_part[a.part_mod ? node % a.part_mod : node] * net.n_hidden;

@@ -428,6 +428,11 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundAr
     const int r = __builtin_amdgcn_readfirstlane(r0);
     const bool v2 = PAIR && r + 1 < a.R;           // second row valid (else it shadows r, no writes)
     const int rb = v2 ? r + 1 : r;
+    if (a.skip_status) {   // BaB: rows of partitions already decided / stopped are not bounded
+      const int8_t s1 = a.skip_status[a.skip_part[a.V > 0 ? r / a.V : r]];
+      const int8_t s2 = a.skip_status[a.skip_part[a.V > 0 ? rb / a.V : rb]];
+      if (s1 != 3 && s1 != 4 && s2 != 3 && s2 != 4) continue;   // wave-uniform (r is)
+    }
     SymBox bxs[2];
 #pragma unroll
     for (int bi = 0; bi < RPW; ++bi) {

@@ -54,6 +54,10 @@ class BaBConfig:
     # clamp(log2(split_target / w), 1, 6) dims (per partition: verdicts do not depend on which
     # partitions share a chunk)
     split_target: int = int(os.environ.get("FAIRIFY_SPLIT_TARGET", "256"))
+    # native runtime inline escalation: a partition that reaches node_budget with a frontier of at
+    # most escalate_max_w nodes continues up to escalate_budget (0 = off)
+    escalate_budget: int = 0
+    escalate_max_w: int = 0
 
 
 @dataclass
@@ -348,7 +352,8 @@ class BaBSolver:
         with self.tm("bab.native"):
             st, cx, cxp, nodes, stats = rt.solve(lo_np.astype(np.float32), hi_np.astype(np.float32), status,
                                                   int(self.cfg.node_budget), float(self.cfg.time_budget), dead_ptr,
-                                                  confirm, stream, exact_models is None)
+                                                  confirm, stream, exact_models is None,
+                                                  int(self.cfg.escalate_budget), int(self.cfg.escalate_max_w))
         self.stats = dict(stats)
         with _STATS_LOCK:
             for k in STATS:

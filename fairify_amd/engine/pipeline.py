@@ -48,6 +48,8 @@ class VerifyConfig:
     escalate_max_open: int = 0           # only escalate partitions that left at most this many
                                          # open nodes in the first pass (0 = all; native BaB only)
     escalate_stages: Tuple[Tuple[int, int], ...] = ()
+    inline_escalate: bool = True         # native BaB: run the escalate_budget stage inside the first
+                                         # pass (escalate_max_open then bounds the frontier size)
                                          # further (budget, max_open) passes after the escalated one,
                                          # each on the residue the previous pass left
     batch_nodes: int = 65536             # BaB nodes per sub-batch launch
@@ -309,8 +311,15 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     # ---------------- stage 3: branch and bound on the original network
     t0 = time.time()
     budget = cfg.soft_timeout if time_budget is None else min(cfg.soft_timeout, time_budget)
+    # inline escalation (native runtime): the first escalation stage runs inside the first pass --
+    # partitions that reach node_budget with a small frontier continue instead of restarting from
+    # the root in a second solve (FAIRIFY_INLINE_ESCALATE=0: the two-pass schedule)
+    inline = (be.hip and cfg.inline_escalate and cfg.escalate_budget > cfg.node_budget and cfg.escalate_max_open > 0
+              and os.environ.get("FAIRIFY_INLINE_ESCALATE", "1") != "0" and os.environ.get("FAIRIFY_TORCH_BAB") != "1")
     solver = BaBSolver(be, q, BaBConfig(node_budget=cfg.node_budget, batch_nodes=cfg.batch_nodes,
-                                        time_budget=budget), timer=tm)
+                                        time_budget=budget,
+                                        escalate_budget=cfg.escalate_budget if inline else 0,
+                                        escalate_max_w=cfg.escalate_max_open if inline else 0), timer=tm)
     with tm("bab"):
         res = solver.solve(lo_np, hi_np, mlp, init_status=status)
     newly_sat = (res.status == SAT) & (status != SAT)
@@ -360,10 +369,10 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     # first pass decides the bulk; only residue partitions whose open frontier stayed small -- the
     # ones a deeper search can still close -- pay for the deep budgets)
     stages = []
-    if cfg.escalate_budget > cfg.node_budget:
+    if cfg.escalate_budget > cfg.node_budget and not inline:
         stages.append((cfg.escalate_budget, cfg.escalate_max_open))
     stages += [tuple(st) for st in cfg.escalate_stages]
-    prev_budget = cfg.node_budget
+    prev_budget = cfg.escalate_budget if inline else cfg.node_budget
     for e_budget, e_open in stages:
         if e_budget <= prev_budget:
             continue

@@ -6,6 +6,7 @@
 # OUT is a directory under gpurun_out/; each STEP is one of
 #   tests[:PYTEST_K]          GPU test tier (optionally -k filter)
 #   bench[:ARGS]              bench.py with ARGS ("_" separates arguments), JSON to OUT/bench*.json
+#   envbench:VAR=VAL[:ARGS]   the same with one environment variable set (A/B of FAIRIFY_* switches)
 #   prof[:ARGS]               rocprofv3 --kernel-trace --stats of bench.py ARGS (the trace csv is
 #                             reduced to OUT/profN.busy.txt by tools/trace_busy.py, then deleted;
 #                             the stats csv kept), default host concurrency
@@ -29,6 +30,10 @@ for step in "$@"; do
       rc=$?; tail -5 $OUT/tests$n.log ;;
     bench)
       timeout -k 10 600 python -u bench.py $args > $OUT/bench$n.json 2> $OUT/bench$n.err
+      rc=$?; cat $OUT/bench$n.json; [ $rc -ne 0 ] && tail -20 $OUT/bench$n.err ;;
+    envbench)
+      ev=${rest%%:*}; a2=${rest#*:}; [ "$a2" = "$rest" ] && a2=""
+      env "$ev" timeout -k 10 600 python -u bench.py ${a2//_/ } > $OUT/bench$n.json 2> $OUT/bench$n.err
       rc=$?; cat $OUT/bench$n.json; [ $rc -ne 0 ] && tail -20 $OUT/bench$n.err ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
