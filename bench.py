@@ -145,8 +145,12 @@ def main() -> None:
 
     dev_type = args.device or ("cuda" if torch.cuda.device_count() > 0 else "cpu")
     info = D.init(dev_type)
-    if dev_type == "cpu" and info.world > 1:      # CPU rehearsal ranks share the host's cores
-        torch.set_num_threads(max(1, (os.cpu_count() or 1) // info.world))
+    if dev_type == "cpu":      # CPU rehearsal ranks share the host's cores; FAIRIFY_CPU_THREADS pins the
+        # intra-op thread count (CPU matmul summation order depends on it, and bounds at a decision
+        # threshold may flip: tests comparing rank counts pin it)
+        nt = os.environ.get("FAIRIFY_CPU_THREADS")
+        if nt or info.world > 1:
+            torch.set_num_threads(int(nt) if nt else max(1, (os.cpu_count() or 1) // info.world))
     if not args.emulate_shard and info.world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={info.world}: launch one rank per GPU")
     if dev_type == "cuda" and info.world > torch.cuda.device_count() and \
@@ -250,16 +254,27 @@ def main() -> None:
                                         for i, (k, j, ids) in enumerate(items)])
 
     sync = (lambda: torch.cuda.synchronize(info.device)) if info.device.type == "cuda" else (lambda: None)
+
+    def marker(tag: int):
+        # fa_trace_marker_kernel brackets the timed steps in a rocprofv3 kernel trace
+        # (tools/trace_busy.py --window: GPU busy fraction of exactly the timed region)
+        if info.device.type == "cuda":
+            from fairify_amd.ops import hip as H
+
+            H.trace_marker(info.device, tag)
+
     for w in range(args.warmup):
         run_step(w)
     sync()
     D.barrier(info)
     sync()
+    marker(1)
     t0 = time.time()
     tot = np.zeros(NC)
     for s in range(args.steps):
         tot += run_step(args.warmup + s)
     sync()
+    marker(2)
     t_local = time.time() - t0          # this rank's own work, before waiting for the others
     D.barrier(info)
     sync()

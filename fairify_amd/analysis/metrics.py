@@ -73,6 +73,16 @@ def consistency(X: np.ndarray, y_pred: np.ndarray, k: int = 5, device=None, chun
     Xt = torch.as_tensor(np.asarray(X, dtype=np.float32), device=dev)
     yp = torch.as_tensor(np.asarray(y_pred, dtype=np.float32), device=dev)
     n = Xt.shape[0]
+    if dev.type == "cuda" and method in ("auto", "gemm", "device"):
+        from ..ops import use_hip
+
+        if use_hip(Xt):
+            from ..ops import hip as H
+
+            if k in H.KNN_K and k <= n and Xt.shape[1] <= 64:
+                # K10 on the device: fa_knn_kernel (exact differences, ties to the lower index)
+                idx, _ = H.knn(Xt, k)
+                return float(1.0 - (yp - yp[idx.long()].mean(1)).abs().mean())
     sq = (Xt * Xt).sum(1)
     acc = 0.0
     for s in range(0, n, chunk):

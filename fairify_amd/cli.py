@@ -54,7 +54,8 @@ def cmd_verify(args):
                        node_budget=args.node_budget, heuristic=not args.no_heuristic,
                        heuristic_p=args.heuristic_p if args.heuristic_p is not None else pre.heuristic_p,
                        heuristic_node_budget=args.node_budget, smt_backend=args.smt,
-                       escalate_budget=args.escalate_budget, escalate_max_open=args.escalate_max_open)
+                       escalate_budget=args.escalate_budget, escalate_max_open=args.escalate_max_open,
+                       keep_masks=args.keep_masks)
     if args.residual_samples is not None:
         cfg.residual_samples = args.residual_samples
     models = args.models.split(",") if args.models else None
@@ -192,6 +193,9 @@ def main(argv=None):
                    help="spend the per-model wall budget (--anytime-budget, default the preset's hard timeout) on "
                         "growing sound BaB budgets and falsifier rounds over the UNKNOWN residue")
     v.add_argument("--anytime-budget", type=float, default=None, help="seconds per model for --anytime")
+    v.add_argument("--keep-masks", action="store_true",
+                   help="gather every partition's final dead-neuron mask (packed bitset) to rank 0 and write "
+                        "OUT/masks/<model>.npz with the unique masks (dedup) for pruned-subnet export")
     v.add_argument("--residual-samples", type=int, default=None)
     v.add_argument("--metrics-csv", action="store_true",
                    help="also write the per-partition metrics CSV of the experiment drivers "

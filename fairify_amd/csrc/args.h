@@ -221,3 +221,15 @@ struct BabInitArgs {
   uint8_t* prob;                          // [P] probation flags or nullptr
   int budget;
 };
+
+// K1 partition decode (fa_decode_kernel): per input dim, the mixed-radix digit of the id and the
+// chunk table slice of its attribute (radix 0 = dim not partitioned: the domain range).
+#define FA_DECODE_MAX_DIMS 64
+struct DecodeDesc {
+  int n0;
+  int radix[FA_DECODE_MAX_DIMS];
+  long long div[FA_DECODE_MAX_DIMS];      // product of the radices of the attributes after this one
+  int chunk_off[FA_DECODE_MAX_DIMS];      // offset of the attribute's chunks in chunk_lo / chunk_hi
+  float base_lo[FA_DECODE_MAX_DIMS];
+  float base_hi[FA_DECODE_MAX_DIMS];
+};

@@ -84,6 +84,7 @@ struct FaSplitPlan {
   int nchild;                 // feasible children to write
   int ncand;                  // candidate pairs to write
   int leaf;
+  int part;                   // partition of an open inner node (-1: nothing to count)
 };
 
 // Possible-violation test of (orientation, pair) t at a leaf node (rows of the node's PA values).
@@ -108,7 +109,11 @@ __device__ __forceinline__ int fa_wave_incl_scan(int v, int lane) {
 //      ballot (lane c = child c), candidate counts by ballots over the leaf's PA pairs;
 //   B  wave 0 scans the block's child / candidate counts and reserves both ranges with ONE
 //      atomic each (a per-node atomic on the level counter serialised ~32 K same-address atomics
-//      per sub-batch in L2: ~135 us of the kernel's time in the round-2 baseline);
+//      per sub-batch in L2: ~135 us of the kernel's time in the round-2 baseline), and adds the
+//      per-partition counters (open inner nodes of the level, children made) with one atomic
+//      per run of equal partitions among the block's 64 nodes -- a partition's nodes are
+//      contiguous in the pool, so a deep partition no longer sends one same-address atomic per
+//      node to L2;
 //   C  each wave writes its children lane-parallel over (child, dim) entries (consecutive lanes
 //      store consecutive floats of the pool) and its candidate pairs.
 #define FA_SPLIT_WAVES 8
@@ -125,7 +130,7 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
   for (int i = 0; i < FA_SPLIT_NPW; ++i) {
     const int loc = wave * FA_SPLIT_NPW + i;
     const int n = blockIdx.x * FA_SPLIT_NB + loc;
-    FaSplitPlan pl{0ull, 0ull, 0, 0, 0, 0};
+    FaSplitPlan pl{0ull, 0ull, 0, 0, 0, 0, -1};
     do {
       if (n >= a.Nn || !a.open[n]) break;                  // wave-uniform
       const int p = a.part[n];
@@ -138,7 +143,7 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
           pl.ncand += __popcll(__ballot(t0 + lane < npair && fa_leaf_poss(a, n, t0 + lane)));
         break;
       }
-      if (lane == 0 && a.lvl_open) atomicAdd(&a.lvl_open[p], 1);
+      pl.part = p;   // counted in phase B: one open inner node of p in this level
       {
         const float lbx = a.pe_lb[n], ubx = a.pe_ub[n];
         const float lbp = a.pe_lb[a.Nn + n], ubp = a.pe_ub[a.Nn + n];
@@ -199,7 +204,6 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
       pl.nchild = __popcll(pl.fmask);
       pl.m = m;
       for (int j = 0; j < m; ++j) pl.dims |= (unsigned long long)dims[j] << (7 * j);
-      if (lane == 0 && pl.nchild) atomicAdd(&a.part_nodes[p], pl.nchild);
     } while (false);
     if (lane == 0) plan[loc] = pl;
   }
@@ -217,6 +221,20 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
     qb = __shfl(qb, 63);
     child_off[lane] = cb + ci - c;
     cand_off[lane] = qb + qi - q;
+    // per-partition counters: segmented sums over runs of equal partition ids
+    const int p = plan[lane].part;
+    const int o = p >= 0 ? 1 : 0;
+    const int oi = fa_wave_incl_scan(o, lane);
+    const int pprev = __shfl_up(p, 1), pnext = __shfl_down(p, 1);
+    const unsigned long long heads = __ballot(lane == 0 || pprev != p);
+    const bool tail = lane == 63 || pnext != p;
+    const int h = 63 - __clzll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
+    const int ci_b = __shfl(ci, h > 0 ? h - 1 : 0), oi_b = __shfl(oi, h > 0 ? h - 1 : 0);
+    if (tail && p >= 0) {
+      const int so = oi - (h > 0 ? oi_b : 0), sc = ci - (h > 0 ? ci_b : 0);
+      if (so && a.lvl_open) atomicAdd(&a.lvl_open[p], so);
+      if (sc) atomicAdd(&a.part_nodes[p], sc);
+    }
   }
   __syncthreads();
   // ---------------- phase C: write candidates and children

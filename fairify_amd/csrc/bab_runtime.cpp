@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "args.h"
+#include "exact_host.h"
 
 namespace py = pybind11;
 
@@ -148,18 +149,25 @@ class BabRuntime {
     for (int l = 0; l < net_.n_layers; ++l) np_ = std::max(np_, net_.b_off[l] + net_.dims[l + 1]);
     std::vector<float> hf(np_);
     ck(hipMemcpy(hf.data(), flat_, np_ * sizeof(float), hipMemcpyDeviceToHost), "cp weights");
-    hw_.assign(hf.begin(), hf.end());
-    is_pa_.assign(n0_, 0);
-    is_ra_.assign(n0_, 0);
-    for (int k : pa_) is_pa_[k] = 1;
+    exact_.n0 = n0_;
+    exact_.n_layers = net_.n_layers;
+    exact_.dims.assign(net_.dims, net_.dims + net_.n_layers + 1);
+    exact_.w_off.assign(net_.w_off, net_.w_off + net_.n_layers);
+    exact_.b_off.assign(net_.b_off, net_.b_off + net_.n_layers);
+    exact_.w.assign(hf.begin(), hf.end());
+    exact_.is_pa.assign(n0_, 0);
+    exact_.is_ra.assign(n0_, 0);
+    for (int k : pa_) exact_.is_pa[k] = 1;
     if (relaxed_)
-      for (int k : ra_) is_ra_[k] = 1;
+      for (int k : ra_) exact_.is_ra[k] = 1;
+    exact_.tau = tau_;
   }
   ~BabRuntime() {
     if (hcount_) hipHostFree(hcount_);
     if (hstage_) hipHostFree(hstage_);
     if (hout_) hipHostFree(hout_);
     if (hcand_) hipHostFree(hcand_);
+    if (hidx_) hipHostFree(hidx_);
   }
 
   py::tuple solve(py::array_t<float, py::array::c_style | py::array::forcecast> lo,
@@ -508,72 +516,22 @@ class BabRuntime {
     }
     if (!newly.empty()) {
       idx_.ensure(newly.size());
-      ck(hipMemcpyAsync(idx_.p, newly.data(), newly.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp idx");
+      ensure_host(hidx_, hidx_n_, newly.size() * sizeof(int));
+      std::memcpy(hidx_, newly.data(), newly.size() * sizeof(int));
+      ck(hipMemcpyAsync(idx_.p, hidx_, newly.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp idx");
       ckl(fa_set_status_launch(idx_.p, (int)newly.size(), status_.p, 1, st), "set_status");
       ck(hipStreamSynchronize(st), "sync");
     }
   }
 
-  // sign of the exact logit at integer point x: +1 / -1, 0 for exactly zero is never returned
-  // (an ambiguous |z| <= err gives 2 = "ask the exact rational check")
-  int exact_sign(const double* x) const {
-    const int L = net_.n_layers;
-    std::vector<double> h(x, x + n0_), m(n0_), e(n0_, 0.0), hn, mn, en;
-    for (int i = 0; i < n0_; ++i) m[i] = std::fabs(h[i]);
-    const double u = std::ldexp(1.0, -53);
-    for (int l = 0; l < L; ++l) {
-      const int nin = net_.dims[l], nout = net_.dims[l + 1];
-      const double* W = hw_.data() + net_.w_off[l];
-      const double* b = hw_.data() + net_.b_off[l];
-      const double ku = (nin + 3) * u;
-      const double g = ku / (1.0 - ku);
-      hn.assign(nout, 0.0); mn.assign(nout, 0.0); en.assign(nout, 0.0);
-      for (int j = 0; j < nout; ++j) {
-        double z = b[j], mm = std::fabs(b[j]), ee = g * std::fabs(b[j]);
-        for (int i = 0; i < nin; ++i) {
-          const double w = W[(size_t)i * nout + j];
-          z += h[i] * w;
-          mm += m[i] * std::fabs(w);
-          ee += (e[i] + g * m[i]) * std::fabs(w);
-        }
-        if (l < L - 1) { z = std::max(z, 0.0); mm = std::max(mm, 0.0); }
-        hn[j] = z; mn[j] = mm; en[j] = ee;
-      }
-      h.swap(hn); m.swap(mn); e.swap(en);
-    }
-    const double err = e[0] * 1.0001 + 1e-300;
-    if (std::fabs(h[0]) <= err) return 2;
-    return h[0] > 0 ? 1 : -1;
-  }
-
   // 1 violation, 0 not a violation, -1 undecided here (Python exact check)
   int exact_check(const float* pair, int p) const {
-    std::vector<double> x(n0_), xp(n0_);
-    const float* lo = box_lo_ + (size_t)p * n0_;
-    const float* hi = box_hi_ + (size_t)p * n0_;
-    for (int d = 0; d < n0_; ++d) {
-      x[d] = std::nearbyint((double)pair[d]);
-      xp[d] = std::nearbyint((double)pair[n0_ + d]);
-      if (x[d] < lo[d] || x[d] > hi[d]) return 0;
-      if (is_pa_[d]) {
-        if (x[d] == xp[d] || xp[d] < lo[d] || xp[d] > hi[d]) return 0;
-      } else if (is_ra_[d]) {
-        if (std::fabs(x[d] - xp[d]) > tau_) return 0;
-      } else if (x[d] != xp[d]) {
-        return 0;
-      }
-    }
-    const int sx = exact_sign(x.data());
-    if (sx == 2) return -1;
-    const int sp = exact_sign(xp.data());
-    if (sp == 2) return -1;
-    return sx * sp < 0 ? 1 : 0;
+    return exact_.check(pair, box_lo_ + (size_t)p * n0_, box_hi_ + (size_t)p * n0_);
   }
 
   NetDesc net_;
   const float* flat_;
-  std::vector<double> hw_;
-  std::vector<char> is_pa_, is_ra_;
+  fa_exact::ExactChecker exact_;   // fp64 host copy of the network + query constraints
   bool native_exact_ = false;
   const float* box_lo_ = nullptr;
   const float* box_hi_ = nullptr;
@@ -608,9 +566,16 @@ class BabRuntime {
   size_t hout_n_ = 0;
   unsigned char* hcand_ = nullptr;
   size_t hcand_n_ = 0;
+  unsigned char* hidx_ = nullptr;   // confirmed-SAT partition ids (H2D before fa_set_status)
+  size_t hidx_n_ = 0;
 
   // grow a pinned host buffer; only called between solves / after a stream sync, so no copy can
-  // still be reading the old one
+  // still be reading the old one.  Buffer-lifetime rule of this runtime (checked by
+  // tests/test_stream_lifetime.py): the host side of EVERY hipMemcpyAsync is one of these
+  // runtime-owned pinned buffers, never a pageable std::vector / numpy temporary, and nothing
+  // writes, frees or regrows it before the hipStreamSynchronize that retires the copy.  Round 1
+  // enqueued pageable H2D copies and then rewrote the source vector in place (relaxed x' boxes);
+  // with 8 host threads that raced the runtime's staging of pageable copies.
   static void ensure_host(unsigned char*& p, size_t& n, size_t need) {
     if (need <= n) return;
     if (p) hipHostFree(p);

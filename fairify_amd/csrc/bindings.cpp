@@ -32,6 +32,15 @@ extern "C" int fa_agree_launch(const NetDesc& net, const float* flat, int Pm, co
                                const float* hi, const int64_t* pids, const uint8_t* dead, int S, uint32_t seed,
                                int* agree, hipStream_t stream);
 
+extern "C" int fa_decode_launch(const DecodeDesc& d, const int64_t* ids, int P, const float* chunk_lo,
+                                const float* chunk_hi, float* lo, float* hi, hipStream_t stream);
+extern "C" int fa_trace_marker_launch(int tag, int* sink, hipStream_t stream);
+extern "C" int fa_knn_launch(const float* X, int n, int d, int k, int* idx, float* dist, hipStream_t stream);
+extern "C" int fa_actdiff_launch(const NetDesc& net, const float* flat, const float* x, const float* xp, int npairs,
+                                 float* sum_out, hipStream_t stream);
+extern "C" int fa_pack_masks_launch(const uint8_t* src, int P, int N, int stride, int sel, uint8_t* out, int NB,
+                                    unsigned long long* hash, hipStream_t stream);
+
 template <typename T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
 
@@ -331,6 +340,45 @@ PYBIND11_MODULE(_C, m) {
     check(fa_certify_launch(a, (hipStream_t)stream), "certify");
   });
 
+  m.def("decode", [](std::vector<int> radix, std::vector<long long> div, std::vector<int> chunk_off,
+                     std::vector<float> base_lo, std::vector<float> base_hi, uintptr_t ids, int Pn,
+                     uintptr_t chunk_lo, uintptr_t chunk_hi, uintptr_t lo, uintptr_t hi, uintptr_t stream) {
+    const size_t n0 = radix.size();
+    if (n0 == 0 || n0 > FA_DECODE_MAX_DIMS || div.size() != n0 || chunk_off.size() != n0 || base_lo.size() != n0 ||
+        base_hi.size() != n0)
+      throw std::invalid_argument("decode: descriptor sizes");
+    DecodeDesc d{};
+    d.n0 = (int)n0;
+    for (size_t k = 0; k < n0; ++k) {
+      if (radix[k] < 0 || (radix[k] > 0 && div[k] <= 0)) throw std::invalid_argument("decode: radix/div");
+      d.radix[k] = radix[k];
+      d.div[k] = div[k];
+      d.chunk_off[k] = chunk_off[k];
+      d.base_lo[k] = base_lo[k];
+      d.base_hi[k] = base_hi[k];
+    }
+    check(fa_decode_launch(d, P<const int64_t>(ids), Pn, P<const float>(chunk_lo), P<const float>(chunk_hi),
+                           P<float>(lo), P<float>(hi), (hipStream_t)stream),
+          "decode");
+  });
+  m.def("pack_masks", [](uintptr_t src, int Pn, int N, int stride, int sel, uintptr_t out, int NB, uintptr_t hash,
+                         uintptr_t stream) {
+    check(fa_pack_masks_launch(P<const uint8_t>(src), Pn, N, stride, sel, P<uint8_t>(out), NB,
+                               P<unsigned long long>(hash), (hipStream_t)stream),
+          "pack_masks");
+  });
+  m.def("knn", [](uintptr_t X, int n, int d, int k, uintptr_t idx, uintptr_t dist, uintptr_t stream) {
+    check(fa_knn_launch(P<const float>(X), n, d, k, P<int>(idx), P<float>(dist), (hipStream_t)stream), "knn");
+  });
+  m.def("actdiff", [](const Net& net, uintptr_t flat, uintptr_t x, uintptr_t xp, int npairs, uintptr_t sum_out,
+                      uintptr_t stream) {
+    check(fa_actdiff_launch(net.d, P<const float>(flat), P<const float>(x), P<const float>(xp), npairs,
+                            P<float>(sum_out), (hipStream_t)stream),
+          "actdiff");
+  });
+  m.def("trace_marker", [](int tag, uintptr_t sink, uintptr_t stream) {
+    check(fa_trace_marker_launch(tag, P<int>(sink), (hipStream_t)stream), "trace_marker");
+  });
   m.def("arch", []() { return std::string("gfx950"); });
   register_bab(m);
   register_csv(m);

@@ -80,6 +80,10 @@ class VerifyConfig:
     anytime_pool: int = 1 << 24          # live BaB nodes per group: group size = pool / budget
     anytime_max_samples: int = 16384
     anytime_milp_seconds: float = 1.0    # first MILP round's per-partition limit (x growth per round)
+    keep_masks: bool = False             # K6: keep every partition's final dead-neuron mask (sound
+                                         # prune, or the heuristic mask of a retried partition) as a
+                                         # packed bitset (core["mask_bits"], ceil(N/8) B) for the
+                                         # rank-0 gather, dedup and pruned-subnet export
 
 
 @dataclass
@@ -208,14 +212,14 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     uniq, inv = np.unique(key, axis=0, return_inverse=True)
     inv = inv.reshape(-1)
     if len(uniq) <= 1:
-        core, seg = _verify_group(be, mlp, q, ids, lo_np, hi_np, cfg, time_budget, timer)
+        core, seg = _verify_group(be, mlp, q, ids, lo_np, hi_np, cfg, time_budget, timer, grid=grid)
     else:
         t0 = time.time()
         core, seg = None, np.zeros(5)
         for g in range(len(uniq)):
             sel = np.nonzero(inv == g)[0]
             left = None if time_budget is None else time_budget - (time.time() - t0)
-            gcore, gseg = _verify_group(be, mlp, q, ids[sel], lo_np[sel], hi_np[sel], cfg, left, timer)
+            gcore, gseg = _verify_group(be, mlp, q, ids[sel], lo_np[sel], hi_np[sel], cfg, left, timer, grid=grid)
             if core is None:
                 core = {k: np.zeros((len(ids),) + v.shape[1:], dtype=v.dtype) for k, v in gcore.items()}
             for k, v in gcore.items():
@@ -226,8 +230,12 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
 
 
 def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_np: np.ndarray, hi_np: np.ndarray,
-                  cfg: VerifyConfig, time_budget: Optional[float], timer: Optional[StageTimer]):
-    """One group of partitions sharing their protected-attribute range: (core columns, segment)."""
+                  cfg: VerifyConfig, time_budget: Optional[float], timer: Optional[StageTimer],
+                  grid: Optional[Grid] = None):
+    """One group of partitions sharing their protected-attribute range: (core columns, segment).
+
+    On the GPU the device boxes are decoded from the ids by ``fa_decode_kernel`` (K1); the host
+    keeps its own decode (``lo_np``/``hi_np``) for the exact confirmation of candidates."""
     tm = timer if timer is not None else StageTimer()
     t_start = time.time()
     dev = be.device
@@ -239,9 +247,14 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     values_np, pairs_np = _pa_table(q, lo_np, hi_np)
     values = torch.from_numpy(values_np).to(dev)
     pairs = torch.from_numpy(pairs_np).to(dev)
-    lo = torch.from_numpy(lo_np).to(dev, torch.float32)
-    hi = torch.from_numpy(hi_np).to(dev, torch.float32)
     pids = torch.from_numpy(ids).to(dev)
+    if be.hip and grid is not None:
+        from ..ops import hip as H
+
+        lo, hi = H.decode(grid, pids)
+    else:
+        lo = torch.from_numpy(lo_np).to(dev, torch.float32)
+        hi = torch.from_numpy(hi_np).to(dev, torch.float32)
 
     # ---------------- stage 1: simulation (profile + falsify)
     t0 = time.time()
@@ -563,6 +576,13 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         sync()
         t_heur = time.time() - t0
 
+    # ---------------- K6: final dead-neuron masks as packed bitsets (optional)
+    mask_bits = None
+    if cfg.keep_masks:
+        with tm("masks"):
+            mask_bits = _final_mask_bits(be, mlp, code if fused else None, None if fused else st_dead, masked, unk,
+                                         hm_t if (fused and masked) else None, Pn)
+
     # ---------------- stage 5: replay / fidelity (batched on the device)
     t0 = time.time()
     with tm("replay"):
@@ -623,7 +643,30 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         h_attempt=h_attempt, h_success=h_success,
         b_cnt=b_cnt, s_cnt=s_cnt, st_cnt=st_cnt, h_cnt=h_cnt, t_cnt=t_cnt, agree=agree, tp=tp, fp=fp, nodes=nodes.astype(np.int64),
         c_check=c_check, v_accurate=v_acc, cex_x=cex_x, cex_xp=cex_xp)
+    if mask_bits is not None:
+        core["mask_bits"] = mask_bits
     return core, (Pn, t_sim + t_prune + t_bab, t_bab, t_heur, t_replay)
+
+
+def _final_mask_bits(be, mlp: MLP, code, st_dead, masked: Dict[int, np.ndarray], unk: np.ndarray, hm_t, Pn: int
+                     ) -> np.ndarray:
+    """[Pn, ceil(N/8)] uint8 (numpy.packbits order) final dead masks: the sound-prune mask
+    (ST = B ∪ S with one neuron kept alive per layer), replaced by the merged heuristic mask for
+    the partitions of the heuristic retry -- the mask whose popcount is the CSV's T-compression
+    numerator.  On the GPU the mask algebra codes are packed by ``fa_pack_masks_kernel``."""
+    N = mlp.n_neurons
+    if code is not None and be.hip:
+        from ..ops import hip as H
+
+        fm = ((code & H.PM_ST) != 0).to(torch.uint8)
+        if hm_t is not None and len(unk):
+            fm[torch.from_numpy(np.asarray(unk)).to(fm.device)] = (hm_t != 0).to(torch.uint8)
+        bits, _ = H.pack_masks(fm)
+        return bits.cpu().numpy()
+    m = np.zeros((Pn, N), dtype=bool) if st_dead is None else st_dead.cpu().numpy().astype(bool)
+    for p, mk in masked.items():
+        m[p] = np.asarray(mk, dtype=bool)[:N]
+    return np.packbits(m, axis=1)
 
 
 class StreamPool:
@@ -673,7 +716,8 @@ def concat_records(parts: Sequence["ChunkRecords"]) -> "ChunkRecords":
         raise ValueError("no records")
     if len(parts) == 1:
         return parts[0]
-    core = {k: np.concatenate([p.core[k] for p in parts]) for k in parts[0].core}
+    keys = [k for k in parts[0].core if all(k in p.core for p in parts)]
+    core = {k: np.concatenate([p.core[k] for p in parts]) for k in keys}
     segs = [sg for p in parts for sg in p.segments]
     return ChunkRecords(core, parts[0].orig_acc, segments=segs, n_neurons=parts[0].n_neurons,
                         sim_size=parts[0].sim_size)
@@ -735,7 +779,8 @@ class ChunkRecords(Sequence):
     like a list of per-partition dicts (the CSV/runner view, built lazily per row)."""
 
     _INT = ("grid_id", "h_attempt", "h_success", "c_check", "v_accurate", "nodes")
-    _HIDE = ("cex_x", "cex_xp", "b_cnt", "s_cnt", "st_cnt", "h_cnt", "t_cnt", "agree", "tp", "fp", "pruned_f1")
+    _HIDE = ("cex_x", "cex_xp", "b_cnt", "s_cnt", "st_cnt", "h_cnt", "t_cnt", "agree", "tp", "fp", "pruned_f1",
+             "mask_bits")
 
     def __init__(self, core: Dict[str, np.ndarray], orig_acc: Optional[float] = None, segments=None,
                  n_neurons: int = 1, sim_size: int = 1):

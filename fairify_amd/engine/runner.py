@@ -273,6 +273,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         pending = []
         wire_bytes = [0, 0]
         table_cols: Dict[str, List[np.ndarray]] = {k: [] for k in _TABLE_COLS}
+        mask_parts: List[tuple] = []        # K6: (positions, grid ids, packed masks) per round
         timer = StageTimer(info.device)
         t0 = time.time()
         per_round = cfg.chunk * streams.workers
@@ -294,6 +295,8 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                 _replace(gpos, grecs, *retried)
             rows = pack(grecs, gpos, n0)
             cols = columns(rows, n0)
+            if cfg.keep_masks and "mask_bits" in grecs.cols:
+                mask_parts.append((gpos, grecs.cols["grid_id"], grecs.cols["mask_bits"]))
             if mwriter is not None:
                 mwriter.write(gpos, grecs)
             for k in _TABLE_COLS:
@@ -380,6 +383,11 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             if anytime_budget:
                 row["anytime_budget_s"] = float(anytime_budget)
             row["wire_bytes_per_partition"] = round(wire_bytes[0] / max(1, wire_bytes[1]), 2)
+            if cfg.keep_masks and mask_parts:
+                from ..report.masks import write_masks
+
+                row["unique_masks"] = write_masks(os.path.join(out_dir, "masks", f"{name}.npz"), mask_parts,
+                                                  mlp.n_neurons, resume=resume)
             rows_out.append(row)
             if verbose:
                 print(f"[{preset.name}] {name}: {row['SAT']} sat / {row['UNSAT']} unsat / {row['UNK']} unknown "

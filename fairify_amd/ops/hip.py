@@ -52,6 +52,81 @@ def _ptr(t: Optional[torch.Tensor]) -> int:
 
 
 # ------------------------------------------------------------------------------------------------
+def decode(grid, ids: torch.Tensor):
+    """K1: grid-linear partition ids (int64, on the device) -> boxes ``lo, hi`` float32 [P, n0]
+    decoded by ``fa_decode_kernel`` (the chunk tables are uploaded once per grid and device)."""
+    dev = ids.device
+    ids = _c(ids, torch.int64, (ids.shape[0],), "ids")
+    tabs = grid.__dict__.setdefault("_dev_decode", {})
+    key = str(dev)
+    if key not in tabs:
+        d = grid.decode_desc()
+        cl = torch.from_numpy(d["chunk_lo"]).to(dev) if d["chunk_lo"].size else torch.zeros(1, device=dev)
+        ch = torch.from_numpy(d["chunk_hi"]).to(dev) if d["chunk_hi"].size else torch.zeros(1, device=dev)
+        tabs[key] = (d, cl, ch)
+    d, cl, ch = tabs[key]
+    n0 = int(d["radix"].shape[0])
+    Pn = int(ids.shape[0])
+    lo = torch.empty(Pn, n0, dtype=torch.float32, device=dev)
+    hi = torch.empty(Pn, n0, dtype=torch.float32, device=dev)
+    if Pn:
+        ext().decode(d["radix"].tolist(), d["div"].tolist(), d["chunk_off"].tolist(), d["base_lo"].tolist(),
+                     d["base_hi"].tolist(), ids.data_ptr(), Pn, cl.data_ptr(), ch.data_ptr(), lo.data_ptr(),
+                     hi.data_ptr(), _stream(dev))
+    return lo, hi
+
+
+def pack_masks(masks: torch.Tensor, sel: int = 0xFF):
+    """K6: [P, N] uint8 masks (dead where ``mask & sel``) -> (packed [P, ceil(N/8)] uint8 in
+    ``numpy.packbits`` order, row hashes [P] int64) via ``fa_pack_masks_kernel``."""
+    m = _c(masks, torch.uint8, name="masks")
+    if m.dim() != 2:
+        raise ValueError("masks: expected [P, N]")
+    Pn, N = m.shape
+    NB = (N + 7) // 8
+    out = torch.empty(Pn, NB, dtype=torch.uint8, device=m.device)
+    hsh = torch.empty(Pn, dtype=torch.int64, device=m.device)
+    if Pn and N:
+        ext().pack_masks(m.data_ptr(), Pn, N, N, int(sel), out.data_ptr(), NB, hsh.data_ptr(), _stream(m.device))
+    return out, hsh
+
+
+KNN_K = (1, 2, 3, 4, 5, 6, 7, 8, 10, 16)
+
+
+def knn(X: torch.Tensor, k: int):
+    """K10: indices [n, k] int32 of every row's k nearest rows of ``X`` (squared Euclidean, the
+    row itself first, ties to the lower index) and their squared distances (``fa_knn_kernel``)."""
+    X = _c(X, torch.float32, name="X")
+    n, d = X.shape
+    if not 1 <= d <= 64 or k not in KNN_K or k > n:
+        raise ValueError(f"knn: unsupported shape n={n} d={d} k={k}")
+    idx = torch.empty(n, k, dtype=torch.int32, device=X.device)
+    dist = torch.empty(n, k, dtype=torch.float32, device=X.device)
+    ext().knn(X.data_ptr(), n, d, k, idx.data_ptr(), dist.data_ptr(), _stream(X.device))
+    return idx, dist
+
+
+def activation_delta_sum(be, x: torch.Tensor, xp: torch.Tensor) -> torch.Tensor:
+    """K13: sum over pairs of |act(x) - act(x')| per neuron [N] (hidden ReLU outputs, then the
+    logit) via ``fa_actdiff_kernel``."""
+    P_ = x.shape[0]
+    x = _c(x, torch.float32, (P_, be.n0), "x")
+    xp = _c(xp, torch.float32, (P_, be.n0), "xp")
+    out = torch.zeros(be.mlp.n_neurons, dtype=torch.float32, device=x.device)
+    if P_:
+        ext().actdiff(_net(be), be.flat.data_ptr(), x.data_ptr(), xp.data_ptr(), P_, out.data_ptr(),
+                      _stream(x.device))
+    return out
+
+
+def trace_marker(dev, tag: int) -> None:
+    """Launch ``fa_trace_marker_kernel`` (a named one-thread kernel) on the current stream: the
+    kernel trace's time-window delimiter (tools/trace_busy.py --window)."""
+    ext().trace_marker(int(tag), 0, _stream(dev))
+
+
+# ------------------------------------------------------------------------------------------------
 def forward(be, x: torch.Tensor, dead: Optional[torch.Tensor] = None) -> torch.Tensor:
     shp = x.shape[:-1]
     x2 = _c(x.reshape(-1, be.n0), torch.float32, name="x")

@@ -3,7 +3,7 @@
 Round 1 shipped fixed-width float64 rows (≈376 B per Adult partition) with an ``all_gather``
 to every rank.  Here a rank ships, per round, one byte buffer:
 
-* header        int64 [4]: records, segments, SAT rows, n0
+* header        int64 [5]: records, segments, SAT rows, n0, mask bytes per record (0 = none)
 * segments      float64 [S, 5]: per verified chunk (count, t_sim+prune+bab, t_bab, t_heur,
                 t_replay) -- the per-partition time columns are apportioned from these on
                 rank 0 by :func:`engine.pipeline.derive_columns`, exactly as the producer would;
@@ -13,7 +13,10 @@ to every rank.  Here a rank ships, per round, one byte buffer:
                 expansions (uint32);
 * counterexamples, SAT partitions only: x [n0] and x' on the protected/relaxed dims only (every
                 other dim of a confirmed pair equals x), int16 when the query domain (widened
-                by tau) fits, else int32 -- 28 B per SAT pair for Adult.
+                by tau) fits, else int32 -- 28 B per SAT pair for Adult;
+* dead masks    optional (VerifyConfig.keep_masks, K6): every partition's final dead-neuron mask
+                as a packed bitset, ceil(N/8) B (numpy.packbits order) -- the bitset all-gather of
+                SURVEY §2.4.2 (26 B for AC-4's 201 neurons).
 
 Partition positions are NOT shipped: rank 0 recomputes every rank's share of the round from
 the seeded order (the same strided split the ranks used).  Verdicts alone travel as int8 in an
@@ -72,16 +75,20 @@ def encode(recs: ChunkRecords, q) -> np.ndarray:
     dims, dt = _cex_layout(q)
     cex = np.concatenate([c["cex_x"][sat], c["cex_xp"][sat][:, dims]], axis=1).astype(dt)
     segs = np.asarray(recs.segments, dtype=np.float64).reshape(-1, 5)
-    head = np.array([n, len(segs), int(sat.sum()), n0], dtype=np.int64)
-    return np.concatenate([head.view(np.uint8), segs.reshape(-1).view(np.uint8), rec.view(np.uint8),
-                           cex.reshape(-1).view(np.uint8)])
+    mb = c.get("mask_bits")
+    nb = 0 if mb is None else int(mb.shape[1])
+    head = np.array([n, len(segs), int(sat.sum()), n0, nb], dtype=np.int64)
+    parts = [head.view(np.uint8), segs.reshape(-1).view(np.uint8), rec.view(np.uint8), cex.reshape(-1).view(np.uint8)]
+    if nb:
+        parts.append(np.ascontiguousarray(mb, dtype=np.uint8).reshape(-1))
+    return np.concatenate(parts)
 
 
 def decode(buf: np.ndarray, grid_ids: np.ndarray, orig_acc, n_neurons: int, sim_size: int, q) -> ChunkRecords:
     """Inverse of :func:`encode`; ``grid_ids`` = the partitions' grid ids (known to rank 0)."""
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
-    n, ns, nsat, n0 = (int(x) for x in buf[:32].view(np.int64))
-    o = 32
+    n, ns, nsat, n0, nb = (int(x) for x in buf[:HEAD].view(np.int64))
+    o = HEAD
     segs = buf[o:o + 40 * ns].view(np.float64).reshape(ns, 5)
     o += 40 * ns
     rec = buf[o:o + REC.itemsize * n].view(REC)
@@ -89,6 +96,8 @@ def decode(buf: np.ndarray, grid_ids: np.ndarray, orig_acc, n_neurons: int, sim_
     dims, dt = _cex_layout(q)
     w = n0 + len(dims)
     cex = buf[o:o + dt.itemsize * w * nsat].view(dt).reshape(nsat, w).astype(np.int64)
+    o += dt.itemsize * w * nsat
+    masks = buf[o:o + n * nb].reshape(n, nb).copy() if nb else None
     if len(grid_ids) != n:
         raise ValueError(f"{n} records but {len(grid_ids)} grid ids")
     f = rec["flags"].astype(np.int64)
@@ -108,6 +117,8 @@ def decode(buf: np.ndarray, grid_ids: np.ndarray, orig_acc, n_neurons: int, sim_
                 tp=rec["tp"].astype(np.int64), fp=rec["fp"].astype(np.int64),
                 nodes=rec["nodes"].astype(np.int64), c_check=(f >> 7) & 1, v_accurate=(f >> 8) & 1,
                 cex_x=cx, cex_xp=cxp)
+    if masks is not None:
+        core["mask_bits"] = masks
     return ChunkRecords(core, orig_acc, segments=[tuple(s) for s in segs.tolist()], n_neurons=n_neurons,
                         sim_size=sim_size)
 
@@ -117,7 +128,10 @@ def bytes_per_partition(buf: np.ndarray, n: int) -> float:
 
 
 def empty(q) -> np.ndarray:
-    return np.array([0, 0, 0, q.n], dtype=np.int64).view(np.uint8).copy()
+    return np.array([0, 0, 0, q.n, 0], dtype=np.int64).view(np.uint8).copy()
+
+
+HEAD = 40   # header bytes (5 x int64)
 
 
 def records_of(bufs: List[np.ndarray]) -> List[int]:

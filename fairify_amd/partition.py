@@ -145,6 +145,26 @@ class Grid:
         lo, hi = self.decode(np.array([pid]))
         return {f.name: [int(lo[0, i]), int(hi[0, i])] for i, f in enumerate(self.domain.features)}
 
+    def decode_desc(self) -> Dict[str, np.ndarray]:
+        """Per-input-dim descriptor of the device decode (``fa_decode_kernel``, K1): the dim's
+        mixed-radix radix (0 = not partitioned), the divisor (product of the radices of the
+        attributes after it in row-major order), its slice of the chunk tables, the domain range."""
+        n = self.domain.n
+        radix = np.zeros(n, dtype=np.int32)
+        div = np.ones(n, dtype=np.int64)
+        off = np.zeros(n, dtype=np.int32)
+        t = self.decode_table()
+        later = 1
+        for k in range(len(self.attrs) - 1, -1, -1):
+            a = self.attrs[k]
+            radix[a.index] = a.count
+            div[a.index] = later
+            off[a.index] = int(t["chunk_off"][k])
+            later *= a.count
+        return {"radix": radix, "div": div, "chunk_off": off,
+                "base_lo": self.base_lo.astype(np.float32), "base_hi": self.base_hi.astype(np.float32),
+                "chunk_lo": t["chunk_lo"].astype(np.float32), "chunk_hi": t["chunk_hi"].astype(np.float32)}
+
     def decode_table(self) -> Dict[str, np.ndarray]:
         """Flat arrays describing the grid for the device-side decode."""
         offs = np.zeros(len(self.attrs) + 1, dtype=np.int64)

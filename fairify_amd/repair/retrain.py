@@ -106,6 +106,16 @@ def activation_deltas(mlp: MLP, X: np.ndarray, pa_index: int, device="cpu") -> n
     xs, xps = xs[valid], xps[valid]
     if len(xs) == 0:
         return np.zeros(mlp.n_neurons)
+    if torch.device(device).type == "cuda":
+        from ..ops import use_hip
+
+        if use_hip(xs):
+            # K13 on the device: both forwards of every pair in one fa_actdiff_kernel launch
+            from ..ops import hip as H
+            from ..ops.backend import Backend
+
+            s = H.activation_delta_sum(Backend(mlp, device), xs, xps)
+            return (s / len(xs)).cpu().numpy().astype(np.float64)
 
     def acts(x):
         out = []

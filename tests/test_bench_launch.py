@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _bench(gpus: int, extra=()):
-    env = dict(os.environ, FAIRIFY_DIST_BACKEND="gloo")
+    env = dict(os.environ, FAIRIFY_DIST_BACKEND="gloo", FAIRIFY_CPU_THREADS="1")
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--device", "cpu",
            "--models", "AC-8,AC-9", "--limit", "48", "--chunk", "16", "--steps", "1", "--warmup", "0",

@@ -1,0 +1,107 @@
+"""Buffer-lifetime rule of the multi-stream BaB path.
+
+Round 1's profiled runs with 8 host threads / HIP streams crashed inside HIP copies.  The native
+runtime then enqueued ``hipMemcpyAsync`` from pageable ``std::vector`` temporaries and, for
+relaxed queries, rewrote a source vector in place right after enqueueing its copy (the x' boxes
+were derived from the x boxes by editing ``hl``/``hh`` between two async copies).  A pageable
+async H2D copy is staged by the HIP runtime after the call returns, so the second edit raced the
+first copy.  The rule the runtime follows now (``csrc/bab_runtime.cpp``, ``ensure_host``):
+
+* the host side of every ``hipMemcpyAsync`` is a runtime-owned pinned buffer (``hipHostMalloc``);
+* such a buffer is only written, regrown or freed after the ``hipStreamSynchronize`` that
+  retires the copy reading it.
+
+The CPU test checks the first point on the source; the GPU test drives the former hazard (a
+relaxed query, the x' pool path) from 8 threads with their own streams and runtimes and requires
+the serial verdicts and counterexamples.
+"""
+import os
+import re
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fairify_amd", "csrc")
+
+
+def _host_operands(src: str):
+    """(direction, host operand) of every hipMemcpyAsync call in ``src``."""
+    out = []
+    for m in re.finditer(r"hipMemcpyAsync\(([^;]*?)\)\s*,\s*\"", src, flags=re.S):
+        args = [a.strip() for a in m.group(1).split(",")]
+        kind = next(a for a in args if a.startswith("hipMemcpy"))
+        host = args[1] if kind == "hipMemcpyHostToDevice" else args[0]
+        out.append((kind, host))
+    return out
+
+
+def test_async_copies_use_pinned_runtime_buffers():
+    src = open(os.path.join(CSRC, "bab_runtime.cpp")).read()
+    ops = _host_operands(src)
+    assert len(ops) >= 4, ops
+    pinned = set(re.findall(r"hipHostMalloc\(\(void\*\*\)&(\w+)", src))
+    pinned |= set(re.findall(r"ensure_host\((\w+),", src))
+    for kind, host in ops:
+        if kind == "hipMemcpyDeviceToDevice":
+            continue
+        name = host.split("+")[0].strip()
+        assert name in pinned, f"{kind} from/to {host!r} is not a runtime-owned pinned buffer"
+        assert ".data()" not in host, host
+    # no other source file enqueues async host copies (they go through torch or this runtime)
+    for f in os.listdir(CSRC):
+        if f.endswith((".hip", ".cpp")) and f != "bab_runtime.cpp":
+            assert "hipMemcpyAsync" not in open(os.path.join(CSRC, f)).read(), f
+
+
+def test_pinned_buffers_regrow_only_after_sync():
+    """Every ensure_host(...) call that can regrow a buffer a copy reads is preceded, within the
+    same function, by a stream synchronisation or sits at the start of a solve (previous solve
+    ended with a sync)."""
+    src = open(os.path.join(CSRC, "bab_runtime.cpp")).read()
+    body = src[src.index("py::tuple solve("):]
+    first_sync = body.index("hipStreamSynchronize")
+    for m in re.finditer(r"ensure_host\((\w+),", body):
+        pos = m.start()
+        fn_start = body.rfind("\n  void ", 0, pos)
+        fn_start = max(fn_start, 0)
+        before = body[fn_start:pos]
+        at_solve_start = pos < first_sync and m.group(1) == "hstage_"
+        assert at_solve_start or "hipStreamSynchronize" in before or m.group(1) in ("hout_", "hcand_"), m.group(1)
+
+
+@pytest.mark.gpu
+def test_relaxed_bab_eight_streams_match_serial(cuda):
+    import torch
+
+    from fairify_amd import presets
+    from fairify_amd.engine.pipeline import VerifyConfig, verify_chunk
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.ops.backend import Backend
+    from fairify_amd.partition import processing_order
+
+    pre = presets.get("relaxed/AC")
+    grid, q = pre.grid(), pre.resolved()
+    assert q.ra_idx and q.tau > 0
+    order = processing_order(grid, 0)
+    chunks = [order[i * 256:(i + 1) * 256] for i in range(8)]
+    m = get_model("AC-3", weights="random", seed=0)
+    be = Backend(m, cuda)
+    cfg = VerifyConfig(sim_size=128, node_budget=256, smt_backend="none", residual_samples=256)
+    serial = [verify_chunk(be, m, q, grid, ids, cfg) for ids in chunks]
+
+    def run(ids):
+        s = torch.cuda.Stream(cuda)
+        with torch.cuda.stream(s):
+            out = verify_chunk(be, m, q, grid, ids, cfg)
+            torch.cuda.current_stream(cuda).synchronize()
+        return out
+
+    for _ in range(2):
+        with ThreadPoolExecutor(8) as ex:
+            conc = list(ex.map(run, chunks))
+        for a, b in zip(serial, conc):
+            assert np.array_equal(a.cols["verdict"], b.cols["verdict"])
+            sat = a.cols["verdict"] == "sat"
+            assert np.array_equal(a.cols["cex_x"][sat], b.cols["cex_x"][sat])
+            assert np.array_equal(a.cols["cex_xp"][sat], b.cols["cex_xp"][sat])

@@ -8,7 +8,8 @@
 #   bench[:ARGS]              bench.py with ARGS ("_" separates arguments), JSON to OUT/bench*.json
 #   envbench:VAR=VAL[:ARGS]   the same with one environment variable set (A/B of FAIRIFY_* switches)
 #   prof[:ARGS]               rocprofv3 --kernel-trace --stats of bench.py ARGS (the trace csv is
-#                             reduced to OUT/profN.busy.txt by tools/trace_busy.py, then deleted;
+#                             reduced to OUT/profN.busy.txt (whole run) and OUT/profN.window.txt (timed
+#                             steps only, between bench.py's marker kernels) by tools/trace_busy.py, then deleted;
 #                             the stats csv kept), default host concurrency
 #   pmc:COUNTERS[:ARGS]       one rocprofv3 --pmc pass (counters comma-separated)
 #   py:SCRIPT[:ARGS]          python SCRIPT ARGS
@@ -25,8 +26,12 @@ for step in "$@"; do
   args=${rest//_/ }
   case $kind in
     tests)
-      k=""; [ -n "$rest" ] && k="-k $rest"
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread $k > $OUT/tests$n.log 2>&1
+      # -k expression: "_" separates words (tests:decode_or_bab -> -k "decode or bab")
+      if [ -n "$rest" ]; then
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$args" > $OUT/tests$n.log 2>&1
+      else
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/tests$n.log 2>&1
+      fi
       rc=$?; tail -5 $OUT/tests$n.log ;;
     bench)
       timeout -k 10 600 python -u bench.py $args > $OUT/bench$n.json 2> $OUT/bench$n.err
@@ -39,7 +44,10 @@ for step in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
         -d $ROOT/$OUT/prof$n -o run -- python3 -u $ROOT/bench.py $args > $ROOT/$OUT/prof$n.out 2> $ROOT/$OUT/prof$n.err)
       rc=$?
-      for t in $(find $OUT/prof$n -name '*kernel_trace.csv'); do python tools/trace_busy.py $t > $OUT/prof$n.busy.txt; done
+      for t in $(find $OUT/prof$n -name '*kernel_trace.csv'); do
+        python tools/trace_busy.py $t > $OUT/prof$n.busy.txt
+        python tools/trace_busy.py $t --window > $OUT/prof$n.window.txt || true
+      done
       find $OUT/prof$n -name '*kernel_trace.csv' -delete
       cat $OUT/prof$n.out; [ $rc -ne 0 ] && tail -30 $OUT/prof$n.err ;;
     pmc)
