@@ -224,6 +224,8 @@ def main() -> None:
     # the longest items first (LPT), so the slowest model's chain starts at t=0 instead of after
     # a wave of cheap items (prior before any measurement: model size)
     item_cost = {}
+    ITEM_LOG = os.environ.get("FAIRIFY_BENCH_ITEMS") == "1"   # per-item start / duration on stderr
+    step_no, step_t0 = [0], [time.time()]
     # counters: attempted, decided, sat, unsat, unsat_heuristic, sat per stage (STAGES order)
     NC = 5 + len(STAGES)
 
@@ -235,6 +237,9 @@ def main() -> None:
             if info.device.type == "cuda":
                 torch.cuda.current_stream(info.device).synchronize()
         item_cost[(k, j)] = time.time() - t_item
+        if ITEM_LOG:
+            print(f"[item] step {step_no[0]} {models[k].name} chunk {j} n={len(ids)} start "
+                  f"{t_item - step_t0[0]:.3f}s took {item_cost[(k, j)]:.3f}s", file=sys.stderr, flush=True)
         v, st = recs.cols["verdict"], recs.cols["stage"]
         sat, uns = v == "sat", v == "unsat"
         out = np.zeros(NC, dtype=np.float64)
@@ -244,6 +249,7 @@ def main() -> None:
         return out
 
     def run_step(step: int):
+        step_no[0], step_t0[0] = step, time.time()
         items = [(k, j, ids) for k in range(len(models)) for j, ids in enumerate(chunks_for_step(step)) if len(ids)]
         items.sort(key=lambda it: (-item_cost.get((it[0], it[1]), 0.0), -models[it[0]].n_neurons))
         if not items:

@@ -85,6 +85,21 @@ struct Net {
     for (int l = 0; l < d.n_layers; ++l) wp += dims[l + 1];
     d.wperm_floats = (wp + 3) & ~3;
     total_floats = d.wperm_off + d.wperm_floats;
+    // packed narrow-network block (ops/backend.py: pack_groups / mfma_packed_block)
+    d.pack_g = 1;
+    if (d.n_layers >= 2 && dims[0] <= 16 && mw <= 16) {
+      int mh = 0;
+      for (int l = 1; l < d.n_layers; ++l) mh = std::max(mh, dims[l]);
+      if (mh <= 8) d.pack_g = std::min(5, 16 / mh);
+    }
+    d.pack_off = total_floats;
+    d.pack_floats = 0;
+    if (d.pack_g > 1) {
+      int pf = d.pack_g * 256 + (d.n_layers - 1) * 256;
+      for (int l = 0; l < d.n_layers; ++l) pf += d.pack_g * dims[l + 1];
+      d.pack_floats = (pf + 3) & ~3;
+      total_floats += d.pack_floats;
+    }
   }
   int n_params;
   int total_floats;
@@ -106,6 +121,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("n_params", &Net::n_params)
       .def_readonly("total_floats", &Net::total_floats)
       .def_property_readonly("wperm_off", [](const Net& n) { return n.d.wperm_off; })
+      .def_property_readonly("pack_g", [](const Net& n) { return n.d.pack_g; })
+      .def_property_readonly("pack_off", [](const Net& n) { return n.d.pack_off; })
       .def_property_readonly("n_hidden", [](const Net& n) { return n.d.n_hidden; })
       .def_property_readonly("n_neurons", [](const Net& n) { return n.d.n_neurons; });
 

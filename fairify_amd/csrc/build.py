@@ -32,7 +32,9 @@ def _flags(debug: bool):
 
     inc = [f"-I{HERE}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
     opt = ["-O0", "-g"] if debug else ["-O3"]
-    return inc + opt + ["-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+    # FAIRIFY_HIPCC_DEFINES="A=1 B=2": extra -D flags (occupancy A/B builds, tools/variants)
+    defs = ["-D" + d for d in os.environ.get("FAIRIFY_HIPCC_DEFINES", "").split() if d]
+    return inc + opt + defs + ["-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 
 def _newer(src: str, obj: str, headers) -> bool:
@@ -42,9 +44,9 @@ def _newer(src: str, obj: str, headers) -> bool:
     return os.path.getmtime(src) > t or any(os.path.getmtime(h) > t for h in headers)
 
 
-def build(debug: bool = False, verbose: bool = False, jobs: int = 4) -> str:
-    out = ext_path()
-    bdir = os.path.join(ROOT, "build", "hip-" + ARCH + ("-dbg" if debug else ""))
+def build(debug: bool = False, verbose: bool = False, jobs: int = 4, out: str = None, tag: str = "") -> str:
+    out = out or ext_path()
+    bdir = os.path.join(ROOT, "build", "hip-" + ARCH + ("-dbg" if debug else "") + (("-" + tag) if tag else ""))
     os.makedirs(bdir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(HERE, "*.hip"))) + sorted(glob.glob(os.path.join(HERE, "*.cpp")))
     headers = glob.glob(os.path.join(HERE, "*.h"))
@@ -82,4 +84,11 @@ def build(debug: bool = False, verbose: bool = False, jobs: int = 4) -> str:
 
 
 if __name__ == "__main__":
-    print(build(debug="--debug" in sys.argv, verbose=True))
+    # python -m fairify_amd.csrc.build [--debug] [--out PATH --tag NAME]  (variant builds go to PATH)
+    argv = sys.argv[1:]
+    kw = {}
+    if "--out" in argv:
+        kw["out"] = argv[argv.index("--out") + 1]
+    if "--tag" in argv:
+        kw["tag"] = argv[argv.index("--tag") + 1]
+    print(build(debug="--debug" in argv, verbose=True, **kw))

@@ -207,8 +207,12 @@ __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_pick_kernel(CertArgs 
 // of QG = next_pow2(Q) consecutive lanes per node evaluates one entry each, a shuffle arg-max
 // inside the group keeps the first maximum (the two-kernel path's rule), and the group's first
 // lane runs the pick.  One launch instead of two per BaB sub-batch, no gmin / tstar round trip.
+#ifndef FA_CERT_WPE16
+#define FA_CERT_WPE16 1
+#endif
 template <int NM>
-__global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_fused_kernel(CertArgs a, int QG) {
+__global__ void __launch_bounds__(FA_CERT_THREADS) __attribute__((amdgpu_waves_per_eu(NM == 16 ? FA_CERT_WPE16 : 1)))
+fa_pair_fused_kernel(CertArgs a, int QG) {
   const int Q = a.Pp * a.norient;
   const int gidx = blockIdx.x * FA_CERT_THREADS + threadIdx.x;
   const int n = gidx / QG, qq = gidx - n * QG;

@@ -31,6 +31,12 @@ struct NetDesc {
   // every layer's bias; staged into LDS by the register-resident kernels with float4 copies
   int wperm_off;
   int wperm_floats;                   // size of that block (multiple of 4)
+  // narrow networks (inputs <= 16, hidden layers <= 8 wide): pack_g boxes share one 16-row MFMA
+  // tile in the symbolic kernel; block-diagonal weights at pack_off (ops/backend.py:
+  // mfma_packed_block), pack_floats long (0 when pack_g == 1)
+  int pack_g;
+  int pack_off;
+  int pack_floats;
 };
 
 // lowbias32 (Wellons) — identical to ops/reference.py:hash32

@@ -235,8 +235,19 @@ struct CrownCfg {
   int floats;
 };
 
+// Minimum waves per SIMD for the 4- and 7-tile kernels (VGPR budget 512 / waves): 220 -> 168
+// and 338 -> 256 VGPRs with 80 / 160 B of scratch spills, 3 and 2 waves per SIMD instead of 2
+// and 1: AC-4 0.71 -> 0.59 ms, AC-7 0.335 -> 0.31 ms per 131 072 rows (tools/ab_variants.sh,
+// profiles/r2/occupancy.md).  -DFA_CROWN_WPE4=1 -DFA_CROWN_WPE7=1 restores the unconstrained build.
+#ifndef FA_CROWN_WPE4
+#define FA_CROWN_WPE4 3
+#endif
+#ifndef FA_CROWN_WPE7
+#define FA_CROWN_WPE7 2
+#endif
 template <int TM>
-__global__ void __launch_bounds__(256) fa_crown_mfma_kernel(NetDesc net, BoundArgs a, CrownCfg cfg) {
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(TM == 4 ? FA_CROWN_WPE4 : (TM == 7 ? FA_CROWN_WPE7 : 1)))) fa_crown_mfma_kernel(NetDesc net, BoundArgs a, CrownCfg cfg) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   // ---- stage every layer's W in backward operand order + biases

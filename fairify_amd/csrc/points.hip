@@ -92,8 +92,9 @@ __device__ __forceinline__ void fa_point_layer(const NetDesc& net, const BoundAr
   }
 }
 
+// 7-tile nets: 260 -> 254 VGPRs (spill-free) doubles the waves per SIMD (1 -> 2)
 template <int TM>
-__global__ void __launch_bounds__(FA_THREADS) fa_point_kernel(NetDesc net, BoundArgs a, PointCfg cfg) {
+__global__ void __launch_bounds__(FA_THREADS) __attribute__((amdgpu_waves_per_eu(TM == 7 ? 2 : 1))) fa_point_kernel(NetDesc net, BoundArgs a, PointCfg cfg) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   // ---- stage the MFMA-operand-order weights + biases (pre-permuted in `flat`) into LDS

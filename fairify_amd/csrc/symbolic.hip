@@ -45,6 +45,8 @@ struct SymCfg {
                                    //   [jt][t][lane][i] = W[16t + 4(lane>>4) + i][16jt + (lane&15)]
   int b_lds[FA_MAX_LAYERS];        // LDS float offset of b_l
   int lds_floats;
+  int stage_off;                   // float offset in `flat` of the staged block (wperm or packed)
+  int stage_floats;                //   and its size (multiple of 4)
 };
 
 struct SymBox {
@@ -66,21 +68,27 @@ struct SymBox {
   }
 };
 
-// per-wave LDS slab: tile staging T[2 blocks][16 neurons][TS] + box values [2 boxes][3][48]
-template <int NT>
+// per-wave LDS slab: tile staging T[2 blocks][16 neurons][TS] + box values [2 PG boxes][3][48]
+// (+ packed mode: the boxes' input ranges [2 PG][lo 16 | hi 16] for the on-the-fly layer-0 operands)
+template <int NT, int PG = 1>
 struct SymSlab {
   static constexpr int TS = 16 * NT + 4;                 // padded row stride (floats)
   static constexpr int TILE1 = 2 * 16 * TS;             // one 16-neuron tile, U and L blocks
   static constexpr int TILE = 2 * TILE1;                 // two tiles per epilogue pass
   static constexpr int BOX = 3 * FA_SYM_MAXC;
-  static constexpr int FLOATS = (TILE + 2 * BOX + 3) & ~3;    // two boxes (paired-row variant)
+  static constexpr int BOXTAB = PG > 1 ? 2 * PG * 32 : 0;
+  static constexpr int FLOATS = (TILE + 2 * PG * BOX + BOXTAB + 3) & ~3;
 };
 
 // Epilogue of one 16-neuron output tile (accumulators U, Lq of tile jt): spill to the wave's
 // LDS slab, one lane per (neuron, block) computes the rigorous bounds and the ReLU relaxation
 // once, the new form rows are reloaded in MFMA operand layout into (nu, nlo).  Returns false on
 // the last layer (outputs written, nothing to reload).
-template <int NT, bool PAIR>
+//
+// Packed mode (PG > 1, narrow networks): tile row `col` of group tsub is neuron col % w of box
+// tsub * PG + col / w of the wave pass (w = the layer's width, rows PG * w .. 15 are padding);
+// the wave's boxes are consecutive rows r_in + b.
+template <int NT, bool PAIR, int PG = 1>
 __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
                                                 const float* smem, float* T, const float* bxv_in, const int* cdim_s,
                                                 int l, int r_in, int node_in, int r2, int node2, bool v2, int lane,
@@ -105,12 +113,14 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
   // two tiles are the same neurons of two box rows (r_in, r2), each with its own box values
   const int tsub = lane >> 5;
   const bool second = PAIR && tsub;
-  const int r = second ? r2 : r_in;
-  const int node = second ? node2 : node_in;
-  const float* bxv = bxv_in + (second ? SymSlab<NT>::BOX : 0);
+  const int gbox = PG > 1 ? col / n_out : 0;            // packed: box of this tile row in its group
+  const int bidx = tsub * PG + gbox;                     // packed: box index within the wave pass
+  const int r = PG > 1 ? r_in + bidx : (second ? r2 : r_in);
+  const int node = PG > 1 ? (a.V > 0 ? r / a.V : r) : (second ? node2 : node_in);
+  const float* bxv = bxv_in + (PG > 1 ? bidx : (second ? 1 : 0)) * SymSlab<NT, PG>::BOX;
   const int jt = PAIR ? jt0 : jt0 + tsub;
   const int n_out_t = net.dims[l + 1];
-  const bool nl_act = 16 * jt < n_out_t && (!second || v2);
+  const bool nl_act = PG > 1 ? (gbox < PG && r < a.R) : (16 * jt < n_out_t && (!second || v2));
   const int ob = (lane >> 4) & 1;
   float* Trow = T + tsub * SymSlab<NT>::TILE1 + (ob * 16 + col) * TS;
     // ---------------- spill both tiles: T[tile][block][neuron][column]
@@ -125,15 +135,15 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
         }
     __builtin_amdgcn_wave_barrier();
     // ---------------- one lane per (tile, neuron, block): bounds, relaxation, new form row
-    const int j = 16 * jt + col;
-    const bool jv = j < n_out;
+    const int j = PG > 1 ? col - gbox * n_out : 16 * jt + col;   // neuron within its box
+    const bool jv = PG > 1 ? gbox < PG : j < n_out;
     float v[16 * NT];
 #pragma unroll
     for (int q = 0; q < 4 * NT; ++q) {
       const float4 x = reinterpret_cast<const float4*>(Trow)[q];
       v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
     }
-    const float b = jv ? sb[j] : 0.f;
+    const float b = jv ? sb[PG > 1 ? col : j] : 0.f;       // packed biases: tiled PG times
     // concretisation of the coefficient part over the box (Σ min, Σ max, Σ |c| m); padding
     // columns hold 0 coefficients and a [0, 0] box, so they add exact zeros
     float mn = 0.f, mx = 0.f, mg = 0.f;
@@ -244,8 +254,10 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
 }
 
 // PAIR (TM == 1 only): the wave carries two box rows; operand/accumulator slot u (the "tile"
-// index) is the box, both use output tile 0 of W.
-template <int NT, int TM, bool PAIR>
+// index) is the box, both use output tile 0 of W.  PG > 1 (packed, PAIR only): slot u is a group
+// of PG boxes sharing the tile (block-diagonal weights); layer 0 builds its identity-form
+// operands on the fly from the boxes' input ranges in the wave's LDS box table.
+template <int NT, int TM, bool PAIR, int PG = 1>
 __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
                                              const float* smem, float* T, const float* bxv, const int* cdim_s,
                                              int l, int r, int node, int r2, int node2, bool v2, int lane,
@@ -272,7 +284,71 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
   const int ob = (lane >> 4) & 1;
   float* Trow = T + (ob * 16 + col) * TS;
 #ifndef FA_SYM_TIMING_NO_EPILOGUE
-  if (last && n_out == 1) {
+  if (PG > 1 && l == 0) {
+    // packed layer 0: group u accumulates its PG boxes, box g through tile g of the packed W_0
+    // (W_0 placed at output rows g * w_1 ..), K = the box's own input dims
+    const float* boxtab = bxv + 2 * PG * SymSlab<NT, PG>::BOX;   // [2 PG][lo 16 | hi 16]
+    const float g0 = net.g_gemm[0];
+    const int n0v = net.dims[0];
+    f32x4 U[2][NT], Lq[2][NT];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) U[u][ct] = Lq[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < PG; ++g) {
+        const float* bt = boxtab + (u * PG + g) * 32;
+        const float4 w4 = reinterpret_cast<const float4*>(sw)[g * 64 + lane];
+        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 4 * grp + i;
+          const bool kv = k < n0v;
+          const float xl = kv ? bt[k] : 0.f, xh = kv ? bt[16 + k] : 0.f;
+          const bool folded = kv && ((cfg.fold >> k) & 1ull);
+          const float m = fmaxf(fabsf(xl), fabsf(xh));
+          const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
+#pragma unroll
+          for (int ct = 0; ct < NT; ++ct) {
+            const int c = ct * 16 + col;
+            float vu = 0.f, vl = 0.f;
+            if (kv) {
+              if (c >= 4) {
+                vu = vl = (!folded && c - 4 < nc && cdim_s[c - 4] == k) ? 1.f : 0.f;
+              } else if (c == 0) {
+                vu = vl = folded ? xl : 0.f;
+              } else if (c == 1) {
+                vu = g0 * m; vl = -vu;
+              } else if (c == 2) {
+                vu = xh; vl = xl;
+              } else {
+                vu = g0 * fabsf(xh); vl = -(g0 * fabsf(xl));
+              }
+            }
+            U[u][ct] = fa_mfma4(wp, vu, U[u][ct]);
+            Lq[u][ct] = fa_mfma4(wp, vl, Lq[u][ct]);
+            U[u][ct] = fa_mfma4(wn, vl, U[u][ct]);
+            Lq[u][ct] = fa_mfma4(wn, vu, Lq[u][ct]);
+          }
+        }
+      }
+    }
+    float nu[2][NT][4], nlo[2][NT][4];
+    if (!fa_sym_epilogue<NT, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
+                                       nu, nlo))
+      return;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          A[ct][u][0][i] = nu[u][ct][i];
+          A[ct][u][1][i] = nlo[u][ct][i];
+        }
+    return;
+  }
+  if (PG == 1 && last && n_out == 1) {
     // single-neuron output layer: a VALU dot product instead of a 16-row MFMA tile of which
     // 15 rows are padding.  Lane (grp, col) sums its 4*tin neurons k = 16t + 4 grp + i for its
     // form column; two cross-group butterflies finish the sum (any summation order stays within
@@ -317,8 +393,8 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
         Lq[bi][ct] = f32x4{grp == 0 ? xl : 0.f, 0.f, 0.f, 0.f};
       }
     float nu[2][NT][4], nlo[2][NT][4];
-    fa_sym_epilogue<NT, PAIR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq, nu,
-                              nlo);
+    fa_sym_epilogue<NT, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
+                                  nu, nlo);
     return;
   }
 #endif
@@ -373,8 +449,8 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
       continue;
     }
 #else
-    if (!fa_sym_epilogue<NT, PAIR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, jt0, U, Lq,
-                                   nu, nlo))
+    if (!fa_sym_epilogue<NT, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, jt0, U,
+                                       Lq, nu, nlo))
       continue;
 #endif
 #pragma unroll
@@ -391,16 +467,25 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
   }
 }
 
-template <int NT, int TM, bool PAIR>
-__global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
-  constexpr int TMS = PAIR ? 2 : TM;   // operand slots: K tiles, or (PAIR) the wave's two boxes
+// Minimum waves per SIMD the register allocator must leave room for (VGPR budget 512 / waves):
+// the paired single-tile kernel needed 180 VGPRs (2 waves/SIMD) and the 4-tile kernel 260 (1 wave),
+// both spill-free at 3 / 2 waves (167 / 242 VGPRs); the 7-tile kernel keeps 366 (its operand
+// ping-pong alone is 112 VGPRs) -- tighter limits spill to scratch.
+#define FA_SYM_WAVES_PER_EU(NT, TM, PAIR) ((PAIR) ? 3 : ((TM) == 2 ? 3 : ((TM) == 4 ? 2 : 1)))
+
+template <int NT, int TM, bool PAIR, int PG = 1>
+__global__ void __launch_bounds__(FA_THREADS) __attribute__((amdgpu_waves_per_eu(FA_SYM_WAVES_PER_EU(NT, TM, PAIR))))
+fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
+  constexpr int TMS = PAIR ? 2 : TM;   // operand slots: K tiles, or (PAIR) the wave's two boxes /
+                                       // (packed) two groups of PG boxes
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
-  // ---- stage the MFMA-operand-order weights + biases (pre-permuted in `flat`) into LDS
+  // ---- stage the MFMA-operand-order weights + biases (pre-permuted in `flat`; the block-diagonal
+  //      packed copy when PG > 1) into LDS
   {
-    const float4* src = reinterpret_cast<const float4*>(a.flat + net.wperm_off);
+    const float4* src = reinterpret_cast<const float4*>(a.flat + cfg.stage_off);
     float4* dst = reinterpret_cast<float4*>(smem);
-    for (int e = tid; e < (net.wperm_floats >> 2); e += FA_THREADS) dst[e] = src[e];
+    for (int e = tid; e < (cfg.stage_floats >> 2); e += FA_THREADS) dst[e] = src[e];
   }
   int* cdim_s = reinterpret_cast<int*>(smem + cfg.lds_floats - FA_SYM_MAXC);
   for (int c = tid; c < FA_SYM_MAXC; c += FA_THREADS) cdim_s[c] = c < cfg.nc ? cfg.cdim[c] : -1;
@@ -412,7 +497,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundAr
   const int n0 = net.dims[0];
   const int nc = cfg.nc;
   const float g0 = net.g_gemm[0];
-  float* T = smem + cfg.lds_floats + wave * SymSlab<NT>::FLOATS;
+  float* T = smem + cfg.lds_floats + wave * SymSlab<NT, PG>::FLOATS;
   float* bxv = T + SymSlab<NT>::TILE;             // [lo | hi | max(|lo|,|hi|)] per coefficient column
   const int tin0 = (n0 + 15) >> 4;
   // column layout: 0 constant, 1 error, 2 interval, 3 interval error, 4.. coefficients
@@ -423,21 +508,26 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundAr
     role[ct] = c == 0 ? 1 : c == 1 ? 2 : c == 2 ? 3 : c == 3 ? 4 : (c - 4 < nc ? 0 : 5);
     cdm[ct] = (role[ct] == 0) ? cdim_s[c - 4] : -1;
   }
-  constexpr int RPW = PAIR ? 2 : 1;   // box rows per wave and pass
+  constexpr int RPW = PAIR ? 2 * PG : 1;   // box rows per wave and pass
   for (int r0 = (blockIdx.x * nw + wave) * RPW; r0 < a.R; r0 += gridDim.x * nw * RPW) {
     const int r = __builtin_amdgcn_readfirstlane(r0);
     const bool v2 = PAIR && r + 1 < a.R;           // second row valid (else it shadows r, no writes)
     const int rb = v2 ? r + 1 : r;
     if (a.skip_status) {   // BaB: rows of partitions already decided / stopped are not bounded
-      const int8_t s1 = a.skip_status[a.skip_part[a.V > 0 ? r / a.V : r]];
-      const int8_t s2 = a.skip_status[a.skip_part[a.V > 0 ? rb / a.V : rb]];
-      if (s1 != 3 && s1 != 4 && s2 != 3 && s2 != 4) continue;   // wave-uniform (r is)
+      bool any = false;
+#pragma unroll
+      for (int bi = 0; bi < RPW; ++bi) {
+        const int rr = min(r + bi, a.R - 1);
+        const int8_t s1 = a.skip_status[a.skip_part[a.V > 0 ? rr / a.V : rr]];
+        any = any || s1 == 3 || s1 == 4;
+      }
+      if (!any) continue;   // wave-uniform (r is)
     }
-    SymBox bxs[2];
+    SymBox bxs[RPW];
 #pragma unroll
     for (int bi = 0; bi < RPW; ++bi) {
       SymBox& bx = bxs[bi];
-      const int rr = bi ? rb : r;
+      const int rr = PG > 1 ? min(r + bi, a.R - 1) : (bi ? rb : r);
       bx.a = &a;
       bx.n0 = n0;
       bx.node = a.V > 0 ? rr / a.V : rr;
@@ -450,6 +540,11 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundAr
         bv[FA_SYM_MAXC + lane] = h0;
         bv[2 * FA_SYM_MAXC + lane] = fmaxf(fabsf(l0), fabsf(h0));
       }
+      if (PG > 1 && lane < 32) {   // packed: the box's input ranges for the layer-0 operands
+        const int d = lane & 15;
+        float* bt = bxv + 2 * PG * SymSlab<NT, PG>::BOX + bi * 32;
+        bt[lane] = d < n0 ? (lane < 16 ? bx.lo(d) : bx.hi(d)) : 0.f;
+      }
     }
     const SymBox& bx = bxs[0];
     float XA[NT][TMS][2][4], XB[NT][TMS][2][4];
@@ -457,6 +552,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundAr
     //      L-block error columns negated
 #pragma unroll
     for (int t = 0; t < TMS; ++t) {
+      if (PG > 1) break;                      // packed: layer-0 operands built on the fly
       if (!PAIR && t >= tin0) break;
       const SymBox& bt = bxs[PAIR ? t : 0];   // PAIR: slot t = box t (n0 <= 16: one K tile)
 #pragma unroll
@@ -491,11 +587,11 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sym_kernel(NetDesc net, BoundAr
     __builtin_amdgcn_wave_barrier();
     for (int l = 0; l < net.n_layers; ++l) {
       if (l & 1)
-        fa_sym_layer<NT, TM, PAIR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
-                                   lane, XB, XA);
+        fa_sym_layer<NT, TM, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
+                                       lane, XB, XA);
       else
-        fa_sym_layer<NT, TM, PAIR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
-                                   lane, XA, XB);
+        fa_sym_layer<NT, TM, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
+                                       lane, XA, XB);
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -510,9 +606,28 @@ namespace {
 
 typedef void (*SymKernel)(NetDesc, BoundArgs, SymCfg);
 
-template <int NT, int TM, bool PAIR = false>
+template <int NT, int TM, bool PAIR = false, int PG = 1>
 SymKernel sym_ptr() {
-  return fa_sym_kernel<NT, TM, PAIR>;
+  return fa_sym_kernel<NT, TM, PAIR, PG>;
+}
+
+// several boxes per MFMA tile for narrow networks (FAIRIFY_SYM_PACK=0 turns it off for A/B runs)
+bool use_pack() {
+  static const bool v = [] {
+    const char* e = getenv("FAIRIFY_SYM_PACK");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
+SymKernel select_packed(int pg) {
+  switch (pg) {
+    case 2: return sym_ptr<1, 1, true, 2>();
+    case 3: return sym_ptr<1, 1, true, 3>();
+    case 4: return sym_ptr<1, 1, true, 4>();
+    case 5: return sym_ptr<1, 1, true, 5>();
+    default: return nullptr;
+  }
 }
 
 // two box rows per wave for single-tile networks (FAIRIFY_SYM_PAIR=0 turns it off for A/B runs)
@@ -597,27 +712,52 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
   TM = std::max(TM, (net.dims[net.n_layers] + 15) / 16);
   SymKernel k = select_kernel(NT, TM);
   if (!k) return 0;
+  const bool pair0 = k == sym_ptr<1, 1, true>();
+  // packed narrow networks: pack_g boxes per tile, block-diagonal weights (NetDesc.pack_*)
+  const int pg = (pair0 && net.pack_g > 1 && net.dims[0] <= 16 && use_pack()) ? net.pack_g : 1;
+  if (pg > 1) k = select_packed(pg);
+  if (!k) return 0;
   int off = 0;
-  for (int l = 0; l < net.n_layers; ++l) {
-    cfg.w_lds[l] = off;
-    off += ((net.dims[l] + 15) / 16) * ((net.dims[l + 1] + 15) / 16) * 256;
+  if (pg > 1) {
+    cfg.w_lds[0] = 0;
+    off = pg * 256;
+    for (int l = 1; l < net.n_layers; ++l) {
+      cfg.w_lds[l] = off;
+      off += 256;
+    }
+    for (int l = 0; l < net.n_layers; ++l) {
+      cfg.b_lds[l] = off;
+      off += pg * net.dims[l + 1];
+    }
+    off = ((off + 3) & ~3);
+    if (off != net.pack_floats) return -1;      // layout mismatch with the packed block
+    cfg.stage_off = net.pack_off;
+  } else {
+    for (int l = 0; l < net.n_layers; ++l) {
+      cfg.w_lds[l] = off;
+      off += ((net.dims[l] + 15) / 16) * ((net.dims[l + 1] + 15) / 16) * 256;
+    }
+    for (int l = 0; l < net.n_layers; ++l) {
+      cfg.b_lds[l] = off;
+      off += net.dims[l + 1];
+    }
+    off = ((off + 3) & ~3);
+    if (off != net.wperm_floats) return -1;       // layout mismatch with the pre-permuted block
+    cfg.stage_off = net.wperm_off;
   }
-  for (int l = 0; l < net.n_layers; ++l) {
-    cfg.b_lds[l] = off;
-    off += net.dims[l + 1];
-  }
-  off = ((off + 3) & ~3);
-  if (off != net.wperm_floats) return -1;       // layout mismatch with the pre-permuted block
+  cfg.stage_floats = off;
   off += FA_SYM_MAXC;                           // + column -> input-dim table (ints)
   cfg.lds_floats = off;
   int slab = 0;
   switch (NT) {
-    case 1: slab = SymSlab<1>::FLOATS; break;
+    case 1:
+      slab = pg == 2 ? SymSlab<1, 2>::FLOATS : pg == 3 ? SymSlab<1, 3>::FLOATS : pg == 4 ? SymSlab<1, 4>::FLOATS
+             : pg == 5 ? SymSlab<1, 5>::FLOATS : SymSlab<1>::FLOATS;
+      break;
     case 2: slab = SymSlab<2>::FLOATS; break;
     default: slab = SymSlab<3>::FLOATS; break;
   }
-  const bool pair = k == sym_ptr<1, 1, true>();   // two box rows per wave
-  const int threads = FA_THREADS, rows_per_block = (FA_THREADS / 64) * (pair ? 2 : 1);
+  const int threads = FA_THREADS, rows_per_block = (FA_THREADS / 64) * (pair0 ? 2 * pg : 1);
   const size_t bytes = (size_t)(off + (FA_THREADS / 64) * slab) * sizeof(float);
   if (bytes > 160 * 1024) return 0;
   // per (kernel, LDS bytes): raise the dynamic-LDS limit once and cache the occupancy

@@ -24,7 +24,9 @@ def _gamma(k: int) -> float:
     return ku / (1 - ku)
 
 
-def logits_with_error(mlp: MLP, X: np.ndarray):
+def logits_with_error(mlp: MLP, X: np.ndarray, with_magnitude: bool = False):
+    """fp64 logits, their rigorous rounding bound, and (``with_magnitude``) the magnitude bound
+    m = |W|^T m + |b| of the logit (m == 0 exactly <=> every term feeding it is exactly 0)."""
     h = np.asarray(X, dtype=np.float64)
     m = np.abs(h)
     e = np.zeros_like(h)
@@ -38,9 +40,16 @@ def logits_with_error(mlp: MLP, X: np.ndarray):
         m = m @ aw + np.abs(b64)
         if l < mlp.n_layers - 1:
             h = np.maximum(z, 0)
-            m = np.maximum(m, 0)
+            # certainly negative pre-activation (z + e < 0): the exact ReLU output is exactly 0,
+            # so that neuron carries no value, magnitude or error into the next layer
+            dead = z + e < 0
+            h[dead] = 0.0
+            m = np.where(dead, 0.0, m)
+            e = np.where(dead, 0.0, e)
         else:
             h = z
+    if with_magnitude:
+        return h[:, 0], e[:, 0] * 1.0001 + 1e-300, m[:, 0]
     return h[:, 0], e[:, 0] * 1.0001 + 1e-300
 
 
@@ -66,9 +75,12 @@ def exact_signs(mlp: MLP, X: np.ndarray) -> np.ndarray:
     X = np.asarray(X)
     if X.shape[0] == 0:
         return np.zeros(0, dtype=np.int64)
-    z, e = logits_with_error(mlp, X)
+    z, e, m = logits_with_error(mlp, X, with_magnitude=True)
     s = np.sign(z).astype(np.int64)
-    amb = np.abs(z) <= e
+    # m == 0: products of fp32 weights and integers are exact in fp64 and sums of non-negative
+    # terms round to 0 only when every term is 0, so the exact logit is 0 (no Fraction needed)
+    s[m == 0.0] = 0
+    amb = (np.abs(z) <= e) & (m != 0.0)
     for i in np.nonzero(amb)[0]:
         v = exact_logit_fraction(mlp, X[i])
         s[i] = (v > 0) - (v < 0)

@@ -36,6 +36,48 @@ def mfma_weight_block(weights, biases) -> np.ndarray:
     return np.concatenate([out, np.zeros((-len(out)) % 4, np.float32)])
 
 
+def pack_groups(dims) -> int:
+    """Boxes packed per 16-row MFMA tile by the symbolic kernel for narrow single-tile networks
+    (csrc/symbolic.hip, ``PG``): inputs <= 16, every hidden layer <= 8 wide -> floor(16 / widest
+    hidden layer), at most 5.  Must equal ``Net::pack_g`` in csrc/bindings.cpp."""
+    dims = list(dims)
+    L = len(dims) - 1
+    if L < 2 or dims[0] > 16 or max(dims) > 16:
+        return 1
+    mh = max(dims[1:L])
+    return min(5, 16 // mh) if mh <= 8 else 1
+
+
+def mfma_packed_block(weights, biases, G: int) -> np.ndarray:
+    """Block-diagonal weights of G boxes per tile (narrow networks, csrc/symbolic.hip ``PG``), MFMA
+    operand order [t][lane][i] = W[16t + 4(lane>>4) + i][lane&15] per tile:
+
+    * layer 0: G tiles, tile g = W_0 (n0 x w_1) at rows 0.., columns g*w_1.. (box g's inputs feed
+      its own output rows);
+    * layer l >= 1: one tile, kron(I_G, W_l) (G*w_l x G*w_{l+1});
+    * then every layer's bias tiled G times; total padded to 4 floats."""
+    lane = np.arange(64)
+    t_, ln, i_ = np.meshgrid(np.arange(1), lane, np.arange(4), indexing="ij")
+
+    def tile(M):
+        T = np.zeros((16, 16), np.float32)
+        T[:M.shape[0], :M.shape[1]] = M
+        return T[4 * (ln >> 4) + i_, ln & 15].reshape(-1)
+
+    parts = []
+    W0 = np.asarray(weights[0], np.float32)
+    n0, w1 = W0.shape
+    for g in range(G):
+        M = np.zeros((n0, G * w1), np.float32)
+        M[:, g * w1:(g + 1) * w1] = W0
+        parts.append(tile(M))
+    for W in weights[1:]:
+        parts.append(tile(np.kron(np.eye(G, dtype=np.float32), np.asarray(W, np.float32))))
+    parts += [np.tile(np.asarray(b, np.float32).reshape(-1), G) for b in biases]
+    out = np.concatenate(parts)
+    return np.concatenate([out, np.zeros((-len(out)) % 4, np.float32)])
+
+
 class Backend:
     def __init__(self, mlp: MLP, device="cpu", dtype=torch.float32):
         self.mlp = mlp
@@ -52,6 +94,9 @@ class Backend:
             flat = np.concatenate([np.concatenate([w.reshape(-1), b]) for w, b in zip(mlp.weights, mlp.biases)])
             flat = np.concatenate([flat.astype(np.float32), np.zeros((-len(flat)) % 4, np.float32),
                                    mfma_weight_block(mlp.weights, mlp.biases)])
+            G = pack_groups([mlp.n_in] + mlp.widths)
+            if G > 1:
+                flat = np.concatenate([flat, mfma_packed_block(mlp.weights, mlp.biases, G)])
             self.flat = torch.from_numpy(flat).to(self.device)
             dims = [mlp.n_in] + mlp.widths
             self.dims = torch.tensor(dims, dtype=torch.int32)

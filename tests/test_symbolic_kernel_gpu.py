@@ -29,6 +29,12 @@ SHAPES = [
     (12, [32, 32], (3, 4)),            # two folded dims
     (16, [150, 100, 50], (0,)),        # BM-4: NT=2, TM=10 (scratch-backed operand tiles)
     (13, [150, 20], (8,)),             # NT=1, TM=10
+    # packed narrow networks (PG boxes per MFMA tile, block-diagonal weights)
+    (13, [3, 3, 3, 3], (8,)),          # AC-9: PG=5
+    (13, [5, 5], (7,)),                # AC-8: PG=3
+    (6, [4, 4, 4], (3,)),              # PG=4
+    (13, [8, 8, 8], (8,)),             # PG=2
+    (13, [5, 1, 5], (8,)),             # PG=3 with a 1-wide hidden layer
 ]
 
 
@@ -71,7 +77,7 @@ def test_symbolic_kernel_matches_reference(cuda, n0, hidden, fold):
     assert rg.dead is not None
 
 
-@pytest.mark.parametrize("n0,hidden,fold", [SHAPES[0], SHAPES[5], SHAPES[7]])
+@pytest.mark.parametrize("n0,hidden,fold", [SHAPES[0], SHAPES[3], SHAPES[5], SHAPES[7], SHAPES[12]])
 def test_symbolic_kernel_forced_dead(cuda, n0, hidden, fold):
     m = random_mlp(n0, hidden, seed=11, bias_scale=0.3)
     lo, hi = _boxes(n0, 128, 7, fold)
@@ -83,7 +89,8 @@ def test_symbolic_kernel_forced_dead(cuda, n0, hidden, fold):
     assert torch.allclose(rg.out_ub.cpu(), rc.out_ub, rtol=1e-4, atol=1e-4 * scale)
 
 
-@pytest.mark.parametrize("n0,hidden", [(13, [100, 100]), (13, [16, 8]), (20, [50]), (6, [16, 8])])
+@pytest.mark.parametrize("n0,hidden", [(13, [100, 100]), (13, [16, 8]), (20, [50]), (6, [16, 8]), (13, [5, 5, 5]),
+                                       (6, [3, 3])])
 def test_symbolic_kernel_sound_vs_bruteforce(cuda, n0, hidden):
     m = random_mlp(n0, hidden, seed=3, bias_scale=0.5)
     g = np.random.default_rng(4)
@@ -192,3 +199,35 @@ def test_crown_kernel_sound_vs_bruteforce(cuda, n0, hidden):
         Uf = pts @ r.Uc[0].double().cpu().numpy() + float(r.U0[0]) + float(r.Ue[0])
         assert np.all(z >= Lf - 1e-9) and np.all(z <= Uf + 1e-9)
         assert z.min() >= float(r.out_lb[0]) and z.max() <= float(r.out_ub[0])
+
+
+@pytest.mark.parametrize("name", ["AC-8", "AC-12", "AC-9"])
+def test_packed_native_bab_matches_bruteforce(cuda, name):
+    """Narrow nets through the native BaB (packed symbolic kernel, node-row expansion): every
+    decided verdict equals exhaustive enumeration of the partition's lattice points."""
+    from fairify_amd import presets
+    from fairify_amd.engine.bab import SAT, UNSAT, BaBConfig, BaBSolver
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.partition import processing_order
+
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    m = get_model(name, weights="random", seed=1)
+    be = Backend(m, cuda)
+    ids = processing_order(grid, 0)[:64]
+    lo, hi = grid.decode(ids)
+    # shrink the boxes so enumeration stays cheap (<= 2 values per free dim)
+    hi = np.minimum(hi, lo + 1)
+    res = BaBSolver(be, q, BaBConfig(node_budget=4096)).solve(lo, hi, m)
+    pa = q.pa_idx[0]
+    for k in range(len(ids)):
+        pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[k], hi[k])])))
+        pts = pts[pts[:, pa] == lo[k, pa]] if lo[k, pa] == hi[k, pa] else pts
+        z0 = m.logits(np.where(np.arange(m.n_in) == pa, 0, pts))
+        z1 = m.logits(np.where(np.arange(m.n_in) == pa, 1, pts))
+        # the query's post-condition: strictly opposite logit signs (an exact 0 is neither)
+        viol = bool((((z0 > 0) & (z1 < 0)) | ((z0 < 0) & (z1 > 0))).any())
+        if res.status[k] == SAT:
+            assert viol, k
+        elif res.status[k] == UNSAT:
+            assert not viol, k
