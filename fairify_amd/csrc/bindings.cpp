@@ -90,14 +90,12 @@ struct Net {
     if (d.n_layers >= 2 && dims[0] <= 16 && mw <= 16) {
       int mh = 0;
       for (int l = 1; l < d.n_layers; ++l) mh = std::max(mh, dims[l]);
-      if (mh <= 8) d.pack_g = std::min(5, 16 / mh);
+      d.pack_g = mh <= 4 ? 4 : (mh <= 8 ? 2 : 1);   // box stride 16 / pack_g: a multiple of 4
     }
     d.pack_off = total_floats;
     d.pack_floats = 0;
     if (d.pack_g > 1) {
-      int pf = d.pack_g * 256 + (d.n_layers - 1) * 256;
-      for (int l = 0; l < d.n_layers; ++l) pf += d.pack_g * dims[l + 1];
-      d.pack_floats = (pf + 3) & ~3;
+      d.pack_floats = d.pack_g * 256 + (d.n_layers - 1) * 256 + d.n_layers * 16;
       total_floats += d.pack_floats;
     }
   }

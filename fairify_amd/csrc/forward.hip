@@ -23,9 +23,11 @@
 #define FA_TR 64
 
 // rows [FA_TR][S] in bufA (cols 0..n0-1) -> logits in zout[FA_TR]; bufA/bufB clobbered.
+// counts (optional): per-neuron activation counts over the valid rows, restricted to the rows
+// with count_rows[r] != 0 when count_rows is given.
 __device__ void fa_tile_forward(const NetDesc& net, const float* __restrict__ flat, float* bufA, float* bufB,
                                 int S, int nvalid, const uint8_t* __restrict__ dead_rows, int dead_stride,
-                                int* counts, float* zout) {
+                                int* counts, float* zout, const uint8_t* count_rows = nullptr) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -65,7 +67,7 @@ __device__ void fa_tile_forward(const NetDesc& net, const float* __restrict__ fl
         if (jval) {
           if (last) zout[r] = v;
           else bufB[r * S + j] = v;
-          cnt += (r < nvalid && v != 0.f) ? 1 : 0;
+          cnt += (r < nvalid && v != 0.f && (!count_rows || count_rows[r])) ? 1 : 0;
         }
       }
       if (counts) {
@@ -168,6 +170,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_kernel(NetDesc net, SimArgs
   float* s_hi = s_lo + n0;
   int* cnt = (int*)(s_hi + n0);             // [n_neurons]
   int* best = cnt + net.n_neurons;          // [1]
+  uint8_t* cmatch = reinterpret_cast<uint8_t*>(best + 4);   // [FA_TR] sampled PA tuple == values[v]
   const int64_t pid = a.pids[p];
   for (int i = tid; i < n0; i += FA_THREADS) {
     s_lo[i] = a.lo[(size_t)p * n0 + i];
@@ -186,9 +189,12 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_kernel(NetDesc net, SimArgs
       bufA[r * S + d] = v;
     }
     __syncthreads();
-    // profile pass (reference semantics: the sampled PA value)
-    fa_tile_forward(net, a.flat, bufA, bufB, S, nvalid, nullptr, 0, cnt, zt);
-    // falsification: every PA assignment (x) and, for relaxed queries, every x' variant
+    // falsification: every PA assignment (x) and, for relaxed queries, every x' variant.  The
+    // profile (reference semantics: activation counts at the SAMPLED point) needs no pass of its
+    // own: the values table holds every PA tuple of the box, so each sampled row equals exactly
+    // one PA-assignment row of the first pass, whose activations are counted for it
+    // (count_rows = cmatch) -- bitwise the same inputs, so the same counts with one forward pass
+    // per tile fewer.
     const int passes = a.nra > 0 ? 2 : 1;
     for (int ps = 0; ps < passes; ++ps) {
       for (int v = 0; v < a.V; ++v) {
@@ -206,9 +212,16 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_kernel(NetDesc net, SimArgs
           }
           bufA[r * S + d] = val;
         }
+        if (ps == 0)
+          for (int r = tid; r < FA_TR; r += FA_THREADS) {
+            bool m = true;
+            for (int k = 0; k < a.npa; ++k) m = m && X[r * n0 + a.pa_idx[k]] == (float)a.values[v * a.npa + k];
+            cmatch[r] = m ? 1 : 0;
+          }
         __syncthreads();
         float* zdst = (ps == 0) ? z : zp;
-        fa_tile_forward(net, a.flat, bufA, bufB, S, nvalid, nullptr, 0, nullptr, zt);
+        fa_tile_forward(net, a.flat, bufA, bufB, S, nvalid, nullptr, 0, ps == 0 ? cnt : nullptr, zt,
+                        ps == 0 ? cmatch : nullptr);
         for (int r = tid; r < FA_TR; r += FA_THREADS) zdst[r * a.V + v] = zt[r];
         __syncthreads();
       }
@@ -252,7 +265,7 @@ extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) 
   a.S = net.max_width | 1;
   const int n0 = net.dims[0];
   size_t floats = 2 * (size_t)FA_TR * a.S + (size_t)FA_TR * n0 + 2 * (size_t)FA_TR * a.V + FA_TR + 2 * n0;
-  size_t bytes = floats * sizeof(float) + (net.n_neurons + 4) * sizeof(int);
+  size_t bytes = floats * sizeof(float) + (net.n_neurons + 4) * sizeof(int) + FA_TR;
   bytes = (bytes + 15) & ~(size_t)15;
   if (bytes > 160 * 1024) return -1;
   if (bytes > 64 * 1024)

@@ -85,9 +85,11 @@ struct SymSlab {
 // once, the new form rows are reloaded in MFMA operand layout into (nu, nlo).  Returns false on
 // the last layer (outputs written, nothing to reload).
 //
-// Packed mode (PG > 1, narrow networks): tile row `col` of group tsub is neuron col % w of box
-// tsub * PG + col / w of the wave pass (w = the layer's width, rows PG * w .. 15 are padding);
-// the wave's boxes are consecutive rows r_in + b.
+// Packed mode (PG > 1, narrow networks): tile row `col` of group tsub is neuron col % S of box
+// tsub * PG + col / S of the wave pass, S = 16 / PG (a multiple of 4, so a box's K terms fill
+// the MFMA K steps exactly as in the unpacked kernel: bitwise the same bounds whatever boxes
+// share the tile); rows j >= the layer's width are padding; the wave's boxes are consecutive
+// rows r_in + b.
 template <int NT, bool PAIR, int PG = 1>
 __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
                                                 const float* smem, float* T, const float* bxv_in, const int* cdim_s,
@@ -113,14 +115,15 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
   // two tiles are the same neurons of two box rows (r_in, r2), each with its own box values
   const int tsub = lane >> 5;
   const bool second = PAIR && tsub;
-  const int gbox = PG > 1 ? col / n_out : 0;            // packed: box of this tile row in its group
+  constexpr int PS = 16 / PG;                            // packed: rows per box
+  const int gbox = PG > 1 ? col / PS : 0;                // packed: box of this tile row in its group
   const int bidx = tsub * PG + gbox;                     // packed: box index within the wave pass
   const int r = PG > 1 ? r_in + bidx : (second ? r2 : r_in);
   const int node = PG > 1 ? (a.V > 0 ? r / a.V : r) : (second ? node2 : node_in);
   const float* bxv = bxv_in + (PG > 1 ? bidx : (second ? 1 : 0)) * SymSlab<NT, PG>::BOX;
   const int jt = PAIR ? jt0 : jt0 + tsub;
   const int n_out_t = net.dims[l + 1];
-  const bool nl_act = PG > 1 ? (gbox < PG && r < a.R) : (16 * jt < n_out_t && (!second || v2));
+  const bool nl_act = PG > 1 ? r < a.R : (16 * jt < n_out_t && (!second || v2));
   const int ob = (lane >> 4) & 1;
   float* Trow = T + tsub * SymSlab<NT>::TILE1 + (ob * 16 + col) * TS;
     // ---------------- spill both tiles: T[tile][block][neuron][column]
@@ -135,15 +138,15 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
         }
     __builtin_amdgcn_wave_barrier();
     // ---------------- one lane per (tile, neuron, block): bounds, relaxation, new form row
-    const int j = PG > 1 ? col - gbox * n_out : 16 * jt + col;   // neuron within its box
-    const bool jv = PG > 1 ? gbox < PG : j < n_out;
+    const int j = PG > 1 ? col - gbox * PS : 16 * jt + col;   // neuron within its box
+    const bool jv = j < n_out;
     float v[16 * NT];
 #pragma unroll
     for (int q = 0; q < 4 * NT; ++q) {
       const float4 x = reinterpret_cast<const float4*>(Trow)[q];
       v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
     }
-    const float b = jv ? sb[PG > 1 ? col : j] : 0.f;       // packed biases: tiled PG times
+    const float b = jv ? sb[PG > 1 ? col : j] : 0.f;       // packed biases: 16 per layer, box g at g * PS
     // concretisation of the coefficient part over the box (Σ min, Σ max, Σ |c| m); padding
     // columns hold 0 coefficients and a [0, 0] box, so they add exact zeros
     float mn = 0.f, mx = 0.f, mg = 0.f;
@@ -286,7 +289,7 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
 #ifndef FA_SYM_TIMING_NO_EPILOGUE
   if (PG > 1 && l == 0) {
     // packed layer 0: group u accumulates its PG boxes, box g through tile g of the packed W_0
-    // (W_0 placed at output rows g * w_1 ..), K = the box's own input dims
+    // (W_0 placed at output rows g * 16 / PG ..), K = the box's own input dims
     const float* boxtab = bxv + 2 * PG * SymSlab<NT, PG>::BOX;   // [2 PG][lo 16 | hi 16]
     const float g0 = net.g_gemm[0];
     const int n0v = net.dims[0];
@@ -469,9 +472,14 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
 
 // Minimum waves per SIMD the register allocator must leave room for (VGPR budget 512 / waves):
 // the paired single-tile kernel needed 180 VGPRs (2 waves/SIMD) and the 4-tile kernel 260 (1 wave),
-// both spill-free at 3 / 2 waves (167 / 242 VGPRs); the 7-tile kernel keeps 366 (its operand
-// ping-pong alone is 112 VGPRs) -- tighter limits spill to scratch.
-#define FA_SYM_WAVES_PER_EU(NT, TM, PAIR) ((PAIR) ? 3 : ((TM) == 2 ? 3 : ((TM) == 4 ? 2 : 1)))
+// both spill-free at 3 / 2 waves (167 / 242 VGPRs).  The 7-tile kernel (366 VGPRs, its operand
+// ping-pong alone is 112) at 2 waves spills 284 B/lane to scratch and still wins where LDS allows
+// a second block: AC-2 1.56 -> 0.99 ms per 131 072 rows; AC-4 (63 KB of staged W) is LDS-bound
+// at one block per CU either way (tools/ab_micro.sh, profiles/r2/s3/).
+#ifndef FA_SYM_WPE7
+#define FA_SYM_WPE7 2
+#endif
+#define FA_SYM_WAVES_PER_EU(NT, TM, PAIR) ((PAIR) ? 3 : ((TM) == 2 ? 3 : ((TM) == 4 ? 2 : ((TM) == 7 ? FA_SYM_WPE7 : 1))))
 
 template <int NT, int TM, bool PAIR, int PG = 1>
 __global__ void __launch_bounds__(FA_THREADS) __attribute__((amdgpu_waves_per_eu(FA_SYM_WAVES_PER_EU(NT, TM, PAIR))))
@@ -623,9 +631,7 @@ bool use_pack() {
 SymKernel select_packed(int pg) {
   switch (pg) {
     case 2: return sym_ptr<1, 1, true, 2>();
-    case 3: return sym_ptr<1, 1, true, 3>();
     case 4: return sym_ptr<1, 1, true, 4>();
-    case 5: return sym_ptr<1, 1, true, 5>();
     default: return nullptr;
   }
 }
@@ -727,9 +733,8 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
     }
     for (int l = 0; l < net.n_layers; ++l) {
       cfg.b_lds[l] = off;
-      off += pg * net.dims[l + 1];
+      off += 16;
     }
-    off = ((off + 3) & ~3);
     if (off != net.pack_floats) return -1;      // layout mismatch with the packed block
     cfg.stage_off = net.pack_off;
   } else {
@@ -751,8 +756,7 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
   int slab = 0;
   switch (NT) {
     case 1:
-      slab = pg == 2 ? SymSlab<1, 2>::FLOATS : pg == 3 ? SymSlab<1, 3>::FLOATS : pg == 4 ? SymSlab<1, 4>::FLOATS
-             : pg == 5 ? SymSlab<1, 5>::FLOATS : SymSlab<1>::FLOATS;
+      slab = pg == 2 ? SymSlab<1, 2>::FLOATS : pg == 4 ? SymSlab<1, 4>::FLOATS : SymSlab<1>::FLOATS;
       break;
     case 2: slab = SymSlab<2>::FLOATS; break;
     default: slab = SymSlab<3>::FLOATS; break;

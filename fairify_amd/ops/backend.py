@@ -38,44 +38,55 @@ def mfma_weight_block(weights, biases) -> np.ndarray:
 
 def pack_groups(dims) -> int:
     """Boxes packed per 16-row MFMA tile by the symbolic kernel for narrow single-tile networks
-    (csrc/symbolic.hip, ``PG``): inputs <= 16, every hidden layer <= 8 wide -> floor(16 / widest
-    hidden layer), at most 5.  Must equal ``Net::pack_g`` in csrc/bindings.cpp."""
+    (csrc/symbolic.hip, ``PG``): inputs <= 16 and every hidden layer <= 8 wide.  Box g owns tile
+    rows g*S .. g*S+S-1 with S = 16 / PG a multiple of 4, so every box's K terms fall into the
+    MFMA's 4-wide K steps exactly as an unpacked box's do: a box's bounds are bitwise those of the
+    unpacked kernel and never depend on which boxes share its tile (node order in the BaB pool
+    follows device atomics).  Widest hidden layer <= 4 -> 4 boxes, <= 8 -> 2.  Must equal
+    ``Net::pack_g`` in csrc/bindings.cpp."""
     dims = list(dims)
     L = len(dims) - 1
     if L < 2 or dims[0] > 16 or max(dims) > 16:
         return 1
     mh = max(dims[1:L])
-    return min(5, 16 // mh) if mh <= 8 else 1
+    return 4 if mh <= 4 else (2 if mh <= 8 else 1)
 
 
 def mfma_packed_block(weights, biases, G: int) -> np.ndarray:
     """Block-diagonal weights of G boxes per tile (narrow networks, csrc/symbolic.hip ``PG``), MFMA
-    operand order [t][lane][i] = W[16t + 4(lane>>4) + i][lane&15] per tile:
+    operand order [t][lane][i] = W[16t + 4(lane>>4) + i][lane&15] per tile, box stride S = 16 / G:
 
-    * layer 0: G tiles, tile g = W_0 (n0 x w_1) at rows 0.., columns g*w_1.. (box g's inputs feed
+    * layer 0: G tiles, tile g = W_0 (n0 x w_1) at rows 0.., columns g*S.. (box g's inputs feed
       its own output rows);
-    * layer l >= 1: one tile, kron(I_G, W_l) (G*w_l x G*w_{l+1});
-    * then every layer's bias tiled G times; total padded to 4 floats."""
+    * layer l >= 1: one tile, W_l at rows g*S.., columns g*S.. for every box g;
+    * then 16 bias floats per layer (b_l at g*S.. for every box g)."""
     lane = np.arange(64)
     t_, ln, i_ = np.meshgrid(np.arange(1), lane, np.arange(4), indexing="ij")
+    S = 16 // G
 
     def tile(M):
-        T = np.zeros((16, 16), np.float32)
-        T[:M.shape[0], :M.shape[1]] = M
-        return T[4 * (ln >> 4) + i_, ln & 15].reshape(-1)
+        return M[4 * (ln >> 4) + i_, ln & 15].reshape(-1)
 
     parts = []
     W0 = np.asarray(weights[0], np.float32)
     n0, w1 = W0.shape
     for g in range(G):
-        M = np.zeros((n0, G * w1), np.float32)
-        M[:, g * w1:(g + 1) * w1] = W0
+        M = np.zeros((16, 16), np.float32)
+        M[:n0, g * S:g * S + w1] = W0
         parts.append(tile(M))
     for W in weights[1:]:
-        parts.append(tile(np.kron(np.eye(G, dtype=np.float32), np.asarray(W, np.float32))))
-    parts += [np.tile(np.asarray(b, np.float32).reshape(-1), G) for b in biases]
-    out = np.concatenate(parts)
-    return np.concatenate([out, np.zeros((-len(out)) % 4, np.float32)])
+        W = np.asarray(W, np.float32)
+        M = np.zeros((16, 16), np.float32)
+        for g in range(G):
+            M[g * S:g * S + W.shape[0], g * S:g * S + W.shape[1]] = W
+        parts.append(tile(M))
+    for b in biases:
+        pb = np.zeros(16, np.float32)
+        b = np.asarray(b, np.float32).reshape(-1)
+        for g in range(G):
+            pb[g * S:g * S + b.size] = b
+        parts.append(pb)
+    return np.concatenate(parts)
 
 
 class Backend:

@@ -63,3 +63,44 @@ def test_concurrent_streams_match_serial(cuda):
         for ra, rb in zip(a, b):
             if ra["verdict"] == "sat":
                 assert np.array_equal(ra["c1"], rb["c1"]) and np.array_equal(ra["c2"], rb["c2"])
+
+
+@pytest.mark.parametrize("hidden", [[5, 5], [5] * 9, [3, 3, 3, 3], [8, 4, 8], [16, 8]])
+def test_symbolic_bounds_independent_of_row_position(cuda, hidden):
+    """A box's bounds must not depend on which rows share its wave / MFMA tile (the packed
+    narrow-network kernel puts several boxes in one tile, and BaB node order follows device
+    atomics): a permuted batch gives bitwise the same bounds per box."""
+    m = random_mlp(13, hidden, seed=len(hidden), bias_scale=0.3)
+    be = Backend(m, cuda)
+    g = torch.Generator().manual_seed(1)
+    R = 1003
+    lo = torch.randint(0, 20, (R, 13), generator=g).float()
+    hi = lo + torch.randint(0, 5, (R, 13), generator=g).float()
+    hi[:, 8] = lo[:, 8]
+    perm = torch.randperm(R, generator=g)
+    a = be.bounds(lo.to(cuda), hi.to(cuda), mode="symbolic", fold=(8,), keep_layers=True)
+    b = be.bounds(lo[perm].to(cuda), hi[perm].to(cuda), mode="symbolic", fold=(8,), keep_layers=True)
+    inv = torch.argsort(perm).to(cuda)
+    for x, y in ((a.out_lb, b.out_lb), (a.out_ub, b.out_ub), (a.Lc, b.Lc), (a.Uc, b.Uc), (a.L0, b.L0),
+                 (a.Ue, b.Ue)):
+        assert torch.equal(x, y[inv])
+    for x, y in zip(a.layer_ub, b.layer_ub):
+        assert torch.equal(x, y[inv])
+
+
+def test_bab_verdicts_independent_of_chunk_composition(cuda):
+    """The same partitions verified in one chunk and split over two chunks (different node pools,
+    other partitions' nodes interleaved) give identical verdicts and counterexamples."""
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, 0)[:1024]
+    cfg = VerifyConfig(sim_size=256, node_budget=512, escalate_budget=4096, escalate_max_open=256,
+                       smt_backend="none")
+    for name in ("AC-12", "AC-8", "AC-9"):
+        m = get_model(name, weights="random", seed=0)
+        be = Backend(m, cuda)
+        whole = verify_chunk(be, m, q, grid, ids, cfg)
+        parts = [verify_chunk(be, m, q, grid, ids[k::2], cfg) for k in range(2)]
+        v = np.empty(len(ids), dtype=object)
+        v[0::2], v[1::2] = parts[0].cols["verdict"], parts[1].cols["verdict"]
+        assert list(v) == list(whole.cols["verdict"]), name
