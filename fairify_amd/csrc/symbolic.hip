@@ -475,14 +475,27 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
 // both spill-free at 3 / 2 waves (167 / 242 VGPRs).  The 7-tile kernel (366 VGPRs, its operand
 // ping-pong alone is 112) at 2 waves spills 284 B/lane to scratch and still wins where LDS allows
 // a second block: AC-2 1.56 -> 0.99 ms per 131 072 rows; AC-4 (63 KB of staged W) is LDS-bound
-// at one block per CU either way (tools/ab_micro.sh, profiles/r2/s3/).
+// at one block per CU, so its workgroups carry 8 waves (FA_SYM_BIG_THREADS): 3.98 -> 2.89 ms.  The
+// 4-tile kernel at 3 waves (244 B/lane scratch): AC-5 1.297 -> 1.237, AC-7 1.363 -> 1.292 ms
+// (tools/ab_micro.sh, profiles/r2/s3/).
 #ifndef FA_SYM_WPE7
 #define FA_SYM_WPE7 2
 #endif
-#define FA_SYM_WAVES_PER_EU(NT, TM, PAIR) ((PAIR) ? 3 : ((TM) == 2 ? 3 : ((TM) == 4 ? 2 : ((TM) == 7 ? FA_SYM_WPE7 : 1))))
+#ifndef FA_SYM_WPE4
+#define FA_SYM_WPE4 3
+#endif
+#define FA_SYM_WAVES_PER_EU(NT, TM, PAIR) \
+  ((PAIR) ? 3 : ((TM) == 2 ? 3 : ((TM) == 4 ? FA_SYM_WPE4 : ((TM) == 7 ? FA_SYM_WPE7 : 1))))
 
 template <int NT, int TM, bool PAIR, int PG = 1>
-__global__ void __launch_bounds__(FA_THREADS) __attribute__((amdgpu_waves_per_eu(FA_SYM_WAVES_PER_EU(NT, TM, PAIR))))
+// Threads per workgroup: the 7-tile kernel's staged W (AC-4: 63 KB) leaves LDS for one workgroup
+// per CU, so it runs 8 waves per workgroup (2 per SIMD, its VGPR limit) instead of 4.
+#ifndef FA_SYM_BIG_THREADS
+#define FA_SYM_BIG_THREADS 512
+#endif
+#define FA_SYM_THREADS(TM) ((TM) == 7 ? FA_SYM_BIG_THREADS : FA_THREADS)
+
+__global__ void __launch_bounds__(FA_SYM_THREADS(TM)) __attribute__((amdgpu_waves_per_eu(FA_SYM_WAVES_PER_EU(NT, TM, PAIR))))
 fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
   constexpr int TMS = PAIR ? 2 : TM;   // operand slots: K tiles, or (PAIR) the wave's two boxes /
                                        // (packed) two groups of PG boxes
@@ -493,15 +506,15 @@ fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
   {
     const float4* src = reinterpret_cast<const float4*>(a.flat + cfg.stage_off);
     float4* dst = reinterpret_cast<float4*>(smem);
-    for (int e = tid; e < (cfg.stage_floats >> 2); e += FA_THREADS) dst[e] = src[e];
+    for (int e = tid; e < (cfg.stage_floats >> 2); e += FA_SYM_THREADS(TM)) dst[e] = src[e];
   }
   int* cdim_s = reinterpret_cast<int*>(smem + cfg.lds_floats - FA_SYM_MAXC);
-  for (int c = tid; c < FA_SYM_MAXC; c += FA_THREADS) cdim_s[c] = c < cfg.nc ? cfg.cdim[c] : -1;
+  for (int c = tid; c < FA_SYM_MAXC; c += FA_SYM_THREADS(TM)) cdim_s[c] = c < cfg.nc ? cfg.cdim[c] : -1;
   __syncthreads();
   const int lane = tid & 63;
   const int grp = lane >> 4;
   const int wave = tid >> 6;
-  const int nw = FA_THREADS / 64;
+  const int nw = FA_SYM_THREADS(TM) / 64;
   const int n0 = net.dims[0];
   const int nc = cfg.nc;
   const float g0 = net.g_gemm[0];
@@ -761,8 +774,9 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
     case 2: slab = SymSlab<2>::FLOATS; break;
     default: slab = SymSlab<3>::FLOATS; break;
   }
-  const int threads = FA_THREADS, rows_per_block = (FA_THREADS / 64) * (pair0 ? 2 * pg : 1);
-  const size_t bytes = (size_t)(off + (FA_THREADS / 64) * slab) * sizeof(float);
+  const int threads = (k == sym_ptr<1, 7>()) ? FA_SYM_BIG_THREADS : FA_THREADS;
+  const int rows_per_block = (threads / 64) * (pair0 ? 2 * pg : 1);
+  const size_t bytes = (size_t)(off + (threads / 64) * slab) * sizeof(float);
   if (bytes > 160 * 1024) return 0;
   // per (kernel, LDS bytes): raise the dynamic-LDS limit once and cache the occupancy
   static std::mutex mu;
