@@ -122,22 +122,53 @@ __device__ __forceinline__ int fa_wave_incl_scan(int v, int lane) {
 __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs a) {
   __shared__ FaSplitPlan plan[FA_SPLIT_NB];
   __shared__ int child_off[FA_SPLIT_NB], cand_off[FA_SPLIT_NB];
+  // per-node scalars of the block's 64 nodes, fetched once by 64 threads in parallel: each wave
+  // then walks its 8 nodes from LDS instead of paying the dependent chain node -> partition ->
+  // status / budget reference (4 global round trips) once per node
+  __shared__ int s_part[FA_SPLIT_NB], s_ns[FA_SPLIT_NB], s_ws[FA_SPLIT_NB], s_bud[FA_SPLIT_NB];
+  __shared__ float s_pe[FA_SPLIT_NB][4];
+  __shared__ int8_t s_st[FA_SPLIT_NB];
+  __shared__ uint8_t s_open[FA_SPLIT_NB], s_leaf[FA_SPLIT_NB];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int n0 = a.n0;
   const int npair = a.norient * a.Pp;
+  if (threadIdx.x < FA_SPLIT_NB) {
+    const int t = threadIdx.x;
+    const int n = blockIdx.x * FA_SPLIT_NB + t;
+    uint8_t op = 0;
+    int p = 0;
+    if (n < a.Nn) {
+      op = a.open[n];
+      p = a.part[n];
+      s_leaf[t] = a.leaf[n];
+      s_pe[t][0] = a.pe_lb[n];
+      s_pe[t][1] = a.pe_ub[n];
+      s_pe[t][2] = a.pe_lb[a.Nn + n];
+      s_pe[t][3] = a.pe_ub[a.Nn + n];
+    }
+    s_open[t] = op;
+    s_part[t] = p;
+    if (op) {
+      s_st[t] = a.status[p];
+      s_ns[t] = a.nodes_start[p];
+      s_ws[t] = a.nodes_start[p] - a.prev_start[p];
+      s_bud[t] = a.pbudget ? a.pbudget[p] : a.budget;
+    }
+  }
+  __syncthreads();
   // ---------------- phase A: plan
   for (int i = 0; i < FA_SPLIT_NPW; ++i) {
     const int loc = wave * FA_SPLIT_NPW + i;
     const int n = blockIdx.x * FA_SPLIT_NB + loc;
     FaSplitPlan pl{0ull, 0ull, 0, 0, 0, 0, -1};
     do {
-      if (n >= a.Nn || !a.open[n]) break;                  // wave-uniform
-      const int p = a.part[n];
+      if (n >= a.Nn || !s_open[loc]) break;                // wave-uniform
+      const int p = s_part[loc];
       // RUNNING or STOPPING (budget ran out earlier in this same level): both still active
-      const int8_t s0 = a.status[p];
+      const int8_t s0 = s_st[loc];
       if (s0 != ST_RUNNING && s0 != ST_STOPPING) break;
-      if (a.leaf[n]) {   // every possible PA pair of the single lattice point goes to the host check
+      if (s_leaf[loc]) {   // every possible PA pair of the single lattice point goes to the host check
         pl.leaf = 1;
         for (int t0 = 0; t0 < npair; t0 += 64)
           pl.ncand += __popcll(__ballot(t0 + lane < npair && fa_leaf_poss(a, n, t0 + lane)));
@@ -145,8 +176,8 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
       }
       pl.part = p;   // counted in phase B: one open inner node of p in this level
       {
-        const float lbx = a.pe_lb[n], ubx = a.pe_ub[n];
-        const float lbp = a.pe_lb[a.Nn + n], ubp = a.pe_ub[a.Nn + n];
+        const float lbx = s_pe[loc][0], ubx = s_pe[loc][1];
+        const float lbp = s_pe[loc][2], ubp = s_pe[loc][3];
         pl.ncand = ((lbx < 0.f && ubp > 0.f) || (ubx > 0.f && lbp < 0.f)) ? 1 : 0;
       }
       // split along the top-m scored dimensions (2 n0 <= 128 scores: two per lane)
@@ -154,7 +185,7 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
       int mreq = 1;
       {
         const int mmax = a.m < FA_MAX_SPLIT ? a.m : FA_MAX_SPLIT;
-        const int w = a.nodes_start[p] - a.prev_start[p];  // this partition's nodes in the level
+        const int w = s_ws[loc];                           // this partition's nodes in the level
         while (mreq < mmax && ((long long)w << (mreq + 1)) <= (long long)a.target) ++mreq;
       }
       const int d0 = lane, d1 = lane + 64;
@@ -176,8 +207,8 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
       }
       if (m == 0) break;   // no splittable dimension: treated as leaf by the certificate
       {
-        const int bud = a.pbudget ? a.pbudget[p] : a.budget;
-        if (a.nodes_start[p] >= bud) {
+        const int bud = s_bud[loc];
+        if (s_ns[loc] >= bud) {
           if (a.prob && bud < a.budget2) {
             // inline escalation: on probation this level (children are made); fa_settle keeps
             // it going with budget2 if its open frontier of this level is small, else UNKNOWN
@@ -243,7 +274,7 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
     const int n = blockIdx.x * FA_SPLIT_NB + loc;
     const FaSplitPlan pl = plan[loc];
     if (pl.ncand == 0 && pl.nchild == 0) continue;         // wave-uniform (LDS broadcast)
-    const int p = a.part[n];
+    const int p = s_part[loc];
     const float* xl = a.xlo + (size_t)n * n0;
     const float* xh = a.xhi + (size_t)n * n0;
     const float* xpl = a.relaxed ? a.xplo + (size_t)n * n0 : xl;

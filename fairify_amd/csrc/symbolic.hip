@@ -71,7 +71,7 @@ struct SymBox {
 // per-wave LDS slab: tile staging T[2 blocks][16 neurons][TS] + box values [2 PG boxes][3][48]
 // (+ packed mode: the boxes' input ranges [2 PG][lo 16 | hi 16] for the on-the-fly layer-0 operands)
 template <int NT, int PG = 1>
-struct SymSlab {
+struct SymSlab {   // box values per column: [mid | rad | m] x FA_SYM_MAXC
   static constexpr int TS = 16 * NT + 4;                 // padded row stride (floats)
   static constexpr int TILE1 = 2 * 16 * TS;             // one 16-neuron tile, U and L blocks
   static constexpr int TILE = 2 * TILE1;                 // two tiles per epilogue pass
@@ -147,16 +147,21 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
       v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
     }
     const float b = jv ? sb[PG > 1 ? col : j] : 0.f;       // packed biases: 16 per layer, box g at g * PS
-    // concretisation of the coefficient part over the box (Σ min, Σ max, Σ |c| m); padding
-    // columns hold 0 coefficients and a [0, 0] box, so they add exact zeros
-    float mn = 0.f, mx = 0.f, mg = 0.f;
+    // concretisation of the coefficient part over the box in centre/radius form:
+    //   min / max = Σ v mid -+ Σ |v| rad,  magnitude Σ |v| m  (m >= |mid| + rad)
+    // three FMAs per column (|v| is a free source modifier) instead of two products, a min, a max
+    // and three adds; rounding: Σ v mid and Σ |v| rad carry gamma_nc each and the final
+    // subtraction / constant add two more roundings, within the gamma_{n0+3} of g_conc times the
+    // magnitude.  Padding columns hold 0 coefficients and a 0 box: exact zeros.
+    float s1 = 0.f, s2 = 0.f, mg = 0.f;
 #pragma unroll
     for (int c = 4; c < 16 * NT; ++c) {
-      const float p = v[c] * bxv[c], h = v[c] * bxv[FA_SYM_MAXC + c];
-      mn += fminf(p, h);
-      mx += fmaxf(p, h);
-      mg += fabsf(v[c]) * bxv[2 * FA_SYM_MAXC + c];
+      const float av = fabsf(v[c]);
+      s1 = fmaf(v[c], bxv[c], s1);
+      s2 = fmaf(av, bxv[FA_SYM_MAXC + c], s2);
+      mg = fmaf(av, bxv[2 * FA_SYM_MAXC + c], mg);
     }
+    float mn = s1 - s2, mx = s1 + s2;
     const float cr = v[0];
     float er = v[1], ivr = v[2], ier = v[3];
     const float sgn = ob ? -1.f : 1.f;            // L block: error columns stored negated
@@ -557,9 +562,18 @@ fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
         float* bv = bxv + bi * SymSlab<NT>::BOX;
         const int d = (lane >= 4 && lane - 4 < nc) ? cdim_s[lane - 4] : -1;
         const float l0 = d >= 0 ? bx.lo(d) : 0.f, h0 = d >= 0 ? bx.hi(d) : 0.f;
-        bv[lane] = l0;
-        bv[FA_SYM_MAXC + lane] = h0;
-        bv[2 * FA_SYM_MAXC + lane] = fmaxf(fabsf(l0), fabsf(h0));
+        // centre / radius / magnitude of the column's range: exact for lattice boxes (integers
+        // below 2^22); any other range is enclosed outward ([mid - rad, mid + rad] contains it and
+        // m >= |mid| + rad), which keeps every bound sound
+        float mid = 0.5f * (l0 + h0), rad = 0.5f * (h0 - l0), mm = fmaxf(fabsf(l0), fabsf(h0));
+        const bool lattice = l0 == rintf(l0) && h0 == rintf(h0) && fabsf(l0) < 4194304.f && fabsf(h0) < 4194304.f;
+        if (!lattice) {
+          rad = nextafterf(fmaxf(h0 - mid, mid - l0), INFINITY);
+          mm = nextafterf(fabsf(mid) + rad, INFINITY);
+        }
+        bv[lane] = mid;
+        bv[FA_SYM_MAXC + lane] = rad;
+        bv[2 * FA_SYM_MAXC + lane] = mm;
       }
       if (PG > 1 && lane < 32) {   // packed: the box's input ranges for the layer-0 operands
         const int d = lane & 15;
