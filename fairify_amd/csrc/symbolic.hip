@@ -80,27 +80,6 @@ struct SymSlab {   // box values per column: [mid | rad | m] x FA_SYM_MAXC
   static constexpr int FLOATS = (TILE + 2 * PG * BOX + BOXTAB + 3) & ~3;
 };
 
-// Centre / radius layer GEMM.  The operands of a layer are stored as C = (U + L) / 2 and
-// R = (U - L) / 2 of the previous layer's upper / lower rows (L rows carry their error columns
-// negated), so  U' = W+ U + W- L = W C + |W| R  and  L' = W+ L + W- U = W C - |W| R:  two MFMA
-// chains (P = W C, Q = |W| R; |w| is a free source modifier) instead of four.  Rounding: every
-// output term passes through at most n_in + 2 roundings (C/R formation, the n_in-term chain,
-// P +- Q), within the gamma_{2 n_in + 1} the error columns carry; the error columns are bounded
-// through the radius (P + Q recombines W+ eU + |W-| eL from (eU - eL)/2 and (eU + eL)/2, so its
-// rounding is bounded by 2 gamma Q rather than relatively: Q is added once more on the error
-// and interval-error columns, 1 and 3).  Each input row's error columns carry the rounding
-// budget of BOTH blocks (gamma (m_U + m_L), gamma max(iv_U, iv_L)) -- the radius couples them.
-__device__ __forceinline__ void fa_pq_to_ul(const f32x4& P, const f32x4& Q, int col, float gg, f32x4& U,
-                                            f32x4& L) {
-  const float sl = (col == 1 || col == 3) ? 2.f * gg : 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float q = Q[i], e = sl * fabsf(q);
-    U[i] = (P[i] + q) + e;
-    L[i] = (P[i] - q) - e;
-  }
-}
-
 // Epilogue of one 16-neuron output tile (accumulators U, Lq of tile jt): spill to the wave's
 // LDS slab, one lane per (neuron, block) computes the rigorous bounds and the ReLU relaxation
 // once, the new form rows are reloaded in MFMA operand layout into (nu, nlo).  Returns false on
@@ -127,10 +106,7 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
   const float gc = net.g_conc;
   const float gi = net.g_one;
   const float unit = net.unit;
-  // next layer's rounding budget: its centre / radius GEMM passes every term through at most
-  // n_in + 2 roundings (gamma_up(n_in + 1) = gamma_{n_in + 3} >= gamma_{n_in + 2}), charged on the
-  // magnitudes of BOTH blocks (m_U + m_L, max(iv_U, iv_L)): see fa_pq_to_ul
-  const float gnext = last ? 0.f : net.g_fwd[l + 1];
+  const float gnext = last ? 0.f : net.g_gemm[l + 1];
   const int noff = net.neuron_off[l];
   const int nc = cfg.nc;
   const int n0 = net.dims[0];
@@ -258,14 +234,11 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
       en = lam1 ? e : 0.f;
       mgn = lam1 ? mg : 0.f;
     }
-    // new row: constant, error, interval, interval error (L errors negated), scaled coefficients;
-    // the rounding budgets cover both blocks (centre / radius GEMM of the next layer)
-    const float mg_both = mgn + __shfl_xor(mgn, 16, 64);
-    const float iv_max = fmaxf(ivn, __shfl_xor(ivn, 16, 64));
+    // new row: constant, error, interval, interval error (L errors negated), scaled coefficients
     v[0] = cnew;
-    v[1] = sgn * (en + gnext * mg_both);
+    v[1] = sgn * (en + gnext * mgn);
     v[2] = ivn;
-    v[3] = sgn * (gnext * iv_max);
+    v[3] = sgn * (gnext * ivn);
 #pragma unroll
     for (int c = 4; c < 16 * NT; ++c) v[c] *= s;
     if (nl_act) {
@@ -274,17 +247,15 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
         reinterpret_cast<float4*>(Trow)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     }
     __builtin_amdgcn_wave_barrier();
-    // ---------------- reload both tiles in MFMA operand layout as centre / radius: next layer's B
+    // ---------------- reload both tiles in MFMA operand layout: next layer's B
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float xu = T[u * SymSlab<NT>::TILE1 + (4 * grp + i) * TS + ct * 16 + col];
-          const float xl = T[u * SymSlab<NT>::TILE1 + (16 + 4 * grp + i) * TS + ct * 16 + col];
-          nu[u][ct][i] = 0.5f * (xu + xl);
-          nlo[u][ct][i] = 0.5f * (xu - xl);
+          nu[u][ct][i] = T[u * SymSlab<NT>::TILE1 + (4 * grp + i) * TS + ct * 16 + col];
+          nlo[u][ct][i] = T[u * SymSlab<NT>::TILE1 + (16 + 4 * grp + i) * TS + ct * 16 + col];
         }
     __builtin_amdgcn_wave_barrier();
     return true;
@@ -330,9 +301,8 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
     f32x4 U[2][NT], Lq[2][NT];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      f32x4 Pa[NT], Qa[NT];
 #pragma unroll
-      for (int ct = 0; ct < NT; ++ct) Pa[ct] = Qa[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ct = 0; ct < NT; ++ct) U[u][ct] = Lq[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < PG; ++g) {
         const float* bt = boxtab + (u * PG + g) * 32;
@@ -345,30 +315,31 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
           const float xl = kv ? bt[k] : 0.f, xh = kv ? bt[16 + k] : 0.f;
           const bool folded = kv && ((cfg.fold >> k) & 1ull);
           const float m = fmaxf(fabsf(xl), fabsf(xh));
+          const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
 #pragma unroll
           for (int ct = 0; ct < NT; ++ct) {
             const int c = ct * 16 + col;
-            float vc = 0.f, vr = 0.f;            // centre / radius of the identity-form operand
+            float vu = 0.f, vl = 0.f;
             if (kv) {
               if (c >= 4) {
-                vc = (!folded && c - 4 < nc && cdim_s[c - 4] == k) ? 1.f : 0.f;
+                vu = vl = (!folded && c - 4 < nc && cdim_s[c - 4] == k) ? 1.f : 0.f;
               } else if (c == 0) {
-                vc = folded ? xl : 0.f;
+                vu = vl = folded ? xl : 0.f;
               } else if (c == 1) {
-                vr = g0 * m;
+                vu = g0 * m; vl = -vu;
               } else if (c == 2) {
-                vc = 0.5f * (xh + xl); vr = 0.5f * (xh - xl);
+                vu = xh; vl = xl;
               } else {
-                vc = 0.5f * g0 * (fabsf(xh) - fabsf(xl)); vr = 0.5f * g0 * (fabsf(xh) + fabsf(xl));
+                vu = g0 * fabsf(xh); vl = -(g0 * fabsf(xl));
               }
             }
-            Pa[ct] = fa_mfma4(wv[i], vc, Pa[ct]);
-            Qa[ct] = fa_mfma4(fabsf(wv[i]), vr, Qa[ct]);
+            U[u][ct] = fa_mfma4(wp, vu, U[u][ct]);
+            Lq[u][ct] = fa_mfma4(wp, vl, Lq[u][ct]);
+            U[u][ct] = fa_mfma4(wn, vl, U[u][ct]);
+            Lq[u][ct] = fa_mfma4(wn, vu, Lq[u][ct]);
           }
         }
       }
-#pragma unroll
-      for (int ct = 0; ct < NT; ++ct) fa_pq_to_ul(Pa[ct], Qa[ct], col, g0, U[u][ct], Lq[u][ct]);
     }
     float nu[2][NT][4], nlo[2][NT][4];
     if (!fa_sym_epilogue<NT, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
@@ -391,11 +362,11 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
     // form column; two cross-group butterflies finish the sum (any summation order stays within
     // the layer's gamma_{2 n_in + 1} bound).  W[k][0] is lane (grp*16) of the permuted block.
     constexpr int NB = PAIR ? 2 : 1;   // boxes carried by the wave
-    float sp[NB][NT], sq[NB][NT];      // W C and |W| R (centre / radius operands)
+    float su[NB][NT], sl[NB][NT];
 #pragma unroll
     for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
-      for (int ct = 0; ct < NT; ++ct) sp[bi][ct] = sq[bi][ct] = 0.f;
+      for (int ct = 0; ct < NT; ++ct) su[bi][ct] = sl[bi][ct] = 0.f;
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
       if (t >= tin) break;
@@ -403,13 +374,14 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
       const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
 #pragma unroll
         for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
           for (int ct = 0; ct < NT; ++ct) {
             const int bt = PAIR ? bi : t;
-            sp[bi][ct] = fmaf(wv[i], B[ct][bt][0][i], sp[bi][ct]);
-            sq[bi][ct] = fmaf(fabsf(wv[i]), B[ct][bt][1][i], sq[bi][ct]);
+            su[bi][ct] = fmaf(wp, B[ct][bt][0][i], fmaf(wn, B[ct][bt][1][i], su[bi][ct]));
+            sl[bi][ct] = fmaf(wp, B[ct][bt][1][i], fmaf(wn, B[ct][bt][0][i], sl[bi][ct]));
           }
       }
     }
@@ -420,14 +392,13 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
     for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
-        float xp = sp[bi][ct], xq = sq[bi][ct];
-        xp += __shfl_xor(xp, 16, 64);
-        xq += __shfl_xor(xq, 16, 64);
-        xp += __shfl_xor(xp, 32, 64);
-        xq += __shfl_xor(xq, 32, 64);
-        const f32x4 P1 = f32x4{grp == 0 ? xp : 0.f, 0.f, 0.f, 0.f};   // row 0 of tile bi = neuron 0
-        const f32x4 Q1 = f32x4{grp == 0 ? xq : 0.f, 0.f, 0.f, 0.f};
-        fa_pq_to_ul(P1, Q1, col, gg, U[bi][ct], Lq[bi][ct]);
+        float xu = su[bi][ct], xl = sl[bi][ct];
+        xu += __shfl_xor(xu, 16, 64);
+        xl += __shfl_xor(xl, 16, 64);
+        xu += __shfl_xor(xu, 32, 64);
+        xl += __shfl_xor(xl, 32, 64);
+        U[bi][ct] = f32x4{grp == 0 ? xu : 0.f, 0.f, 0.f, 0.f};     // row 0 of tile bi = neuron 0
+        Lq[bi][ct] = f32x4{grp == 0 ? xl : 0.f, 0.f, 0.f, 0.f};
       }
     float nu[2][NT][4], nlo[2][NT][4];
     fa_sym_epilogue<NT, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
@@ -442,32 +413,32 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int jt = jt0 + u;
-      f32x4 Pa[NT], Qa[NT];
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
-        Pa[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-        Qa[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        U[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        Lq[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if (!(PAIR ? (jt0 > 0) : (jt >= tout || jt >= TM))) {
-        const float4* wq = reinterpret_cast<const float4*>(sw) + (size_t)(PAIR ? 0 : jt) * tin * 64 + lane;
+      if (PAIR ? (jt0 > 0) : (jt >= tout || jt >= TM)) continue;
+      const float4* wq = reinterpret_cast<const float4*>(sw) + (size_t)(PAIR ? 0 : jt) * tin * 64 + lane;
 #pragma unroll
-        for (int t = 0; t < TM; ++t) {
-          if (t >= tin) break;
-          const float4 w4 = wq[t * 64];
-          const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+      for (int t = 0; t < TM; ++t) {
+        if (t >= tin) break;
+        const float4 w4 = wq[t * 64];
+        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 4; ++i) {
+          const float wp = fmaxf(wv[i], 0.f), wn = fminf(wv[i], 0.f);
 #pragma unroll
-            for (int ct = 0; ct < NT; ++ct) {
-              const int bt = PAIR ? u : t;
-              Pa[ct] = fa_mfma4(wv[i], B[ct][bt][0][i], Pa[ct]);
-              Qa[ct] = fa_mfma4(fabsf(wv[i]), B[ct][bt][1][i], Qa[ct]);
-            }
+          for (int ct = 0; ct < NT; ++ct) {
+            const int bt = PAIR ? u : t;
+            const float bu = B[ct][bt][0][i], bl = B[ct][bt][1][i];
+            U[u][ct] = fa_mfma4(wp, bu, U[u][ct]);
+            Lq[u][ct] = fa_mfma4(wp, bl, Lq[u][ct]);
+            U[u][ct] = fa_mfma4(wn, bl, U[u][ct]);
+            Lq[u][ct] = fa_mfma4(wn, bu, Lq[u][ct]);
           }
         }
       }
-#pragma unroll
-      for (int ct = 0; ct < NT; ++ct) fa_pq_to_ul(Pa[ct], Qa[ct], col, gg, U[u][ct], Lq[u][ct]);
     }
     float nu[2][NT][4], nlo[2][NT][4];
 #ifdef FA_SYM_TIMING_NO_EPILOGUE
@@ -632,19 +603,19 @@ fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
         const float m = fmaxf(fabsf(xl), fabsf(xh));
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
-          float vc = 0.f, vr = 0.f;          // centre / radius of the identity-form operand
+          float vu = 0.f, vl = 0.f;
           if (kv) {
             switch (role[ct]) {
-              case 0: vc = (!folded && cdm[ct] == k) ? 1.f : 0.f; break;
-              case 1: vc = folded ? xl : 0.f; break;
-              case 2: vr = g0 * m; break;
-              case 3: vc = 0.5f * (xh + xl); vr = 0.5f * (xh - xl); break;
-              case 4: vc = 0.5f * g0 * (fabsf(xh) - fabsf(xl)); vr = 0.5f * g0 * (fabsf(xh) + fabsf(xl)); break;
+              case 0: vu = vl = (!folded && cdm[ct] == k) ? 1.f : 0.f; break;
+              case 1: vu = vl = folded ? xl : 0.f; break;
+              case 2: vu = g0 * m; vl = -vu; break;
+              case 3: vu = xh; vl = xl; break;
+              case 4: vu = g0 * fabsf(xh); vl = -(g0 * fabsf(xl)); break;
               default: break;
             }
           }
-          XA[ct][t][0][i] = vc;
-          XA[ct][t][1][i] = vr;
+          XA[ct][t][0][i] = vu;
+          XA[ct][t][1][i] = vl;
         }
       }
     }
