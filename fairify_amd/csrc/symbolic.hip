@@ -90,7 +90,38 @@ struct SymSlab {   // box values per column: [mid | rad | m] x FA_SYM_MAXC
 // the MFMA K steps exactly as in the unpacked kernel: bitwise the same bounds whatever boxes
 // share the tile); rows j >= the layer's width are padding; the wave's boxes are consecutive
 // rows r_in + b.
-template <int NT, bool PAIR, int PG = 1>
+// Centre / radius layer GEMM (multi-tile kernels, FA_SYM_CR): the operands of a layer are
+// C = (U + L) / 2 and R = (U - L) / 2 of the previous layer's upper / lower rows (L rows carry
+// their error columns negated), so  U' = W+ U + W- L = W C + |W| R  and  L' = W C - |W| R:  two
+// MFMA chains (P = W C, Q = |W| R; |w| is a free source modifier) instead of four.  Rounding:
+// every output term passes through at most n_in + 2 roundings (C/R formation, the n_in-term
+// chain, P +- Q); the error columns recombine W+ eU + |W-| eL from (eU - eL)/2 and (eU + eL)/2,
+// so their rounding is bounded by 2 gamma Q (added once more on columns 1 and 3), and each input
+// row's error columns carry the rounding budget of BOTH blocks (gamma (m_U + m_L),
+// gamma max(iv_U, iv_L)): the radius couples them.
+//
+// The coupling costs exactness: a lower row that is exactly zero (dead neuron, lambda = 0) picks
+// up the upper row's rounding budget.  Narrow random-init nets decide many partitions through an
+// exactly zero logit, and the C/R form on the paired / packed kernels cost the bench 6.3 points
+// of verified partitions (profiles/r2/s4/README.md), so only the multi-tile kernels (wide
+// layers, where an all-dead layer does not occur) use it.
+template <bool PAIR, int TM>
+struct SymForm {
+  static constexpr bool CR = !PAIR && TM >= 2;
+};
+
+__device__ __forceinline__ void fa_pq_to_ul(const f32x4& P, const f32x4& Q, int col, float gg, f32x4& U,
+                                            f32x4& L) {
+  const float sl = (col == 1 || col == 3) ? 2.f * gg : 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float q = Q[i], e = sl * fabsf(q);
+    U[i] = (P[i] + q) + e;
+    L[i] = (P[i] - q) - e;
+  }
+}
+
+template <int NT, bool PAIR, int PG = 1, bool CR = false>
 __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
                                                 const float* smem, float* T, const float* bxv_in, const int* cdim_s,
                                                 int l, int r_in, int node_in, int r2, int node2, bool v2, int lane,
@@ -106,7 +137,8 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
   const float gc = net.g_conc;
   const float gi = net.g_one;
   const float unit = net.unit;
-  const float gnext = last ? 0.f : net.g_gemm[l + 1];
+  // next layer's rounding budget; C/R: gamma_{n_in + 3} (n_in + 2 roundings), charged on both blocks
+  const float gnext = last ? 0.f : (CR ? net.g_fwd[l + 1] : net.g_gemm[l + 1]);
   const int noff = net.neuron_off[l];
   const int nc = cfg.nc;
   const int n0 = net.dims[0];
@@ -235,10 +267,12 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
       mgn = lam1 ? mg : 0.f;
     }
     // new row: constant, error, interval, interval error (L errors negated), scaled coefficients
+    const float mg_b = CR ? mgn + __shfl_xor(mgn, 16, 64) : mgn;            // C/R: both blocks
+    const float iv_b = CR ? fmaxf(ivn, __shfl_xor(ivn, 16, 64)) : ivn;
     v[0] = cnew;
-    v[1] = sgn * (en + gnext * mgn);
+    v[1] = sgn * (en + gnext * mg_b);
     v[2] = ivn;
-    v[3] = sgn * (gnext * ivn);
+    v[3] = sgn * (gnext * iv_b);
 #pragma unroll
     for (int c = 4; c < 16 * NT; ++c) v[c] *= s;
     if (nl_act) {
@@ -254,8 +288,10 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
       for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          nu[u][ct][i] = T[u * SymSlab<NT>::TILE1 + (4 * grp + i) * TS + ct * 16 + col];
-          nlo[u][ct][i] = T[u * SymSlab<NT>::TILE1 + (16 + 4 * grp + i) * TS + ct * 16 + col];
+          const float xu = T[u * SymSlab<NT>::TILE1 + (4 * grp + i) * TS + ct * 16 + col];
+          const float xl = T[u * SymSlab<NT>::TILE1 + (16 + 4 * grp + i) * TS + ct * 16 + col];
+          nu[u][ct][i] = CR ? 0.5f * (xu + xl) : xu;     // C/R: centre / radius operands
+          nlo[u][ct][i] = CR ? 0.5f * (xu - xl) : xl;
         }
     __builtin_amdgcn_wave_barrier();
     return true;
@@ -272,6 +308,7 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
                                              const float (&B)[NT][PAIR ? 2 : TM][2][4],
                                              float (&A)[NT][PAIR ? 2 : TM][2][4]) {
   constexpr int TMS = PAIR ? 2 : TM;
+  constexpr bool CR = SymForm<PAIR, TM>::CR;
   constexpr int TS = SymSlab<NT>::TS;
   const int col = lane & 15, grp = lane >> 4;
   const int n_in = net.dims[l], n_out = net.dims[l + 1];
@@ -342,7 +379,7 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
       }
     }
     float nu[2][NT][4], nlo[2][NT][4];
-    if (!fa_sym_epilogue<NT, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
+    if (!fa_sym_epilogue<NT, PAIR, PG, CR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
                                        nu, nlo))
       return;
 #pragma unroll
@@ -380,8 +417,13 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
 #pragma unroll
           for (int ct = 0; ct < NT; ++ct) {
             const int bt = PAIR ? bi : t;
-            su[bi][ct] = fmaf(wp, B[ct][bt][0][i], fmaf(wn, B[ct][bt][1][i], su[bi][ct]));
-            sl[bi][ct] = fmaf(wp, B[ct][bt][1][i], fmaf(wn, B[ct][bt][0][i], sl[bi][ct]));
+            if (CR) {   // su = W C, sl = |W| R
+              su[bi][ct] = fmaf(wv[i], B[ct][bt][0][i], su[bi][ct]);
+              sl[bi][ct] = fmaf(fabsf(wv[i]), B[ct][bt][1][i], sl[bi][ct]);
+            } else {
+              su[bi][ct] = fmaf(wp, B[ct][bt][0][i], fmaf(wn, B[ct][bt][1][i], su[bi][ct]));
+              sl[bi][ct] = fmaf(wp, B[ct][bt][1][i], fmaf(wn, B[ct][bt][0][i], sl[bi][ct]));
+            }
           }
       }
     }
@@ -399,9 +441,10 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
         xl += __shfl_xor(xl, 32, 64);
         U[bi][ct] = f32x4{grp == 0 ? xu : 0.f, 0.f, 0.f, 0.f};     // row 0 of tile bi = neuron 0
         Lq[bi][ct] = f32x4{grp == 0 ? xl : 0.f, 0.f, 0.f, 0.f};
+        if (CR) fa_pq_to_ul(f32x4(U[bi][ct]), f32x4(Lq[bi][ct]), col, gg, U[bi][ct], Lq[bi][ct]);
       }
     float nu[2][NT][4], nlo[2][NT][4];
-    fa_sym_epilogue<NT, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
+    fa_sym_epilogue<NT, PAIR, PG, CR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
                                   nu, nlo);
     return;
   }
@@ -432,12 +475,21 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
           for (int ct = 0; ct < NT; ++ct) {
             const int bt = PAIR ? u : t;
             const float bu = B[ct][bt][0][i], bl = B[ct][bt][1][i];
-            U[u][ct] = fa_mfma4(wp, bu, U[u][ct]);
-            Lq[u][ct] = fa_mfma4(wp, bl, Lq[u][ct]);
-            U[u][ct] = fa_mfma4(wn, bl, U[u][ct]);
-            Lq[u][ct] = fa_mfma4(wn, bu, Lq[u][ct]);
+            if (CR) {   // U = P = W C, Lq = Q = |W| R
+              U[u][ct] = fa_mfma4(wv[i], bu, U[u][ct]);
+              Lq[u][ct] = fa_mfma4(fabsf(wv[i]), bl, Lq[u][ct]);
+            } else {
+              U[u][ct] = fa_mfma4(wp, bu, U[u][ct]);
+              Lq[u][ct] = fa_mfma4(wp, bl, Lq[u][ct]);
+              U[u][ct] = fa_mfma4(wn, bl, U[u][ct]);
+              Lq[u][ct] = fa_mfma4(wn, bu, Lq[u][ct]);
+            }
           }
         }
+      }
+      if (CR) {
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) fa_pq_to_ul(f32x4(U[u][ct]), f32x4(Lq[u][ct]), col, gg, U[u][ct], Lq[u][ct]);
       }
     }
     float nu[2][NT][4], nlo[2][NT][4];
@@ -457,7 +509,7 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
       continue;
     }
 #else
-    if (!fa_sym_epilogue<NT, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, jt0, U,
+    if (!fa_sym_epilogue<NT, PAIR, PG, CR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, jt0, U,
                                        Lq, nu, nlo))
       continue;
 #endif
@@ -502,6 +554,7 @@ template <int NT, int TM, bool PAIR, int PG = 1>
 
 __global__ void __launch_bounds__(FA_SYM_THREADS(TM)) __attribute__((amdgpu_waves_per_eu(FA_SYM_WAVES_PER_EU(NT, TM, PAIR))))
 fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
+  constexpr bool CR = SymForm<PAIR, TM>::CR;   // centre / radius operands (multi-tile kernels)
   constexpr int TMS = PAIR ? 2 : TM;   // operand slots: K tiles, or (PAIR) the wave's two boxes /
                                        // (packed) two groups of PG boxes
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -606,11 +659,18 @@ fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
           float vu = 0.f, vl = 0.f;
           if (kv) {
             switch (role[ct]) {
-              case 0: vu = vl = (!folded && cdm[ct] == k) ? 1.f : 0.f; break;
-              case 1: vu = vl = folded ? xl : 0.f; break;
-              case 2: vu = g0 * m; vl = -vu; break;
-              case 3: vu = xh; vl = xl; break;
-              case 4: vu = g0 * fabsf(xh); vl = -(g0 * fabsf(xl)); break;
+              // C/R kernels: (vu, vl) hold the centre / radius of the [upper | lower] operand pair
+              case 0: vu = (!folded && cdm[ct] == k) ? 1.f : 0.f; vl = CR ? 0.f : vu; break;
+              case 1: vu = folded ? xl : 0.f; vl = CR ? 0.f : vu; break;
+              case 2: vu = CR ? 0.f : g0 * m; vl = CR ? g0 * m : -vu; break;
+              case 3:
+                vu = CR ? 0.5f * (xh + xl) : xh;
+                vl = CR ? 0.5f * (xh - xl) : xl;
+                break;
+              case 4:
+                vu = CR ? 0.5f * g0 * (fabsf(xh) - fabsf(xl)) : g0 * fabsf(xh);
+                vl = CR ? 0.5f * g0 * (fabsf(xh) + fabsf(xl)) : -(g0 * fabsf(xl));
+                break;
               default: break;
             }
           }

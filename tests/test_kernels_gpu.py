@@ -40,8 +40,27 @@ def test_bounds_match_reference(cuda, n0, hidden, mode):
     for a, b in zip(r_g.layer_ub, r_c.layer_ub):
         assert torch.allclose(a.cpu(), b, rtol=1e-4, atol=1e-3 * float(b.abs().max() + 1))
     if mode == "symbolic":
-        assert torch.allclose(r_g.Lc.cpu(), r_c.Lc, rtol=1e-4, atol=1e-4 * float(r_c.Lc.abs().max() + 1))
-        assert torch.allclose(r_g.U0.cpu(), r_c.U0, rtol=1e-4, atol=1e-4 * float(r_c.U0.abs().max() + 1))
+        # output forms: equal to the reference's up to rounding, except rows where a hidden
+        # neuron's relaxation choice (chord / identity, lambda) flipped on a bound within
+        # rounding of its threshold -- at most 1 % of the rows, and those rows' GPU forms must
+        # still bound the network pointwise on the box's lattice points
+        def close(g, c):
+            tol = 1e-4 * (c.abs().max(dim=-1).values if c.dim() == 2 else c.abs()) + 1e-4 * (float(c.abs().max()) + 1)
+            d = (g - c).abs()
+            return (d <= tol[:, None]).all(dim=1) if d.dim() == 2 else d <= tol
+        ok = torch.ones(lo.shape[0], dtype=torch.bool)
+        for g_, c_ in ((r_g.Lc.cpu(), r_c.Lc), (r_g.Uc.cpu(), r_c.Uc), (r_g.L0.cpu(), r_c.L0), (r_g.U0.cpu(), r_c.U0)):
+            ok &= close(g_, c_)
+        bad = torch.nonzero(~ok).flatten()
+        assert bad.numel() <= max(1, lo.shape[0] // 100), bad.numel()
+        g = np.random.default_rng(0)
+        for r in bad.tolist():
+            pts = g.integers(lo[r].numpy().astype(np.int64), hi[r].numpy().astype(np.int64) + 1, size=(256, n0))
+            z = m.logits(pts)
+            X = torch.from_numpy(pts).double()
+            up = X @ r_g.Uc[r].cpu().double() + float(r_g.U0[r]) + float(r_g.Ue[r])
+            dn = X @ r_g.Lc[r].cpu().double() + float(r_g.L0[r]) - float(r_g.Le[r])
+            assert (up.numpy() >= z - 1e-9).all() and (dn.numpy() <= z + 1e-9).all(), r
 
 
 @pytest.mark.parametrize("n0,hidden", NETS[:4])
