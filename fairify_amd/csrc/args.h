@@ -42,6 +42,11 @@ struct BoundArgs {
   // STOPPING are skipped (nothing written; the split kernel ignores those nodes)
   const int8_t* skip_status;
   const int* skip_part;
+  // point kernel in the BaB level: point r is the candidate x (r < open_mod) or x' of node
+  // r % open_mod; tiles whose 16 points all belong to closed nodes (open == 0, the certificate
+  // excluded every pair) are skipped -- the split kernel reads point bounds of open nodes only
+  const uint8_t* row_open;
+  int open_mod;
 };
 
 struct FwdArgs {

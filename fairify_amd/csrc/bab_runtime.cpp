@@ -74,6 +74,15 @@ struct DevBuf {
   }
 };
 
+// A/B switch of the closed-node skip in the candidate point kernel (FAIRIFY_POINT_SKIP_CLOSED=0: off)
+bool point_skip_closed() {
+  static const bool v = [] {
+    const char* e = getenv("FAIRIFY_POINT_SKIP_CLOSED");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 float gamma_up(int k, double unit) {
   const double ku = (k + 2) * unit;
   return std::nextafter((float)(ku / (1.0 - ku)), INFINITY);
@@ -304,6 +313,7 @@ class BabRuntime {
         // per-point partition ids only matter for the heuristic (masked) nets: points k and
         // nb + k (x and x' of node k) both read bpart[k]
         if (dead_part) { b.node_part = bpart; b.part_mod = nb; b.dead_part = (const uint8_t*)dead_part; }
+        if (point_skip_closed()) { b.row_open = open_.p; b.open_mod = nb; }
         const int prc = fa_point_try_launch(net_, b, st);
         if (prc < 0) ckl(-prc, "points");
         if (prc == 0) ckl(fa_bounds_launch(net_, b, st), "bounds(points)");

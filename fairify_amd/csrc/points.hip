@@ -113,6 +113,7 @@ __global__ void __launch_bounds__(FA_THREADS) __attribute__((amdgpu_waves_per_eu
   for (int tile = blockIdx.x * nw + wave; tile < ntile; tile += gridDim.x * nw) {
     const int p0 = tile * 16;
     const int p = p0 + col;
+    if (a.row_open && !__any(p < a.R && a.row_open[p % a.open_mod])) continue;   // wave-uniform
     float HA[TM][4], EA[TM][4], HB[TM][4], EB[TM][4];
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
