@@ -70,6 +70,9 @@ def parse_args(argv=None):
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
     ap.add_argument("--escalate-max-open", type=int, default=384,
                     help="escalate only partitions that left <= this many open BaB nodes (0 = all)")
+    ap.add_argument("--escalate-probation", default="2048:768,4096:1024",
+                    help="intermediate inline-escalation steps 'budget:max_open,...' between --node-budget and "
+                         "--escalate-budget")
     ap.add_argument("--stages", default="",
                     help="further escalation passes 'budget:max_open,...' after --escalate-budget")
     ap.add_argument("--batch-nodes", type=int, default=65536,
@@ -178,6 +181,8 @@ def main() -> None:
                        heuristic_node_budget=args.node_budget, escalate_budget=args.escalate_budget,
                        escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
                        smt_backend=args.smt,
+                       escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
+                                                for st in args.escalate_probation.split(",") if st),
                        escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
     if args.residual_samples is not None:
         cfg.residual_samples = args.residual_samples
@@ -309,6 +314,7 @@ def main() -> None:
                    "parallelism": f"dp{info.world}", "preset": args.preset, "grid_per_model": len(order),
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
+                   "escalate_probation": [list(st) for st in cfg.escalate_probation],
                    "stages": [list(st) for st in cfg.escalate_stages], "heuristic": cfg.heuristic,
                    "batch_nodes": cfg.batch_nodes,
                    "chunk": args.chunk, "concurrency": conc, "priority_items": args.priority_items},

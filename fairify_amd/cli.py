@@ -55,6 +55,8 @@ def cmd_verify(args):
                        heuristic_p=args.heuristic_p if args.heuristic_p is not None else pre.heuristic_p,
                        heuristic_node_budget=args.node_budget, smt_backend=args.smt,
                        escalate_budget=args.escalate_budget, escalate_max_open=args.escalate_max_open,
+                       escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
+                                                for st in args.escalate_probation.split(",") if st),
                        keep_masks=args.keep_masks)
     if args.residual_samples is not None:
         cfg.residual_samples = args.residual_samples
@@ -184,6 +186,9 @@ def main(argv=None):
                    help="retry each round's UNKNOWN partitions on all ranks with N x the node budget")
     v.add_argument("--escalate-budget", type=int, default=0,
                    help="second sound BaB pass with this node budget on each chunk's UNKNOWN residue")
+    v.add_argument("--escalate-probation", default="",
+                   help="inline escalation steps 'budget:max_open,...' between the node budget and "
+                        "--escalate-budget (native BaB; bench default 2048:768,4096:1024)")
     v.add_argument("--escalate-max-open", type=int, default=0,
                    help="escalate only residue partitions that left <= this many open BaB nodes (0 = all)")
     v.add_argument("--concurrency", type=int, default=0,

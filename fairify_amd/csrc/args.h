@@ -49,6 +49,16 @@ struct BoundArgs {
   int open_mod;
 };
 
+// Inline escalation steps between the first budget and budget2 (fa_settle_kernel): step k has
+// budget[k] (increasing, strictly between the two) and the frontier limit open[k] checked at its
+// probation level.  n = 0: one step (budget -> budget2, frontier <= max_open).
+#define FA_MAX_ESC 4
+struct EscSteps {
+  int n;
+  int budget[FA_MAX_ESC];
+  int open[FA_MAX_ESC];
+};
+
 struct FwdArgs {
   const float* flat;
   const float* x;          // [B, n0]

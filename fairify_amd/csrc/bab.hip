@@ -421,7 +421,8 @@ __global__ void fa_mark_unknown_kernel(const int* part, int n, int8_t* status) {
 // first pass.  Its surplus children are skipped by the bound kernels (status filter).
 __global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
                                  int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
-                                 int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open) {
+                                 int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open,
+                                 EscSteps esc) {
   const int p = blockIdx.x * FA_THREADS + threadIdx.x;
   if (p == 0) {
     // level counters straight into pinned host memory (no blit per level), next slot cleared
@@ -435,8 +436,14 @@ __global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part
     status[p] = ST_UNKNOWN;
     if (part_open) part_open[p] = lvl_open[p];
   } else if (prob && prob[p] && status[p] == ST_RUNNING) {
-    if (lvl_open[p] <= max_open) {
-      pbudget[p] = budget2;
+    // stepped escalation: budget -> esc.budget[0] -> ... -> budget2; at each step's probation
+    // level the frontier must be at most max_open (first step) / esc.open[k-1] (step k)
+    const int cur = pbudget[p];
+    int k = 0;
+    while (k < esc.n && esc.budget[k] <= cur) ++k;
+    const int thr = k == 0 ? max_open : esc.open[k - 1];
+    if (lvl_open[p] <= thr) {
+      pbudget[p] = k < esc.n ? esc.budget[k] : budget2;
     } else {
       status[p] = ST_UNKNOWN;
       if (part_open) part_open[p] = lvl_open[p];
@@ -478,11 +485,11 @@ extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_
 extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
                                 int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
                                 int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open,
-                                hipStream_t stream) {
+                                EscSteps esc, hipStream_t stream) {
   const int n = P > 0 ? P : 1;
   hipLaunchKernelGGL(fa_settle_kernel, dim3((n + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, P,
                      status, lvl_open, part_open, part_nodes, nodes_start, prev_start, counters_cur, counters_next,
-                     host_counts, pbudget, prob, budget2, max_open);
+                     host_counts, pbudget, prob, budget2, max_open, esc);
   return (int)hipGetLastError();
 }
 

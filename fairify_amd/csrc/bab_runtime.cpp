@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
+#include <utility>
 #include <vector>
 
 #include "args.h"
@@ -40,7 +41,7 @@ extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_
 extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
                                 int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
                                 int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open,
-                                hipStream_t stream);
+                                EscSteps esc, hipStream_t stream);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_bab_init_launch(BabInitArgs a, hipStream_t stream);
 extern "C" int fa_bab_finish_launch(int P, const int8_t* status, const int* nodes, const int* open_left, int* out,
@@ -183,8 +184,16 @@ class BabRuntime {
                   py::array_t<float, py::array::c_style | py::array::forcecast> hi,
                   py::array_t<int8_t, py::array::c_style | py::array::forcecast> status0, int budget,
                   double time_budget, uintptr_t dead_part, py::object confirm, uintptr_t stream_i,
-                  bool native_exact, int budget2, int max_w) {
+                  bool native_exact, int budget2, int max_w, std::vector<std::pair<int, int>> esc_steps) {
     const bool inline_esc = budget2 > budget && max_w > 0;
+    // intermediate escalation steps strictly between budget and budget2, increasing budgets
+    EscSteps esc{};
+    for (const auto& bo : esc_steps)
+      if (bo.first > (esc.n ? esc.budget[esc.n - 1] : budget) && bo.first < budget2 && esc.n < FA_MAX_ESC) {
+        esc.budget[esc.n] = bo.first;
+        esc.open[esc.n] = bo.second;
+        ++esc.n;
+      }
     hipStream_t st = (hipStream_t)stream_i;
     native_exact_ = native_exact;
     box_lo_ = lo.data();
@@ -345,7 +354,7 @@ class BabRuntime {
       }
       ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, nodes_.p, nodes_start_.p, prev_start_.p, cnt,
                            counters_.p + 2 * (slot ^ 1), hcount_, inline_esc ? pbudget_.p : nullptr,
-                           inline_esc ? prob_.p : nullptr, budget2, max_w, st),
+                           inline_esc ? prob_.p : nullptr, budget2, max_w, esc, st),
           "settle");
       ck(hipStreamSynchronize(st), "sync");
       slot ^= 1;
@@ -608,5 +617,6 @@ void register_bab(py::module& m) {
            py::arg("split_target") = 256)
       .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"),
-           py::arg("native_exact") = false, py::arg("budget2") = 0, py::arg("max_w") = 0);
+           py::arg("native_exact") = false, py::arg("budget2") = 0, py::arg("max_w") = 0,
+           py::arg("esc_steps") = std::vector<std::pair<int, int>>{});
 }

@@ -22,7 +22,7 @@ import os
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -58,6 +58,10 @@ class BaBConfig:
     # most escalate_max_w nodes continues up to escalate_budget (0 = off)
     escalate_budget: int = 0
     escalate_max_w: int = 0
+    # intermediate (budget, max frontier) steps of the inline escalation, between node_budget and
+    # escalate_budget: a partition continues past step k's budget only with a frontier of at most
+    # its limit (fa_settle_kernel)
+    escalate_steps: Tuple[Tuple[int, int], ...] = ()
 
 
 @dataclass
@@ -353,7 +357,8 @@ class BaBSolver:
             st, cx, cxp, nodes, stats = rt.solve(lo_np.astype(np.float32), hi_np.astype(np.float32), status,
                                                   int(self.cfg.node_budget), float(self.cfg.time_budget), dead_ptr,
                                                   confirm, stream, exact_models is None,
-                                                  int(self.cfg.escalate_budget), int(self.cfg.escalate_max_w))
+                                                  int(self.cfg.escalate_budget), int(self.cfg.escalate_max_w),
+                                                  [(int(b), int(o)) for b, o in self.cfg.escalate_steps])
         self.stats = dict(stats)
         with _STATS_LOCK:
             for k in STATS:

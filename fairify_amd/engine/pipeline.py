@@ -48,6 +48,10 @@ class VerifyConfig:
     escalate_max_open: int = 0           # only escalate partitions that left at most this many
                                          # open nodes in the first pass (0 = all; native BaB only)
     escalate_stages: Tuple[Tuple[int, int], ...] = ()
+    # inline escalation steps between node_budget and escalate_budget: (budget, max frontier) --
+    # a partition continues past each step's budget only if its open frontier at that level is at
+    # most the limit (the first step uses escalate_max_open)
+    escalate_probation: Tuple[Tuple[int, int], ...] = ()
     inline_escalate: bool = True         # native BaB: run the escalate_budget stage inside the first
                                          # pass (escalate_max_open then bounds the frontier size)
                                          # further (budget, max_open) passes after the escalated one,
@@ -332,7 +336,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     solver = BaBSolver(be, q, BaBConfig(node_budget=cfg.node_budget, batch_nodes=cfg.batch_nodes,
                                         time_budget=budget,
                                         escalate_budget=cfg.escalate_budget if inline else 0,
-                                        escalate_max_w=cfg.escalate_max_open if inline else 0), timer=tm)
+                                        escalate_max_w=cfg.escalate_max_open if inline else 0,
+                                        escalate_steps=tuple(cfg.escalate_probation) if inline else ()), timer=tm)
     with tm("bab"):
         res = solver.solve(lo_np, hi_np, mlp, init_status=status)
     newly_sat = (res.status == SAT) & (status != SAT)

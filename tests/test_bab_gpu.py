@@ -94,3 +94,27 @@ def test_open_left_reported_only_for_unknown(cuda):
         assert np.all(res.open_left >= 0)
         if np.any(res.status == 0):
             assert np.all(res.open_left[res.status == 0] > 0)
+
+
+@pytest.mark.parametrize("name", ["AC-7", "AC-8", "AC-12"])
+def test_escalation_steps_only_stop_earlier(cuda, name):
+    """Stepped inline escalation (fa_settle_kernel: budget -> 2048 -> 4096 -> 8192 with frontier
+    limits) follows the same per-partition search tree as the one-step schedule and only stops
+    partitions earlier: every partition it decides has the one-step verdict, and it decides no
+    partition the one-step schedule leaves UNKNOWN."""
+    from fairify_amd import presets
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.partition import processing_order
+
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    lo, hi = grid.decode(processing_order(grid, 0)[:512])
+    m = get_model(name, weights="random", seed=0)
+    be = Backend(m, cuda)
+    base = dict(node_budget=512, escalate_budget=8192, escalate_max_w=384)
+    one = BaBSolver(be, q, BaBConfig(**base)).solve(lo, hi, m)
+    steps = BaBSolver(be, q, BaBConfig(**base, escalate_steps=((2048, 768), (4096, 1024)))).solve(lo, hi, m)
+    dec = steps.status != 0
+    assert np.array_equal(steps.status[dec], one.status[dec])
+    assert not np.any(dec & (one.status == 0))
+    assert (one.status != 0).sum() >= dec.sum()

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--models", default="AC-12")
     ap.add_argument("--shard", default="0/8")
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--escalate-budget", type=int, default=8192)
+    ap.add_argument("--escalate-max-open", type=int, default=384)
+    ap.add_argument("--no-heuristic", action="store_true")
     args = ap.parse_args()
     import torch
 
@@ -45,7 +48,8 @@ def main():
     ids = order[r::n][:4096]
     cfg = VerifyConfig(sim_size=pre.sim_size, chunk=4096, soft_timeout=pre.soft_timeout,
                        hard_timeout=pre.hard_timeout, node_budget=512, heuristic_p=pre.heuristic_p,
-                       heuristic_node_budget=512, escalate_budget=8192, escalate_max_open=384, smt_backend="none")
+                       heuristic_node_budget=512, escalate_budget=args.escalate_budget,
+                       escalate_max_open=args.escalate_max_open, heuristic=not args.no_heuristic, smt_backend="none")
     for name in args.models.split(","):
         m = get_model(name, weights="random", seed=0)
         be = Backend(m, device=dev)
@@ -65,7 +69,9 @@ def main():
                        bab=dict(B.STATS), nodes_sum=int(c["nodes"].sum()),
                        nodes_p50=float(np.median(c["nodes"])), nodes_max=int(c["nodes"].max()),
                        verdicts={v: int((c["verdict"] == v).sum()) for v in ("sat", "unsat", "unknown")},
-                       heuristic=int((c["stage"] == "heuristic").sum()))
+                       heuristic=int((c["stage"] == "heuristic").sum()),
+                       nodes_unknown=int(c["nodes"][c["verdict"] == "unknown"].sum()),
+                       escalate=args.escalate_budget)
             print(json.dumps(row), flush=True)
 
 
