@@ -70,7 +70,7 @@ def parse_args(argv=None):
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
     ap.add_argument("--escalate-max-open", type=int, default=384,
                     help="escalate only partitions that left <= this many open BaB nodes (0 = all)")
-    ap.add_argument("--escalate-probation", default="2048:768,4096:1024",
+    ap.add_argument("--escalate-probation", default="2048:768,4096:768",
                     help="intermediate inline-escalation steps 'budget:max_open,...' between --node-budget and "
                          "--escalate-budget")
     ap.add_argument("--stages", default="",

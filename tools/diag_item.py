@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--escalate-budget", type=int, default=8192)
     ap.add_argument("--escalate-max-open", type=int, default=384)
     ap.add_argument("--no-heuristic", action="store_true")
+    ap.add_argument("--escalate-probation", default="2048:768,4096:1024")
     args = ap.parse_args()
     import torch
 
@@ -49,7 +50,9 @@ def main():
     cfg = VerifyConfig(sim_size=pre.sim_size, chunk=4096, soft_timeout=pre.soft_timeout,
                        hard_timeout=pre.hard_timeout, node_budget=512, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=512, escalate_budget=args.escalate_budget,
-                       escalate_max_open=args.escalate_max_open, heuristic=not args.no_heuristic, smt_backend="none")
+                       escalate_max_open=args.escalate_max_open, heuristic=not args.no_heuristic, smt_backend="none",
+                       escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
+                                                for st in args.escalate_probation.split(",") if st))
     for name in args.models.split(","):
         m = get_model(name, weights="random", seed=0)
         be = Backend(m, device=dev)
