@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--escalate-budget", type=int, default=8192)
     ap.add_argument("--escalate-max-open", type=int, default=384)
     ap.add_argument("--no-heuristic", action="store_true")
-    ap.add_argument("--escalate-probation", default="2048:768,4096:1024")
+    ap.add_argument("--escalate-probation", default="2048:768,4096:768")
     args = ap.parse_args()
     import torch
 
