@@ -66,6 +66,8 @@ def parse_args(argv=None):
     ap.add_argument("--limit", type=int, default=0,
                     help="verify only the first LIMIT partitions of the seeded order per model (tests)")
     ap.add_argument("--node-budget", type=int, default=512)
+    ap.add_argument("--heuristic-node-budget", type=int, default=512,
+                    help="BaB node budget of the heuristic retry on the pruned network")
     ap.add_argument("--escalate-budget", type=int, default=8192,
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
     ap.add_argument("--escalate-max-open", type=int, default=384,
@@ -178,7 +180,7 @@ def main() -> None:
     cfg = VerifyConfig(sim_size=args.sim_size or pre.sim_size, seed=args.seed, chunk=args.chunk,
                        soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
                        node_budget=args.node_budget, heuristic=not args.no_heuristic, heuristic_p=pre.heuristic_p,
-                       heuristic_node_budget=args.node_budget, escalate_budget=args.escalate_budget,
+                       heuristic_node_budget=args.heuristic_node_budget, escalate_budget=args.escalate_budget,
                        escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
                        smt_backend=args.smt,
                        escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
@@ -314,6 +316,7 @@ def main() -> None:
                    "parallelism": f"dp{info.world}", "preset": args.preset, "grid_per_model": len(order),
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
+                   "heuristic_node_budget": cfg.heuristic_node_budget,
                    "escalate_probation": [list(st) for st in cfg.escalate_probation],
                    "stages": [list(st) for st in cfg.escalate_stages], "heuristic": cfg.heuristic,
                    "batch_nodes": cfg.batch_nodes,
