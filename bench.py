@@ -60,9 +60,10 @@ def parse_args(argv=None):
     ap.add_argument("--scope", default="suite", choices=["suite", "chunk"],
                     help="suite: one step = whole grid of every model (strong scaling); "
                          "chunk: one step = --chunk partitions per model per rank (weak scaling)")
-    ap.add_argument("--chunk", type=int, default=4096,
-                    help="partitions per work item (big chunks win even for small per-rank shards: a 1/8 "
-                         "shard takes 1.02 s per step at 4096 vs 1.76 s at 667, profiles/scaling_emulation.md)")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="partitions per work item; 0 = by shard size: 8192 when a rank holds more than 8192 "
+                         "partitions per model (N=1: two 8000-partition items per model), else 4096 "
+                         "(profiles/r2/s4/chunk/)")
     ap.add_argument("--limit", type=int, default=0,
                     help="verify only the first LIMIT partitions of the seeded order per model (tests)")
     ap.add_argument("--node-budget", type=int, default=512)
@@ -172,6 +173,11 @@ def main() -> None:
     if args.emulate_shard:
         er, en = (int(v) for v in args.emulate_shard.split("/"))
         shard = order[er::en]
+    if args.chunk <= 0:
+        # big items make big launches; below 8192 partitions per model a second item per model
+        # beats a bigger one (N=1: 8192 1 237-1 265 ms vs 4096 1 285-1 328 ms; half shard: 4096
+        # 645 ms vs 8192 692-711 ms)
+        args.chunk = 8192 if len(shard) > 8192 else 4096
     names = args.models.split(",") if args.models else list(pre.models)
     models = [get_model(n, weights=args.weights, seed=args.seed) for n in names]
     backends = [Backend(m, device=info.device) for m in models]
