@@ -539,7 +539,9 @@ class BabRuntime {
       std::memcpy(hidx_, newly.data(), newly.size() * sizeof(int));
       ck(hipMemcpyAsync(idx_.p, hidx_, newly.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp idx");
       ckl(fa_set_status_launch(idx_.p, (int)newly.size(), status_.p, 1, st), "set_status");
-      ck(hipStreamSynchronize(st), "sync");
+      // no sync: the next level's kernels are stream-ordered after set_status, and hidx_ / idx_
+      // are only rewritten by the next call, which runs after the next level-end sync (the sync
+      // that retires this copy -- the buffer-lifetime rule of tests/test_stream_lifetime.py)
     }
   }
 
