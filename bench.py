@@ -69,11 +69,11 @@ def parse_args(argv=None):
     ap.add_argument("--node-budget", type=int, default=512)
     ap.add_argument("--heuristic-node-budget", type=int, default=512,
                     help="BaB node budget of the heuristic retry on the pruned network")
-    ap.add_argument("--escalate-budget", type=int, default=8192,
+    ap.add_argument("--escalate-budget", type=int, default=32768,
                     help="second sound BaB pass with this node budget on the first pass's UNKNOWN residue")
     ap.add_argument("--escalate-max-open", type=int, default=384,
                     help="escalate only partitions that left <= this many open BaB nodes (0 = all)")
-    ap.add_argument("--escalate-probation", default="2048:768,4096:768",
+    ap.add_argument("--escalate-probation", default="2048:768,4096:768,8192:768,16384:1024",
                     help="intermediate inline-escalation steps 'budget:max_open,...' between --node-budget and "
                          "--escalate-budget")
     ap.add_argument("--stages", default="",

@@ -188,7 +188,7 @@ def main(argv=None):
                    help="second sound BaB pass with this node budget on each chunk's UNKNOWN residue")
     v.add_argument("--escalate-probation", default="",
                    help="inline escalation steps 'budget:max_open,...' between the node budget and "
-                        "--escalate-budget (native BaB; bench default 2048:768,4096:768)")
+                        "--escalate-budget (native BaB; bench default 2048:768,4096:768,8192:768,16384:1024 with --escalate-budget 32768)")
     v.add_argument("--escalate-max-open", type=int, default=0,
                    help="escalate only residue partitions that left <= this many open BaB nodes (0 = all)")
     v.add_argument("--concurrency", type=int, default=0,

@@ -26,10 +26,10 @@ def main():
     ap.add_argument("--models", default="AC-12")
     ap.add_argument("--shard", default="0/8")
     ap.add_argument("--repeat", type=int, default=2)
-    ap.add_argument("--escalate-budget", type=int, default=8192)
+    ap.add_argument("--escalate-budget", type=int, default=32768)
     ap.add_argument("--escalate-max-open", type=int, default=384)
     ap.add_argument("--no-heuristic", action="store_true")
-    ap.add_argument("--escalate-probation", default="2048:768,4096:768")
+    ap.add_argument("--escalate-probation", default="2048:768,4096:768,8192:768,16384:1024")
     args = ap.parse_args()
     import torch
 
