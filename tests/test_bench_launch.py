@@ -14,7 +14,7 @@ def _bench(gpus: int, extra=()):
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--device", "cpu",
            "--models", "AC-8,AC-9", "--limit", "48", "--chunk", "16", "--steps", "1", "--warmup", "0",
-           "--budget-pass", "0", *extra]
+           "--budget-pass", "0", "--escalate-budget", "4096", *extra]   # CPU: the torch BaB path
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
