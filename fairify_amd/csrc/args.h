@@ -173,6 +173,13 @@ struct CertArgs {
   int64_t* cand_o;
   float* scores;                                  // [Nn, 2*n0] split scores or nullptr
   uint8_t* leaf;                                  // [Nn] single lattice point (x and x') or nullptr
+  // native BaB runtime only: closed nodes write open / score and skip the split scores and the
+  // candidate pair (the split kernel reads those for open nodes only), and nodes of partitions
+  // that are no longer RUNNING / STOPPING (status[part[n]], the bound kernels' status filter)
+  // are closed without evaluating their pairs
+  int skip_closed;
+  const int8_t* status;
+  const int* part;
 };
 
 // Branch step: close / flag / split the nodes of one sub-batch into the next BFS level.

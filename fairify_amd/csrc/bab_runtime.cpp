@@ -84,6 +84,15 @@ bool point_skip_closed() {
   return v;
 }
 
+// A/B switch of the closed-node early-out in the pair certificate (FAIRIFY_CERT_SKIP_CLOSED=0: off)
+bool cert_skip_closed() {
+  static const bool v = [] {
+    const char* e = getenv("FAIRIFY_CERT_SKIP_CLOSED");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 float gamma_up(int k, double unit) {
   const double ku = (k + 2) * unit;
   return std::nextafter((float)(ku / (1.0 - ku)), INFINITY);
@@ -314,6 +323,7 @@ class BabRuntime {
         c.cand_x = cand_.p; c.cand_xp = cand_.p + (size_t)nb * n0_;
         c.cand_v = cv_.p; c.cand_o = co_.p;
         c.scores = scores_.p; c.leaf = leaf_.p;
+        if (cert_skip_closed()) { c.skip_closed = 1; c.status = status_.p; c.part = bpart; }
         ckl(fa_certify_launch(c, st), "certify");
         // rigorous interval evaluation of the candidate pairs (rows: x then x')
         BoundArgs b{};

@@ -181,8 +181,10 @@ __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_eval_kernel(CertArgs 
   const int Q = a.Pp * a.norient;
   const int64_t idx = (int64_t)blockIdx.x * FA_CERT_THREADS + threadIdx.x;
   if (idx >= (int64_t)a.Nn * Q) return;
-  float g, t;
-  fa_pair_eval_one<NM>(a, (int)(idx / Q), (int)(idx % Q), g, t);
+  float g = -INFINITY, t = 0.f;
+  const int n = (int)(idx / Q);
+  const int8_t st = a.status ? a.status[a.part[n]] : (int8_t)3;
+  if (st == 3 || st == 4) fa_pair_eval_one<NM>(a, n, (int)(idx % Q), g, t);
   a.gmin[idx] = g;
   a.tstar[idx] = t;
 }
@@ -216,7 +218,11 @@ fa_pair_fused_kernel(CertArgs a, int QG) {
   const int Q = a.Pp * a.norient;
   const int gidx = blockIdx.x * FA_CERT_THREADS + threadIdx.x;
   const int n = gidx / QG, qq = gidx - n * QG;
-  const bool live = n < a.Nn && qq < Q;
+  bool live = n < a.Nn && qq < Q;
+  if (live && a.status) {   // node of a decided / stopped partition: closed, nothing evaluated
+    const int8_t st = a.status[a.part[n]];
+    live = st == 3 || st == 4;
+  }
   float g = -INFINITY, t = 0.f;
   if (live) fa_pair_eval_one<NM>(a, n, qq, g, t);
   int bq = live ? qq : 0x7fffffff;
@@ -230,6 +236,12 @@ fa_pair_fused_kernel(CertArgs a, int QG) {
 }
 
 __device__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t) {
+  if (a.skip_closed && !(bg > 0.f)) {
+    a.open[n] = 0;
+    a.score[n] = bg;
+    if (a.leaf) a.leaf[n] = 0;
+    return;
+  }
   const int o = bq / a.Pp, q = bq % a.Pp;
   Form A, B;
   float sA, sB;
