@@ -46,7 +46,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_DECIDED_PER_S = 553.0 / 22143.5
 METRIC = "% partitions verified + partitions/sec on AC suite at 1/2/4/8 MI355X"
-STAGES = ("sim", "bab", "falsify", "smt", "milp", "heuristic")
+STAGES = ("sim", "bab", "relu", "falsify", "smt", "milp", "heuristic", "heuristic-confirmed")
+UNSOUND_UNSAT = ("heuristic", "milp")     # engine/stages.py: UNSAT verdicts that are not proofs
 
 
 def parse_args(argv=None):
@@ -83,6 +84,9 @@ def parse_args(argv=None):
     ap.add_argument("--smt", default="none",
                     help="exact host solver on the residue in the timed steps: none (fixed-budget throughput "
                          "bench) | auto | milp | z3py | z3bin")
+    ap.add_argument("--trust-milp", action="store_true",
+                    help="count a HiGHS MILP 'unsat' (floating-point dual bound) as an UNSAT verdict (stage "
+                         "'milp', excluded from the sound figures); default: recorded, partition stays UNKNOWN")
     ap.add_argument("--budget-pass", type=float, default=10.0,
                     help="after the timed steps, one untimed pass over the same grid in anytime mode with this "
                          "many seconds per model (growing BaB budgets + falsifier + MILP rounds on the residue): "
@@ -188,7 +192,7 @@ def main() -> None:
                        node_budget=args.node_budget, heuristic=not args.no_heuristic, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=args.heuristic_node_budget, escalate_budget=args.escalate_budget,
                        escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
-                       smt_backend=args.smt,
+                       smt_backend=args.smt, trust_milp=args.trust_milp,
                        escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
                                                 for st in args.escalate_probation.split(",") if st),
                        escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
@@ -239,8 +243,9 @@ def main() -> None:
     item_cost = {}
     ITEM_LOG = os.environ.get("FAIRIFY_BENCH_ITEMS") == "1"   # per-item start / duration on stderr
     step_no, step_t0 = [0], [time.time()]
-    # counters: attempted, decided, sat, unsat, unsat_heuristic, sat per stage (STAGES order)
-    NC = 5 + len(STAGES)
+    # counters: attempted, decided, sat, unsat, unsat_heuristic, sat per stage, unsat per stage
+    # (STAGES order)
+    NC = 5 + 2 * len(STAGES)
 
     def one_item(k: int, j: int, ids: np.ndarray, high: bool = False):
         m, be = models[k], backends[k]
@@ -259,6 +264,7 @@ def main() -> None:
         out[:5] = [len(recs), sat.sum() + uns.sum(), sat.sum(), uns.sum(), (uns & (st == "heuristic")).sum()]
         for i, name in enumerate(STAGES):
             out[5 + i] = (sat & (st == name)).sum()
+            out[5 + len(STAGES) + i] = (uns & (st == name)).sum()
         return out
 
     def run_step(step: int):
@@ -303,6 +309,12 @@ def main() -> None:
     tot = D.all_reduce_sum(info, tot)
     att, dec, sat, uns, uns_h = tot[:5].tolist()
     sat_stage = {name: int(tot[5 + i]) for i, name in enumerate(STAGES)}
+    unsat_stage = {name: int(tot[5 + len(STAGES) + i]) for i, name in enumerate(STAGES)}
+    # sound = SAT confirmed on the original network + UNSAT from rigorous proofs (heuristic-retry
+    # UNSAT and a trusted MILP's floating-point UNSAT excluded; a heuristic SAT that does not flip
+    # the original network excluded)
+    uns_unsound = sum(unsat_stage[k] for k in UNSOUND_UNSAT)
+    dec_sound = dec - uns_unsound - sat_stage["heuristic"]
     value = dec / dt_max if dt_max > 0 else 0.0
     per_step = att / max(1, args.steps)
     out = {
@@ -328,10 +340,11 @@ def main() -> None:
                    "batch_nodes": cfg.batch_nodes,
                    "chunk": args.chunk, "concurrency": conc, "priority_items": args.priority_items},
         "pct_verified": round(100.0 * dec / max(1.0, att), 3),
-        "pct_verified_sound": round(100.0 * (dec - uns_h - sat_stage["heuristic"]) / max(1.0, att), 3),
+        "pct_verified_sound": round(100.0 * dec_sound / max(1.0, att), 3),
         "partitions_per_s": round(att / dt_max, 3) if dt_max > 0 else 0.0,
         "sat": int(sat), "unsat": int(uns), "unknown": int(att - dec),
-        "unsat_sound": int(uns - uns_h), "unsat_heuristic": int(uns_h), "sat_by_stage": sat_stage,
+        "unsat_sound": int(uns - uns_unsound), "unsat_heuristic": int(uns_h), "sat_by_stage": sat_stage,
+        "unsat_by_stage": unsat_stage,
         "dist": {"world": info.world, "backend": backend_name,
                  "rank_ms_per_step": [round(x, 1) for x in rank_ms],
                  "skew_ms": round(max(rank_ms) - min(rank_ms), 1) if rank_ms else 0.0},
@@ -348,7 +361,7 @@ def main() -> None:
         n_shard = max(1, sum(len(c) for c in chunks))
         bcfg = {k: _replace(cfg, smt_backend="auto", anytime_seconds=args.budget_pass * len(c) / n_shard)
                 for k, c in enumerate(chunks)}
-        NB = 2 + len(STAGES) + 2
+        NB = 2 + len(STAGES) + 2 + len(STAGES)
 
         def budget_item(k: int, j: int, ids: np.ndarray):
             with thread_stream():
@@ -363,6 +376,8 @@ def main() -> None:
                 o[2 + i] = (uns & (st == name)).sum()
             o[2 + len(STAGES)] = sat.sum()
             o[3 + len(STAGES)] = uns.sum()
+            for i, name in enumerate(STAGES):
+                o[4 + len(STAGES) + i] = (sat & (st == name)).sum()
             return o
 
         D.barrier(info)
@@ -378,12 +393,18 @@ def main() -> None:
         bwall = D.all_reduce_max(info, time.time() - tb)
         btot = D.all_reduce_sum(info, np.asarray(btot, dtype=np.float64))
         out["pct_verified_at_budget"] = round(100.0 * btot[1] / max(1.0, btot[0]), 3)
+        b_uns = {name: int(btot[2 + i]) for i, name in enumerate(STAGES)}
+        b_sat = {name: int(btot[4 + len(STAGES) + i]) for i, name in enumerate(STAGES)}
+        b_sound = btot[1] - sum(b_uns[k] for k in UNSOUND_UNSAT) - b_sat["heuristic"]
+        out["pct_verified_at_budget_sound"] = round(100.0 * b_sound / max(1.0, btot[0]), 3)
         out["budget_pass"] = {
             "seconds_per_model": args.budget_pass, "wall_s": round(bwall, 2), "attempted": int(btot[0]),
             "decided": int(btot[1]), "sat": int(btot[2 + len(STAGES)]), "unsat": int(btot[3 + len(STAGES)]),
             "unsat_by_stage": {name: int(btot[2 + i]) for i, name in enumerate(STAGES) if btot[2 + i]},
+            "sat_by_stage": {k: v for k, v in b_sat.items() if v},
             "note": "untimed; anytime mode: BaB budgets x4 per round, falsifier rounds, HiGHS MILP rounds "
-                    "(UNSAT 'milp' = floating-point dual bound), heuristic retry last"}
+                    "(a MILP 'unsat' is a floating-point dual bound: recorded, partition left UNKNOWN), "
+                    "heuristic retry last; pct_verified_at_budget_sound excludes heuristic verdicts"}
     if args.profile and info.is_main:
         print(timer.report(), file=sys.stderr, flush=True)
     if info.is_main:

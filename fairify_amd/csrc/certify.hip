@@ -199,7 +199,8 @@ __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_pick_kernel(CertArgs 
   float bg = -INFINITY;
   int bq = 0;
   for (int qq = 0; qq < Q; ++qq) {
-    const float g = a.gmin[(size_t)n * Q + qq];
+    float g = a.gmin[(size_t)n * Q + qq];
+    if (g != g) g = INFINITY;     // a non-finite certificate value never closes a node
     if (g > bg) { bg = g; bq = qq; }
   }
   fa_pick_node(a, n, bg, bq, a.tstar[(size_t)n * Q + bq]);
@@ -225,6 +226,7 @@ fa_pair_fused_kernel(CertArgs a, int QG) {
   }
   float g = -INFINITY, t = 0.f;
   if (live) fa_pair_eval_one<NM>(a, n, qq, g, t);
+  if (g != g) g = INFINITY;       // NaN -> keep the node open (same rule as fa_pair_pick_kernel)
   int bq = live ? qq : 0x7fffffff;
   for (int o = 1; o < QG; o <<= 1) {     // groups are aligned to QG lanes (QG divides 64)
     const float g2 = __shfl_xor(g, o);

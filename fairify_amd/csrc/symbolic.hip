@@ -110,9 +110,13 @@ struct SymForm {
   static constexpr bool CR = !PAIR && TM >= 2;
 };
 
-__device__ __forceinline__ void fa_pq_to_ul(const f32x4& P, const f32x4& Q, int col, float gg, f32x4& U,
+// fc = FORM column of the lane (ct * 16 + (lane & 15)): only the two error columns (1 and 3 of
+// column tile 0) carry the recombination slack; a coefficient column of a later tile with the same
+// lane index must not move (round-2 advisor finding: +-e on coefficient columns 17 / 19 shifted
+// the forms instead of widening them)
+__device__ __forceinline__ void fa_pq_to_ul(const f32x4& P, const f32x4& Q, int fc, float gg, f32x4& U,
                                             f32x4& L) {
-  const float sl = (col == 1 || col == 3) ? 2.f * gg : 0.f;
+  const float sl = (fc == 1 || fc == 3) ? 2.f * gg : 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float q = Q[i], e = sl * fabsf(q);
@@ -441,7 +445,7 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
         xl += __shfl_xor(xl, 32, 64);
         U[bi][ct] = f32x4{grp == 0 ? xu : 0.f, 0.f, 0.f, 0.f};     // row 0 of tile bi = neuron 0
         Lq[bi][ct] = f32x4{grp == 0 ? xl : 0.f, 0.f, 0.f, 0.f};
-        if (CR) fa_pq_to_ul(f32x4(U[bi][ct]), f32x4(Lq[bi][ct]), col, gg, U[bi][ct], Lq[bi][ct]);
+        if (CR) fa_pq_to_ul(f32x4(U[bi][ct]), f32x4(Lq[bi][ct]), ct * 16 + col, gg, U[bi][ct], Lq[bi][ct]);
       }
     float nu[2][NT][4], nlo[2][NT][4];
     fa_sym_epilogue<NT, PAIR, PG, CR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
@@ -489,7 +493,8 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
       }
       if (CR) {
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) fa_pq_to_ul(f32x4(U[u][ct]), f32x4(Lq[u][ct]), col, gg, U[u][ct], Lq[u][ct]);
+        for (int ct = 0; ct < NT; ++ct)
+          fa_pq_to_ul(f32x4(U[u][ct]), f32x4(Lq[u][ct]), ct * 16 + col, gg, U[u][ct], Lq[u][ct]);
       }
     }
     float nu[2][NT][4], nlo[2][NT][4];

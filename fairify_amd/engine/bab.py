@@ -21,7 +21,7 @@ from __future__ import annotations
 import os
 import threading
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -76,11 +76,23 @@ class BaBResult:
                                              # (native runtime; the escalation filter's predictor)
 
 
-def _pa_table(q: ResolvedQuery, lo: np.ndarray, hi: np.ndarray):
-    """PA assignments shared by all partitions (PA ranges must be identical across the chunk)."""
+def pa_groups(q: ResolvedQuery, lo: np.ndarray, hi: np.ndarray) -> List[np.ndarray]:
+    """Row indices of the partitions sharing one protected-attribute range (one group when the
+    chunk's PA ranges are identical, e.g. a PA that the partition size does not split)."""
     pa = list(q.pa_idx)
-    if not np.all(lo[:, pa] == lo[:1, pa]) or not np.all(hi[:, pa] == hi[:1, pa]):
-        raise NotImplementedError("protected-attribute ranges differ between partitions of one chunk")
+    if len(lo) == 0 or (np.all(lo[:, pa] == lo[:1, pa]) and np.all(hi[:, pa] == hi[:1, pa])):
+        return [np.arange(len(lo))]
+    key = np.concatenate([lo[:, pa], hi[:, pa]], axis=1)
+    _, inv = np.unique(key, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    return [np.nonzero(inv == g)[0] for g in range(int(inv.max()) + 1)]
+
+
+def _pa_table(q: ResolvedQuery, lo: np.ndarray, hi: np.ndarray):
+    """PA assignments shared by all partitions of one PA group (:func:`pa_groups`)."""
+    pa = list(q.pa_idx)
+    assert np.all(lo[:, pa] == lo[:1, pa]) and np.all(hi[:, pa] == hi[:1, pa]), \
+        "internal: one PA table per group (callers split with pa_groups)"
     values = q.pa_values(lo[0], hi[0])
     pairs = q.pa_pairs(values)
     return values, pairs
@@ -137,6 +149,9 @@ class BaBSolver:
         ``exact_models`` when heuristic masks are active).
         """
         t0 = time.time()
+        groups = pa_groups(self.q, lo_np, hi_np)
+        if len(groups) > 1:
+            return self._solve_groups(groups, lo_np, hi_np, mlp_exact, init_status, exact_models, t0)
         cfg = self.cfg
         dev = self.dev
         P, n = lo_np.shape
@@ -300,6 +315,31 @@ class BaBSolver:
         st[status == SAT] = SAT
         nodes_np = nodes_t.cpu().numpy()
         return BaBResult(st.astype(np.int8), cex_x, cex_xp, nodes_np, it, time.time() - t0)
+
+    def _solve_groups(self, groups, lo_np, hi_np, mlp_exact, init_status, exact_models, t0) -> BaBResult:
+        """Partitions with different protected-attribute ranges: one solve per PA group (each has
+        its own table of PA assignments), results scattered back in input order.  Per-partition
+        forced-dead masks and masked exact models follow their partitions into the group."""
+        P, n = lo_np.shape
+        status = np.full(P, RUNNING, dtype=np.int8) if init_status is None else init_status.astype(np.int8).copy()
+        cex_x = np.zeros((P, n), dtype=np.int64)
+        cex_xp = np.zeros((P, n), dtype=np.int64)
+        nodes = np.zeros(P, dtype=np.int64)
+        open_left = np.zeros(P, dtype=np.int64)
+        iters = 0
+        dead_all = self.dead
+        for g in groups:
+            sub = BaBSolver(self.be, self.q, replace(self.cfg, time_budget=max(0.0, self.cfg.time_budget -
+                                                                                  (time.time() - t0))),
+                            dead=None if dead_all is None else dead_all[torch.from_numpy(g).to(dead_all.device)],
+                            timer=self.tm)
+            em = None if exact_models is None else [exact_models[int(k)] for k in g]
+            r = sub.solve(lo_np[g], hi_np[g], mlp_exact, init_status=status[g], exact_models=em)
+            status[g], cex_x[g], cex_xp[g], nodes[g] = r.status, r.cex_x, r.cex_xp, r.nodes
+            if r.open_left is not None:
+                open_left[g] = r.open_left
+            iters += r.iters
+        return BaBResult(status, cex_x, cex_xp, nodes, iters, time.time() - t0, open_left=open_left)
 
     # --------------------------------------------------------------------------------------
     def _runtime(self, values_np: np.ndarray, pairs_np: np.ndarray, n_run: int):

@@ -28,7 +28,7 @@ from ..partition import Grid
 from ..spec import ResolvedQuery
 from . import exact
 from . import prune as P_
-from .bab import SAT, UNKNOWN, UNSAT, RUNNING, VERDICT_NAMES, BaBConfig, BaBSolver, _pa_table
+from .bab import SAT, UNKNOWN, UNSAT, RUNNING, VERDICT_NAMES, BaBConfig, BaBSolver, _pa_table, pa_groups
 from .falsify import residual_falsify
 from .sim import simulate
 from ..utils import faults
@@ -84,10 +84,21 @@ class VerifyConfig:
     anytime_pool: int = 1 << 24          # live BaB nodes per group: group size = pool / budget
     anytime_max_samples: int = 16384
     anytime_milp_seconds: float = 1.0    # first MILP round's per-partition limit (x growth per round)
+    trust_milp: bool = False             # HiGHS MILP UNSAT rests on a floating-point dual bound: by
+                                         # default it is recorded (stage "milp") but the partition
+                                         # stays UNKNOWN for the rigorous stages; True = round-2
+                                         # behaviour (UNSAT, stage "milp", excluded from sound counts)
     keep_masks: bool = False             # K6: keep every partition's final dead-neuron mask (sound
                                          # prune, or the heuristic mask of a retried partition) as a
                                          # packed bitset (core["mask_bits"], ceil(N/8) B) for the
                                          # rank-0 gather, dedup and pruned-subnet export
+
+    def __post_init__(self):
+        # the rank-0 wire records (parallel/wire.py) carry the agree / tp / fp counts of the
+        # simulation points as uint16: reject a sample count they cannot hold here, before any
+        # rank has done GPU work (a late OverflowError would leave the other ranks in the gather)
+        if not 0 < int(self.sim_size) <= 65535:
+            raise ValueError(f"sim_size must be in 1..65535 (got {self.sim_size})")
 
 
 @dataclass
@@ -169,10 +180,11 @@ def _amortize(total: float, work: np.ndarray) -> np.ndarray:
 
 
 def _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, limit, workers, status, stage, cex_x, cex_xp,
-                deadline=None):
+                deadline=None, trust: bool = False):
     """HiGHS MILP on the partitions ``unk`` (per-partition time limit ``limit``, nothing starts
-    after ``deadline``); UNSAT and exactly confirmed SAT verdicts are written into the stage
-    arrays."""
+    after ``deadline``); exactly confirmed SAT verdicts are written into the stage arrays.  An
+    UNSAT answer (floating-point dual bound) is only recorded as stage ``milp`` on a partition that
+    stays UNKNOWN, unless ``trust`` (then it is an UNSAT verdict of stage ``milp``)."""
     from ..smt import milp
 
     futs = milp.submit(be, mlp, q, lo_np[unk], hi_np[unk], values_np, pairs_np, limit, workers=workers,
@@ -185,7 +197,9 @@ def _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, limit, worke
             t_note = time.time()
             print(f"[milp] {mlp.name}: {i + 1}/{len(unk)} partitions, limit {limit:.1f}s", flush=True)
         if verdict == "unsat":
-            status[k], stage[k] = UNSAT, "milp"
+            stage[k] = "milp"
+            if trust:
+                status[k] = UNSAT
         elif verdict == "sat" and pair is not None:
             cand_k.append(k)
             cand_x.append(pair[0])
@@ -211,17 +225,13 @@ def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.nd
     age with P=10) is verified as one group per distinct PA range; the records come back in
     ``ids`` order with the chunk's stage times apportioned over all of its partitions."""
     lo_np, hi_np = grid.decode(ids)
-    pa = list(q.pa_idx)
-    key = np.concatenate([lo_np[:, pa], hi_np[:, pa]], axis=1)
-    uniq, inv = np.unique(key, axis=0, return_inverse=True)
-    inv = inv.reshape(-1)
-    if len(uniq) <= 1:
+    groups = pa_groups(q, lo_np, hi_np)
+    if len(groups) <= 1:
         core, seg = _verify_group(be, mlp, q, ids, lo_np, hi_np, cfg, time_budget, timer, grid=grid)
     else:
         t0 = time.time()
         core, seg = None, np.zeros(5)
-        for g in range(len(uniq)):
-            sel = np.nonzero(inv == g)[0]
+        for sel in groups:
             left = None if time_budget is None else time_budget - (time.time() - t0)
             gcore, gseg = _verify_group(be, mlp, q, ids[sel], lo_np[sel], hi_np[sel], cfg, left, timer, grid=grid)
             if core is None:
@@ -434,7 +444,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             t0 = time.time()
             with tm("milp"):
                 _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, cfg.smt_timeout or cfg.soft_timeout,
-                            cfg.smt_workers, status, stage, cex_x, cex_xp)
+                            cfg.smt_workers, status, stage, cex_x, cex_xp, trust=cfg.trust_milp)
             t_smt = time.time() - t0
         elif backend != "milp":
             hs = _host_smt(cfg)
@@ -498,12 +508,14 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                     stage[hit] = "falsify"
                 # (b) exact host MILP with a growing per-partition time limit
                 if use_milp:
-                    unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+                    # partitions the MILP already claimed UNSAT (unverified) are not re-solved
+                    unk = np.nonzero((status == UNKNOWN) & ~forced & (stage != "milp"))[0]
                     left = deadline - time.time()
                     if unk.size and left > 0:
                         with tm("milp"):
                             _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, min(milp_limit, left),
-                                        cfg.smt_workers, status, stage, cex_x, cex_xp, deadline=deadline)
+                                        cfg.smt_workers, status, stage, cex_x, cex_xp, deadline=deadline,
+                                        trust=cfg.trust_milp)
                     milp_limit *= cfg.anytime_growth
                 # (c) deeper sound BaB, in groups that fit the node pool
                 e_budget *= cfg.anytime_growth
@@ -577,6 +589,13 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         hs = unk[hres.status == SAT]
         cex_x[hs] = hres.cex_x[hres.status == SAT]
         cex_xp[hs] = hres.cex_xp[hres.status == SAT]
+        if hs.size:
+            # a heuristic SAT pair was confirmed on the MASKED net; one that also flips the original
+            # network (the reference's V-accurate replay, src/AC/Verify-AC.py:225-258) is a sound
+            # counterexample: stage "heuristic-confirmed"
+            ok = exact.check_pair_constraints(cex_x[hs], cex_xp[hs], lo_np[hs], hi_np[hs], q.pa_idx, q.ra_idx, q.tau)
+            real = exact.is_violation(mlp, cex_x[hs], cex_xp[hs]) & ok
+            stage[hs[real]] = "heuristic-confirmed"
         nodes[unk] += hres.nodes
         sync()
         t_heur = time.time() - t0

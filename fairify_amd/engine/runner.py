@@ -32,11 +32,12 @@ from ..presets import Preset
 from ..report.csv_report import PartitionCSV, format_table, table_v_row_columns, write_summary
 from ..utils import faults
 from ..utils.timer import StageTimer
+from .stages import STAGES as _STAGES
 from .pipeline import PartitionRecord, StreamPool, VerifyConfig, concat_records, verify_chunk
 
 VCODE = {"sat": 1, "unsat": 2, "unknown": 0}
 VNAME = {v: k for k, v in VCODE.items()}
-STAGES = ["", "sim", "bab", "heuristic", "smt", "falsify", "milp"]
+STAGES = list(_STAGES)
 _SCALARS = ["h_attempt", "h_success", "b_comp", "s_comp", "st_comp", "h_comp", "t_comp", "sv_time", "s_time",
             "hv_time", "h_time", "total_time", "c_check", "v_accurate", "pruned_acc", "nodes"]
 
@@ -380,6 +381,10 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                                                                         STAGES.index("milp")])).sum())
             row["UNSAT_heuristic"] = int(((v == 2) & (stage_codes == STAGES.index("heuristic"))).sum())
             row["UNSAT_milp"] = int(((v == 2) & (stage_codes == STAGES.index("milp"))).sum())
+            # MILP "unsat" claims left UNKNOWN (default: a floating-point dual bound is no proof)
+            row["UNK_milp_unverified"] = int(((v == 0) & (stage_codes == STAGES.index("milp"))).sum())
+            sound_sat = int(((v == 1) & (stage_codes != STAGES.index("heuristic"))).sum())
+            row["Cov_sound%"] = round(100.0 * (sound_sat + row["UNSAT_sound"]) / max(1, len(grid)), 2)
             if anytime_budget:
                 row["anytime_budget_s"] = float(anytime_budget)
             row["wire_bytes_per_partition"] = round(wire_bytes[0] / max(1, wire_bytes[1]), 2)

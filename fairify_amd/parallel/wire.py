@@ -7,8 +7,8 @@ to every rank.  Here a rank ships, per round, one byte buffer:
 * segments      float64 [S, 5]: per verified chunk (count, t_sim+prune+bab, t_bab, t_heur,
                 t_replay) -- the per-partition time columns are apportioned from these on
                 rank 0 by :func:`engine.pipeline.derive_columns`, exactly as the producer would;
-* records       22 B each (``REC``): flags (verdict 2 b | stage 3 b | h_attempt | h_success |
-                c_check | v_accurate), dead-neuron counts b/s/st/h/t (uint16), Pruned-acc
+* records       22 B each (``REC``): flags (verdict 2 b | stage low 3 b | h_attempt | h_success |
+                c_check | v_accurate | stage high bit, engine/stages.py codes), dead-neuron counts b/s/st/h/t (uint16), Pruned-acc
                 numerator and the Pruned-F1 true / false positives (uint16), BaB node
                 expansions (uint32);
 * counterexamples, SAT partitions only: x [n0] and x' on the protected/relaxed dims only (every
@@ -31,7 +31,7 @@ import numpy as np
 from ..engine.pipeline import ChunkRecords
 
 VERDICTS = ("unknown", "sat", "unsat")
-STAGES = ("", "sim", "bab", "heuristic", "smt", "falsify", "milp")
+from ..engine.stages import STAGES
 REC = np.dtype([("flags", "<u2"), ("b", "<u2"), ("s", "<u2"), ("st", "<u2"), ("h", "<u2"), ("t", "<u2"),
                 ("agree", "<u2"), ("tp", "<u2"), ("fp", "<u2"), ("nodes", "<u4")])
 assert REC.itemsize == 22
@@ -62,7 +62,8 @@ def encode(recs: ChunkRecords, q) -> np.ndarray:
         if n and int(np.max(c[k])) > 0xFFFF:
             raise OverflowError(f"{k} exceeds 16 bits")
     stage = np.array([STAGES.index(s) if s in STAGES else 0 for s in c["stage"]], dtype=np.uint16)
-    flags = (verdict_codes(recs).astype(np.uint16) | (stage << 2) | ((c["h_attempt"] > 0).astype(np.uint16) << 5)
+    flags = (verdict_codes(recs).astype(np.uint16) | ((stage & 7) << 2) | ((stage >> 3) << 9)
+             | ((c["h_attempt"] > 0).astype(np.uint16) << 5)
              | ((c["h_success"] > 0).astype(np.uint16) << 6) | ((c["c_check"] > 0).astype(np.uint16) << 7)
              | ((c["v_accurate"] > 0).astype(np.uint16) << 8))
     rec = np.zeros(n, dtype=REC)
@@ -110,7 +111,7 @@ def decode(buf: np.ndarray, grid_ids: np.ndarray, orig_acc, n_neurons: int, sim_
     xp[:, dims] = cex[:, n0:]
     cxp[sat] = xp
     core = dict(grid_id=np.asarray(grid_ids, np.int64), verdict=verdict,
-                stage=np.array(STAGES, dtype=object)[(f >> 2) & 7],
+                stage=np.array(STAGES, dtype=object)[((f >> 2) & 7) | (((f >> 9) & 1) << 3)],
                 h_attempt=(f >> 5) & 1, h_success=(f >> 6) & 1,
                 b_cnt=rec["b"].astype(np.int64), s_cnt=rec["s"].astype(np.int64), st_cnt=rec["st"].astype(np.int64),
                 h_cnt=rec["h"].astype(np.int64), t_cnt=rec["t"].astype(np.int64), agree=rec["agree"].astype(np.int64),

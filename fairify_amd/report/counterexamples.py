@@ -5,10 +5,11 @@ Reference: ``decode_counterexample`` + ``counterexample.csv`` writers of the for
 src/BM/...-new2.py:343-404): encoded integers are mapped back to category strings with the
 training LabelEncoders, KBins bins to their midpoints, and each row gets the model output
 (sigmoid) and the predicted class; German rows are mapped back to the raw dataset's A-codes
-(sex A91/A92 and the grouped categories, src/GC/Verify-GC-experiment-new2.py:364-414).  Rows
-that cannot be decoded (codes outside the encoder's
-classes) are dropped, like the reference's BM variant.  An ``.npz`` with the raw pairs is
-written next to it (input of ``repair``).
+(sex A91/A92 and the grouped categories, src/GC/Verify-GC-experiment-new2.py:364-414).  A code
+outside an encoder's classes follows the reference per suite: Adult and German write the string
+``f"{col}_{value}"`` and keep the row (src/AC/...-new2.py:373-374, src/GC/...-new2.py:355-356),
+Bank drops the pair (src/BM/...-new2.py:360-368).  An ``.npz`` with the raw pairs is written next to
+it (input of ``repair``).
 """
 from __future__ import annotations
 
@@ -19,7 +20,14 @@ import numpy as np
 import pandas as pd
 
 
-def _decode_column(vals: np.ndarray, enc) -> Optional[np.ndarray]:
+def _fmt_code(v) -> str:
+    f = float(v)
+    return str(int(f)) if f == int(f) else str(f)
+
+
+def _decode_column(vals: np.ndarray, enc, name: str = "", keep_undecodable: bool = True) -> np.ndarray:
+    """Encoded column -> decoded values.  An undecodable label code becomes ``f"{name}_{code}"``
+    (``keep_undecodable``) or None (the row pair is dropped)."""
     if enc is None:
         return vals
     if hasattr(enc, "classes_"):            # LabelEncoder
@@ -27,12 +35,17 @@ def _decode_column(vals: np.ndarray, enc) -> Optional[np.ndarray]:
         ok = (codes >= 0) & (codes < len(enc.classes_))
         out = np.empty(len(vals), dtype=object)
         out[ok] = enc.classes_[codes[ok]]
-        out[~ok] = None
+        out[~ok] = [f"{name}_{_fmt_code(v)}" for v in vals[~ok]] if keep_undecodable else None
         return out
-    if hasattr(enc, "bin_edges_"):          # KBinsDiscretizer -> bin midpoints
+    if hasattr(enc, "bin_edges_"):          # KBinsDiscretizer -> integer bin midpoint
         e = enc.bin_edges_[0]
-        b = np.clip(np.rint(vals).astype(int), 0, len(e) - 2)
-        return 0.5 * (e[b] + e[b + 1])
+        b = np.rint(vals).astype(int)
+        out = np.empty(len(vals), dtype=object)
+        inner = (b >= 0) & (b < len(e) - 1)
+        bi = np.clip(b, 0, len(e) - 2)
+        # int((start + end) / 2), the last edge past the last bin (src/AC/...-new2.py:360-370)
+        out[:] = np.where(inner, np.trunc(0.5 * (e[bi] + e[bi + 1])), np.trunc(e[-1])).astype(np.int64)
+        return out
     return vals
 
 
@@ -82,7 +95,9 @@ def export_counterexamples(preset: str, model: str, results: str, out: Optional[
     except Exception:
         enc = {}
     z = mlp.logits(pairs)
-    out_df = pd.DataFrame({name: _decode_column(pairs[:, i], enc.get(name)) for i, name in enumerate(dom.names)})
+    keep_und = pre.suite != "bank"
+    out_df = pd.DataFrame({name: _decode_column(pairs[:, i], enc.get(name), name, keep_und)
+                           for i, name in enumerate(dom.names)})
     out_df["output"] = 0.5 * (1 + np.tanh(0.5 * z))
     label_col = "decision" if pre.suite == "german" else "prediction"
     out_df[label_col] = (z > 0).astype(int)

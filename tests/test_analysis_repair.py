@@ -142,3 +142,21 @@ def test_experiment_metrics_csv(tmp_path):
         acc, f1 = float(r[3]), float(r[4])
         assert 0.0 <= acc <= 1.0 and 0.0 <= f1 <= 1.0
         assert r[1] == rows[1][1] and r[5:] == rows[1][5:]          # model-level columns
+
+
+def test_decode_undecodable_codes_follow_reference():
+    """A code outside the LabelEncoder's classes: Adult / German keep the row with the string
+    f"{col}_{value}" (src/GC/Verify-GC-experiment-new2.py:355-356, src/AC/...-new2.py:373-374),
+    Bank drops the pair (src/BM/...-new2.py:360-368); KBins bins decode to int((a + b) / 2) and
+    past the last bin to the last edge (src/AC/...-new2.py:360-370)."""
+    from types import SimpleNamespace
+
+    from fairify_amd.report.counterexamples import _decode_column
+
+    le = SimpleNamespace(classes_=np.array(["A", "B", "C"], dtype=object))
+    out = _decode_column(np.array([0.0, 2.0, 3.0, -1.0]), le, "purpose")
+    assert out.tolist() == ["A", "C", "purpose_3", "purpose_-1"]
+    out = _decode_column(np.array([1.0, 7.0]), le, "job", keep_undecodable=False)
+    assert out.tolist() == ["B", None]
+    kb = SimpleNamespace(bin_edges_=[np.array([0.0, 5.0, 15.0])])
+    assert _decode_column(np.array([0.0, 1.0, 2.0]), kb, "capital-gain").tolist() == [2, 10, 15]

@@ -50,3 +50,21 @@ def test_world_size_must_match_gpus():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
                         "--steps", "1"], capture_output=True, text=True, env=env, timeout=120, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_sound_fields_exclude_heuristic_and_milp():
+    """pct_verified_sound / unsat_sound = decided minus heuristic-retry verdicts minus MILP UNSAT
+    (a trusted HiGHS dual bound is still no proof), on a small run where both stages fire."""
+    d = _bench(1, ("--models", "AC-8", "--node-budget", "8", "--escalate-budget", "0", "--smt", "milp",
+                   "--trust-milp"))
+    att = d["sat"] + d["unsat"] + d["unknown"]
+    us = d["unsat_by_stage"]
+    assert sum(us.values()) == d["unsat"] and sum(d["sat_by_stage"].values()) == d["sat"]
+    assert us["milp"] > 0, us                     # the test exercises the MILP stage
+    assert d["unsat_sound"] == d["unsat"] - us["milp"] - us["heuristic"]
+    sound = d["sat"] + d["unsat"] - us["milp"] - us["heuristic"] - d["sat_by_stage"]["heuristic"]
+    assert abs(d["pct_verified_sound"] - round(100.0 * sound / att, 3)) < 1e-9
+    # default: an untrusted MILP 'unsat' is no verdict
+    d2 = _bench(1, ("--models", "AC-8", "--node-budget", "8", "--escalate-budget", "0", "--smt", "milp"))
+    assert d2["unsat_by_stage"]["milp"] == 0
+    assert d2["unsat"] + d2["unknown"] >= d["unsat"] + d["unknown"] - 1e-9

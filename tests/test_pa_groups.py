@@ -36,3 +36,24 @@ def test_mixed_pa_ranges_in_one_chunk():
     X, XP = recs.cols["cex_x"][sat], recs.cols["cex_xp"][sat]
     assert exact.check_pair_constraints(X, XP, lo[sat], hi[sat], q.pa_idx, q.ra_idx, q.tau).all()
     assert exact.is_violation(m, X, XP).all()
+
+
+def test_bab_solver_groups_pa_ranges_itself():
+    """BaBSolver.solve splits a mixed-PA chunk into PA groups internally (no caller grouping
+    needed): same verdicts as one solve per group, in input order."""
+    from fairify_amd.engine.bab import BaBConfig, BaBSolver, pa_groups
+
+    pre = replace(presets.get("src/AC-sex"), query=Query(("age",)), partition_size=30)
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, 0)[:32]
+    lo, hi = grid.decode(ids)
+    groups = pa_groups(q, lo, hi)
+    assert len(groups) > 1 and sorted(np.concatenate(groups).tolist()) == list(range(len(ids)))
+    m = get_model("AC-8", weights="random", seed=1)
+    be = Backend(m)
+    bc = BaBConfig(node_budget=32)
+    whole = BaBSolver(be, q, bc).solve(lo, hi, m)
+    for g in groups:
+        part = BaBSolver(be, q, bc).solve(lo[g], hi[g], m)
+        assert np.array_equal(part.status, whole.status[g])
+        assert np.array_equal(part.cex_x, whole.cex_x[g]) and np.array_equal(part.nodes, whole.nodes[g])

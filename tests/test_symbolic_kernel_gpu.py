@@ -231,3 +231,47 @@ def test_packed_native_bab_matches_bruteforce(cuda, name):
             assert viol, k
         elif res.status[k] == UNSAT:
             assert not viol, k
+
+
+@pytest.mark.parametrize("hidden2", [False, True])
+def test_cr_kernel_error_slack_only_on_error_columns(cuda, hidden2):
+    """Centre/radius multi-tile kernel (DF shape: 30 inputs, PA SEX_2 folded -> NT=3, TM=2).
+
+    Round-2 advisor finding: the 2 gamma |Q| recombination slack meant for the error columns 1 / 3
+    also landed on coefficient columns 17 / 19 of the second column tile, moving a zero upper
+    coefficient by +e.  cdim[13] = BILL_AMT6 has a negative domain (-339 603 ..), so e * |x|
+    pulled the upper form below the network.  The net is built so that the logit's upper form has
+    an exactly zero coefficient on dim 13 next to a large radius: hidden neuron 0 is unstable with
+    the lambda = 0 lower relaxation, the next weight is -1.  Bounds must enclose the brute-force
+    logits of every lattice point of the box."""
+    from fairify_amd.models.mlp import MLP
+
+    n0 = 30
+    W1 = np.zeros((n0, 16), np.float32)
+    b1 = np.zeros(16, np.float32)
+    W1[13, 0], b1[0] = 1.0, 339543.0            # z1 in [-60, 40] over the box: lambda = 0, s = 0.4
+    if hidden2:
+        W2 = np.zeros((16, 16), np.float32)
+        b2 = np.zeros(16, np.float32)
+        W2[0, 0], b2[0] = -1.0, 10.0             # z2 = 10 - relu(z1) in [-30, 10]
+        W3 = np.zeros((16, 1), np.float32)
+        W3[0, 0] = 1.0
+        m = MLP([W1, W2, W3], [b1, b2, np.zeros(1, np.float32)], name="cr-probe2")
+    else:
+        W2 = np.zeros((16, 1), np.float32)
+        W2[0, 0] = -1.0
+        m = MLP([W1, W2], [b1, np.zeros(1, np.float32)], name="cr-probe")
+    lo = np.zeros((4, n0), np.float32)
+    hi = np.zeros((4, n0), np.float32)
+    lo[:, 13], hi[:, 13] = -339603.0, -339503.0
+    lo[:, 20] = hi[:, 20] = np.array([0, 1, 0, 1], np.float32)
+    be = Backend(m, cuda)
+    r = be.bounds(torch.from_numpy(lo).to(cuda), torch.from_numpy(hi).to(cuda), mode="symbolic", fold=(20,))
+    pts = np.zeros((101, n0))
+    pts[:, 13] = np.arange(-339603, -339502)
+    z = m.logits(pts)
+    assert float(r.out_ub.max()) >= z.max() and float(r.out_lb.min()) <= z.min()
+    for k in range(4):
+        Lf = pts @ r.Lc[k].double().cpu().numpy() + float(r.L0[k]) - float(r.Le[k])
+        Uf = pts @ r.Uc[k].double().cpu().numpy() + float(r.U0[k]) + float(r.Ue[k])
+        assert np.all(z >= Lf - 1e-9) and np.all(z <= Uf + 1e-9), k

@@ -1,0 +1,63 @@
+#!/usr/bin/env python
+"""Dump the sound-UNKNOWN residue of the bench configuration (heuristic retry off) per model.
+
+Runs bench.py's default sound schedule (node budget 512, inline escalation to 32 768 behind the
+frontier gates, residual falsifier) on the first --limit partitions of the seeded order and
+writes OUT/<model>.npz with the grid ids, verdicts, stages, nodes and open-frontier sizes, the
+input of the CPU experiments on the residue (tools/exp_*.py).
+
+    python tools/dump_residue.py --models AC-8,AC-12,AC-7 --limit 4000 --out gpurun_out/residue
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default="src/AC-sex")
+    ap.add_argument("--models", default="AC-8,AC-12,AC-7")
+    ap.add_argument("--limit", type=int, default=4000)
+    ap.add_argument("--out", default="gpurun_out/residue")
+    args = ap.parse_args()
+    import torch
+
+    from fairify_amd import presets
+    from fairify_amd.engine.pipeline import VerifyConfig, verify_chunk
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.ops.backend import Backend
+    from fairify_amd.partition import processing_order
+
+    dev = torch.device("cuda" if torch.cuda.device_count() else "cpu")
+    pre = presets.get(args.preset)
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, seed=0)[:args.limit]
+    cfg = VerifyConfig(sim_size=pre.sim_size, chunk=4096, soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
+                       node_budget=512, heuristic=False, heuristic_p=pre.heuristic_p, escalate_budget=32768,
+                       escalate_max_open=384, smt_backend="none",
+                       escalate_probation=((2048, 768), (4096, 768), (8192, 768), (16384, 1024)))
+    os.makedirs(args.out, exist_ok=True)
+    for name in args.models.split(","):
+        m = get_model(name, weights="random", seed=0)
+        be = Backend(m, device=dev)
+        t0 = time.time()
+        recs = verify_chunk(be, m, q, grid, ids, cfg)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        c = recs.cols
+        v = c["verdict"]
+        np.savez(os.path.join(args.out, f"{name}.npz"), grid_id=c["grid_id"], verdict=v.astype(str),
+                 stage=c["stage"].astype(str), nodes=c["nodes"])
+        print(f"{name}: {len(ids)} partitions in {time.time() - t0:.2f}s: sat {(v == 'sat').sum()} "
+              f"unsat {(v == 'unsat').sum()} unknown {(v == 'unknown').sum()}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
