@@ -136,20 +136,34 @@ class Backend:
     # ----------------------------------------------------------------------------- bounds
     def bounds(self, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic",
                dead: Optional[torch.Tensor] = None, keep_layers: bool = False, fold=(),
-               crown: bool = False) -> ref.BoundResult:
+               crown: bool = False, phase: Optional[torch.Tensor] = None) -> ref.BoundResult:
         """``fold``: dims degenerate (lo == hi) in every row — a HIP-kernel layout hint only.
-        ``crown``: refine the logit forms/bounds with the backward pass (symbolic mode only)."""
+        ``crown``: refine the logit forms/bounds with the backward pass (symbolic mode only).
+        ``phase``: [R, N_hidden] int8 ReLU phases of the rows' branch regions (-1 / 0 / +1,
+        ref.bounds); the result's ``infeasible`` flags rows whose region is empty."""
         lo = lo.to(self.dtype)
         hi = hi.to(self.dtype)
         crown = crown and mode == "symbolic"
         if self.hip:
             from . import hip
 
-            r = hip.bounds(self, lo, hi, mode=mode, dead=dead, keep_layers=keep_layers or crown, fold=fold)
+            r = hip.bounds(self, lo, hi, mode=mode, dead=dead, keep_layers=keep_layers or crown, fold=fold,
+                           phase=phase)
             return hip.crown(self, lo, hi, r, dead) if crown else r
         r = ref.bounds(self.ws, self.bs, lo, hi, mode=mode, dead=dead, unit=self.unit,
-                       keep_layers=keep_layers or crown)
+                       keep_layers=keep_layers or crown, phase=phase)
         return ref.crown_output(self.ws, self.bs, lo, hi, r, dead, unit=self.unit) if crown else r
+
+    def crown_phase(self, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult,
+                    phase: Optional[torch.Tensor] = None):
+        """Backward bounds of the ReLU-phase search concretised at every layer (ref.crown_phase)."""
+        lo = lo.to(self.dtype)
+        hi = hi.to(self.dtype)
+        if self.hip:
+            from . import hip
+
+            return hip.crown_phase(self, lo, hi, res, phase)
+        return ref.crown_phase(self.ws, self.bs, lo, hi, res, phase, unit=self.unit)
 
     def point_bounds(self, x: torch.Tensor, dead: Optional[torch.Tensor] = None):
         """Rigorous [lb, ub] of the logit at points x [R, n0] (candidate-pair screening)."""

@@ -200,6 +200,9 @@ class BoundResult:
     lay_lb_full: Optional[torch.Tensor] = None
     lay_ub_full: Optional[torch.Tensor] = None
     dead_u8: Optional[torch.Tensor] = None
+    # ReLU-phase rows (``phase`` given): the row's branch region is empty (a neuron fixed inactive
+    # with lb > 0, or fixed active with ub < 0)
+    infeasible: Optional[torch.Tensor] = None
 
 
 def _concretize(E: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor):
@@ -219,7 +222,8 @@ def _concretize(E: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor):
 
 def bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Tensor, hi: torch.Tensor,
            mode: str = "symbolic", dead: Optional[torch.Tensor] = None, unit: Optional[float] = None,
-           keep_layers: bool = False, lower_slope: str = "adaptive") -> BoundResult:
+           keep_layers: bool = False, lower_slope: str = "adaptive",
+           phase: Optional[torch.Tensor] = None) -> BoundResult:
     """Sound bounds of every neuron and of the logit over boxes ``[lo, hi]`` [R, n0].
 
     Symbolic mode keeps linear forms ``E(x) = sum_i E_i x_i + E_c`` per neuron as matrices
@@ -232,6 +236,14 @@ def bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Ten
     summed, so sign-structured sums (e.g. non-positive weights on non-negative ReLU outputs)
     keep exact zeros exact — essential under the strict ``N(x) < 0 < N(x')`` semantics.
     ``mode='ibp'`` keeps only the interval rows.
+
+    ``phase`` [R, N_hidden] int8 (ReLU-split branch-and-bound, engine/relu_bab.py): -1 = the row's
+    branch region has z <= 0 at that neuron (output 0, like a forced-dead neuron), +1 = z >= 0
+    there (relu(z) = z: the upper relaxation is the identity instead of the chord; the lower one
+    stays lambda * L, valid because z >= 0 on the region; the range of the output is still
+    [max(lb, 0), max(ub, 0)]).  Every bound then holds on the branch region, which is all the
+    search needs; a region proven empty (fixed inactive with lb > 0, fixed active with ub < 0) is
+    flagged in ``infeasible``.
     """
     dt = lo.dtype
     if unit is None:
@@ -253,6 +265,7 @@ def bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Ten
     gi = gamma(1, unit)
     layer_lb, layer_ub, deads, actives = [], [], [], []
     off = 0
+    infeas = None
     nL = len(ws)
     res = None
     for l in range(nL):
@@ -300,6 +313,13 @@ def bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Ten
             forced = dead[:, off:off + n].bool()
         else:
             forced = torch.zeros_like(is_dead)
+        fact = torch.zeros_like(is_dead)
+        if phase is not None:
+            ph = phase[:, off:off + n]
+            forced = forced | (ph < 0)
+            fact = ph > 0
+            bad = ((ph < 0) & (lb > 0)) | ((ph > 0) & (ub < 0))
+            infeas = bad.any(dim=1) if infeas is None else (infeas | bad.any(dim=1))
         off += n
         deads.append(is_dead)
         actives.append(is_act)
@@ -313,7 +333,7 @@ def bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Ten
         # zero if dead, else the chord over [a, bb] of T
         a = lbU - gc * MUn + eUn
         bb = ubU + gc * MUn + eUn
-        identU = (is_act | (a >= 0)) & ~zero
+        identU = (is_act | (a >= 0) | fact) & ~zero
         cross = ~(zero | identU)
         denom = torch.where(cross, bb - a, torch.ones_like(bb))
         s = torch.where(cross, (bb / denom) * (1 + 4 * unit), torch.ones_like(bb))
@@ -340,6 +360,8 @@ def bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Ten
     if deads:
         res.dead = torch.cat(deads, dim=1)
         res.active = torch.cat(actives, dim=1)
+    if phase is not None:
+        res.infeasible = infeas if infeas is not None else torch.zeros(R, dtype=torch.bool, device=dev)
     if keep_layers:
         res.layer_lb, res.layer_ub = layer_lb, layer_ub
     return res
@@ -433,6 +455,156 @@ def crown_output(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: tor
     r.U0 = torch.where(useU[:, 0], -cU, res.U0.to(dt)).to(res.U0.dtype)
     r.Ue = torch.where(useU[:, 0], eU, res.Ue.to(dt)).to(res.Ue.dtype)
     return r
+
+
+@dataclass
+class PhaseCrown:
+    """Backward bounds of the ReLU-split search (:func:`crown_phase`), per row and sign
+    (column 0: lower bound of N, column 1: lower bound of -N)."""
+    low: torch.Tensor           # [R, 2] best lower bound over concretisation layers and slope policies
+    split: torch.Tensor         # [R, 2] int64 hidden-neuron index to split for that bound (-1: none)
+    score: torch.Tensor         # [R, 2] its score
+
+
+ALPHA_POLICIES = ("adaptive", "zero", "one")
+
+
+def crown_phase(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Tensor, hi: torch.Tensor,
+                res: BoundResult, phase: Optional[torch.Tensor] = None, unit: Optional[float] = None,
+                policies: Sequence[str] = ALPHA_POLICIES):
+    """Backward (CROWN) bounds of the logit for the ReLU-phase search, concretised at EVERY layer.
+
+    ``res`` = forward bounds of the rows (with ``phase``, keep_layers).  For each sign and each
+    lower-slope policy (adaptive = the forward pass's rule, all 0, all 1) the multipliers are
+    back-substituted from the logit; at every hidden layer the bound ``sigma N >= sum lambda_j a_j +
+    c`` is concretised over the post-activation ranges ``a_j in [max(lb, 0), max(ub, 0)]`` before
+    the layer is relaxed, and finally over the input box.  The best value wins.
+
+    Exact zeros: the coefficient errors are kept per coefficient (``E``, the rounding of
+    ``lambda = W mu``) until the next layer, so a term whose range starts at 0 and whose
+    coefficient is certainly >= 0 contributes exactly 0 with no rounding charge.  On zero-bias
+    networks (the random-init bench models) a branch where every path to a positive logit is
+    closed then bounds the logit by exactly 0 -- the strict ``N(x) < 0 < N(x')`` query needs that
+    (csrc/relu.hip: fa_crown_phase_kernel has the same arithmetic).
+
+    Split choice per (row, sign), from the policy with the best bound: the unstable unsplit neuron
+    with the largest chord intercept ``|mu_j l_j|`` the bound pays (+ 1e-3 |lambda_j| x triangle
+    gap as a tie-break); forced-active neurons have no intercept.  Returns (:class:`PhaseCrown`,
+    input forms {sign: (coef [R, n0], const [R], err [R], low_at_input [R])} of the policy with
+    the best input-level bound).
+    """
+    dt = lo.dtype
+    if unit is None:
+        unit = FP64_UNIT if dt == torch.float64 else FP32_UNIT
+    R, n0 = lo.shape
+    L = len(ws)
+    dev = lo.device
+    lbs, ubs = res.layer_lb, res.layer_ub
+    offs = [0]
+    for l in range(L - 1):
+        offs.append(offs[-1] + ws[l].shape[1])
+    mx_in = torch.maximum(lo.abs(), hi.abs())
+    K = 4 * L + 4 + sum(2 * int(w.shape[1]) for w in ws)
+    gK = gamma(K, unit)
+    low = torch.full((R, 2), -float("inf"), dtype=dt, device=dev)
+    split = torch.full((R, 2), -1, dtype=torch.int64, device=dev)
+    score = torch.zeros(R, 2, dtype=dt, device=dev)
+    forms = {}
+    ar = torch.arange(R, device=dev)
+    for si, sg in enumerate((1.0, -1.0)):
+        best_in = None
+        for pol in policies:
+            lam = (sg * ws[L - 1][:, 0].to(dt))[None].expand(R, -1).clone()
+            E = torch.zeros_like(lam)
+            c = torch.full((R,), sg * float(bs[L - 1][0]), dtype=dt, device=dev)
+            err = torch.zeros(R, dtype=dt, device=dev)
+            pol_best = torch.full((R,), -float("inf"), dtype=dt, device=dev)
+            sc_best = torch.full((R,), -1.0, dtype=dt, device=dev)
+            sc_idx = torch.full((R,), -1, dtype=torch.int64, device=dev)
+            for l in range(L - 2, -1, -1):
+                W = ws[l].to(dt)
+                b = bs[l].to(dt)
+                n = W.shape[1]
+                lb, ub = lbs[l].to(dt), ubs[l].to(dt)
+                ph = phase[:, offs[l]:offs[l] + n] if phase is not None else torch.zeros_like(lb, dtype=torch.int8)
+                dd = (ub <= 0) | (ph < 0)
+                fact = (ph > 0) & ~dd
+                act = (lb >= 0) & ~dd
+                unst = ~(dd | act)
+                # ---- concretise at this layer's post-activations a_j in [alo, ahi]
+                alo = torch.where(dd, torch.zeros_like(lb), lb.clamp(min=0))
+                ahi = torch.where(dd, torch.zeros_like(ub), ub.clamp(min=0))
+                exact0 = (ahi == 0) | ((alo == 0) & (lam - E >= 0))
+                prod = torch.minimum(lam * alo, lam * ahi)
+                eprod = E * ahi
+                term = torch.where(exact0, torch.zeros_like(prod), prod - eprod)
+                tv = term.sum(1) + c
+                tmag = torch.where(exact0, torch.zeros_like(prod), prod.abs() + eprod).sum(1) + c.abs()
+                v = tv - err * (1 + 2 * gK) - gamma(n + 3, unit) * tmag
+                pol_best = torch.maximum(pol_best, v)
+                # ---- coefficients of uncertain sign (|lambda| <= E): relax lambda (the computed
+                # value) and charge the difference E |a| to the constant; certain signs keep the
+                # interval [lambda - E, lambda + E] through the relaxation (no charge)
+                unc = ((lam - E) < 0) & ((lam + E) > 0) & ~dd
+                err = err + torch.where(unc, E * ahi, torch.zeros_like(E)).sum(1)
+                E = torch.where(unc | dd, torch.zeros_like(E), E)
+                # ---- relax this layer's ReLUs
+                if pol == "adaptive":
+                    alpha = (ub > -lb).to(dt)
+                elif pol == "zero":
+                    alpha = torch.zeros_like(ub)
+                else:
+                    alpha = torch.ones_like(ub)
+                chord_ok = unst & ~fact
+                den = torch.where(chord_ok, ub - lb, torch.ones_like(ub))
+                s_ch = torch.where(chord_ok, (ub / den) * (1 + 4 * unit), torch.ones_like(ub))
+                slope = torch.where(act, torch.ones_like(ub), torch.where(dd, torch.zeros_like(ub),
+                                    torch.where(lam >= 0, alpha, s_ch)))
+                mu = lam * slope
+                chord = chord_ok & (lam < 0)
+                t = torch.where(chord, -mu * lb, torch.zeros_like(ub))
+                zmax = torch.maximum(lb.abs(), ub.abs())
+                # chord multipliers / intercepts are rounded (and carry E through the intercept)
+                e_rel = torch.where(chord, 3 * unit * (mu.abs() * zmax + t.abs()) + E * s_ch * lb.abs(),
+                                    torch.zeros_like(ub))
+                Emu = E * slope * (1 + 4 * unit)            # |mu_hat - mu| from the coefficient interval
+                # split score: the chord intercept this bound pays (+ tie-break on the triangle gap)
+                gap = torch.where(chord_ok, -ub * lb / den, torch.zeros_like(ub))
+                sc = torch.where(chord_ok, t.abs() + 1e-3 * lam.abs() * gap, torch.full_like(ub, -1.0))
+                if phase is not None:
+                    sc = torch.where(ph != 0, torch.full_like(sc, -1.0), sc)
+                smax, sarg = sc.max(dim=1)
+                better = smax > sc_best
+                sc_best = torch.where(better, smax, sc_best)
+                sc_idx = torch.where(better, sarg + offs[l], sc_idx)
+                csum = (mu * b[None]).sum(1) + t.sum(1)
+                cmag = c.abs() + (mu * b[None]).abs().sum(1) + t.abs().sum(1)
+                c = c + csum
+                err = err + e_rel.sum(1) + gamma(2 * n + 1, unit) * cmag + (Emu * b[None].abs()).sum(1)
+                lam = mu @ W.T
+                # new coefficient interval: propagated E through |W| plus the rounding of W mu
+                E = (Emu @ W.abs().T) * (1 + gamma(n + 1, unit)) + gamma(n + 1, unit) * (mu.abs() @ W.abs().T)
+            # ---- concretise over the input box
+            err_in = (err + (E * mx_in).sum(1)) * (1 + 2 * gK)
+            a_ = lam * lo
+            b_ = lam * hi
+            conc = torch.minimum(a_, b_).sum(1) + c
+            cmg = (lam.abs() * mx_in).sum(1) + c.abs()
+            low_in = conc - err_in - gamma(n0 + 1, unit) * cmg - gamma(1, unit) * conc.abs()
+            pol_best = torch.maximum(pol_best, low_in)
+            take = pol_best > low[:, si]
+            low[:, si] = torch.where(take, pol_best, low[:, si])
+            split[:, si] = torch.where(take, sc_idx, split[:, si])
+            score[:, si] = torch.where(take, sc_best, score[:, si])
+            if best_in is None:
+                best_in = (lam, c, err_in, low_in)
+            else:
+                tk = low_in > best_in[3]
+                best_in = (torch.where(tk[:, None], lam, best_in[0]), torch.where(tk, c, best_in[1]),
+                           torch.where(tk, err_in, best_in[2]), torch.where(tk, low_in, best_in[3]))
+        forms[sg] = best_in
+    split = torch.where(score > 0, split, torch.full_like(split, -1))
+    return PhaseCrown(low=low, split=split, score=score), forms
 
 
 # ======================================================================================

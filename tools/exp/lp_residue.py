@@ -32,6 +32,16 @@ def ibp(ws, bs, lo, hi):
     return out
 
 
+def lp_a_index(lp, c, l, j):
+    idx = lp.n0
+    for cc in range(lp.V):
+        for ll, h in enumerate(lp.H):
+            if (cc, ll) == (c, l):
+                return idx + j
+            idx += h
+    raise KeyError
+
+
 class PairLP:
     """Triangle LP of V copies of the net on a shared box; PA dims fixed per copy."""
 
@@ -93,13 +103,13 @@ class PairLP:
                     lj, uj = zl[j], zh[j]
                     if ph < 0 or uj <= 0:
                         vb[o + j] = (0, 0)
-                        if ph < 0:      # z <= 0
+                        if ph < 0 and not NOCON:      # z <= 0
                             A.append(M[j]); bvec.append(-k[j])
                         continue
                     if ph > 0 or lj >= 0:
                         r = -M[j].copy(); r[o + j] += 1   # a - z = 0
                         Aeq.append(r); beq.append(k[j])
-                        if ph > 0:      # z >= 0  ->  -z <= 0
+                        if ph > 0 and not NOCON:      # z >= 0  ->  -z <= 0
                             A.append(-M[j]); bvec.append(k[j])
                         continue
                     vb[o + j] = (0, None)
@@ -129,6 +139,11 @@ class PairLP:
         return -res.fun, res.x
 
 
+BRANCH = "area"
+NOCON = False
+VERB = os.environ.get("VERB") == "1"
+
+
 def relu_bab(lp: PairLP, orient, max_nodes=2000):
     """DFS ReLU-phase BaB on the coupled LP; returns (closed?, nodes)."""
     stack = [dict()]
@@ -141,6 +156,8 @@ def relu_bab(lp: PairLP, orient, max_nodes=2000):
         val, x = lp.solve(orient, ph)
         if val <= 1e-9:
             continue
+        if x is None:
+            return None, nodes
         # pick the unstable unfixed neuron with the largest triangle violation at the LP point
         best, bk = -1.0, None
         n0 = lp.n0
@@ -156,11 +173,20 @@ def relu_bab(lp: PairLP, orient, max_nodes=2000):
                     if (c, l, j) in ph or zh[j] <= 0 or zl[j] >= 0:
                         continue
                     sc = -zl[j] * zh[j] / (zh[j] - zl[j])
+                    if BRANCH == "viol":      # triangle violation at the LP point
+                        aj = x[lp_a_index(lp, c, l, j)]
+                        sc = aj - max(z[j], 0.0)
+                    elif BRANCH == "late":    # last hidden layer first
+                        sc = sc + 1e6 * l
+                    elif BRANCH == "late_copy":  # only the copy whose output must be positive
+                        sc = sc + 1e6 * l + (1e9 if c == orient[1] else 0)
                     if sc > best:
                         best, bk = sc, (c, l, j)
                 act = np.maximum(z, 0)
         if bk is None:
+            if VERB: print("   open leaf", ph, val)
             return False, nodes        # LP exact with all phases fixed: real-valued violation
+        if VERB: print("   split", bk, "at", ph, "val", round(val, 5))
         for s in (-1, 1):
             d = dict(ph); d[bk] = s
             stack.append(d)
@@ -173,7 +199,13 @@ def main():
     ap.add_argument("--residue", default=None)
     ap.add_argument("--n", type=int, default=30)
     ap.add_argument("--max-nodes", type=int, default=2000)
+    ap.add_argument("--branch", default="area")
+    ap.add_argument("--nocon", action="store_true")
     args = ap.parse_args()
+    global BRANCH
+    BRANCH = args.branch
+    global NOCON
+    NOCON = args.nocon
     from fairify_amd import presets
     from fairify_amd.models.zoo import get_model
     from fairify_amd.partition import processing_order
