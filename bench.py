@@ -79,6 +79,8 @@ def parse_args(argv=None):
                          "--escalate-budget")
     ap.add_argument("--stages", default="",
                     help="further escalation passes 'budget:max_open,...' after --escalate-budget")
+    ap.add_argument("--relu-budget", type=int, default=2048,
+                    help="ReLU-phase BaB (stage 'relu') on the input-split residue: nodes per partition (0 = off)")
     ap.add_argument("--batch-nodes", type=int, default=65536,
                     help="BaB nodes bounded per sub-batch launch (memory per runtime scales with it)")
     ap.add_argument("--smt", default="none",
@@ -192,7 +194,7 @@ def main() -> None:
                        node_budget=args.node_budget, heuristic=not args.no_heuristic, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=args.heuristic_node_budget, escalate_budget=args.escalate_budget,
                        escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
-                       smt_backend=args.smt, trust_milp=args.trust_milp,
+                       smt_backend=args.smt, trust_milp=args.trust_milp, relu_budget=args.relu_budget,
                        escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
                                                 for st in args.escalate_probation.split(",") if st),
                        escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
@@ -334,7 +336,7 @@ def main() -> None:
                    "parallelism": f"dp{info.world}", "preset": args.preset, "grid_per_model": len(order),
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
-                   "heuristic_node_budget": cfg.heuristic_node_budget,
+                   "heuristic_node_budget": cfg.heuristic_node_budget, "relu_budget": cfg.relu_budget,
                    "escalate_probation": [list(st) for st in cfg.escalate_probation],
                    "stages": [list(st) for st in cfg.escalate_stages], "heuristic": cfg.heuristic,
                    "batch_nodes": cfg.batch_nodes,

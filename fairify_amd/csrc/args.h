@@ -47,6 +47,11 @@ struct BoundArgs {
   // excluded every pair) are skipped -- the split kernel reads point bounds of open nodes only
   const uint8_t* row_open;
   int open_mod;
+  // ReLU-phase rows (relu BaB): [R, n_hidden] int8, -1 = neuron fixed inactive on the row's branch
+  // region, +1 = fixed active (identity upper relaxation), 0 = free; rows whose region is proven
+  // empty get infeas[r] = 1 (the caller zeroes infeas)
+  const int8_t* phase_in;
+  uint8_t* infeas;
 };
 
 // Inline escalation steps between the first budget and budget2 (fa_settle_kernel): step k has
@@ -254,4 +259,77 @@ struct DecodeDesc {
   int chunk_off[FA_DECODE_MAX_DIMS];      // offset of the attribute's chunks in chunk_lo / chunk_hi
   float base_lo[FA_DECODE_MAX_DIMS];
   float base_hi[FA_DECODE_MAX_DIMS];
+};
+
+// ReLU-phase backward bounds (relu.hip: fa_crown_phase_kernel, ops/reference.py:crown_phase).
+struct CrownPhaseArgs {
+  const float* flat;
+  const float* lo;          // [R, n0] row boxes (PA dims degenerate)
+  const float* hi;
+  int R;
+  const int8_t* phase;      // [R, n_hidden] or nullptr
+  const float* layer_lb;    // [R, n_neurons] forward pre-activation bounds (phase-aware)
+  const float* layer_ub;
+  const uint8_t* infeas;    // [R] region proven empty by the forward pass, or nullptr
+  float* out_lb;            // [R] in: forward logit bounds, out: intersected with the backward ones
+  float* out_ub;
+  float *Lc, *L0, *Le, *Uc, *U0, *Ue;   // in/out: replaced where the backward input form is tighter
+  int* split;               // [R, 2] hidden neuron to split for the lower (0) / upper (1) bound, -1 none
+  float* score;             // [R, 2]
+  float* low;               // [R, 2] best backward lower bounds of N / -N (or nullptr)
+  const int8_t* skip_status;   // rows of partitions no longer RUNNING are skipped (or nullptr)
+  const int* skip_part;        // [R]
+};
+
+// One BFS level of the ReLU-phase branch-and-bound (relu.hip, csrc/relu_runtime.cpp).  Node n owns
+// rows 2n (PA value of its pair's first entry, the copy that must be < 0) and 2n+1 (the copy that
+// must be > 0).
+struct ReluLevelArgs {
+  int Nn, n0, nh;
+  int npa;
+  int pa_idx[FA_CMAX_PA];
+  const int64_t* pairs;     // [Pp, 2] indices into values
+  const float* values;      // [V, npa]
+  // input pool
+  const int* part;          // [Nn]
+  const int* pair;          // [Nn]
+  const float* xlo;         // [Nn, n0]
+  const float* xhi;
+  const int8_t* phase;      // [Nn, 2, nh]
+  // rows (written by fa_relu_rows_kernel)
+  float* rlo;               // [2 Nn, n0]
+  float* rhi;
+  int* rpart;               // [2 Nn]
+  // per-row bounds (after fa_crown_phase)
+  const float* olb;
+  const float* oub;
+  const uint8_t* infeas;
+  const float *Lc, *L0, *Le, *Uc, *U0, *Ue;
+  const int* split;         // [2 Nn, 2]
+  // certificate outputs
+  uint8_t* open;            // [Nn]
+  int* choice;              // [Nn] >= 0: row * 65536 + neuron; -1 input split along idim; -2 leaf
+  int* idim;                // [Nn]
+  float* cpts;              // [2 Nn, n0] candidate points (x with each row's PA values)
+  // candidate point bounds
+  const float* pe_lb;       // [2 Nn]
+  const float* pe_ub;
+  // partition state
+  int8_t* status;
+  int* part_nodes;          // [P] nodes bounded so far (incremented by the rows kernel)
+  const int* nodes_start;   // [P] part_nodes at the start of this level (the budget reference)
+  int budget;
+  // output pool
+  int* opart;
+  int* opair;
+  float* oxlo;
+  float* oxhi;
+  int8_t* ophase;
+  int* count_out;
+  int cap;
+  float* cand_buf;          // [cand_cap, 2 n0 + 1] x, x', partition id (int bits)
+  int* cand_count;
+  int cand_cap;
+  float unit;
+  float gmarg;              // gamma(2 n0 + 4)
 };

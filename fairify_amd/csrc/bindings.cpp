@@ -17,6 +17,7 @@
 namespace py = pybind11;
 
 extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream);
+extern "C" int fa_crown_phase_launch(const NetDesc& net, CrownPhaseArgs a, hipStream_t stream);
 extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_forward_launch(const NetDesc& net, FwdArgs a, hipStream_t stream);
 extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream);
@@ -105,6 +106,7 @@ struct Net {
 
 const NetDesc& fa_net_desc(py::handle h) { return h.cast<const Net&>().d; }
 void register_bab(py::module& m);
+void register_relu(py::module& m);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 void register_csv(py::module& m);
 
@@ -127,7 +129,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bounds", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t dead_in, int R,
                      int symbolic, uintptr_t out_lb, uintptr_t out_ub, uintptr_t Lc, uintptr_t L0, uintptr_t Le,
                      uintptr_t Uc, uintptr_t U0, uintptr_t Ue, uintptr_t layer_lb, uintptr_t layer_ub,
-                     uintptr_t dead_out, int G, uintptr_t stream, unsigned long long fold) {
+                     uintptr_t dead_out, int G, uintptr_t stream, unsigned long long fold, uintptr_t phase_in,
+                     uintptr_t infeas) {
     NetDesc d = net.d;
     BoundArgs a{};
     a.flat = P<const float>(flat);
@@ -145,11 +148,38 @@ PYBIND11_MODULE(_C, m) {
     a.layer_ub = P<float>(layer_ub);
     a.dead_out = P<uint8_t>(dead_out);
     a.fold = fold;
+    a.phase_in = P<const int8_t>(phase_in);
+    a.infeas = P<uint8_t>(infeas);
     check(fa_bounds_launch(d, a, (hipStream_t)stream), "bounds");
   }, py::arg("net"), py::arg("flat"), py::arg("lo"), py::arg("hi"), py::arg("dead_in"), py::arg("R"),
      py::arg("symbolic"), py::arg("out_lb"), py::arg("out_ub"), py::arg("Lc"), py::arg("L0"), py::arg("Le"),
      py::arg("Uc"), py::arg("U0"), py::arg("Ue"), py::arg("layer_lb"), py::arg("layer_ub"), py::arg("dead_out"),
-     py::arg("G"), py::arg("stream"), py::arg("fold") = 0ull);
+     py::arg("G"), py::arg("stream"), py::arg("fold") = 0ull, py::arg("phase_in") = 0, py::arg("infeas") = 0);
+
+  // ReLU-phase backward bounds (relu.hip), refining a preceding phase-aware `bounds` call in place
+  m.def("crown_phase", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, int R, uintptr_t phase,
+                          uintptr_t layer_lb, uintptr_t layer_ub, uintptr_t infeas, uintptr_t out_lb, uintptr_t out_ub,
+                          uintptr_t Lc, uintptr_t L0, uintptr_t Le, uintptr_t Uc, uintptr_t U0, uintptr_t Ue,
+                          uintptr_t split, uintptr_t score, uintptr_t low, uintptr_t stream) {
+    CrownPhaseArgs a{};
+    a.flat = P<const float>(flat);
+    a.lo = P<const float>(lo);
+    a.hi = P<const float>(hi);
+    a.R = R;
+    a.phase = P<const int8_t>(phase);
+    a.layer_lb = P<const float>(layer_lb);
+    a.layer_ub = P<const float>(layer_ub);
+    a.infeas = P<const uint8_t>(infeas);
+    a.out_lb = P<float>(out_lb);
+    a.out_ub = P<float>(out_ub);
+    a.Lc = P<float>(Lc); a.L0 = P<float>(L0); a.Le = P<float>(Le);
+    a.Uc = P<float>(Uc); a.U0 = P<float>(U0); a.Ue = P<float>(Ue);
+    a.split = P<int>(split);
+    a.score = P<float>(score);
+    a.low = P<float>(low);
+    const int rc = fa_crown_phase_launch(net.d, a, (hipStream_t)stream);
+    if (rc != 0) throw std::runtime_error("crown_phase launch failed, code " + std::to_string(rc));
+  });
 
   // backward output bounds refining forms/out bounds written by a preceding `bounds` call
   m.def("crown", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t dead_in, int R,
@@ -396,5 +426,6 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("arch", []() { return std::string("gfx950"); });
   register_bab(m);
+  register_relu(m);
   register_csv(m);
 }

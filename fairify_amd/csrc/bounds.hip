@@ -208,6 +208,13 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
         if (a.part_mod) node %= a.part_mod;
         forced = a.dead_part[(size_t)a.node_part[node] * net.n_hidden + noff + j] != 0;
       }
+      bool fact = false;
+      if (a.phase_in && rv) {   // ReLU-phase rows (symbolic.hip: same rule)
+        const int8_t ph = a.phase_in[(size_t)rglob * net.n_hidden + noff + j];
+        forced = forced || ph < 0;
+        fact = ph > 0;
+        if (a.infeas && ((ph < 0 && lb > 0.f) || (ph > 0 && ub < 0.f))) a.infeas[rglob] = 1;
+      }
       const bool isdead = ub <= 0.f;
       const bool isact = lb >= 0.f;
       if (rv && a.dead_out) a.dead_out[(size_t)rglob * net.n_hidden + noff + j] = isdead ? 1 : 0;
@@ -226,7 +233,7 @@ fa_bounds_kernel(NetDesc net, BoundArgs a) {
       const float aa = mnU - gc * mgU + eU;
       if (zero) {
         for (int i = 0; i <= crow; ++i) cu[i * S] = 0.f;
-      } else if (isact || aa >= 0.f) {
+      } else if (isact || fact || aa >= 0.f) {
         cu[crow * S] = cU;
         eUn = eU;
         mgUn = mgU;

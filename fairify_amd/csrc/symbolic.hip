@@ -233,10 +233,16 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
       }
       return false;
     }
-    bool forced = false;
+    bool forced = false, fact = false;
     if (nl_act && jv) {
       if (a.dead_in) forced = a.dead_in[(size_t)r * net.n_hidden + noff + j] != 0;
       else if (a.dead_part) forced = a.dead_part[(size_t)a.node_part[node] * net.n_hidden + noff + j] != 0;
+      if (a.phase_in) {   // ReLU-phase rows: fixed inactive = forced dead, fixed active = no chord
+        const int8_t ph = a.phase_in[(size_t)r * net.n_hidden + noff + j];
+        forced = forced || ph < 0;
+        fact = ph > 0;
+        if (ob == 0 && a.infeas && ((ph < 0 && lb > 0.f) || (ph > 0 && ub < 0.f))) a.infeas[r] = 1;
+      }
     }
     const bool isdead = ub <= 0.f;
     const bool isact = lb >= 0.f;
@@ -251,7 +257,7 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
       const float aa = mn - gc * mg + e;
       if (zero) {
         s = 0.f; cnew = 0.f; en = 0.f; mgn = 0.f;
-      } else if (!isact && aa < 0.f) {
+      } else if (!isact && !fact && aa < 0.f) {
         const float bb = mx + gc * mg + e;
         s = (bb / (bb - aa)) * (1.f + 4.f * unit);
         const float shift = e - aa;

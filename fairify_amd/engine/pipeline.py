@@ -84,6 +84,8 @@ class VerifyConfig:
     anytime_pool: int = 1 << 24          # live BaB nodes per group: group size = pool / budget
     anytime_max_samples: int = 16384
     anytime_milp_seconds: float = 1.0    # first MILP round's per-partition limit (x growth per round)
+    relu_budget: int = 2048              # ReLU-phase BaB (stage "relu", engine/relu_bab.py) on the
+                                         # input-split residue: nodes per partition (0 = off)
     trust_milp: bool = False             # HiGHS MILP UNSAT rests on a floating-point dual bound: by
                                          # default it is recorded (stage "milp") but the partition
                                          # stays UNKNOWN for the rigorous stages; True = round-2
@@ -430,6 +432,30 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             open_left[unk] = eres.open_left
         sync()
         t_bab += time.time() - t0
+
+    # ---------------- stage 3r: ReLU-phase branch-and-bound on the residue (rigorous GPU bounds
+    # with neuron-phase splits: the exact-zero partitions input splitting cannot close)
+    if cfg.relu_budget > 0:
+        from .relu_bab import ReluBaBSolver, ReluConfig, supported
+
+        unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+        if unk.size and supported(q):
+            t0 = time.time()
+            el = time.time() - t_start
+            rsolver = ReluBaBSolver(be, q, ReluConfig(node_budget=cfg.relu_budget, batch_nodes=cfg.batch_nodes,
+                                                      time_budget=max(0.0, budget - el)), timer=tm)
+            with tm("relu"):
+                rres = rsolver.solve(lo_np[unk], hi_np[unk], mlp)
+            dec_r = np.isin(rres.status, (SAT, UNSAT))
+            hit = unk[dec_r]
+            status[hit] = rres.status[dec_r]
+            stage[hit] = "relu"
+            rs = rres.status == SAT
+            cex_x[unk[rs]] = rres.cex_x[rs]
+            cex_xp[unk[rs]] = rres.cex_xp[rs]
+            nodes[unk] += rres.nodes
+            sync()
+            t_bab += time.time() - t0
 
     # ---------------- stage 3c: exact host solver on the residue (the reference's Z3 check,
     # src/AC/Verify-AC.py:145-158): Z3 when installed, else the HiGHS MILP back-end fed the

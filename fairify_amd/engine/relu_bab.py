@@ -189,17 +189,25 @@ class ReluBaBSolver:
             with self.tm("relu.bounds"):
                 res = be.bounds(rlo, rhi, mode="symbolic", keep_layers=True, phase=rph)
                 pc, forms = be.crown_phase(rlo, rhi, res, rph)
-            olb = torch.maximum(res.out_lb.to(dt), pc.low[:, 0].to(dt))
-            oub = torch.minimum(res.out_ub.to(dt), -pc.low[:, 1].to(dt))
-            inf = res.infeasible if res.infeasible is not None else torch.zeros(2 * N, dtype=torch.bool, device=dev)
-            olb = torch.where(inf, torch.full_like(olb, float("inf")), olb)
-            oub = torch.where(inf, torch.full_like(oub, -float("inf")), oub)
             A, B = slice(0, None, 2), slice(1, None, 2)
+            if forms is None:
+                # HIP kernel: logit bounds intersected, infeasible rows set to (+inf, -inf) and the
+                # tighter input forms written into ``res`` in place
+                olb, oub = res.out_lb.to(dt), res.out_ub.to(dt)
+                LAc, LA0, LAe = res.Lc, res.L0, res.Le
+                UBc, UB0, UBe = res.Uc, res.U0, res.Ue
+            else:
+                olb = torch.maximum(res.out_lb.to(dt), pc.low[:, 0].to(dt))
+                oub = torch.minimum(res.out_ub.to(dt), -pc.low[:, 1].to(dt))
+                inf = res.infeasible if res.infeasible is not None else torch.zeros(2 * N, dtype=torch.bool,
+                                                                                    device=dev)
+                olb = torch.where(inf, torch.full_like(olb, float("inf")), olb)
+                oub = torch.where(inf, torch.full_like(oub, -float("inf")), oub)
+                # coupled certificate on the input forms (the tighter of forward / backward per row)
+                LAc, LA0, LAe = _pick_form(res.Lc, res.L0, res.Le, res.out_lb, forms[1.0])
+                lamU, cU, eU, lowU = forms[-1.0]
+                UBc, UB0, UBe = _pick_form(res.Uc, res.U0, res.Ue, -res.out_ub, (-lamU, -cU, eU, lowU))
             closed = (olb[A] >= 0) | (oub[B] <= 0)
-            # coupled certificate on the input forms (the tighter of forward / backward per row)
-            LAc, LA0, LAe = _pick_form(res.Lc, res.L0, res.Le, res.out_lb, forms[1.0])
-            lamU, cU, eU, lowU = forms[-1.0]
-            UBc, UB0, UBe = _pick_form(res.Uc, res.U0, res.Ue, -res.out_ub, (-lamU, -cU, eU, lowU))
             LAc, LA0, LAe = LAc[A], LA0[A], LAe[A]
             UBc, UB0, UBe = UBc[B], UB0[B], UBe[B]
             # fold the PA coordinates (fixed per row) into the constants
@@ -296,5 +304,49 @@ class ReluBaBSolver:
                 cex_x[p], cex_xp[p] = X[k], XP[k]
 
     # ------------------------------------------------------------------------------------------
+    def _runtime(self, values_np: np.ndarray, pairs_np: np.ndarray, n_root: int):
+        """Native (C++/HIP) ReLU-phase runtime, cached on the backend per (query, host thread)."""
+        import threading
+
+        from ..ops import ext
+        from ..ops.hip import _net
+
+        key = (tuple(self.q.pa_idx), values_np.tobytes(), pairs_np.tobytes(), threading.get_ident(),
+               int(self.cfg.batch_nodes))
+        cache = self.be.__dict__.setdefault("_relu_rt", {})
+        cap = max(self.cfg.max_pool, 2 * n_root)
+        rt = cache.get(key)
+        if rt is None or rt[1] < cap:
+            rt = (ext().ReluRuntime(_net(self.be), self.be.flat.data_ptr(), list(self.q.pa_idx),
+                                    values_np.astype(np.float32).reshape(-1).tolist(),
+                                    pairs_np.astype(np.int64).reshape(-1).tolist(), int(cap),
+                                    int(self.cfg.batch_nodes), float(self.be.unit)), cap)
+            cache[key] = rt
+        return rt[0]
+
     def _solve_native(self, lo_np, hi_np, mlp_exact, status, values_np, pairs_np, time_budget):
-        raise NotImplementedError("native ReLU-phase runtime not built yet")
+        P, n0 = lo_np.shape
+        n_root = int((status == RUNNING).sum()) * max(1, pairs_np.shape[0])
+        if pairs_np.shape[0] == 0:
+            status = status.copy()
+            status[status == RUNNING] = UNSAT
+            return status, np.zeros((P, n0), np.int64), np.zeros((P, n0), np.int64), np.zeros(P, np.int64)
+        rt = self._runtime(values_np, pairs_np, n_root)
+        q = self.q
+
+        def confirm(parts: np.ndarray, buf: np.ndarray) -> np.ndarray:
+            X = np.rint(buf[:, :n0]).astype(np.int64)
+            XP = np.rint(buf[:, n0:]).astype(np.int64)
+            ok = exact.check_pair_constraints(X, XP, lo_np[parts], hi_np[parts], q.pa_idx, q.ra_idx, q.tau)
+            out = np.zeros(len(parts), dtype=bool)
+            idx = np.nonzero(ok)[0]
+            if idx.size:
+                out[idx] = exact.is_violation(mlp_exact, X[idx], XP[idx])
+            return out
+
+        stream = torch.cuda.current_stream(self.dev).cuda_stream
+        with self.tm("relu.native"):
+            st, cx, cxp, nodes, stats = rt.solve(lo_np.astype(np.float32), hi_np.astype(np.float32), status,
+                                                 int(self.cfg.node_budget), float(time_budget), confirm, stream)
+        self.stats = dict(stats)
+        return (np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes, dtype=np.int64))

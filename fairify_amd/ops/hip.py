@@ -164,7 +164,8 @@ def point_bounds(be, x: torch.Tensor, dead: Optional[torch.Tensor] = None):
 
 # ------------------------------------------------------------------------------------------------
 def bounds(be, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic", dead: Optional[torch.Tensor] = None,
-           keep_layers: bool = False, G: int = 0, fold: Sequence[int] = ()) -> ref.BoundResult:
+           keep_layers: bool = False, G: int = 0, fold: Sequence[int] = (),
+           phase: Optional[torch.Tensor] = None) -> ref.BoundResult:
     """``fold``: input dims with lo == hi in EVERY row (folded into the constant column of the
     register-resident symbolic kernel; the caller guarantees degeneracy)."""
     R, n0 = lo.shape
@@ -196,10 +197,17 @@ def bounds(be, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic", dead:
     d = None
     if dead is not None:
         d = _c(dead, torch.uint8, (R, be.n_hidden), "dead")
+    ph = infeas = None
+    if phase is not None:
+        ph = _c(phase, torch.int8, (R, be.n_hidden), "phase")
+        infeas = torch.zeros(R, dtype=torch.uint8, device=dev)
     if R:
         ext().bounds(_net(be), be.flat.data_ptr(), lo.data_ptr(), hi.data_ptr(), _ptr(d), R, sym,
                      out_lb.data_ptr(), out_ub.data_ptr(), *[_ptr(t) for t in forms],
-                     _ptr(lay_lb), _ptr(lay_ub), _ptr(dead_out), G, _stream(dev), _fold_mask(fold, n0))
+                     _ptr(lay_lb), _ptr(lay_ub), _ptr(dead_out), G, _stream(dev), _fold_mask(fold, n0),
+                     _ptr(ph), _ptr(infeas))
+    if infeas is not None:
+        res.infeasible = infeas.bool()
     if keep_layers:
         widths = be.mlp.widths
         offs = [0]
@@ -239,6 +247,32 @@ def crown(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, dead: Op
                     res.Le.data_ptr(), res.Uc.data_ptr(), res.U0.data_ptr(), res.Ue.data_ptr(),
                     lay_lb.data_ptr(), lay_ub.data_ptr(), _stream(lo.device))
     return res
+
+
+# ------------------------------------------------------------------------------------------------
+def crown_phase(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, phase: Optional[torch.Tensor] = None):
+    """ReLU-phase backward bounds (csrc/relu.hip: fa_crown_phase_kernel) on rows bounded by
+    :func:`bounds` (symbolic, keep_layers, same ``phase``).  Refines ``res`` (logit bounds, forms)
+    in place like ref.crown_phase + the caller's intersection, and returns
+    (ref.PhaseCrown, None) -- the kernel writes the better input forms into ``res`` directly."""
+    R, n0 = lo.shape
+    dev = lo.device
+    lo = _c(lo, torch.float32, (R, n0), "lo")
+    hi = _c(hi, torch.float32, (R, n0), "hi")
+    if res.lay_lb_full is None:
+        raise ValueError("crown_phase needs bounds(..., keep_layers=True) from the HIP path")
+    ph = _c(phase, torch.int8, (R, be.n_hidden), "phase") if phase is not None else None
+    split = torch.full((R, 2), -1, dtype=torch.int32, device=dev)
+    score = torch.zeros(R, 2, dtype=torch.float32, device=dev)
+    low = torch.zeros(R, 2, dtype=torch.float32, device=dev)
+    infeas = res.infeasible.to(torch.uint8).contiguous() if res.infeasible is not None else None
+    if R:
+        ext().crown_phase(_net(be), be.flat.data_ptr(), lo.data_ptr(), hi.data_ptr(), R, _ptr(ph),
+                          res.lay_lb_full.data_ptr(), res.lay_ub_full.data_ptr(), _ptr(infeas),
+                          res.out_lb.data_ptr(), res.out_ub.data_ptr(), res.Lc.data_ptr(), res.L0.data_ptr(),
+                          res.Le.data_ptr(), res.Uc.data_ptr(), res.U0.data_ptr(), res.Ue.data_ptr(),
+                          split.data_ptr(), score.data_ptr(), low.data_ptr(), _stream(dev))
+    return ref.PhaseCrown(low=low, split=split.long(), score=score), None
 
 
 # ------------------------------------------------------------------------------------------------
