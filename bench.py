@@ -81,6 +81,8 @@ def parse_args(argv=None):
                     help="further escalation passes 'budget:max_open,...' after --escalate-budget")
     ap.add_argument("--relu-budget", type=int, default=2048,
                     help="ReLU-phase BaB (stage 'relu') on the input-split residue: nodes per partition (0 = off)")
+    ap.add_argument("--relu-max-width", type=int, default=16,
+                    help="run the relu stage only on networks whose hidden layers are at most this wide")
     ap.add_argument("--batch-nodes", type=int, default=65536,
                     help="BaB nodes bounded per sub-batch launch (memory per runtime scales with it)")
     ap.add_argument("--smt", default="none",
@@ -195,6 +197,7 @@ def main() -> None:
                        heuristic_node_budget=args.heuristic_node_budget, escalate_budget=args.escalate_budget,
                        escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
                        smt_backend=args.smt, trust_milp=args.trust_milp, relu_budget=args.relu_budget,
+                       relu_max_width=args.relu_max_width,
                        escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
                                                 for st in args.escalate_probation.split(",") if st),
                        escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
@@ -337,6 +340,7 @@ def main() -> None:
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
                    "heuristic_node_budget": cfg.heuristic_node_budget, "relu_budget": cfg.relu_budget,
+                   "relu_max_width": cfg.relu_max_width,
                    "escalate_probation": [list(st) for st in cfg.escalate_probation],
                    "stages": [list(st) for st in cfg.escalate_stages], "heuristic": cfg.heuristic,
                    "batch_nodes": cfg.batch_nodes,

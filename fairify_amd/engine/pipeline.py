@@ -86,6 +86,9 @@ class VerifyConfig:
     anytime_milp_seconds: float = 1.0    # first MILP round's per-partition limit (x growth per round)
     relu_budget: int = 2048              # ReLU-phase BaB (stage "relu", engine/relu_bab.py) on the
                                          # input-split residue: nodes per partition (0 = off)
+    relu_max_width: int = 16             # ... only for networks whose hidden layers are at most this
+                                         # wide (the narrow zero-bias shapes it closes; on the wide AC
+                                         # shapes it spends its budget without deciding: tools/diag_relu.py)
     trust_milp: bool = False             # HiGHS MILP UNSAT rests on a floating-point dual bound: by
                                          # default it is recorded (stage "milp") but the partition
                                          # stays UNKNOWN for the rigorous stages; True = round-2
@@ -435,7 +438,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
 
     # ---------------- stage 3r: ReLU-phase branch-and-bound on the residue (rigorous GPU bounds
     # with neuron-phase splits: the exact-zero partitions input splitting cannot close)
-    if cfg.relu_budget > 0:
+    if cfg.relu_budget > 0 and max(mlp.hidden or [0]) <= cfg.relu_max_width:
         from .relu_bab import ReluBaBSolver, ReluConfig, supported
 
         unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
