@@ -111,7 +111,13 @@ def parse_args(argv=None):
                          "HIP streams (0 = off)")
     ap.add_argument("--profile", action="store_true", help="per-stage timing breakdown on stderr (syncs)")
     ap.add_argument("--concurrency", type=int, default=0,
-                    help="host threads / HIP streams verifying (model, chunk) items concurrently (default 8 on GPU)")
+                    help="host threads / HIP streams verifying (model, chunk) items concurrently (default: the "
+                         "rank's CPUs, at most 8, on GPU)")
+    ap.add_argument("--unit", type=int, default=250,
+                    help="N > 1: partitions per load-balancing unit (LPT over ranks on the previous step's BaB node "
+                         "counts; parallel/balance.py)")
+    ap.add_argument("--no-balance", action="store_true",
+                    help="N > 1: the strided shard of round 2 instead of the LPT unit assignment")
     return ap.parse_args(argv)
 
 
@@ -146,6 +152,13 @@ def main() -> None:
         raise SystemExit("bench.py refuses FAIRIFY_FORCE_REFERENCE=1: the benchmark must run the HIP kernels")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.emulate_shard:
         raise SystemExit(launch(args))
+    # one node runs LOCAL_WORLD_SIZE ranks: each takes its own slice of the host CPUs for its host
+    # threads / HIP streams / MILP pool, pinned before anything touches the GPU (self-launch and
+    # torchrun alike; FAIRIFY_NO_PIN=1 disables it)
+    from fairify_amd.parallel import balance as BL
+
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    cpus = BL.pin_rank(int(os.environ.get("LOCAL_RANK", "0")), lw)
 
     import torch
 
@@ -216,7 +229,42 @@ def main() -> None:
         idx = (start + np.arange(args.chunk)) % max(1, n)
         return [shard[idx]]
 
-    conc = args.concurrency or (8 if info.device.type == "cuda" else 1)
+    # N > 1 (strong scaling): every model's order is cut into units of --unit partitions, assigned
+    # to ranks by LPT on the previous step's cost (sum of BaB node expansions + a fixed cost per
+    # partition; a size prior before the first step), all-reduced once per step
+    balanced = args.scope == "suite" and info.world > 1 and not args.emulate_shard and not args.no_balance
+    U = max(1, args.unit)
+    units = BL.make_units(len(models), len(order), U) if balanced else []
+    ucost = np.array([len(BL.unit_ids(order, j, U)) * models[k].n_neurons for k, j in units], dtype=np.float64)
+    FIXED_COST = 64.0                      # node-equivalents per partition (sim, prune, replay)
+    assigned_cost = []
+
+    def items_for_step(step: int):
+        """[(model, item key, ids, unit indices or None)] of this rank for step ``step``."""
+        if not balanced:
+            return [(k, j, ids, None) for k in range(len(models)) for j, ids in enumerate(chunks_for_step(step))
+                    if len(ids)]
+        assign = BL.lpt_assign(ucost, info.world)
+        assigned_cost.append(BL.rank_loads(assign, ucost))
+        by_model = {}
+        for ui in assign[info.rank]:
+            by_model.setdefault(units[ui][0], []).append(ui)
+        out = []
+        for k, lst in sorted(by_model.items()):
+            lst.sort(key=lambda ui: units[ui][1])
+            cur, n = [], 0
+            for ui in lst:
+                cur.append(ui)
+                n += len(BL.unit_ids(order, units[ui][1], U))
+                if n >= args.chunk:
+                    out.append((k, ("u", cur[0]), np.concatenate([BL.unit_ids(order, units[x][1], U) for x in cur]), cur))
+                    cur, n = [], 0
+            if cur:
+                out.append((k, ("u", cur[0]), np.concatenate([BL.unit_ids(order, units[x][1], U) for x in cur]), cur))
+        return out
+
+    conc = args.concurrency or (BL.host_threads(8, 2) if info.device.type == "cuda" else 1)
+    cfg.smt_workers = BL.host_threads(12, 1)
 
     timer = StageTimer(info.device, sync=args.profile)
 
@@ -252,7 +300,7 @@ def main() -> None:
     # (STAGES order)
     NC = 5 + 2 * len(STAGES)
 
-    def one_item(k: int, j: int, ids: np.ndarray, high: bool = False):
+    def one_item(k: int, j, ids: np.ndarray, uis=None, high: bool = False):
         m, be = models[k], backends[k]
         t_item = time.time()
         with thread_stream(high):
@@ -270,18 +318,33 @@ def main() -> None:
         for i, name in enumerate(STAGES):
             out[5 + i] = (sat & (st == name)).sum()
             out[5 + len(STAGES) + i] = (uns & (st == name)).sum()
-        return out
+        costs = {}
+        if uis is not None:      # per-unit cost of the next step's LPT: node expansions + fixed cost
+            nodes = recs.cols["nodes"].astype(np.float64)
+            o = 0
+            for ui in uis:
+                nu = len(BL.unit_ids(order, units[ui][1], U))
+                costs[ui] = float(nodes[o:o + nu].sum()) + FIXED_COST * nu
+                o += nu
+        return out, costs
 
     def run_step(step: int):
         step_no[0], step_t0[0] = step, time.time()
-        items = [(k, j, ids) for k in range(len(models)) for j, ids in enumerate(chunks_for_step(step)) if len(ids)]
+        items = items_for_step(step)
         items.sort(key=lambda it: (-item_cost.get((it[0], it[1]), 0.0), -models[it[0]].n_neurons))
-        if not items:
-            return np.zeros(NC)
+        res = []
         if pool is None:
-            return sum(one_item(k, j, ids) for k, j, ids in items)
-        return sum(f.result() for f in [pool.submit(one_item, k, j, ids, i < n_hi)
-                                        for i, (k, j, ids) in enumerate(items)])
+            res = [one_item(k, j, ids, uis) for k, j, ids, uis in items]
+        else:
+            res = [f.result() for f in [pool.submit(one_item, k, j, ids, uis, i < n_hi)
+                                        for i, (k, j, ids, uis) in enumerate(items)]]
+        if balanced:
+            local = np.zeros(len(units))
+            for _, costs in res:
+                for ui, cval in costs.items():
+                    local[ui] = cval
+            ucost[:] = D.all_reduce_sum(info, local)          # every unit ran on exactly one rank
+        return sum((o for o, _ in res), np.zeros(NC))
 
     sync = (lambda: torch.cuda.synchronize(info.device)) if info.device.type == "cuda" else (lambda: None)
 
@@ -353,7 +416,12 @@ def main() -> None:
         "unsat_by_stage": unsat_stage,
         "dist": {"world": info.world, "backend": backend_name,
                  "rank_ms_per_step": [round(x, 1) for x in rank_ms],
-                 "skew_ms": round(max(rank_ms) - min(rank_ms), 1) if rank_ms else 0.0},
+                 "skew_ms": round(max(rank_ms) - min(rank_ms), 1) if rank_ms else 0.0,
+                 "balance": ("lpt" if balanced else "strided"), "unit": U if balanced else None,
+                 "rank_cost": [round(float(c), 1) for c in assigned_cost[-1]] if assigned_cost else None,
+                 "cost_ratio": (round(float(max(assigned_cost[-1]) / max(1e-9, min(assigned_cost[-1]))), 4)
+                                if assigned_cost else None),
+                 "host_cpus": len(cpus), "host_threads": conc},
         "baseline": {"decided_per_s": round(BASELINE_DECIDED_PER_S, 5), "pct_verified_of_attempted": 89.0,
                      "coverage_of_grid_pct": 0.29},
     }

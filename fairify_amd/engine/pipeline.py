@@ -35,6 +35,12 @@ from ..utils import faults
 from ..utils.timer import StageTimer
 
 
+def _host_workers(cap: int) -> int:
+    from ..parallel.balance import host_threads
+
+    return host_threads(cap, 1)
+
+
 @dataclass
 class VerifyConfig:
     sim_size: int = 1000                 # reference sim_size (src/AC/Verify-AC.py:115)
@@ -69,7 +75,9 @@ class VerifyConfig:
     residual_iters: int = 12             # coordinate-ascent rounds
     smt_backend: str = "auto"            # exact host solver on the BaB residue: auto (Z3 if installed,
                                          # else the HiGHS MILP back-end) | z3py | z3bin | milp | none
-    smt_workers: int = 12                # host solver threads (the GPU box gives a process 16 CPUs)
+    smt_workers: int = field(default_factory=lambda: _host_workers(12))
+                                         # host solver threads: this rank's CPUs (its node slice when
+                                         # several ranks share a node, parallel/balance.py), at most 12
     smt_timeout: Optional[float] = None  # per query; defaults to soft_timeout
     smt_fork_params: bool = False        # Z3 seed/restart/phase options of the fork's drivers
     # anytime mode: after the fixed passes, keep growing the node budget (x anytime_growth per

@@ -13,7 +13,7 @@ def _bench(gpus: int, extra=()):
     env = dict(os.environ, FAIRIFY_DIST_BACKEND="gloo", FAIRIFY_CPU_THREADS="1")
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--device", "cpu",
-           "--models", "AC-8,AC-9", "--limit", "48", "--chunk", "16", "--steps", "1", "--warmup", "0",
+           "--models", "AC-8,AC-9", "--limit", "48", "--chunk", "16", "--steps", "1", "--warmup", "1", "--unit", "4",
            "--budget-pass", "0", "--escalate-budget", "4096", *extra]   # CPU: the torch BaB path
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -23,9 +23,11 @@ def _bench(gpus: int, extra=()):
 
 
 def test_self_launch_totals_match_one_rank():
+    """Totals do not depend on the rank count, and the LPT unit assignment of the timed step
+    (previous step's node counts) balances the ranks' cost within 10 %."""
     one = _bench(1)
     assert one["n_gpus"] == 1 and one["dist"]["backend"] == "none"
-    for n in (2, 4):
+    for n in (2, 4, 8):
         d = _bench(n)
         assert d["n_gpus"] == n and d["dist"]["world"] == n and d["dist"]["backend"] == "gloo"
         assert len(d["dist"]["rank_ms_per_step"]) == n
@@ -33,6 +35,7 @@ def test_self_launch_totals_match_one_rank():
         for k in ("sat", "unsat", "unknown", "unsat_sound", "unsat_heuristic"):
             assert d[k] == one[k], (n, k)
         assert d["sat_by_stage"] == one["sat_by_stage"]
+        assert d["dist"]["balance"] == "lpt" and d["dist"]["cost_ratio"] <= 1.1, d["dist"]
     # honest accounting fields add up
     assert one["unsat_sound"] + one["unsat_heuristic"] == one["unsat"]
     assert sum(one["sat_by_stage"].values()) == one["sat"]
@@ -56,7 +59,7 @@ def test_sound_fields_exclude_heuristic_and_milp():
     """pct_verified_sound / unsat_sound = decided minus heuristic-retry verdicts minus MILP UNSAT
     (a trusted HiGHS dual bound is still no proof), on a small run where both stages fire."""
     d = _bench(1, ("--models", "AC-8", "--node-budget", "8", "--escalate-budget", "0", "--smt", "milp",
-                   "--trust-milp"))
+                   "--trust-milp", "--relu-budget", "0"))
     att = d["sat"] + d["unsat"] + d["unknown"]
     us = d["unsat_by_stage"]
     assert sum(us.values()) == d["unsat"] and sum(d["sat_by_stage"].values()) == d["sat"]
@@ -65,6 +68,7 @@ def test_sound_fields_exclude_heuristic_and_milp():
     sound = d["sat"] + d["unsat"] - us["milp"] - us["heuristic"] - d["sat_by_stage"]["heuristic"]
     assert abs(d["pct_verified_sound"] - round(100.0 * sound / att, 3)) < 1e-9
     # default: an untrusted MILP 'unsat' is no verdict
-    d2 = _bench(1, ("--models", "AC-8", "--node-budget", "8", "--escalate-budget", "0", "--smt", "milp"))
+    d2 = _bench(1, ("--models", "AC-8", "--node-budget", "8", "--escalate-budget", "0", "--smt", "milp",
+                    "--relu-budget", "0"))
     assert d2["unsat_by_stage"]["milp"] == 0
     assert d2["unsat"] + d2["unknown"] >= d["unsat"] + d["unknown"] - 1e-9
