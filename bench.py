@@ -83,6 +83,8 @@ def parse_args(argv=None):
                     help="ReLU-phase BaB (stage 'relu') on the input-split residue: nodes per partition (0 = off)")
     ap.add_argument("--relu-max-width", type=int, default=16,
                     help="run the relu stage only on networks whose hidden layers are at most this wide")
+    ap.add_argument("--relu-escalate-cap", type=int, default=2048,
+                    help="models the relu stage runs on: cap the input-split escalation budget (0 = no cap)")
     ap.add_argument("--batch-nodes", type=int, default=65536,
                     help="BaB nodes bounded per sub-batch launch (memory per runtime scales with it)")
     ap.add_argument("--smt", default="none",
@@ -210,7 +212,7 @@ def main() -> None:
                        heuristic_node_budget=args.heuristic_node_budget, escalate_budget=args.escalate_budget,
                        escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
                        smt_backend=args.smt, trust_milp=args.trust_milp, relu_budget=args.relu_budget,
-                       relu_max_width=args.relu_max_width,
+                       relu_max_width=args.relu_max_width, relu_escalate_cap=args.relu_escalate_cap,
                        escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
                                                 for st in args.escalate_probation.split(",") if st),
                        escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
@@ -403,7 +405,7 @@ def main() -> None:
                    "sim_size": cfg.sim_size, "node_budget": cfg.node_budget,
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
                    "heuristic_node_budget": cfg.heuristic_node_budget, "relu_budget": cfg.relu_budget,
-                   "relu_max_width": cfg.relu_max_width,
+                   "relu_max_width": cfg.relu_max_width, "relu_escalate_cap": cfg.relu_escalate_cap,
                    "escalate_probation": [list(st) for st in cfg.escalate_probation],
                    "stages": [list(st) for st in cfg.escalate_stages], "heuristic": cfg.heuristic,
                    "batch_nodes": cfg.batch_nodes,

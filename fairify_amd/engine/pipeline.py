@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import os
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -97,6 +97,9 @@ class VerifyConfig:
     relu_max_width: int = 16             # ... only for networks whose hidden layers are at most this
                                          # wide (the narrow zero-bias shapes it closes; on the wide AC
                                          # shapes it spends its budget without deciding: tools/diag_relu.py)
+    relu_escalate_cap: int = 0           # networks the relu stage runs on: cap the input-split
+                                         # escalation budget at this (their residue goes to the cheaper
+                                         # relu stage instead of deep input splitting; 0 = no cap)
     trust_milp: bool = False             # HiGHS MILP UNSAT rests on a floating-point dual bound: by
                                          # default it is recorded (stage "milp") but the partition
                                          # stays UNKNOWN for the rigorous stages; True = round-2
@@ -351,6 +354,14 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     # ---------------- stage 3: branch and bound on the original network
     t0 = time.time()
     budget = cfg.soft_timeout if time_budget is None else min(cfg.soft_timeout, time_budget)
+    from .relu_bab import supported as _relu_supported
+
+    relu_on = cfg.relu_budget > 0 and max(mlp.hidden or [0]) <= cfg.relu_max_width and _relu_supported(q)
+    if relu_on and cfg.relu_escalate_cap > 0 and cfg.escalate_budget > cfg.relu_escalate_cap:
+        # the residue of these networks goes to the relu stage: stop the input-split escalation early
+        cap = max(cfg.relu_escalate_cap, cfg.node_budget)
+        cfg = replace(cfg, escalate_budget=cap if cap > cfg.node_budget else 0,
+                      escalate_probation=tuple(st for st in cfg.escalate_probation if st[0] < cap))
     # inline escalation (native runtime): the first escalation stage runs inside the first pass --
     # partitions that reach node_budget with a small frontier continue instead of restarting from
     # the root in a second solve (FAIRIFY_INLINE_ESCALATE=0: the two-pass schedule)
@@ -446,11 +457,11 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
 
     # ---------------- stage 3r: ReLU-phase branch-and-bound on the residue (rigorous GPU bounds
     # with neuron-phase splits: the exact-zero partitions input splitting cannot close)
-    if cfg.relu_budget > 0 and max(mlp.hidden or [0]) <= cfg.relu_max_width:
-        from .relu_bab import ReluBaBSolver, ReluConfig, supported
+    if relu_on:
+        from .relu_bab import ReluBaBSolver, ReluConfig
 
         unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
-        if unk.size and supported(q):
+        if unk.size:
             t0 = time.time()
             el = time.time() - t_start
             rsolver = ReluBaBSolver(be, q, ReluConfig(node_budget=cfg.relu_budget, batch_nodes=cfg.batch_nodes,
