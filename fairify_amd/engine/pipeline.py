@@ -530,6 +530,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
 
             use_milp = smt_solver.resolve(cfg.smt_backend) == "milp"
         milp_limit = cfg.anytime_milp_seconds
+        relu_any = _relu_supported(q)
+        r_budget = max(cfg.relu_budget, 1) if relu_on else 64      # x growth before the first round
         with tm("anytime"):
             while True:
                 unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
@@ -591,6 +593,32 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                     cex_x[grp[sa]] = ares.cex_x[sa]
                     cex_xp[grp[sa]] = ares.cex_xp[sa]
                     nodes[grp] += ares.nodes
+                # (d) ReLU-phase BaB with a growing budget, any layer width (the anytime budget pays
+                # for the wide nets too; it re-proves partitions the MILP only claims)
+                if relu_any and cfg.relu_budget > 0:
+                    r_budget *= cfg.anytime_growth
+                    unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+                    left = deadline - time.time()
+                    if unk.size and left > 0:
+                        from .relu_bab import ReluBaBSolver, ReluConfig
+
+                        G = max(1, cfg.anytime_pool // max(1, r_budget))
+                        for g0 in range(0, unk.size, G):
+                            left = deadline - time.time()
+                            if left <= 0:
+                                break
+                            grp = unk[g0:g0 + G]
+                            rs = ReluBaBSolver(be, q, ReluConfig(node_budget=r_budget, batch_nodes=cfg.batch_nodes,
+                                                                 time_budget=left), timer=tm)
+                            with tm("relu"):
+                                rr = rs.solve(lo_np[grp], hi_np[grp], mlp)
+                            dec_r = np.isin(rr.status, (SAT, UNSAT))
+                            status[grp[dec_r]] = rr.status[dec_r]
+                            stage[grp[dec_r]] = "relu"
+                            sr = rr.status == SAT
+                            cex_x[grp[sr]] = rr.cex_x[sr]
+                            cex_xp[grp[sr]] = rr.cex_xp[sr]
+                            nodes[grp] += rr.nodes
         sync()
         t_bab += time.time() - t0
 

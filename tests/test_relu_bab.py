@@ -148,3 +148,32 @@ def test_exact_zero_survives_rounding():
     res = ref.bounds(ws, bs, L, H, keep_layers=True, phase=ph)
     pc, _ = ref.crown_phase(ws, bs, L, H, res, ph)
     assert -float(pc.low[0, 1]) == 0.0 or float(res.out_ub[0]) == 0.0
+
+
+def test_pipeline_relu_stage_and_anytime_rounds():
+    """verify_chunk: the relu stage decides the input-split residue (stage "relu"); in anytime mode
+    relu rounds with growing budgets run for networks outside the width gate too; verdicts agree
+    with the plain input-split ones wherever both decided, every SAT pair is exact."""
+    from fairify_amd.engine import exact
+    from fairify_amd.engine.pipeline import VerifyConfig, verify_chunk
+
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    m = get_model("AC-8", weights="random", seed=0)
+    ids = processing_order(grid, 0)[:64]
+    be = Backend(m)
+    base = dict(sim_size=200, node_budget=64, heuristic=False, smt_backend="none")
+    off = verify_chunk(be, m, q, grid, ids, VerifyConfig(relu_budget=0, **base))
+    on = verify_chunk(be, m, q, grid, ids, VerifyConfig(relu_budget=256, **base))
+    wide = verify_chunk(be, m, q, grid, ids, VerifyConfig(relu_budget=256, relu_max_width=1, anytime_seconds=30,
+                                                          **base))
+    for r in (on, wide):
+        assert (r.cols["stage"] == "relu").sum() > 10
+        assert (r.cols["verdict"] != "unknown").sum() > (off.cols["verdict"] != "unknown").sum()
+        both = (off.cols["verdict"] != "unknown") & (r.cols["verdict"] != "unknown")
+        assert (off.cols["verdict"][both] == r.cols["verdict"][both]).all()
+        sat = np.nonzero(r.cols["verdict"] == "sat")[0]
+        lo, hi = grid.decode(ids[sat])
+        X, XP = r.cols["cex_x"][sat], r.cols["cex_xp"][sat]
+        assert exact.check_pair_constraints(X, XP, lo, hi, q.pa_idx, q.ra_idx, q.tau).all()
+        assert exact.is_violation(m, X, XP).all()
