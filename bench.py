@@ -160,7 +160,11 @@ def main() -> None:
     from fairify_amd.parallel import balance as BL
 
     lw = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
-    cpus = BL.pin_rank(int(os.environ.get("LOCAL_RANK", "0")), lw)
+    if args.emulate_shard and lw <= 1:
+        # one rank of an N-rank node on this process: its CPU slice too
+        cpus = BL.pin_rank(*(int(v) for v in args.emulate_shard.split("/")))
+    else:
+        cpus = BL.pin_rank(int(os.environ.get("LOCAL_RANK", "0")), lw)
 
     import torch
 
@@ -234,7 +238,12 @@ def main() -> None:
     # N > 1 (strong scaling): every model's order is cut into units of --unit partitions, assigned
     # to ranks by LPT on the previous step's cost (sum of BaB node expansions + a fixed cost per
     # partition; a size prior before the first step), all-reduced once per step
-    balanced = args.scope == "suite" and info.world > 1 and not args.emulate_shard and not args.no_balance
+    # --emulate-shard r/N: rank r's share of an N-rank job -- with the LPT balancer, the warmup steps
+    # run EVERY unit here (the costs all ranks would all-reduce) and the timed steps rank r's units
+    em_r, em_n = (int(v) for v in args.emulate_shard.split("/")) if args.emulate_shard else (0, 1)
+    world_b = em_n if args.emulate_shard else info.world
+    rank_b = em_r if args.emulate_shard else info.rank
+    balanced = args.scope == "suite" and world_b > 1 and not args.no_balance
     U = max(1, args.unit)
     units = BL.make_units(len(models), len(order), U) if balanced else []
     ucost = np.array([len(BL.unit_ids(order, j, U)) * models[k].n_neurons for k, j in units], dtype=np.float64)
@@ -246,10 +255,11 @@ def main() -> None:
         if not balanced:
             return [(k, j, ids, None) for k in range(len(models)) for j, ids in enumerate(chunks_for_step(step))
                     if len(ids)]
-        assign = BL.lpt_assign(ucost, info.world)
+        assign = BL.lpt_assign(ucost, world_b)
         assigned_cost.append(BL.rank_loads(assign, ucost))
         by_model = {}
-        for ui in assign[info.rank]:
+        mine = assign[rank_b] if not (args.emulate_shard and step < args.warmup) else range(len(units))
+        for ui in mine:
             by_model.setdefault(units[ui][0], []).append(ui)
         out = []
         for k, lst in sorted(by_model.items()):
@@ -345,7 +355,11 @@ def main() -> None:
             for _, costs in res:
                 for ui, cval in costs.items():
                     local[ui] = cval
-            ucost[:] = D.all_reduce_sum(info, local)          # every unit ran on exactly one rank
+            if args.emulate_shard:
+                if step < args.warmup:
+                    ucost[:] = local                             # every unit ran here
+            else:
+                ucost[:] = D.all_reduce_sum(info, local)         # every unit ran on exactly one rank
         return sum((o for o, _ in res), np.zeros(NC))
 
     sync = (lambda: torch.cuda.synchronize(info.device)) if info.device.type == "cuda" else (lambda: None)

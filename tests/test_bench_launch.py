@@ -72,3 +72,18 @@ def test_sound_fields_exclude_heuristic_and_milp():
                     "--relu-budget", "0"))
     assert d2["unsat_by_stage"]["milp"] == 0
     assert d2["unsat"] + d2["unknown"] >= d["unsat"] + d["unknown"] - 1e-9
+
+
+def test_emulated_lpt_shards_cover_the_grid():
+    """--emulate-shard r/N with the LPT balancer: the warmup step measures every unit, the timed
+    step runs rank r's units; the N emulated shards partition the grid (attempted and decided
+    totals add up to the one-rank run) and their assigned costs are balanced."""
+    one = _bench(1)
+    tot = {"sat": 0, "unsat": 0, "unknown": 0}
+    for r in range(4):
+        d = _bench(1, ("--emulate-shard", f"{r}/4"))
+        assert d["dist"]["balance"] == "lpt" and d["dist"]["cost_ratio"] <= 1.1, d["dist"]
+        for k in tot:
+            tot[k] += d[k]
+    for k in tot:
+        assert tot[k] == one[k], (k, tot, one)
