@@ -79,7 +79,7 @@ def parse_args(argv=None):
                          "--escalate-budget")
     ap.add_argument("--stages", default="",
                     help="further escalation passes 'budget:max_open,...' after --escalate-budget")
-    ap.add_argument("--relu-budget", type=int, default=2048,
+    ap.add_argument("--relu-budget", type=int, default=1024,
                     help="ReLU-phase BaB (stage 'relu') on the input-split residue: nodes per partition (0 = off)")
     ap.add_argument("--relu-max-width", type=int, default=16,
                     help="run the relu stage only on networks whose hidden layers are at most this wide")
