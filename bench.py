@@ -246,8 +246,16 @@ def main() -> None:
     balanced = args.scope == "suite" and world_b > 1 and not args.no_balance
     U = max(1, args.unit)
     units = BL.make_units(len(models), len(order), U) if balanced else []
-    ucost = np.array([len(BL.unit_ids(order, j, U)) * models[k].n_neurons for k, j in units], dtype=np.float64)
-    FIXED_COST = 64.0                      # node-equivalents per partition (sim, prune, replay)
+    # cost of a BaB node / of a partition's fixed stages (sim, prune, replay) by model: a node of
+    # AC-4 (100-100) costs ~30x one of AC-8 (5-5) in the bound kernels -- weight by the network's
+    # multiply-adds (plus a launch / latency floor)
+    def _macs(m):
+        d = [m.n_in] + m.widths
+        return float(sum(d[i] * d[i + 1] for i in range(len(d) - 1)))
+
+    node_w = [1.0 + _macs(m) / 256.0 for m in models]
+    FIXED_COST = 64.0                      # node-equivalents per partition
+    ucost = np.array([len(BL.unit_ids(order, j, U)) * FIXED_COST * node_w[k] for k, j in units], dtype=np.float64)
     assigned_cost = []
 
     def items_for_step(step: int):
@@ -336,7 +344,7 @@ def main() -> None:
             o = 0
             for ui in uis:
                 nu = len(BL.unit_ids(order, units[ui][1], U))
-                costs[ui] = float(nodes[o:o + nu].sum()) + FIXED_COST * nu
+                costs[ui] = node_w[k] * (float(nodes[o:o + nu].sum()) + FIXED_COST * nu)
                 o += nu
         return out, costs
 
@@ -435,7 +443,11 @@ def main() -> None:
                  "skew_ms": round(max(rank_ms) - min(rank_ms), 1) if rank_ms else 0.0,
                  "balance": ("lpt" if balanced else "strided"), "unit": U if balanced else None,
                  "rank_cost": [round(float(c), 1) for c in assigned_cost[-1]] if assigned_cost else None,
-                 "cost_ratio": (round(float(max(assigned_cost[-1]) / max(1e-9, min(assigned_cost[-1]))), 4)
+                 # makespan over the ideal even split, and LPT's guarantee for these units
+                 # (mean + largest unit) / mean: units are indivisible
+                 "cost_ratio": (round(float(max(assigned_cost[-1]) / max(1e-9, np.mean(assigned_cost[-1]))), 4)
+                                if assigned_cost else None),
+                 "cost_bound": (round(float(1.0 + ucost.max() / max(1e-9, np.mean(assigned_cost[-1]))), 4)
                                 if assigned_cost else None),
                  "host_cpus": len(cpus), "host_threads": conc},
         "baseline": {"decided_per_s": round(BASELINE_DECIDED_PER_S, 5), "pct_verified_of_attempted": 89.0,

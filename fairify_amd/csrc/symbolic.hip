@@ -550,7 +550,8 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
 #define FA_SYM_WPE7 2
 #endif
 #ifndef FA_SYM_WPE4
-#define FA_SYM_WPE4 3
+#define FA_SYM_WPE4 2   // round 3: 2 waves/SIMD beat 3 (1157 vs 1174 ms/step, 3 alternating runs each,
+                        // profiles/r3/ab/wpe4.md)
 #endif
 #define FA_SYM_WAVES_PER_EU(NT, TM, PAIR) \
   ((PAIR) ? 3 : ((TM) == 2 ? 3 : ((TM) == 4 ? FA_SYM_WPE4 : ((TM) == 7 ? FA_SYM_WPE7 : 1))))

@@ -12,6 +12,6 @@ n=0
 for v in "$@"; do
   n=$((n+1))
   cp $DIR/_C.$v.so $SO || exit 1
-  timeout -k 10 300 python -u bench.py --steps 3 --warmup 2 --budget-pass 0 > $OUT/$n.$v.json 2> $OUT/$n.$v.err || exit 1
-  python -c "import json;d=json.load(open('$OUT/$n.$v.json'));print('$v', d['ms_per_step'], d['pct_verified'])"
+  timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --budget-pass 0 > $OUT/$v.$n.json 2> $OUT/$v.$n.err || exit 1
+  python -c "import json;d=json.load(open('$OUT/$v.$n.json'));print('$v', d['ms_per_step'], d['pct_verified'])"
 done
