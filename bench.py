@@ -148,6 +148,23 @@ def launch(args) -> int:
     return bad[0] if bad else 0
 
 
+def _native_mem():
+    try:
+        from fairify_amd.ops import ext
+
+        return dict(ext().mem_stats())
+    except Exception:
+        return None
+
+
+def _mem_delta(a, b):
+    if not a or not b:
+        return None
+    return {"driver_frees": b["driver_frees"] - a["driver_frees"], "dev_mallocs": b["dev_mallocs"] - a["dev_mallocs"],
+            "dev_cache_hits": b["dev_hits"] - a["dev_hits"], "host_mallocs": b["host_mallocs"] - a["host_mallocs"],
+            "dev_gb": round((b["dev_live_bytes"] + b["dev_cached_bytes"]) / 2 ** 30, 3)}
+
+
 def main() -> None:
     args = parse_args()
     if os.environ.get("FAIRIFY_FORCE_REFERENCE") == "1":
@@ -315,6 +332,20 @@ def main() -> None:
     # a wave of cheap items (prior before any measurement: model size)
     item_cost = {}
     ITEM_LOG = os.environ.get("FAIRIFY_BENCH_ITEMS") == "1"   # per-item start / duration on stderr
+    if ITEM_LOG:   # Python garbage collections (they hold the GIL: every host thread stalls)
+        import gc
+
+        _gc_t = {}
+
+        def _gc_cb(phase, info_):
+            if phase == "start":
+                _gc_t["t"] = time.time()
+            elif info_.get("generation", 0) >= 1:
+                print(f"[gc] step {step_no[0]} gen {info_['generation']} at {_gc_t['t'] - step_t0[0]:.3f}s "
+                      f"took {1e3 * (time.time() - _gc_t['t']):.2f} ms collected {info_.get('collected')}",
+                      file=sys.stderr, flush=True)
+
+        gc.callbacks.append(_gc_cb)
     step_no, step_t0 = [0], [time.time()]
     # counters: attempted, decided, sat, unsat, unsat_heuristic, sat per stage, unsat per stage
     # (STAGES order)
@@ -383,8 +414,13 @@ def main() -> None:
     for w in range(args.warmup):
         run_step(w)
     sync()
+    from fairify_amd.utils import heap
+
+    if os.environ.get("FAIRIFY_GC_FREEZE", "1") != "0":
+        heap.freeze()     # no generation-2 pass over the setup heap inside the timed steps
     D.barrier(info)
     sync()
+    mem0 = _native_mem()
     marker(1)
     t0 = time.time()
     tot = np.zeros(NC)
@@ -449,7 +485,10 @@ def main() -> None:
                                 if assigned_cost else None),
                  "cost_bound": (round(float(1.0 + ucost.max() / max(1e-9, np.mean(assigned_cost[-1]))), 4)
                                 if assigned_cost else None),
-                 "host_cpus": len(cpus), "host_threads": conc},
+                 "host_cpus": len(cpus), "host_threads": conc,
+                 # native runtimes' caching allocator (csrc/devmem.h) over the timed steps:
+                 # driver-level frees stall every host thread; steady state = 0
+                 "native_mem": _mem_delta(mem0, _native_mem())},
         "baseline": {"decided_per_s": round(BASELINE_DECIDED_PER_S, 5), "pct_verified_of_attempted": 89.0,
                      "coverage_of_grid_pct": 0.29},
     }

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "args.h"
+#include "devmem.h"
 #include "exact_host.h"
 
 namespace py = pybind11;
@@ -59,21 +60,7 @@ void ckl(int rc, const char* what) {
   if (rc != 0) throw std::runtime_error(std::string(what) + " launch failed, code " + std::to_string(rc));
 }
 
-template <typename T>
-struct DevBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  void ensure(size_t cnt) {
-    if (cnt <= n) return;
-    if (p) hipFree(p);
-    p = nullptr;
-    ck(hipMalloc((void**)&p, std::max<size_t>(cnt, 1) * sizeof(T)), "hipMalloc");
-    n = cnt;
-  }
-  ~DevBuf() {
-    if (p) hipFree(p);
-  }
-};
+using fa_mem::DevBuf;
 
 // A/B switch of the closed-node skip in the candidate point kernel (FAIRIFY_POINT_SKIP_CLOSED=0: off)
 bool point_skip_closed() {
@@ -162,7 +149,8 @@ class BabRuntime {
     ensure_cand(cand_cap_);
     counters_.ensure(4);   // two slots of (children, candidates), alternating per level
     // fine-grained (coherent) pinned words: the settle kernel writes the level counters here
-    ck(hipHostMalloc((void**)&hcount_, 2 * sizeof(int), hipHostMallocCoherent), "hipHostMalloc");
+    hcount_buf_.ensure(2 * sizeof(int));
+    hcount_ = reinterpret_cast<int*>(hcount_buf_.p);
     // host fp64 copy of [W_0|b_0|W_1|b_1|...] for the native exact confirmation
     int np_ = 0;
     for (int l = 0; l < net_.n_layers; ++l) np_ = std::max(np_, net_.b_off[l] + net_.dims[l + 1]);
@@ -180,13 +168,6 @@ class BabRuntime {
     if (relaxed_)
       for (int k : ra_) exact_.is_ra[k] = 1;
     exact_.tau = tau_;
-  }
-  ~BabRuntime() {
-    if (hcount_) hipHostFree(hcount_);
-    if (hstage_) hipHostFree(hstage_);
-    if (hout_) hipHostFree(hout_);
-    if (hcand_) hipHostFree(hcand_);
-    if (hidx_) hipHostFree(hidx_);
   }
 
   py::tuple solve(py::array_t<float, py::array::c_style | py::array::forcecast> lo,
@@ -233,10 +214,10 @@ class BabRuntime {
     ensure_pool(0, std::max<long long>((long long)run.size(), 1));
     const size_t nrun = run.size();
     const size_t st_bytes = (size_t)((P + 3) & ~3) + nrun * sizeof(int) + 2 * nrun * n0_ * sizeof(float);
-    ensure_host(hstage_, hstage_n_, st_bytes);
+    hstage_.ensure(st_bytes);
     stage_.ensure(st_bytes);
     {
-      unsigned char* h = hstage_;
+      unsigned char* h = hstage_.p;
       std::memcpy(h, hstatus, P);
       int* hr = reinterpret_cast<int*>(h + ((P + 3) & ~3));
       std::memcpy(hr, run.data(), nrun * sizeof(int));
@@ -248,7 +229,7 @@ class BabRuntime {
           hh[i * n0_ + d] = hi.data()[(size_t)run[i] * n0_ + d];
         }
     }
-    ck(hipMemcpyAsync(stage_.p, hstage_, st_bytes, hipMemcpyHostToDevice, st), "cp stage");
+    ck(hipMemcpyAsync(stage_.p, hstage_.p, st_bytes, hipMemcpyHostToDevice, st), "cp stage");
     {
       BabInitArgs ia{};
       ia.P = P; ia.n_run = (int)nrun; ia.n0 = n0_;
@@ -381,11 +362,11 @@ class BabRuntime {
     }
     // results: one pack kernel + one D2H copy into pinned memory
     out_.ensure((size_t)3 * P);
-    ensure_host(hout_, hout_n_, (size_t)3 * P * sizeof(int));
+    hout_.ensure((size_t)3 * P * sizeof(int));
     ckl(fa_bab_finish_launch(P, status_.p, nodes_.p, open_left_.p, out_.p, st), "bab_finish");
-    ck(hipMemcpyAsync(hout_, out_.p, (size_t)3 * P * sizeof(int), hipMemcpyDeviceToHost, st), "cp out");
+    ck(hipMemcpyAsync(hout_.p, out_.p, (size_t)3 * P * sizeof(int), hipMemcpyDeviceToHost, st), "cp out");
     ck(hipStreamSynchronize(st), "sync");
-    const int* hres = reinterpret_cast<const int*>(hout_);
+    const int* hres = reinterpret_cast<const int*>(hout_.p);
     py::array_t<int8_t> status_out(P);
     py::array_t<int64_t> nodes_out(P), open_out(P);
     for (int p = 0; p < P; ++p) {
@@ -480,14 +461,14 @@ class BabRuntime {
   void confirm_candidates(int n_cand, py::object& confirm, std::vector<char>& got, std::vector<int64_t>& cex_x,
                           std::vector<int64_t>& cex_xp, hipStream_t st) {
     const size_t rec = (size_t)2 * n0_ + 1;             // x, x', partition id (int bits)
-    ensure_host(hcand_, hcand_n_, (size_t)n_cand * rec * sizeof(float));
-    ck(hipMemcpyAsync(hcand_, cand_buf_.p, (size_t)n_cand * rec * sizeof(float), hipMemcpyDeviceToHost, st),
+    hcand_.ensure((size_t)n_cand * rec * sizeof(float));
+    ck(hipMemcpyAsync(hcand_.p, cand_buf_.p, (size_t)n_cand * rec * sizeof(float), hipMemcpyDeviceToHost, st),
        "cp cand");
     ck(hipStreamSynchronize(st), "sync");
     std::vector<float> buf((size_t)n_cand * 2 * n0_);
     std::vector<int> parts(n_cand);
     {
-      const float* hc = reinterpret_cast<const float*>(hcand_);
+      const float* hc = reinterpret_cast<const float*>(hcand_.p);
       for (int i = 0; i < n_cand; ++i) {
         std::memcpy(buf.data() + (size_t)i * 2 * n0_, hc + (size_t)i * rec, sizeof(float) * 2 * n0_);
         std::memcpy(&parts[i], hc + (size_t)i * rec + 2 * n0_, sizeof(int));
@@ -545,11 +526,11 @@ class BabRuntime {
     }
     if (!newly.empty()) {
       idx_.ensure(newly.size());
-      ensure_host(hidx_, hidx_n_, newly.size() * sizeof(int));
-      std::memcpy(hidx_, newly.data(), newly.size() * sizeof(int));
-      ck(hipMemcpyAsync(idx_.p, hidx_, newly.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp idx");
+      hidx_.ensure(newly.size() * sizeof(int));
+      std::memcpy(hidx_.p, newly.data(), newly.size() * sizeof(int));
+      ck(hipMemcpyAsync(idx_.p, hidx_.p, newly.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp idx");
       ckl(fa_set_status_launch(idx_.p, (int)newly.size(), status_.p, 1, st), "set_status");
-      // no sync: the next level's kernels are stream-ordered after set_status, and hidx_ / idx_
+      // no sync: the next level's kernels are stream-ordered after set_status, and hidx_.p / idx_
       // are only rewritten by the next call, which runs after the next level-end sync (the sync
       // that retires this copy -- the buffer-lifetime rule of tests/test_stream_lifetime.py)
     }
@@ -589,33 +570,18 @@ class BabRuntime {
   DevBuf<int8_t> status_;
   DevBuf<uint8_t> prob_;
   DevBuf<unsigned char> stage_;
+  fa_mem::HostBuf hcount_buf_{true};   // coherent: the settle kernel writes the level counters
   int* hcount_ = nullptr;
-  // pinned host staging (solve start, solve end, per-level candidate records)
-  unsigned char* hstage_ = nullptr;
-  size_t hstage_n_ = 0;
-  unsigned char* hout_ = nullptr;
-  size_t hout_n_ = 0;
-  unsigned char* hcand_ = nullptr;
-  size_t hcand_n_ = 0;
-  unsigned char* hidx_ = nullptr;   // confirmed-SAT partition ids (H2D before fa_set_status)
-  size_t hidx_n_ = 0;
-
-  // grow a pinned host buffer; only called between solves / after a stream sync, so no copy can
-  // still be reading the old one.  Buffer-lifetime rule of this runtime (checked by
-  // tests/test_stream_lifetime.py): the host side of EVERY hipMemcpyAsync is one of these
-  // runtime-owned pinned buffers, never a pageable std::vector / numpy temporary, and nothing
-  // writes, frees or regrows it before the hipStreamSynchronize that retires the copy.  Round 1
-  // enqueued pageable H2D copies and then rewrote the source vector in place (relaxed x' boxes);
-  // with 8 host threads that raced the runtime's staging of pageable copies.
-  static void ensure_host(unsigned char*& p, size_t& n, size_t need) {
-    if (need <= n) return;
-    if (p) hipHostFree(p);
-    p = nullptr;
-    size_t m = std::max<size_t>(need, 4096);
-    m = std::max(m, n * 2);
-    ck(hipHostMalloc((void**)&p, m, hipHostMallocDefault), "hipHostMalloc");
-    n = m;
-  }
+  // pinned host staging (solve start, solve end, per-level candidate records, confirmed-SAT
+  // partition ids before fa_set_status), grown through the caching allocator (devmem.h).
+  // Buffer-lifetime rule of this runtime (checked by tests/test_stream_lifetime.py): the host side
+  // of EVERY hipMemcpyAsync is one of these runtime-owned pinned buffers, never a pageable
+  // std::vector / numpy temporary, and nothing writes, releases or regrows it before the
+  // hipStreamSynchronize that retires the copy (so a released block is idle when the cache hands
+  // it to another runtime).  Round 1 enqueued pageable H2D copies and then rewrote the source
+  // vector in place (relaxed x' boxes); with 8 host threads that raced the runtime's staging of
+  // pageable copies.
+  fa_mem::HostBuf hstage_, hout_, hcand_, hidx_;
 };
 
 void register_bab(py::module& m) {

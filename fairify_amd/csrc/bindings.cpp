@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "args.h"
+#include "devmem.h"
 
 namespace py = pybind11;
 
@@ -427,5 +428,22 @@ PYBIND11_MODULE(_C, m) {
   m.def("arch", []() { return std::string("gfx950"); });
   register_bab(m);
   register_relu(m);
+  // caching allocator of the native runtimes (devmem.h): hipFree / hipHostFree calls reaching the
+  // driver stay 0 in steady state
+  m.def("mem_stats", [] {
+    const fa_mem::Stats s = fa_mem::stats();
+    py::dict d;
+    d["dev_cached_bytes"] = s.dev_cached_bytes;
+    d["dev_live_bytes"] = s.dev_live_bytes;
+    d["host_cached_bytes"] = s.host_cached_bytes;
+    d["host_live_bytes"] = s.host_live_bytes;
+    d["dev_mallocs"] = s.dev_mallocs;
+    d["dev_hits"] = s.dev_hits;
+    d["host_mallocs"] = s.host_mallocs;
+    d["host_hits"] = s.host_hits;
+    d["driver_frees"] = s.driver_frees;
+    return d;
+  });
+  m.def("mem_release_cached", [] { fa_mem::release_cached(); });
   register_csv(m);
 }

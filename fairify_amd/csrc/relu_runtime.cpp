@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "args.h"
+#include "devmem.h"
 #include "exact_host.h"
 
 namespace py = pybind11;
@@ -45,33 +46,11 @@ void rckl(int rc, const char* what) {
 }
 
 template <typename T>
-struct RBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  void ensure(size_t cnt) {
-    if (cnt <= n) return;
-    if (p) hipFree(p);
-    p = nullptr;
-    rck(hipMalloc((void**)&p, std::max<size_t>(cnt, 1) * sizeof(T)), "hipMalloc");
-    n = cnt;
-  }
-  ~RBuf() {
-    if (p) hipFree(p);
-  }
-};
+using RBuf = fa_mem::DevBuf<T>;
 
 float rgamma(int k, double unit) {
   const double ku = (k + 2) * unit;
   return std::nextafter((float)(ku / (1.0 - ku)), INFINITY);
-}
-
-void host_grow(unsigned char*& p, size_t& n, size_t need) {
-  if (need <= n) return;
-  if (p) hipHostFree(p);
-  p = nullptr;
-  const size_t m = std::max(std::max<size_t>(need, 4096), 2 * n);
-  rck(hipHostMalloc((void**)&p, m, hipHostMallocDefault), "hipHostMalloc");
-  n = m;
 }
 
 }  // namespace
@@ -102,7 +81,8 @@ class ReluRuntime {
     open_.ensure(batch_); choice_.ensure(batch_); idim_.ensure(batch_);
     cpts_.ensure(R * n0_); pe_lb_.ensure(R); pe_ub_.ensure(R);
     counters_.ensure(2);
-    rck(hipHostMalloc((void**)&hcount_, 2 * sizeof(int), hipHostMallocCoherent), "hipHostMalloc");
+    hcount_buf_.ensure(2 * sizeof(int));
+    hcount_ = reinterpret_cast<int*>(hcount_buf_.p);
     // fp64 host copy of the network for the exact confirmation
     int np_ = 0;
     for (int l = 0; l < net_.n_layers; ++l) np_ = std::max(np_, net_.b_off[l] + net_.dims[l + 1]);
@@ -117,13 +97,6 @@ class ReluRuntime {
     exact_.is_pa.assign(n0_, 0);
     exact_.is_ra.assign(n0_, 0);
     for (int k : pa_) exact_.is_pa[k] = 1;
-  }
-  ~ReluRuntime() {
-    if (hcount_) hipHostFree(hcount_);
-    if (hstage_) hipHostFree(hstage_);
-    if (hout_) hipHostFree(hout_);
-    if (hcand_) hipHostFree(hcand_);
-    if (hidx_) hipHostFree(hidx_);
   }
 
   py::tuple solve(py::array_t<float, py::array::c_style | py::array::forcecast> lo,
@@ -148,9 +121,9 @@ class ReluRuntime {
     ensure_pool(0, std::max<long long>(n_root, 1));
     // staged host block: status | part | pair | lo | hi (one H2D copy), then device memsets
     const size_t sb = (size_t)((P + 3) & ~3) + (size_t)n_root * (2 * sizeof(int) + 2 * n0_ * sizeof(float));
-    host_grow(hstage_, hstage_n_, sb);
+    hstage_.ensure(sb);
     {
-      unsigned char* h = hstage_;
+      unsigned char* h = hstage_.p;
       std::memcpy(h, status0.data(), P);
       int* hp = reinterpret_cast<int*>(h + ((P + 3) & ~3));
       int* hq = hp + n_root;
@@ -167,7 +140,7 @@ class ReluRuntime {
           }
         }
       stage_.ensure(sb);
-      rck(hipMemcpyAsync(stage_.p, hstage_, sb, hipMemcpyHostToDevice, st), "cp stage");
+      rck(hipMemcpyAsync(stage_.p, hstage_.p, sb, hipMemcpyHostToDevice, st), "cp stage");
       const unsigned char* d = stage_.p;
       rck(hipMemcpyAsync(status_.p, d, P, hipMemcpyDeviceToDevice, st), "cp status");
       d += (P + 3) & ~3;
@@ -217,11 +190,13 @@ class ReluRuntime {
       }
     }
     // results
-    std::vector<int8_t> hs(P);
-    std::vector<int> hn(P);
-    rck(hipMemcpyAsync(hs.data(), status_.p, P, hipMemcpyDeviceToHost, st), "cp status out");
-    rck(hipMemcpyAsync(hn.data(), nodes_.p, P * sizeof(int), hipMemcpyDeviceToHost, st), "cp nodes out");
+    const size_t hn_off = ((size_t)P + 15) & ~size_t(15);
+    hout_.ensure(hn_off + (size_t)P * sizeof(int));
+    rck(hipMemcpyAsync(hout_.p, status_.p, P, hipMemcpyDeviceToHost, st), "cp status out");
+    rck(hipMemcpyAsync(hout_.p + hn_off, nodes_.p, P * sizeof(int), hipMemcpyDeviceToHost, st), "cp nodes out");
     rck(hipStreamSynchronize(st), "sync");
+    const int8_t* hs = reinterpret_cast<const int8_t*>(hout_.p);
+    const int* hn = reinterpret_cast<const int*>(hout_.p + hn_off);
     // partitions with nodes left after a time-out
     std::vector<char> left(P, 0);
     if (timed_out && n_in > 0) {
@@ -332,10 +307,10 @@ class ReluRuntime {
   void confirm_candidates(int n_cand, py::object& confirm, std::vector<char>& got, std::vector<int64_t>& cex_x,
                           std::vector<int64_t>& cex_xp, hipStream_t st) {
     const size_t rec = (size_t)2 * n0_ + 1;
-    host_grow(hcand_, hcand_n_, (size_t)n_cand * rec * sizeof(float));
-    rck(hipMemcpyAsync(hcand_, cand_.p, (size_t)n_cand * rec * sizeof(float), hipMemcpyDeviceToHost, st), "cp cand");
+    hcand_.ensure((size_t)n_cand * rec * sizeof(float));
+    rck(hipMemcpyAsync(hcand_.p, cand_.p, (size_t)n_cand * rec * sizeof(float), hipMemcpyDeviceToHost, st), "cp cand");
     rck(hipStreamSynchronize(st), "sync");
-    const float* hc = reinterpret_cast<const float*>(hcand_);
+    const float* hc = reinterpret_cast<const float*>(hcand_.p);
     std::vector<float> buf((size_t)n_cand * 2 * n0_);
     std::vector<int> parts(n_cand);
     for (int i = 0; i < n_cand; ++i) {
@@ -385,9 +360,9 @@ class ReluRuntime {
     if (!newly.empty()) {
       // SAT partitions stop: their nodes are skipped from the next level on (status filter)
       idx_.ensure(newly.size());
-      host_grow(hidx_, hidx_n_, newly.size() * sizeof(int));
-      std::memcpy(hidx_, newly.data(), newly.size() * sizeof(int));
-      rck(hipMemcpyAsync(idx_.p, hidx_, newly.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp idx");
+      hidx_.ensure(newly.size() * sizeof(int));
+      std::memcpy(hidx_.p, newly.data(), newly.size() * sizeof(int));
+      rck(hipMemcpyAsync(idx_.p, hidx_.p, newly.size() * sizeof(int), hipMemcpyHostToDevice, st), "cp idx");
       // status 1 (SAT) for each: a tiny host loop of memsets keeps this file free of extra kernels
       for (size_t k = 0; k < newly.size(); ++k)
         rck(hipMemsetAsync(status_.p + newly[k], 1, 1, st), "set sat");
@@ -417,15 +392,11 @@ class ReluRuntime {
   RBuf<uint8_t> infeas_, open_;
   RBuf<int8_t> status_;
   RBuf<unsigned char> stage_;
+  fa_mem::HostBuf hcount_buf_{true};   // coherent: the settle kernel writes the level counters
   int* hcount_ = nullptr;
-  unsigned char* hstage_ = nullptr;
-  size_t hstage_n_ = 0;
-  unsigned char* hout_ = nullptr;
-  size_t hout_n_ = 0;
-  unsigned char* hcand_ = nullptr;
-  size_t hcand_n_ = 0;
-  unsigned char* hidx_ = nullptr;
-  size_t hidx_n_ = 0;
+  // pinned staging; same buffer-lifetime rule as BabRuntime (released / regrown only after the
+  // stream synchronisation that retires its last copy)
+  fa_mem::HostBuf hstage_, hout_, hcand_, hidx_;
 };
 
 void register_relu(py::module& m) {

@@ -343,33 +343,29 @@ class BaBSolver:
 
     # --------------------------------------------------------------------------------------
     def _runtime(self, values_np: np.ndarray, pairs_np: np.ndarray, n_run: int):
-        """Native (C++/HIP) BaB runtime, cached on the backend per query signature."""
+        """Native (C++/HIP) BaB runtime checked out of the backend's pool (engine/rtpool.py)."""
         from ..ops import ext
         from ..ops.hip import _net
+        from .rtpool import checkout
 
-        # one runtime per (query, host thread): concurrent chunks of one model on several
-        # streams must not share device work buffers
         key = (tuple(self.q.pa_idx), tuple(self.q.ra_idx), self.q.tau, values_np.tobytes(), pairs_np.tobytes(),
-               threading.get_ident(), bool(self.cfg.crown), int(self.cfg.split_target))
-        cache = self.be.__dict__.setdefault("_bab_rt", {})
-        cap = max(self.cfg.max_pool, n_run)
-        rt = cache.get(key)
-        if rt is None or rt[1] < cap:
-            shared = np.ones(self.q.n, dtype=np.uint8)
-            shared[list(self.q.ra_idx)] = 0
-            rt = (ext().BabRuntime(_net(self.be), self.be.flat.data_ptr(), list(self.q.pa_idx),
-                                   values_np.astype(np.float32).reshape(-1).tolist(),
-                                   values_np.astype(np.int64).reshape(-1).tolist(),
-                                   pairs_np.astype(np.int64).reshape(-1).tolist(),
-                                   list(self.q.ra_idx) if self.relaxed else [], float(self.q.tau),
-                                   shared.tolist(), int(cap), int(self.cfg.batch_nodes), int(self.cfg.cand_cap),
-                                   float(self.be.unit), bool(self.cfg.crown), int(self.cfg.split_target)), cap)
-            cache[key] = rt
-        return rt[0]
+               bool(self.cfg.crown), int(self.cfg.split_target))
+        shared = np.ones(self.q.n, dtype=np.uint8)
+        shared[list(self.q.ra_idx)] = 0
+
+        def make(cap):
+            return ext().BabRuntime(_net(self.be), self.be.flat.data_ptr(), list(self.q.pa_idx),
+                                    values_np.astype(np.float32).reshape(-1).tolist(),
+                                    values_np.astype(np.int64).reshape(-1).tolist(),
+                                    pairs_np.astype(np.int64).reshape(-1).tolist(),
+                                    list(self.q.ra_idx) if self.relaxed else [], float(self.q.tau),
+                                    shared.tolist(), int(cap), int(self.cfg.batch_nodes), int(self.cfg.cand_cap),
+                                    float(self.be.unit), bool(self.cfg.crown), int(self.cfg.split_target))
+
+        return checkout(self.be, "_bab_rt", key, max(self.cfg.max_pool, n_run), make)
 
     def _solve_native(self, lo_np, hi_np, status, values_np, pairs_np, mlp_exact, exact_models, t0) -> BaBResult:
         n_run = int((status == RUNNING).sum())
-        rt = self._runtime(values_np, pairs_np, n_run)
         q = self.q
 
         def confirm(parts: np.ndarray, buf: np.ndarray) -> np.ndarray:
@@ -393,7 +389,7 @@ class BaBSolver:
             self._dead_u8 = self.dead.to(torch.uint8).contiguous()
             dead_ptr = self._dead_u8.data_ptr()
         stream = torch.cuda.current_stream(self.dev).cuda_stream
-        with self.tm("bab.native"):
+        with self.tm("bab.native"), self._runtime(values_np, pairs_np, n_run) as rt:
             st, cx, cxp, nodes, stats = rt.solve(lo_np.astype(np.float32), hi_np.astype(np.float32), status,
                                                   int(self.cfg.node_budget), float(self.cfg.time_budget), dead_ptr,
                                                   confirm, stream, exact_models is None,

@@ -305,24 +305,20 @@ class ReluBaBSolver:
 
     # ------------------------------------------------------------------------------------------
     def _runtime(self, values_np: np.ndarray, pairs_np: np.ndarray, n_root: int):
-        """Native (C++/HIP) ReLU-phase runtime, cached on the backend per (query, host thread)."""
-        import threading
-
+        """Native (C++/HIP) ReLU-phase runtime checked out of the backend's pool (engine/rtpool.py)."""
         from ..ops import ext
         from ..ops.hip import _net
+        from .rtpool import checkout
 
-        key = (tuple(self.q.pa_idx), values_np.tobytes(), pairs_np.tobytes(), threading.get_ident(),
-               int(self.cfg.batch_nodes))
-        cache = self.be.__dict__.setdefault("_relu_rt", {})
-        cap = max(self.cfg.max_pool, 2 * n_root)
-        rt = cache.get(key)
-        if rt is None or rt[1] < cap:
-            rt = (ext().ReluRuntime(_net(self.be), self.be.flat.data_ptr(), list(self.q.pa_idx),
-                                    values_np.astype(np.float32).reshape(-1).tolist(),
-                                    pairs_np.astype(np.int64).reshape(-1).tolist(), int(cap),
-                                    int(self.cfg.batch_nodes), float(self.be.unit)), cap)
-            cache[key] = rt
-        return rt[0]
+        key = (tuple(self.q.pa_idx), values_np.tobytes(), pairs_np.tobytes(), int(self.cfg.batch_nodes))
+
+        def make(cap):
+            return ext().ReluRuntime(_net(self.be), self.be.flat.data_ptr(), list(self.q.pa_idx),
+                                     values_np.astype(np.float32).reshape(-1).tolist(),
+                                     pairs_np.astype(np.int64).reshape(-1).tolist(), int(cap),
+                                     int(self.cfg.batch_nodes), float(self.be.unit))
+
+        return checkout(self.be, "_relu_rt", key, max(self.cfg.max_pool, 2 * n_root), make)
 
     def _solve_native(self, lo_np, hi_np, mlp_exact, status, values_np, pairs_np, time_budget):
         P, n0 = lo_np.shape
@@ -331,7 +327,6 @@ class ReluBaBSolver:
             status = status.copy()
             status[status == RUNNING] = UNSAT
             return status, np.zeros((P, n0), np.int64), np.zeros((P, n0), np.int64), np.zeros(P, np.int64)
-        rt = self._runtime(values_np, pairs_np, n_root)
         q = self.q
 
         def confirm(parts: np.ndarray, buf: np.ndarray) -> np.ndarray:
@@ -345,7 +340,7 @@ class ReluBaBSolver:
             return out
 
         stream = torch.cuda.current_stream(self.dev).cuda_stream
-        with self.tm("relu.native"):
+        with self.tm("relu.native"), self._runtime(values_np, pairs_np, n_root) as rt:
             st, cx, cxp, nodes, stats = rt.solve(lo_np.astype(np.float32), hi_np.astype(np.float32), status,
                                                  int(self.cfg.node_budget), float(time_budget), confirm, stream)
         self.stats = dict(stats)

@@ -30,7 +30,7 @@ from ..parallel import wire
 from ..partition import processing_order
 from ..presets import Preset
 from ..report.csv_report import PartitionCSV, format_table, table_v_row_columns, write_summary
-from ..utils import faults
+from ..utils import faults, heap
 from ..utils.timer import StageTimer
 from .stages import STAGES as _STAGES
 from .pipeline import PartitionRecord, StreamPool, VerifyConfig, concat_records, verify_chunk
@@ -258,6 +258,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
     for name in (models or list(preset.models)):
         mlp = get_model(name, weights=weights, seed=seed)
         be = Backend(mlp, device=info.device)
+        heap.freeze()                # the model's setup objects: out of the cycle collector's scans
         acc, acc_src = model_accuracy(mlp, preset.suite, seed, with_source=True) if accuracy else (None, None)
         state_path = os.path.join(out_dir, "state", f"{name}.npz")
         csv_path = os.path.join(out_dir, f"{name}.csv")

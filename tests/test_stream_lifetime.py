@@ -36,38 +36,95 @@ def _host_operands(src: str):
     return out
 
 
+RUNTIMES = ("bab_runtime.cpp", "relu_runtime.cpp")
+
+
+def _pinned_names(src: str):
+    """Runtime-owned pinned buffers: fa_mem::HostBuf members (csrc/devmem.h)."""
+    names = set()
+    for m in re.finditer(r"fa_mem::HostBuf\s+([^;]+);", src):
+        for part in m.group(1).split(","):
+            names.add(re.split(r"[{\s]", part.strip())[0])
+    return names
+
+
 def test_async_copies_use_pinned_runtime_buffers():
-    src = open(os.path.join(CSRC, "bab_runtime.cpp")).read()
-    ops = _host_operands(src)
-    assert len(ops) >= 4, ops
-    pinned = set(re.findall(r"hipHostMalloc\(\(void\*\*\)&(\w+)", src))
-    pinned |= set(re.findall(r"ensure_host\((\w+),", src))
-    for kind, host in ops:
-        if kind == "hipMemcpyDeviceToDevice":
-            continue
-        name = host.split("+")[0].strip()
-        assert name in pinned, f"{kind} from/to {host!r} is not a runtime-owned pinned buffer"
-        assert ".data()" not in host, host
-    # no other source file enqueues async host copies (they go through torch or this runtime)
+    for f in RUNTIMES:
+        src = open(os.path.join(CSRC, f)).read()
+        ops = _host_operands(src)
+        assert len(ops) >= 3, (f, ops)
+        pinned = _pinned_names(src)
+        for kind, host in ops:
+            if kind == "hipMemcpyDeviceToDevice":
+                continue
+            name = host.split("+")[0].strip()
+            assert name.endswith(".p") and name[:-2] in pinned, \
+                f"{f}: {kind} from/to {host!r} is not a runtime-owned pinned buffer"
+            assert ".data()" not in host, host
+        # no raw driver allocation / free in the runtimes: everything goes through the cache
+        assert "hipHostFree" not in src and "hipFree(" not in src and "hipHostMalloc" not in src, f
+    # no other source file enqueues async host copies (they go through torch or the runtimes)
     for f in os.listdir(CSRC):
-        if f.endswith((".hip", ".cpp")) and f != "bab_runtime.cpp":
+        if f.endswith((".hip", ".cpp")) and f not in RUNTIMES:
             assert "hipMemcpyAsync" not in open(os.path.join(CSRC, f)).read(), f
 
 
 def test_pinned_buffers_regrow_only_after_sync():
-    """Every ensure_host(...) call that can regrow a buffer a copy reads is preceded, within the
-    same function, by a stream synchronisation or sits at the start of a solve (previous solve
-    ended with a sync)."""
-    src = open(os.path.join(CSRC, "bab_runtime.cpp")).read()
-    body = src[src.index("py::tuple solve("):]
-    first_sync = body.index("hipStreamSynchronize")
-    for m in re.finditer(r"ensure_host\((\w+),", body):
-        pos = m.start()
-        fn_start = body.rfind("\n  void ", 0, pos)
-        fn_start = max(fn_start, 0)
-        before = body[fn_start:pos]
-        at_solve_start = pos < first_sync and m.group(1) == "hstage_"
-        assert at_solve_start or "hipStreamSynchronize" in before or m.group(1) in ("hout_", "hcand_"), m.group(1)
+    """Every pinned-buffer regrowth (HostBuf::ensure, which releases the old block to the shared
+    cache) is preceded, within the same function, by a stream synchronisation, or sits at the
+    start of a solve (the previous solve ended with a sync), or is the D2H target that the
+    synchronisation right after it retires."""
+    for f in RUNTIMES:
+        src = open(os.path.join(CSRC, f)).read()
+        pinned = _pinned_names(src)
+        body = src[src.index("py::tuple solve("):]
+        first_sync = body.index("hipStreamSynchronize")
+        for m in re.finditer(r"\b(\w+)\.ensure\(", body):
+            if m.group(1) not in pinned:
+                continue
+            pos = m.start()
+            fn_start = max(body.rfind("\n  void ", 0, pos), 0)
+            before = body[fn_start:pos]
+            at_solve_start = pos < first_sync and m.group(1) == "hstage_"
+            assert at_solve_start or "hipStreamSynchronize" in before or m.group(1) in ("hout_", "hcand_"), \
+                (f, m.group(1))
+
+
+def test_runtime_pool_reuses_idle_runtimes():
+    """engine/rtpool.py: an idle runtime of the same key is handed to the next caller whatever its
+    thread; a larger capacity builds a new one and drops the outgrown idle ones."""
+    import threading
+
+    from fairify_amd.engine.rtpool import checkout, count
+
+    class Owner:
+        pass
+
+    o, made = Owner(), []
+
+    def make(cap):
+        made.append(cap)
+        return ("rt", cap, len(made))
+
+    with checkout(o, "_p", "k", 10, make) as a:
+        pass
+    got, held = [], []
+
+    def other_thread():
+        cm = checkout(o, "_p", "k", 8, make)
+        held.append(cm)                          # keep it checked out
+        got.append(cm.__enter__())
+
+    t = threading.Thread(target=other_thread)
+    t.start()
+    t.join()
+    assert got[0] is a and made == [10]          # reused from another thread
+    with checkout(o, "_p", "k", 10, make) as b:  # the first one is checked out: build another
+        assert b is not a
+    assert made == [10, 10]
+    with checkout(o, "_p", "k", 40, make) as c:
+        assert c[1] == 40
+    assert count(o, "_p") == 1                   # the outgrown idle runtime was dropped
 
 
 @pytest.mark.gpu
