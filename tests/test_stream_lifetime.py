@@ -162,3 +162,44 @@ def test_relaxed_bab_eight_streams_match_serial(cuda):
             sat = a.cols["verdict"] == "sat"
             assert np.array_equal(a.cols["cex_x"][sat], b.cols["cex_x"][sat])
             assert np.array_equal(a.cols["cex_xp"][sat], b.cols["cex_xp"][sat])
+
+
+@pytest.mark.gpu
+def test_steady_state_issues_no_driver_frees(cuda):
+    """After a first pass over a set of chunks (8 threads, pooled runtimes), running the same
+    chunks again from other threads allocates nothing new from the driver and frees nothing:
+    every runtime buffer comes out of the caching allocator (csrc/devmem.h)."""
+    import torch
+
+    from fairify_amd import presets
+    from fairify_amd.engine.pipeline import VerifyConfig, verify_chunk
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.ops import ext
+    from fairify_amd.ops.backend import Backend
+    from fairify_amd.partition import processing_order
+
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    order = processing_order(grid, 0)
+    m = get_model("AC-8", weights="random", seed=0)
+    be = Backend(m, cuda)
+    cfg = VerifyConfig(sim_size=128, node_budget=256, smt_backend="none", residual_samples=256, relu_budget=256)
+    chunks = [order[i * 512:(i + 1) * 512] for i in range(8)]
+
+    def run(ids):
+        s = torch.cuda.Stream(cuda)
+        with torch.cuda.stream(s):
+            out = verify_chunk(be, m, q, grid, ids, cfg)
+            torch.cuda.current_stream(cuda).synchronize()
+        return out
+
+    with ThreadPoolExecutor(8) as ex:
+        first = list(ex.map(run, chunks))
+    s0 = ext().mem_stats()
+    with ThreadPoolExecutor(8) as ex:
+        second = list(ex.map(run, chunks[::-1]))     # other threads get other chunks
+    s1 = ext().mem_stats()
+    for a, b in zip(first, second[::-1]):
+        assert np.array_equal(a.cols["verdict"], b.cols["verdict"])
+    assert s1["driver_frees"] == s0["driver_frees"] == 0, (s0, s1)
+    assert s1["dev_hits"] >= s0["dev_hits"]
