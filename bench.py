@@ -46,7 +46,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_DECIDED_PER_S = 553.0 / 22143.5
 METRIC = "% partitions verified + partitions/sec on AC suite at 1/2/4/8 MI355X"
-STAGES = ("sim", "bab", "relu", "falsify", "smt", "milp", "heuristic", "heuristic-confirmed")
+STAGES = ("sim", "bab", "relu", "lp", "falsify", "smt", "milp", "heuristic", "heuristic-confirmed")
 UNSOUND_UNSAT = ("heuristic", "milp")     # engine/stages.py: UNSAT verdicts that are not proofs
 
 

@@ -57,7 +57,7 @@ def cmd_verify(args):
                        escalate_budget=args.escalate_budget, escalate_max_open=args.escalate_max_open,
                        escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
                                                 for st in args.escalate_probation.split(",") if st),
-                       keep_masks=args.keep_masks)
+                       keep_masks=args.keep_masks, lp_budget=args.lp_budget, trust_milp=args.trust_milp)
     if args.residual_samples is not None:
         cfg.residual_samples = args.residual_samples
     models = args.models.split(",") if args.models else None
@@ -194,6 +194,12 @@ def main(argv=None):
     v.add_argument("--concurrency", type=int, default=0,
                    help="chunks verified at once per rank, one HIP stream each (default 4 on GPU, 1 on CPU)")
     v.add_argument("--smt", default="auto", help="host SMT back-end for the residue: auto | z3py | z3bin | none")
+    v.add_argument("--lp-budget", type=int, default=4096,
+                   help="without Z3 (--smt auto/milp): verified-LP branch-and-bound nodes per partition on the "
+                        "residue, sound UNSAT (smt/lpbab.py); 0 = the HiGHS MILP, whose UNSAT is not a proof")
+    v.add_argument("--trust-milp", action="store_true",
+                   help="count HiGHS MILP UNSAT (floating-point dual bound) as verdicts (stage 'milp', excluded "
+                        "from the sound figures); implies the MILP stage")
     v.add_argument("--anytime", action="store_true",
                    help="spend the per-model wall budget (--anytime-budget, default the preset's hard timeout) on "
                         "growing sound BaB budgets and falsifier rounds over the UNKNOWN residue")

@@ -100,6 +100,9 @@ class VerifyConfig:
     relu_escalate_cap: int = 0           # networks the relu stage runs on: cap the input-split
                                          # escalation budget at this (their residue goes to the cheaper
                                          # relu stage instead of deep input splitting; 0 = no cap)
+    lp_budget: int = 4096                # verified-LP branch-and-bound (stage "lp", smt/lpbab.py) in
+                                         # place of the untrusted MILP: LP nodes per partition (x growth
+                                         # per anytime round); 0 = the round-2 MILP stage
     trust_milp: bool = False             # HiGHS MILP UNSAT rests on a floating-point dual bound: by
                                          # default it is recorded (stage "milp") but the partition
                                          # stays UNKNOWN for the rigorous stages; True = round-2
@@ -229,6 +232,34 @@ def _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, limit, worke
         status[hit] = SAT
         cex_x[hit], cex_xp[hit] = X[viol], XP[viol]
         stage[hit] = "milp"
+
+
+def _lp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, budget, limit, workers, status, stage, cex_x,
+              cex_xp, deadline=None):
+    """Verified-LP branch-and-bound (smt/lpbab.py) on the partitions ``unk``: HiGHS solves, a
+    rigorous weak-duality bound from its multipliers closes nodes, lattice points and LP optima
+    are checked exactly.  UNSAT and SAT verdicts are both sound (stage ``lp``)."""
+    from ..smt import lpbab
+
+    futs = lpbab.submit(be, mlp, q, lo_np[unk], hi_np[unk], values_np, pairs_np, budget, limit, workers=workers,
+                        deadline=deadline)
+    t_note = time.time()
+    for i, (k, f) in enumerate(zip(unk, futs)):
+        verdict, pair, _ = f.result()
+        if _VERBOSE_ANYTIME and time.time() - t_note > 30.0:
+            t_note = time.time()
+            print(f"[lp] {mlp.name}: {i + 1}/{len(unk)} partitions, budget {budget}", flush=True)
+        if verdict == "unsat":
+            status[k], stage[k] = UNSAT, "lp"
+        elif verdict == "sat" and pair is not None:
+            status[k], stage[k] = SAT, "lp"
+            cex_x[k], cex_xp[k] = pair[0], pair[1]
+
+
+def _use_lp(cfg, q) -> bool:
+    from ..smt import lpbab  # noqa: F401  (SciPy present: the MILP back-end resolved)
+
+    return cfg.lp_budget > 0 and not cfg.trust_milp and not q.relaxed
 
 
 def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.ndarray, cfg: VerifyConfig,
@@ -488,11 +519,17 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
 
         backend = smt_solver.resolve(cfg.smt_backend)
         unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
-        if backend == "milp" and unk.size and cfg.anytime_seconds <= 0:   # anytime: MILP rounds inside 3d
+        if backend == "milp" and unk.size and cfg.anytime_seconds <= 0:   # anytime: rounds inside 3d
             t0 = time.time()
-            with tm("milp"):
-                _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, cfg.smt_timeout or cfg.soft_timeout,
-                            cfg.smt_workers, status, stage, cex_x, cex_xp, trust=cfg.trust_milp)
+            if _use_lp(cfg, q):
+                with tm("lp"):
+                    _lp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, cfg.lp_budget,
+                              cfg.smt_timeout or cfg.soft_timeout, cfg.smt_workers, status, stage, cex_x, cex_xp)
+            else:
+                with tm("milp"):
+                    _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np,
+                                cfg.smt_timeout or cfg.soft_timeout, cfg.smt_workers, status, stage, cex_x, cex_xp,
+                                trust=cfg.trust_milp)
             t_smt = time.time() - t0
         elif backend != "milp":
             hs = _host_smt(cfg)
@@ -530,6 +567,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
 
             use_milp = smt_solver.resolve(cfg.smt_backend) == "milp"
         milp_limit = cfg.anytime_milp_seconds
+        lp_budget = max(1, cfg.lp_budget // 16)                     # x growth per round
         relu_any = _relu_supported(q)
         r_budget = max(cfg.relu_budget, 1) if relu_on else 64      # x growth before the first round
         with tm("anytime"):
@@ -556,8 +594,19 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                     status[hit] = SAT
                     cex_x[hit], cex_xp[hit] = X[viol], XP[viol]
                     stage[hit] = "falsify"
-                # (b) exact host MILP with a growing per-partition time limit
-                if use_milp:
+                # (b) verified-LP branch-and-bound with a growing node budget (sound UNSAT), or
+                # -- trust_milp / lp_budget 0 -- the HiGHS MILP with a growing time limit
+                if use_milp and _use_lp(cfg, q):
+                    unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+                    left = deadline - time.time()
+                    if unk.size and left > 0:
+                        with tm("lp"):
+                            _lp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, lp_budget,
+                                      min(milp_limit * 4, left), cfg.smt_workers, status, stage, cex_x, cex_xp,
+                                      deadline=deadline)
+                    lp_budget *= cfg.anytime_growth
+                    milp_limit *= cfg.anytime_growth
+                elif use_milp:
                     # partitions the MILP already claimed UNSAT (unverified) are not re-solved
                     unk = np.nonzero((status == UNKNOWN) & ~forced & (stage != "milp"))[0]
                     left = deadline - time.time()

@@ -11,6 +11,9 @@ Verdict / stage combinations:
 * ``bab`` UNSAT: every node of the partition closed by a rigorous input-split certificate.
 * ``relu`` UNSAT: closed by the ReLU phase-split search (engine/relu_bab.py), rigorous bounds.
 * ``smt`` UNSAT: Z3 (exact rational arithmetic), when installed.
+* ``lp`` UNSAT: verified-LP branch-and-bound (smt/lpbab.py): HiGHS LP relaxations, every closed
+  node certified by a rigorously evaluated weak-duality bound from the solver's multipliers;
+  ``lp`` SAT: a lattice point confirmed exactly.
 * ``milp``: HiGHS MILP on the residue.  Its UNSAT rests on a floating-point dual bound, so by
   default it is NOT a verdict: the partition stays UNKNOWN with stage ``milp`` (the solver's
   claim is recorded, unverified); ``VerifyConfig.trust_milp`` restores the round-2 behaviour
@@ -21,11 +24,11 @@ Verdict / stage combinations:
 """
 from __future__ import annotations
 
-STAGES = ("", "sim", "bab", "heuristic", "smt", "falsify", "milp", "heuristic-confirmed", "relu")
+STAGES = ("", "sim", "bab", "heuristic", "smt", "falsify", "milp", "heuristic-confirmed", "relu", "lp")
 CODE = {s: k for k, s in enumerate(STAGES)}
 
-SOUND_SAT = frozenset({"sim", "bab", "falsify", "smt", "milp", "heuristic-confirmed", "relu", ""})
-SOUND_UNSAT = frozenset({"bab", "smt", "relu", ""})
+SOUND_SAT = frozenset({"sim", "bab", "falsify", "smt", "milp", "heuristic-confirmed", "relu", "lp", ""})
+SOUND_UNSAT = frozenset({"bab", "smt", "relu", "lp", ""})
 UNSOUND_UNSAT = frozenset({"heuristic", "milp"})
 
 

@@ -1,0 +1,370 @@
+"""LP branch-and-bound with rigorously verified dual certificates (stage ``lp``).
+
+The reference decides every partition with Z3 (exact rationals; utils/verif_utils.py:525-528,
+src/AC/Verify-AC.py:127-163).  Round 2 used a HiGHS MILP on the residue, whose UNSAT is HiGHS's
+floating-point branch-and-cut dual bound -- no proof (smt/milp.py).  This stage keeps HiGHS as an
+UNTRUSTED oracle and checks what it returns:
+
+* per ordered PA pair (v, v'): the LP relaxation of the two-copy encoding of smt/milp.py
+  (maximise t s.t. t <= -N(x, v), t <= N(x', v'); x real in the partition box; each unstable
+  neuron's big-M binary relaxed to [0, 1], i.e. the triangle relaxation over the GPU's rigorous
+  per-layer bounds; stable neurons exact).  ``t* > 0`` is necessary for a violation.
+* the LP is solved by HiGHS (scipy ``linprog``); its dual multipliers y are then used in the
+  weak-duality bound   t <= y_ub.b_ub + y_eq.b_eq + sum_j max(r_j l_j, r_j u_j),
+  r = c - A^T y,  valid for ANY y_ub >= 0 and any y_eq.  The bound is evaluated in fp64 with a
+  rigorous rounding term (Higham gamma_k over every dot product and the final sum), so the
+  certificate does not depend on the solver being right -- only on the constraint data, which is
+  exact: float32 weights / biases / GPU bounds are exact in fp64, and every constant is carried by
+  a variable fixed to 1 (no rounded right-hand sides).
+* a node whose certified bound is <= 0 is closed (no x with N(x, v) < 0 < N(x', v'));
+  otherwise it branches on the unstable neuron whose relaxation the LP optimum exploits most
+  (largest h - relu(z) at the LP point, ties: lower index), fixing its binary to 0 / 1 -- the
+  exact phase constraints -- and, with no unstable neuron left, splits the widest input dimension
+  of the integer box (lattice points are decided exactly, so the search is complete);
+* the LP primal point, rounded to the lattice, is a counterexample candidate: the pipeline
+  confirms it with the exact checker before counting a SAT.
+
+Cost: one small LP per node (~12 + 2 x 124 + binaries variables for AC-7), milliseconds on the
+host; the stage runs in the anytime mode (Table V), where the round-2 MILP ran.  CPU tests pin
+its verdicts to brute-force lattice enumeration (tests/test_lpbab.py).
+"""
+from __future__ import annotations
+
+import heapq
+import math
+import time
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+U64 = 2.0 ** -53
+
+
+def _gamma(k: int) -> float:
+    ku = k * U64
+    return ku / (1.0 - ku)
+
+
+class _LP:
+    """Two-copy LP of one ordered PA pair with exact data.  Variables: [one | x (n0) | PA dims of
+    x' | per copy and layer: h (w_l), a (unstable) | t]; rows two-sided (lo <= A v <= hi)."""
+
+    def __init__(self, weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b):
+        self.nv = 0
+        self.lb: List[float] = []
+        self.ub: List[float] = []
+        ri, rj, rv, rlo, rhi = [], [], [], [], []
+        self.nr = 0
+
+        def var(lb, ub):
+            lb = np.atleast_1d(np.asarray(lb, np.float64))
+            ub = np.atleast_1d(np.asarray(ub, np.float64))
+            idx = np.arange(self.nv, self.nv + lb.size)
+            self.nv += lb.size
+            self.lb.extend(lb.tolist())
+            self.ub.extend(ub.tolist())
+            return idx
+
+        def row(js, vs, lo_, hi_):
+            ri.append(np.full(len(js), self.nr, np.int64))
+            rj.append(np.asarray(js, np.int64))
+            rv.append(np.asarray(vs, np.float64))
+            rlo.append(lo_)
+            rhi.append(hi_)
+            self.nr += 1
+
+        n0 = lo.size
+        pa = list(pa_idx)
+        self.one = var([1.0], [1.0])[0]
+        self.one2 = var([1.0], [1.0])[0]        # second constant: -b and +lb stay separate exact terms
+        xlo = lo.astype(np.float64).copy()
+        xhi = hi.astype(np.float64).copy()
+        xlo[pa] = va
+        xhi[pa] = va
+        self.x = var(xlo, xhi)
+        xb = self.x.copy()
+        xpa = var(np.asarray(vb, np.float64), np.asarray(vb, np.float64))
+        for k, d in enumerate(pa):
+            xb[d] = xpa[k]
+        self.a_vars: List[Tuple[int, int, int, int, int]] = []   # (a var, h var, copy, layer, neuron)
+        self.z_rows = []                                       # (copy, layer, neuron) -> (h, prev, W col, b)
+        outs = []
+        for cp, (xin, (lbs, ubs)) in enumerate(((self.x, bounds_a), (xb, bounds_b))):
+            prev = xin
+            L = len(weights)
+            for l in range(L - 1):
+                W = np.asarray(weights[l], np.float64)
+                b = np.asarray(biases[l], np.float64)
+                lb = np.asarray(lbs[l], np.float64)
+                ub = np.asarray(ubs[l], np.float64)
+                w = W.shape[1]
+                dead = ub <= 0
+                h = var(np.zeros(w), np.where(dead, 0.0, np.maximum(ub, 0.0)))
+                for j in range(w):
+                    if dead[j]:
+                        continue
+                    js = np.concatenate([[h[j]], prev, [self.one]])
+                    base = np.concatenate([[1.0], -W[:, j], [-b[j]]])       # h - W.prev - b
+                    if lb[j] >= 0:
+                        row(js, base, 0.0, 0.0)                             # h = z
+                        continue
+                    a = var([0.0], [1.0])[0]
+                    self.a_vars.append((a, h[j], cp, l, j))
+                    row(js, base, 0.0, np.inf)                              # h >= z
+                    # h - z - lb a + lb <= 0   (h <= z - lb (1 - a))
+                    row(np.concatenate([js, [self.one2, a]]), np.concatenate([base, [lb[j]], [-lb[j]]]),
+                        -np.inf, 0.0)
+                    row([h[j], a], [1.0, -ub[j]], -np.inf, 0.0)             # h <= ub a
+                    self.z_rows.append((h[j], prev, W[:, j], b[j], lb[j], ub[j]))
+                prev = h
+            outs.append((prev, np.asarray(weights[-1], np.float64)[:, 0], float(np.asarray(biases[-1])[0])))
+        # bound on |t|: valid because t <= N(x', v') <= its output bound, and any lower bound below
+        # min(-N, N') keeps every feasible point (t is maximised)
+        (pa_h, wa, ba), (pb_h, wb, bb) = outs
+        M = 1.0 + abs(ba) + abs(bb) + float(np.abs(wa) @ np.maximum(np.asarray(self.ub)[pa_h], 0)) \
+            + float(np.abs(wb) @ np.maximum(np.asarray(self.ub)[pb_h], 0))
+        M = float(np.nextafter(2.0 * M, np.inf))
+        self.t = var([-M], [M])[0]
+        row(np.concatenate([[self.t], pa_h, [self.one]]), np.concatenate([[1.0], wa, [ba]]), -np.inf, 0.0)
+        row(np.concatenate([[self.t], pb_h, [self.one]]), np.concatenate([[1.0], -wb, [-bb]]), -np.inf, 0.0)
+        from scipy.sparse import coo_matrix
+
+        self.A = coo_matrix((np.concatenate(rv), (np.concatenate(ri), np.concatenate(rj))),
+                            shape=(self.nr, self.nv)).tocsr()
+        self.rlo = np.asarray(rlo, np.float64)
+        self.rhi = np.asarray(rhi, np.float64)
+        self.lb = np.asarray(self.lb)
+        self.ub = np.asarray(self.ub)
+        self.n0 = n0
+        eq = self.rlo == self.rhi
+        up = ~eq & np.isfinite(self.rhi)
+        lo_ = ~eq & np.isfinite(self.rlo)
+        self.A_eq, self.b_eq = self.A[eq], self.rhi[eq]
+        self.A_ub = _vstack(self.A[up], -self.A[lo_])
+        self.b_ub = np.concatenate([self.rhi[up], -self.rlo[lo_]])
+        self.c = np.zeros(self.nv)
+        self.c[self.t] = -1.0
+
+    # ------------------------------------------------------------------------------------------
+    def solve(self, lb: np.ndarray, ub: np.ndarray):
+        """LP with variable bounds (lb, ub) (binaries fixed by the node) -> (t_lp or None,
+        certified upper bound on t, primal v or None)."""
+        from scipy.optimize import linprog
+
+        c, A_ub, b_ub, A_eq, b_eq = self.c, self.A_ub, self.b_ub, self.A_eq, self.b_eq
+        try:
+            res = linprog(c, A_ub=A_ub, b_ub=b_ub, A_eq=A_eq if A_eq.shape[0] else None,
+                          b_eq=b_eq if A_eq.shape[0] else None, bounds=np.stack([lb, ub], 1), method="highs")
+        except ValueError:
+            return None, math.inf, None
+        if res.status == 2:                       # infeasible region (phase constraints): closed
+            return None, -math.inf, None
+        if res.status != 0 or res.x is None:
+            return None, math.inf, None
+        y_ub = np.maximum(-np.asarray(res.ineqlin.marginals, np.float64), 0.0) if b_ub.size else np.zeros(0)
+        y_eq = -np.asarray(res.eqlin.marginals, np.float64) if A_eq.shape[0] else np.zeros(0)
+        cert = certified_bound(-c, A_ub, b_ub, A_eq, b_eq, y_ub, y_eq, lb, ub)
+        return -float(res.fun), cert, res.x
+
+
+def _vstack(a, b):
+    from scipy.sparse import vstack
+
+    return vstack([a, b]).tocsr()
+
+
+def certified_bound(c, A_ub, b_ub, A_eq, b_eq, y_ub, y_eq, lb, ub) -> float:
+    """Rigorous upper bound on  max c.v  s.t.  A_ub v <= b_ub, A_eq v = b_eq, lb <= v <= ub,
+    from ANY multipliers y_ub >= 0, y_eq (weak duality), evaluated in fp64 with Higham gamma
+    terms on every dot product and sum.  Infinite if a variable with an infinite bound keeps a
+    nonzero reduced coefficient."""
+    y_ub = np.maximum(np.asarray(y_ub, np.float64), 0.0)
+    y_eq = np.asarray(y_eq, np.float64)
+    m = A_ub.shape[0] + (A_eq.shape[0] if A_eq is not None else 0)
+    ATy = A_ub.T @ y_ub if A_ub.shape[0] else np.zeros(len(c))
+    ATy_abs = abs(A_ub).T @ y_ub if A_ub.shape[0] else np.zeros(len(c))
+    if A_eq is not None and A_eq.shape[0]:
+        ATy = ATy + A_eq.T @ y_eq
+        ATy_abs = ATy_abs + abs(A_eq).T @ np.abs(y_eq)
+    r = np.asarray(c, np.float64) - ATy
+    g = 2.0 * _gamma(m + 2)                                  # x2: the rounding of ATy_abs itself
+    er = g * (np.abs(c) + ATy_abs)                          # |r_fl - r_exact| <= er
+    r_hi, r_lo = r + er, r - er                             # r_exact in [r_lo, r_hi] (up to the
+    # rounding of these two additions, covered by the 2x slack below)
+    lb = np.asarray(lb, np.float64)
+    ub = np.asarray(ub, np.float64)
+    # max over v_j in [lb_j, ub_j] and r_j in [r_lo, r_hi] of r_j v_j: the four corners
+    with np.errstate(invalid="ignore", over="ignore"):
+        corners = np.stack([r_lo * lb, r_lo * ub, r_hi * lb, r_hi * ub])
+    corners = np.where(np.isnan(corners), 0.0, corners)      # 0 * inf: the coefficient is exactly 0
+    term = corners.max(0)
+    exact_zero = (r_lo == 0.0) & (r_hi == 0.0)
+    term[exact_zero] = 0.0
+    if not np.all(np.isfinite(term)):
+        return math.inf
+    parts = [y_ub * np.asarray(b_ub, np.float64), term]
+    if A_eq is not None and A_eq.shape[0]:
+        parts.append(y_eq * np.asarray(b_eq, np.float64))
+    allp = np.concatenate(parts)
+    s = float(np.sum(allp))
+    k = allp.size + 4
+    cabs = np.abs(corners).max(0)
+    cabs[exact_zero] = 0.0
+    slack = 2.0 * _gamma(k) * float(np.sum(np.abs(allp))) + 2.0 * _gamma(3) * float(np.sum(cabs))
+    bound = s + slack
+    return float(np.nextafter(bound, np.inf)) if math.isfinite(bound) else math.inf
+
+
+def lp_bab_pair(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, node_budget: int, deadline: float,
+                confirm) -> Tuple[str, Optional[tuple], int]:
+    """LP branch-and-bound of one ordered PA pair (v, v'): ('unsat', None, nodes) when every node
+    closed, ('sat', (x, x'), nodes) with an exactly confirmed pair (``confirm(x, x') -> bool``),
+    ('unknown', None, nodes) at the node budget / deadline."""
+    lp = _LP(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b)
+    pa = list(pa_idx)
+    vb_i = np.asarray(vb, np.int64)
+    isx = np.ones(lp.n0, bool)
+    isx[pa] = False
+    tried = set()
+
+    def check(xs) -> bool:
+        key = xs.tobytes()
+        if key in tried:
+            return False
+        tried.add(key)
+        xps = xs.copy()
+        xps[pa] = vb_i
+        return bool(confirm(xs, xps))
+
+    heap = [(0.0, 0, lp.lb.copy(), lp.ub.copy())]     # best-first on the certified bound
+    tick = 1
+    nodes = 0
+    while heap:
+        if nodes >= node_budget or time.time() > deadline:
+            return "unknown", None, nodes
+        _, _, nlb, nub = heapq.heappop(heap)
+        nodes += 1
+        xl, xh = nlb[lp.x], nub[lp.x]
+        point = bool(np.all(xl[isx] == xh[isx]))
+        if point:
+            # a single lattice point: decided exactly (the LP's rounding slack cannot close an
+            # exactly-zero logit, the exact checker can)
+            xs = xl.astype(np.int64)
+            xps = xs.copy()
+            xps[pa] = vb_i
+            if confirm(xs, xps):
+                return "sat", (xs.tolist(), xps.tolist()), nodes
+            continue
+        t_lp, cert, v = lp.solve(nlb, nub)
+        if cert <= 0.0:
+            continue
+        if v is None:
+            return "unknown", None, nodes
+        if t_lp is not None and t_lp > 0:
+            xs = np.clip(np.rint(v[lp.x]), xl, xh).astype(np.int64)
+            if check(xs):
+                xps = xs.copy()
+                xps[pa] = vb_i
+                return "sat", (xs.tolist(), xps.tolist()), nodes
+        # branch: the unfixed binary whose relaxation the LP optimum exploits most
+        best, bi = 0.0, -1
+        for i, (a, h, cp, l, j) in enumerate(lp.a_vars):
+            if nlb[a] == nub[a]:
+                continue
+            hv, prev, wcol, bj, zl, zu = lp.z_rows[i]
+            gap = float(v[h]) - max(float(v[prev] @ wcol + bj), 0.0)
+            if gap > best + 1e-12:
+                best, bi = gap, i
+        children = []
+        if bi >= 0 and best > 1e-9:
+            a = lp.a_vars[bi][0]
+            for val in (0.0, 1.0):
+                clb, cub = nlb.copy(), nub.copy()
+                clb[a] = cub[a] = val
+                children.append((clb, cub))
+        else:
+            # the relaxation is not what keeps the node open: split the widest input dimension
+            wdt = np.where(isx, xh - xl, -1.0)
+            d = int(np.argmax(wdt))
+            mid = math.floor(0.5 * (xl[d] + xh[d]))
+            for lo_d, hi_d in ((xl[d], mid), (mid + 1, xh[d])):
+                clb, cub = nlb.copy(), nub.copy()
+                clb[lp.x[d]], cub[lp.x[d]] = lo_d, hi_d
+                children.append((clb, cub))
+        for clb, cub in children:
+            heapq.heappush(heap, (-cert, tick, clb, cub))
+            tick += 1
+    return "unsat", None, nodes
+
+
+def solve_partition(weights, biases, lo, hi, pa_idx, values, pairs, row_bounds, node_budget: int,
+                    time_limit: float, confirm) -> Tuple[str, Optional[tuple], int]:
+    """Decide one partition over all ordered PA pairs: 'unsat' (every pair's LP-BaB closed),
+    'sat' with an exactly confirmed pair (``confirm(x, x') -> bool``), else 'unknown'."""
+    deadline = time.time() + time_limit
+    nodes = 0
+    for vi, vj in pairs:
+        st, wit, n = lp_bab_pair(weights, biases, lo, hi, pa_idx, values[int(vi)], values[int(vj)],
+                                 row_bounds[int(vi)], row_bounds[int(vj)], max(1, node_budget - nodes), deadline,
+                                 confirm)
+        nodes += n
+        if st == "sat":
+            return "sat", wit, nodes
+        if st != "unsat":
+            return "unknown", None, nodes
+    return "unsat", None, nodes
+
+
+_PPOOL = None
+_PPOOL_N = 0
+
+
+def process_pool(workers: int):
+    """Worker processes of the LP stage (spawned children: numpy / SciPy only, no GPU context).
+    HiGHS through SciPy keeps the GIL, so threads do not scale (measured 1.2x on 4 threads)."""
+    global _PPOOL, _PPOOL_N
+    if _PPOOL is None or _PPOOL_N < workers:
+        import multiprocessing as mp
+        from concurrent.futures import ProcessPoolExecutor
+
+        if _PPOOL is not None:
+            _PPOOL.shutdown(wait=True)
+        _PPOOL = ProcessPoolExecutor(max_workers=max(1, workers), mp_context=mp.get_context("spawn"))
+        _PPOOL_N = workers
+    return _PPOOL
+
+
+def _partition_task(mlp, lo, hi, pa_idx, ra_idx, tau, values, pairs, rb, node_budget, limit, deadline):
+    from ..engine import exact
+
+    if deadline is not None:
+        limit = min(limit, deadline - time.time())
+        if limit <= 0.05:
+            return "unknown", None, 0
+
+    def confirm(xs, xps):
+        ok = exact.check_pair_constraints(xs[None], xps[None], lo[None], hi[None], pa_idx, ra_idx, tau)
+        return bool(ok[0] and exact.is_violation(mlp, xs[None], xps[None])[0])
+
+    return solve_partition(mlp.weights, mlp.biases, lo, hi, pa_idx, values, pairs, rb, node_budget, limit, confirm)
+
+
+def submit(be, mlp, q, lo: np.ndarray, hi: np.ndarray, values: np.ndarray, pairs: np.ndarray, node_budget: int,
+           time_limit: float, workers: int = 8, deadline: Optional[float] = None):
+    """One future per partition -> (verdict, (x, x') or None, nodes).  Rigorous per-layer bounds
+    come from the device in one launch (smt/milp.py:layer_bounds_rows); the LP-BaBs run in the
+    worker processes.  ``deadline``: absolute time.time() after which nothing starts."""
+    from . import milp
+
+    if len(lo) == 0:
+        return []
+    assert not q.relaxed, "lp stage: PA-only queries"
+    lbs, ubs = milp.layer_bounds_rows(be, lo, hi, q, values, widen_ra=False)
+    V = values.shape[0]
+    ex = process_pool(workers)
+    futs = []
+    for k in range(len(lo)):
+        rb = {v: ([lb[k, v] for lb in lbs], [ub[k, v] for ub in ubs]) for v in range(V)}
+        futs.append(ex.submit(_partition_task, mlp, lo[k], hi[k], tuple(q.pa_idx), tuple(q.ra_idx), float(q.tau),
+                              values, pairs, rb, int(node_budget), float(time_limit), deadline))
+    return futs

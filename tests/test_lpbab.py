@@ -1,0 +1,100 @@
+"""Verified-LP branch-and-bound (smt/lpbab.py, stage "lp"): verdicts against brute-force lattice
+enumeration, and the rigour of the dual certificate (it never undercuts the true optimum, even
+from perturbed or wrong multipliers)."""
+import itertools
+
+import numpy as np
+import pytest
+
+from fairify_amd import presets
+from fairify_amd.engine import exact
+from fairify_amd.models.mlp import random_mlp
+from fairify_amd.ops import reference as ref
+from fairify_amd.partition import processing_order
+
+scipy = pytest.importorskip("scipy")
+
+
+def _brute(m, lo, hi, pa):
+    pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo, hi)])))
+    z0 = m.logits(np.where(np.arange(m.n_in) == pa, 0, pts))
+    z1 = m.logits(np.where(np.arange(m.n_in) == pa, 1, pts))
+    return bool((((z0 > 0) & (z1 < 0)) | ((z0 < 0) & (z1 > 0))).any())
+
+
+def _row_bounds(m, lo, hi, q, values):
+    import torch
+
+    out = {}
+    for v in range(len(values)):
+        rl = lo.astype(np.float32).copy()
+        rh = hi.astype(np.float32).copy()
+        rl[list(q.pa_idx)] = values[v]
+        rh[list(q.pa_idx)] = values[v]
+        ws = [torch.from_numpy(np.asarray(w, np.float32)) for w in m.weights]
+        bs = [torch.from_numpy(np.asarray(b, np.float32)) for b in m.biases]
+        r = ref.bounds(ws, bs, torch.from_numpy(rl[None]), torch.from_numpy(rh[None]), mode="symbolic",
+                       keep_layers=True)
+        out[v] = ([t[0].double().numpy() for t in r.layer_lb], [t[0].double().numpy() for t in r.layer_ub])
+    return out
+
+
+@pytest.mark.parametrize("seed", [3, 4, 5])
+def test_lpbab_matches_bruteforce(seed):
+    from fairify_amd.smt import lpbab
+
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, 0)[:24]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 1)                  # <= 2 values per free dim: enumerable
+    m = random_mlp(13, [6, 5], seed=seed, bias_scale=0.5)
+    from fairify_amd.engine.bab import _pa_table
+
+    values, pairs = _pa_table(q, lo[:1], hi[:1])
+    pa = q.pa_idx[0]
+    decided = 0
+    for k in range(len(ids)):
+        rb = _row_bounds(m, lo[k], hi[k], q, values)
+
+        def confirm(xs, xps):
+            ok = exact.check_pair_constraints(xs[None], xps[None], lo[k:k + 1], hi[k:k + 1], q.pa_idx, q.ra_idx, q.tau)
+            return bool(ok[0] and exact.is_violation(m, xs[None], xps[None])[0])
+
+        st, wit, nodes = lpbab.solve_partition(m.weights, m.biases, lo[k], hi[k], q.pa_idx, values, pairs, rb,
+                                               4096, 60.0, confirm)
+        truth = _brute(m, lo[k], hi[k], pa)
+        if st == "sat":
+            assert truth, k
+            assert exact.is_violation(m, np.asarray(wit[0])[None], np.asarray(wit[1])[None])[0]
+        elif st == "unsat":
+            assert not truth, k
+        decided += st != "unknown"
+    assert decided == len(ids)                   # complete within the budget on these boxes
+
+
+def test_certified_bound_never_undercuts_the_optimum():
+    """Weak duality with rounding terms: any multipliers (optimal, perturbed, random) give a bound
+    >= the LP optimum."""
+    from scipy.optimize import linprog
+    from scipy.sparse import csr_matrix
+
+    from fairify_amd.smt.lpbab import certified_bound
+
+    rng = np.random.default_rng(0)
+    for trial in range(20):
+        n, m = 8, 12
+        A = rng.normal(size=(m, n))
+        b = rng.uniform(1, 3, size=m)
+        c = rng.normal(size=n)
+        lb, ub = -rng.uniform(0.5, 2, n), rng.uniform(0.5, 2, n)
+        res = linprog(-c, A_ub=A, b_ub=b, bounds=np.stack([lb, ub], 1), method="highs")
+        assert res.status == 0
+        opt = -res.fun
+        y = np.maximum(-res.ineqlin.marginals, 0)
+        A_s = csr_matrix(A)
+        empty = csr_matrix((0, n))
+        tight = certified_bound(c, A_s, b, empty, np.zeros(0), y, np.zeros(0), lb, ub)
+        assert tight >= opt - 1e-12 and tight <= opt + 1e-6
+        for yy in (y * (1 + 0.1 * rng.normal(size=m)), rng.uniform(0, 1, m), np.zeros(m)):
+            assert certified_bound(c, A_s, b, empty, np.zeros(0), yy, np.zeros(0), lb, ub) >= opt - 1e-12

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--budgets", default="0,2048")
     ap.add_argument("--escalate-budget", type=int, default=32768)
     ap.add_argument("--escalate-probation", default="2048:768,4096:768,8192:768,16384:1024")
+    ap.add_argument("--weights", default="random", help="random | zoo (the reference's trained nets)")
+    ap.add_argument("--offset", type=int, default=0, help="first position of the seeded order")
     args = ap.parse_args()
     import torch
 
@@ -40,9 +42,9 @@ def main():
     dev = torch.device("cuda" if torch.cuda.device_count() else "cpu")
     pre = presets.get(args.preset)
     grid, q = pre.grid(), pre.resolved()
-    ids = processing_order(grid, seed=0)[:args.limit]
+    ids = processing_order(grid, seed=0)[args.offset:args.offset + args.limit]
     for name in args.models.split(","):
-        m = get_model(name, weights="random", seed=0)
+        m = get_model(name, weights=args.weights, seed=0)
         be = Backend(m, device=dev)
         for rb in (int(b) for b in args.budgets.split(",")):
             cfg = VerifyConfig(sim_size=pre.sim_size, chunk=4096, soft_timeout=pre.soft_timeout,
