@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--no-heuristic", action="store_true")
     ap.add_argument("--weights", default="random")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--bench-config", action="store_true",
+                    help="bench.py's defaults (inline escalation to 32768 with probation, relu stage, "
+                         "chunk 8192) instead of the fixed-budget config above")
     ap.add_argument("--residual-samples", type=int, default=8192)
     ap.add_argument("--residual-iters", type=int, default=24)
     ap.add_argument("--residual-starts", type=int, default=16)
@@ -57,6 +60,12 @@ def main():
                        heuristic=not args.no_heuristic, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=args.node_budget, residual_samples=args.residual_samples,
                        residual_iters=args.residual_iters, residual_starts=args.residual_starts)
+    if args.bench_config:
+        cfg = VerifyConfig(sim_size=pre.sim_size, chunk=8192, node_budget=512, heuristic=not args.no_heuristic,
+                           heuristic_p=pre.heuristic_p, heuristic_node_budget=512, escalate_budget=32768,
+                           escalate_max_open=384, batch_nodes=65536, smt_backend="none", relu_budget=1024,
+                           relu_max_width=16, relu_escalate_cap=2048,
+                           escalate_probation=((2048, 768), (4096, 768), (8192, 768), (16384, 1024)))
     out = []
     for name in names:
         m = get_model(name, weights=args.weights, seed=0)
@@ -80,7 +89,11 @@ def main():
                    sat=int((v == "sat").sum()), unsat=int((v == "unsat").sum()), unk=int((v == "unknown").sum()),
                    by_stage={k: int((st == k).sum()) for k in set(st.tolist())},
                    nodes_sum=int(nodes.sum()), nodes_p50=float(np.median(nodes)), nodes_p99=float(np.percentile(nodes, 99)),
-                   nodes_max=int(nodes.max()), stages={k: round(t, 3) for k, t in tm.t.items()})
+                   nodes_max=int(nodes.max()), stages={k: round(t, 3) for k, t in tm.t.items()},
+                   # where the node expansions go: by final verdict / stage, and past the first budget
+                   nodes_by={f"{vv}/{ss}": int(nodes[(v == vv) & (st == ss)].sum())
+                             for vv, ss in sorted(set(zip(v.tolist(), st.tolist())))},
+                   nodes_over_first=int(np.maximum(nodes - cfg.node_budget, 0).sum()))
         if args.deep_budget:
             from fairify_amd.engine.bab import SAT, UNSAT, BaBConfig, BaBSolver
 
