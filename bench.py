@@ -93,6 +93,9 @@ def parse_args(argv=None):
     ap.add_argument("--trust-milp", action="store_true",
                     help="count a HiGHS MILP 'unsat' (floating-point dual bound) as an UNSAT verdict (stage "
                          "'milp', excluded from the sound figures); default: recorded, partition stays UNKNOWN")
+    ap.add_argument("--lp-budget", type=int, default=4096,
+                    help="with --smt milp/auto: verified-LP branch-and-bound nodes per partition (stage 'lp', "
+                         "sound UNSAT); 0 = the HiGHS MILP")
     ap.add_argument("--budget-pass", type=float, default=10.0,
                     help="after the timed steps, one untimed pass over the same grid in anytime mode with this "
                          "many seconds per model (growing BaB budgets + falsifier + MILP rounds on the residue): "
@@ -232,7 +235,7 @@ def main() -> None:
                        node_budget=args.node_budget, heuristic=not args.no_heuristic, heuristic_p=pre.heuristic_p,
                        heuristic_node_budget=args.heuristic_node_budget, escalate_budget=args.escalate_budget,
                        escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
-                       smt_backend=args.smt, trust_milp=args.trust_milp, relu_budget=args.relu_budget,
+                       smt_backend=args.smt, trust_milp=args.trust_milp, lp_budget=args.lp_budget, relu_budget=args.relu_budget,
                        relu_max_width=args.relu_max_width, relu_escalate_cap=args.relu_escalate_cap,
                        escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
                                                 for st in args.escalate_probation.split(",") if st),

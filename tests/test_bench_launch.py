@@ -69,11 +69,17 @@ def test_sound_fields_exclude_heuristic_and_milp():
     assert d["unsat_sound"] == d["unsat"] - us["milp"] - us["heuristic"]
     sound = d["sat"] + d["unsat"] - us["milp"] - us["heuristic"] - d["sat_by_stage"]["heuristic"]
     assert abs(d["pct_verified_sound"] - round(100.0 * sound / att, 3)) < 1e-9
-    # default: an untrusted MILP 'unsat' is no verdict
+    # default: an untrusted MILP 'unsat' is no verdict (MILP stage: --lp-budget 0) ...
     d2 = _bench(1, ("--models", "AC-8", "--node-budget", "8", "--escalate-budget", "0", "--smt", "milp",
-                    "--relu-budget", "0"))
+                    "--relu-budget", "0", "--lp-budget", "0"))
     assert d2["unsat_by_stage"]["milp"] == 0
     assert d2["unsat"] + d2["unknown"] >= d["unsat"] + d["unknown"] - 1e-9
+    # ... and the verified-LP stage's UNSAT (rigorous dual certificates) counts as sound
+    d3 = _bench(1, ("--models", "AC-8", "--limit", "16", "--node-budget", "8", "--escalate-budget", "0",
+                    "--smt", "milp", "--relu-budget", "0", "--lp-budget", "64"))
+    us3 = d3["unsat_by_stage"]
+    assert us3["milp"] == 0 and us3["lp"] > 0, us3
+    assert d3["unsat_sound"] == d3["unsat"] - us3["heuristic"]
 
 
 def test_emulated_lpt_shards_cover_the_grid():
