@@ -594,28 +594,6 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                     status[hit] = SAT
                     cex_x[hit], cex_xp[hit] = X[viol], XP[viol]
                     stage[hit] = "falsify"
-                # (b) verified-LP branch-and-bound with a growing node budget (sound UNSAT), or
-                # -- trust_milp / lp_budget 0 -- the HiGHS MILP with a growing time limit
-                if use_milp and _use_lp(cfg, q):
-                    unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
-                    left = deadline - time.time()
-                    if unk.size and left > 0:
-                        with tm("lp"):
-                            _lp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, lp_budget,
-                                      min(milp_limit * 4, left), cfg.smt_workers, status, stage, cex_x, cex_xp,
-                                      deadline=deadline)
-                    lp_budget *= cfg.anytime_growth
-                    milp_limit *= cfg.anytime_growth
-                elif use_milp:
-                    # partitions the MILP already claimed UNSAT (unverified) are not re-solved
-                    unk = np.nonzero((status == UNKNOWN) & ~forced & (stage != "milp"))[0]
-                    left = deadline - time.time()
-                    if unk.size and left > 0:
-                        with tm("milp"):
-                            _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, min(milp_limit, left),
-                                        cfg.smt_workers, status, stage, cex_x, cex_xp, deadline=deadline,
-                                        trust=cfg.trust_milp)
-                    milp_limit *= cfg.anytime_growth
                 # (c) deeper sound BaB, in groups that fit the node pool
                 e_budget *= cfg.anytime_growth
                 if e_budget > cfg.anytime_max_budget:
@@ -668,6 +646,30 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                             cex_x[grp[sr]] = rr.cex_x[sr]
                             cex_xp[grp[sr]] = rr.cex_xp[sr]
                             nodes[grp] += rr.nodes
+                # (e) verified-LP branch-and-bound with a growing node budget (sound UNSAT), or
+                # -- trust_milp / lp_budget 0 -- the HiGHS MILP with a growing time limit.  Last in the
+                # round: host LPs cost ~10-30 ms per node (AC-7: 341 variables), the GPU stages above
+                # decide most of the residue first
+                if use_milp and _use_lp(cfg, q):
+                    unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+                    left = deadline - time.time()
+                    if unk.size and left > 0:
+                        with tm("lp"):
+                            _lp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, lp_budget,
+                                      min(milp_limit * 4, left), cfg.smt_workers, status, stage, cex_x, cex_xp,
+                                      deadline=deadline)
+                    lp_budget *= cfg.anytime_growth
+                    milp_limit *= cfg.anytime_growth
+                elif use_milp:
+                    # partitions the MILP already claimed UNSAT (unverified) are not re-solved
+                    unk = np.nonzero((status == UNKNOWN) & ~forced & (stage != "milp"))[0]
+                    left = deadline - time.time()
+                    if unk.size and left > 0:
+                        with tm("milp"):
+                            _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, min(milp_limit, left),
+                                        cfg.smt_workers, status, stage, cex_x, cex_xp, deadline=deadline,
+                                        trust=cfg.trust_milp)
+                    milp_limit *= cfg.anytime_growth
         sync()
         t_bab += time.time() - t0
 

@@ -98,3 +98,59 @@ def test_certified_bound_never_undercuts_the_optimum():
         assert tight >= opt - 1e-12 and tight <= opt + 1e-6
         for yy in (y * (1 + 0.1 * rng.normal(size=m)), rng.uniform(0, 1, m), np.zeros(m)):
             assert certified_bound(c, A_s, b, empty, np.zeros(0), yy, np.zeros(0), lb, ub) >= opt - 1e-12
+
+
+def test_certified_bound_rows_any_sign_never_undercuts():
+    """Two-sided rows, multipliers of either sign (optimal, flipped, random): the bound is never
+    below the LP optimum, and tight for the optimal ones."""
+    from scipy.optimize import linprog
+    from scipy.sparse import csr_matrix
+
+    from fairify_amd.smt.lpbab import certified_bound_rows
+
+    rng = np.random.default_rng(1)
+    for trial in range(20):
+        n, m = 8, 10
+        A = rng.normal(size=(m, n))
+        rlo = np.where(rng.uniform(size=m) < 0.3, -np.inf, -rng.uniform(1, 3, size=m))
+        rhi = rng.uniform(1, 3, size=m)
+        d = rng.normal(size=n)
+        lb, ub = -rng.uniform(0.5, 2, n), rng.uniform(0.5, 2, n)
+        fin = np.isfinite(rlo)
+        A_ub = np.concatenate([A, -A[fin]])
+        b_ub = np.concatenate([rhi, -rlo[fin]])
+        res = linprog(-d, A_ub=A_ub, b_ub=b_ub, bounds=np.stack([lb, ub], 1), method="highs")
+        assert res.status == 0
+        opt = -res.fun
+        y = -res.ineqlin.marginals
+        lam = y[:m].copy()
+        lam[fin] -= y[m:]
+        A_s = csr_matrix(A)
+        tight = certified_bound_rows(d, A_s, rlo, rhi, lam, lb, ub)
+        assert opt - 1e-12 <= tight <= opt + 1e-6
+        for ll in (-lam, rng.normal(size=m), np.zeros(m)):
+            assert certified_bound_rows(d, A_s, rlo, rhi, ll, lb, ub) >= opt - 1e-12
+
+
+def test_lp_infeasible_node_needs_a_certificate():
+    """A phase pattern no point of the box satisfies: the warm-started LP reports it infeasible
+    and the elastic phase-1 certificate proves it (bound -inf); both phases of that neuron
+    together cover the box, so exactly one child is provably empty."""
+    from fairify_amd.smt import lpbab
+
+    W0 = np.array([[1.0], [0.0]])            # z = x0 + 0.5 on x0 in [0, 3]: always active
+    b0 = np.array([0.5])
+    W1 = np.array([[1.0]])
+    b1 = np.array([-1.0])
+    lo = np.array([0.0, 0.0])
+    hi = np.array([3.0, 1.0])
+    rb = ([np.array([-0.5])], [np.array([3.5])])   # loose bounds keep the neuron "unstable"
+    lp = lpbab._LP([W0, W1], [b0, b1], lo, hi, [1], [0.0], [1.0], rb, rb)
+    a = lp.a_vars[0][0]
+    lb, ub = lp.lb.copy(), lp.ub.copy()
+    lb[a] = ub[a] = 0.0                            # inactive: z <= 0 impossible
+    t0, cert0, v0, _ = lp.solve(lb, ub)
+    assert v0 is None and cert0 == -np.inf
+    lb[a] = ub[a] = 1.0
+    t1, cert1, v1, _ = lp.solve(lb, ub)
+    assert v1 is not None and np.isfinite(cert1)
