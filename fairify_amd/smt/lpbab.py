@@ -165,7 +165,6 @@ class _LP:
         inf = hc.kHighsInf
         h = hc._Highs()
         h.setOptionValue("output_flag", False)
-        h.setOptionValue("threads", 1)
         lp = hc.HighsLp()
         lp.num_col_ = A.shape[1]
         lp.num_row_ = A.shape[0]

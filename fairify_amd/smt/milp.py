@@ -306,9 +306,44 @@ def layer_bounds_rows(be, lo: np.ndarray, hi: np.ndarray, q, values: np.ndarray,
     dev = be.device
     res = be.bounds(torch.from_numpy(rlo.reshape(P * V, n)).to(dev), torch.from_numpy(rhi.reshape(P * V, n)).to(dev),
                     mode="symbolic", keep_layers=True)
-    lbs = [t.float().cpu().numpy().reshape(P, V, -1).astype(np.float64) for t in res.layer_lb]
-    ubs = [t.float().cpu().numpy().reshape(P, V, -1).astype(np.float64) for t in res.layer_ub]
-    return lbs, ubs
+    # every layer's [lb | ub] rows packed on the device, ONE async copy into pinned host memory on a
+    # side stream (the north star's pinned hipMemcpyAsync feed of the host solver) instead of 2L
+    # blocking .cpu() copies
+    parts = [t.float() for t in res.layer_lb] + [t.float() for t in res.layer_ub]
+    packed = torch.cat(parts, dim=1)
+    if packed.device.type == "cuda":
+        host = torch.empty(packed.shape, dtype=torch.float32, pin_memory=True)
+        side = _side_stream(packed.device)
+        side.wait_stream(torch.cuda.current_stream(packed.device))
+        with torch.cuda.stream(side):
+            host.copy_(packed, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        packed.record_stream(side)
+        ev.synchronize()
+        hp = host.numpy()
+    else:
+        hp = packed.numpy()
+    widths = [t.shape[1] for t in parts]
+    offs = np.concatenate([[0], np.cumsum(widths)])
+    cols = [hp[:, offs[i]:offs[i + 1]].reshape(P, V, -1).astype(np.float64) for i in range(len(parts))]
+    L = len(res.layer_lb)
+    return cols[:L], cols[L:]
+
+
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """One side stream per (device, host thread) for the bounds copy to the host solver."""
+    import threading
+
+    import torch
+
+    k = (dev.index or 0, threading.get_ident())
+    if k not in _SIDE:
+        _SIDE[k] = torch.cuda.Stream(dev)
+    return _SIDE[k]
 
 
 def submit(be, mlp, q, lo: np.ndarray, hi: np.ndarray, values: np.ndarray, pairs: np.ndarray, time_limit: float,

@@ -154,3 +154,23 @@ def test_lp_infeasible_node_needs_a_certificate():
     lb[a] = ub[a] = 1.0
     t1, cert1, v1, _ = lp.solve(lb, ub)
     assert v1 is not None and np.isfinite(cert1)
+
+
+def test_lp_model_runs_after_other_highs_users():
+    """HiGHS keeps a process-global thread scheduler: a model configured with its own thread
+    count after SciPy's MILP / linprog had started it failed every solve (every node stayed open).
+    The LP stage's models must keep working in a process where other HiGHS users ran first."""
+    from scipy.optimize import LinearConstraint, milp
+
+    from fairify_amd.smt import lpbab
+
+    milp(c=np.array([1.0, 1.0]), constraints=LinearConstraint(np.array([[1.0, 2.0]]), 1.0, np.inf),
+         integrality=np.array([1, 1]))
+    W0 = np.array([[1.0], [0.0]])
+    b0 = np.array([0.5])
+    W1 = np.array([[1.0]])
+    b1 = np.array([-1.0])
+    rb = ([np.array([0.5])], [np.array([3.5])])
+    lp = lpbab._LP([W0, W1], [b0, b1], np.array([0.0, 0.0]), np.array([3.0, 1.0]), [1], [0.0], [1.0], rb, rb)
+    t, cert, v, basis = lp.solve(lp.lb, lp.ub)
+    assert v is not None and np.isfinite(cert) and basis is not None
