@@ -100,6 +100,13 @@ class VerifyConfig:
     relu_escalate_cap: int = 0           # networks the relu stage runs on: cap the input-split
                                          # escalation budget at this (their residue goes to the cheaper
                                          # relu stage instead of deep input splitting; 0 = no cap)
+    relu_first: bool = True              # relu-covered networks: the (capped) input-split escalation
+                                         # runs AFTER the relu stage, on what it left, instead of inline
+                                         # in the first pass -- most of their escalated partitions are
+                                         # zero-logit boxes the relu stage closes in a few nodes
+                                         # (profiles/r3/shard/diag_models_bench_config.jsonl: 38 % of a
+                                         # bench step's nodes were AC-8 / AC-12 escalation spent on
+                                         # partitions the relu stage then decided)
     lp_budget: int = 4096                # verified-LP branch-and-bound (stage "lp", smt/lpbab.py) in
                                          # place of the untrusted MILP: LP nodes per partition (x growth
                                          # per anytime round); 0 = the round-2 MILP stage
@@ -393,10 +400,14 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         cap = max(cfg.relu_escalate_cap, cfg.node_budget)
         cfg = replace(cfg, escalate_budget=cap if cap > cfg.node_budget else 0,
                       escalate_probation=tuple(st for st in cfg.escalate_probation if st[0] < cap))
+    # relu_first: the escalation pass (one budget, open-frontier gate) runs after stage 3r
+    esc_after_relu = relu_on and cfg.relu_first and cfg.escalate_budget > cfg.node_budget and \
+        os.environ.get("FAIRIFY_RELU_FIRST", "1") != "0"
     # inline escalation (native runtime): the first escalation stage runs inside the first pass --
     # partitions that reach node_budget with a small frontier continue instead of restarting from
     # the root in a second solve (FAIRIFY_INLINE_ESCALATE=0: the two-pass schedule)
     inline = (be.hip and cfg.inline_escalate and cfg.escalate_budget > cfg.node_budget and cfg.escalate_max_open > 0
+              and not esc_after_relu
               and os.environ.get("FAIRIFY_INLINE_ESCALATE", "1") != "0" and os.environ.get("FAIRIFY_TORCH_BAB") != "1")
     solver = BaBSolver(be, q, BaBConfig(node_budget=cfg.node_budget, batch_nodes=cfg.batch_nodes,
                                         time_budget=budget,
@@ -450,41 +461,47 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
 
     # ---------------- stage 3b: escalated sound BaB passes on what is still UNKNOWN (the cheap
     # first pass decides the bulk; only residue partitions whose open frontier stayed small -- the
-    # ones a deeper search can still close -- pay for the deep budgets)
+    # ones a deeper search can still close -- pay for the deep budgets).  relu_first: after 3r.
     stages = []
     if cfg.escalate_budget > cfg.node_budget and not inline:
         stages.append((cfg.escalate_budget, cfg.escalate_max_open))
     stages += [tuple(st) for st in cfg.escalate_stages]
     prev_budget = cfg.escalate_budget if inline else cfg.node_budget
-    for e_budget, e_open in stages:
-        if e_budget <= prev_budget:
-            continue
-        prev_budget = e_budget
-        want = (status == UNKNOWN) & ~forced
-        if e_open > 0 and open_left is not None:
-            want &= open_left <= e_open
-        unk = np.nonzero(want)[0]
-        if not unk.size:
-            continue
-        t0 = time.time()
-        el = time.time() - t_start
-        esolver = BaBSolver(be, q, BaBConfig(node_budget=e_budget, batch_nodes=cfg.batch_nodes,
-                                             time_budget=max(0.0, budget - el)), timer=tm)
-        with tm("bab.escalate"):
-            eres = esolver.solve(lo_np[unk], hi_np[unk], mlp)
-        dec_e = np.isin(eres.status, (SAT, UNSAT))
-        hit = unk[dec_e]
-        status[hit] = eres.status[dec_e]
-        stage[hit] = "bab"
-        es = eres.status == SAT
-        cex_x[unk[es]] = eres.cex_x[es]
-        cex_xp[unk[es]] = eres.cex_xp[es]
-        nodes[unk] += eres.nodes
-        if open_left is not None and eres.open_left is not None:
-            open_left = open_left.copy()
-            open_left[unk] = eres.open_left
-        sync()
-        t_bab += time.time() - t0
+
+    def escalate():
+        nonlocal prev_budget, open_left, t_bab
+        for e_budget, e_open in stages:
+            if e_budget <= prev_budget:
+                continue
+            prev_budget = e_budget
+            want = (status == UNKNOWN) & ~forced
+            if e_open > 0 and open_left is not None:
+                want &= open_left <= e_open
+            unk = np.nonzero(want)[0]
+            if not unk.size:
+                continue
+            t0 = time.time()
+            el = time.time() - t_start
+            esolver = BaBSolver(be, q, BaBConfig(node_budget=e_budget, batch_nodes=cfg.batch_nodes,
+                                                 time_budget=max(0.0, budget - el)), timer=tm)
+            with tm("bab.escalate"):
+                eres = esolver.solve(lo_np[unk], hi_np[unk], mlp)
+            dec_e = np.isin(eres.status, (SAT, UNSAT))
+            hit = unk[dec_e]
+            status[hit] = eres.status[dec_e]
+            stage[hit] = "bab"
+            es = eres.status == SAT
+            cex_x[unk[es]] = eres.cex_x[es]
+            cex_xp[unk[es]] = eres.cex_xp[es]
+            nodes[unk] += eres.nodes
+            if open_left is not None and eres.open_left is not None:
+                open_left = open_left.copy()
+                open_left[unk] = eres.open_left
+            sync()
+            t_bab += time.time() - t0
+
+    if not esc_after_relu:
+        escalate()
 
     # ---------------- stage 3r: ReLU-phase branch-and-bound on the residue (rigorous GPU bounds
     # with neuron-phase splits: the exact-zero partitions input splitting cannot close)
@@ -509,6 +526,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             nodes[unk] += rres.nodes
             sync()
             t_bab += time.time() - t0
+    if esc_after_relu:
+        escalate()
 
     # ---------------- stage 3c: exact host solver on the residue (the reference's Z3 check,
     # src/AC/Verify-AC.py:145-158): Z3 when installed, else the HiGHS MILP back-end fed the
