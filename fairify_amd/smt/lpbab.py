@@ -52,7 +52,10 @@ class _LP:
     """Two-copy LP of one ordered PA pair with exact data.  Variables: [one | x (n0) | PA dims of
     x' | per copy and layer: h (w_l), a (unstable) | t]; rows two-sided (lo <= A v <= hi)."""
 
-    def __init__(self, weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b):
+    def __init__(self, weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, sign: int = 0):
+        """``sign`` = 0: the pair LP (maximise t, t <= -N(x, va), t <= N(x', vb)); ``sign`` = -1 / +1:
+        ONE copy, maximise t with t <= -N(x, va) / t <= N(x, va) (a certified t <= 0 proves that
+        no point of the box has N(x, va) < 0 / > 0)."""
         self.nv = 0
         self.lb: List[float] = []
         self.ub: List[float] = []
@@ -92,7 +95,8 @@ class _LP:
         self.a_vars: List[Tuple[int, int, int, int, int]] = []   # (a var, h var, copy, layer, neuron)
         self.z_rows = []                                       # (copy, layer, neuron) -> (h, prev, W col, b)
         outs = []
-        for cp, (xin, (lbs, ubs)) in enumerate(((self.x, bounds_a), (xb, bounds_b))):
+        copies = ((self.x, bounds_a),) if sign else ((self.x, bounds_a), (xb, bounds_b))
+        for cp, (xin, (lbs, ubs)) in enumerate(copies):
             prev = xin
             L = len(weights)
             for l in range(L - 1):
@@ -123,13 +127,17 @@ class _LP:
             outs.append((prev, np.asarray(weights[-1], np.float64)[:, 0], float(np.asarray(biases[-1])[0])))
         # bound on |t|: valid because t <= N(x', v') <= its output bound, and any lower bound below
         # min(-N, N') keeps every feasible point (t is maximised)
+        if sign:
+            outs.append(outs[0])
         (pa_h, wa, ba), (pb_h, wb, bb) = outs
         M = 1.0 + abs(ba) + abs(bb) + float(np.abs(wa) @ np.maximum(np.asarray(self.ub)[pa_h], 0)) \
             + float(np.abs(wb) @ np.maximum(np.asarray(self.ub)[pb_h], 0))
         M = float(np.nextafter(2.0 * M, np.inf))
         self.t = var([-M], [M])[0]
-        row(np.concatenate([[self.t], pa_h, [self.one]]), np.concatenate([[1.0], wa, [ba]]), -np.inf, 0.0)
-        row(np.concatenate([[self.t], pb_h, [self.one]]), np.concatenate([[1.0], -wb, [-bb]]), -np.inf, 0.0)
+        if sign <= 0:    # t <= -N(x, va)
+            row(np.concatenate([[self.t], pa_h, [self.one]]), np.concatenate([[1.0], wa, [ba]]), -np.inf, 0.0)
+        if sign >= 0:    # t <= N(x', vb)  (sign mode: N(x, va))
+            row(np.concatenate([[self.t], pb_h, [self.one]]), np.concatenate([[1.0], -wb, [-bb]]), -np.inf, 0.0)
         from scipy.sparse import coo_matrix
 
         self.A = coo_matrix((np.concatenate(rv), (np.concatenate(ri), np.concatenate(rj))),
@@ -322,14 +330,11 @@ def certified_bound_rows(d, A, rlo, rhi, lam, lb, ub) -> float:
     return float(np.nextafter(bound, np.inf)) if math.isfinite(bound) else math.inf
 
 
-def lp_bab_pair(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, node_budget: int, deadline: float,
-                confirm) -> Tuple[str, Optional[tuple], int]:
-    """LP branch-and-bound of one ordered PA pair (v, v'): ('unsat', None, nodes) when every node
-    closed, ('sat', (x, x'), nodes) with an exactly confirmed pair (``confirm(x, x') -> bool``),
-    ('unknown', None, nodes) at the node budget / deadline."""
-    lp = _LP(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b)
-    pa = list(pa_idx)
-    vb_i = np.asarray(vb, np.int64)
+def _lp_bab(lp: "_LP", pa, va, node_budget: int, deadline: float, hit) -> Tuple[str, Optional[np.ndarray], int]:
+    """Best-first LP branch-and-bound over ``lp``: ('closed', None, nodes) when every node closed,
+    ('hit', x, nodes) when ``hit(x)`` (integer x, PA dims = va) accepted a lattice point (a leaf,
+    or the rounded LP optimum of a node whose LP value is > 0), ('unknown', None, nodes) at the node
+    budget / deadline."""
     isx = np.ones(lp.n0, bool)
     isx[pa] = False
     tried = set()
@@ -339,9 +344,7 @@ def lp_bab_pair(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, nod
         if key in tried:
             return False
         tried.add(key)
-        xps = xs.copy()
-        xps[pa] = vb_i
-        return bool(confirm(xs, xps))
+        return bool(hit(xs))
 
     heap = [(0.0, 0, lp.lb.copy(), lp.ub.copy(), None)]   # best-first on the certified bound;
     # each entry carries its parent's simplex basis (a child differs by one bound: ~1 pivot)
@@ -353,15 +356,12 @@ def lp_bab_pair(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, nod
         _, _, nlb, nub, pbasis = heapq.heappop(heap)
         nodes += 1
         xl, xh = nlb[lp.x], nub[lp.x]
-        point = bool(np.all(xl[isx] == xh[isx]))
-        if point:
+        if bool(np.all(xl[isx] == xh[isx])):
             # a single lattice point: decided exactly (the LP's rounding slack cannot close an
             # exactly-zero logit, the exact checker can)
             xs = xl.astype(np.int64)
-            xps = xs.copy()
-            xps[pa] = vb_i
-            if confirm(xs, xps):
-                return "sat", (xs.tolist(), xps.tolist()), nodes
+            if check(xs):
+                return "hit", xs, nodes
             continue
         t_lp, cert, v, basis = lp.solve(nlb, nub, pbasis)
         if cert <= 0.0:
@@ -369,9 +369,7 @@ def lp_bab_pair(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, nod
         if t_lp is not None and t_lp > 0:
             xs = np.clip(np.rint(v[lp.x]), xl, xh).astype(np.int64)
             if check(xs):
-                xps = xs.copy()
-                xps[pa] = vb_i
-                return "sat", (xs.tolist(), xps.tolist()), nodes
+                return "hit", xs, nodes
         # branch: the unfixed binary whose relaxation the LP optimum exploits most
         best, bi = 0.0, -1
         for i, (a, h, cp, l, j) in enumerate(lp.a_vars if v is not None else ()):
@@ -401,16 +399,67 @@ def lp_bab_pair(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, nod
         for clb, cub in children:
             heapq.heappush(heap, (-cert, tick, clb, cub, basis))
             tick += 1
-    return "unsat", None, nodes
+    return "closed", None, nodes
+
+
+def lp_bab_pair(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, node_budget: int, deadline: float,
+                confirm) -> Tuple[str, Optional[tuple], int]:
+    """LP branch-and-bound of one ordered PA pair (v, v'): ('unsat', None, nodes) when every node
+    closed, ('sat', (x, x'), nodes) with an exactly confirmed pair (``confirm(x, x') -> bool``),
+    ('unknown', None, nodes) at the node budget / deadline."""
+    lp = _LP(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b)
+    pa = list(pa_idx)
+    vb_i = np.asarray(vb, np.int64)
+
+    def hit(xs):
+        xps = xs.copy()
+        xps[pa] = vb_i
+        return confirm(xs, xps)
+
+    st, xs, nodes = _lp_bab(lp, pa, va, node_budget, deadline, hit)
+    if st == "hit":
+        xps = xs.copy()
+        xps[pa] = vb_i
+        return "sat", (xs.tolist(), xps.tolist()), nodes
+    return ("unsat" if st == "closed" else "unknown"), None, nodes
+
+
+def lp_sign_free(weights, biases, lo, hi, pa_idx, va, bounds_a, sign: int, node_budget: int, deadline: float,
+                 exact_sign) -> Tuple[bool, int]:
+    """Single-copy LP branch-and-bound: True when no lattice point of the box (PA dims = va) has
+    sign(N(x, va)) == ``sign`` (-1 / +1) -- certified by the same weak-duality bounds, leaves by
+    ``exact_sign(x) -> -1 / 0 / +1``."""
+    lp = _LP(weights, biases, lo, hi, pa_idx, va, va, bounds_a, bounds_a, sign=sign)
+    st, _, nodes = _lp_bab(lp, list(pa_idx), va, node_budget, deadline, lambda xs: exact_sign(xs) == sign)
+    return st == "closed", nodes
 
 
 def solve_partition(weights, biases, lo, hi, pa_idx, values, pairs, row_bounds, node_budget: int,
-                    time_limit: float, confirm) -> Tuple[str, Optional[tuple], int]:
+                    time_limit: float, confirm, exact_sign=None) -> Tuple[str, Optional[tuple], int]:
     """Decide one partition over all ordered PA pairs: 'unsat' (every pair's LP-BaB closed),
-    'sat' with an exactly confirmed pair (``confirm(x, x') -> bool``), else 'unknown'."""
+    'sat' with an exactly confirmed pair (``confirm(x, x') -> bool``), else 'unknown'.
+
+    With more than two ordered pairs (a PA of 3+ values: race has 5, i.e. 20 pairs) and
+    ``exact_sign(x) -> -1/0/+1`` given, each value first gets two single-copy sign tests: a value
+    v whose logit is certainly never < 0 on the box closes every pair (v, .), one whose logit is
+    never > 0 closes every pair (., v) -- 2V half-size searches shared by V(V-1) pairs."""
     deadline = time.time() + time_limit
     nodes = 0
+    never_neg, never_pos = {}, {}
+    if exact_sign is not None and len(pairs) > 2:
+        vals = sorted({int(v) for pr in pairs for v in pr})
+        sb = max(16, node_budget // (8 * len(vals)))
+        for v in vals:
+            def es(xs, v=v):
+                return exact_sign(xs)
+            never_neg[v], n1 = lp_sign_free(weights, biases, lo, hi, pa_idx, values[v], row_bounds[v], -1, sb,
+                                            deadline, es)
+            never_pos[v], n2 = lp_sign_free(weights, biases, lo, hi, pa_idx, values[v], row_bounds[v], +1, sb,
+                                            deadline, es)
+            nodes += n1 + n2
     for vi, vj in pairs:
+        if never_neg.get(int(vi)) or never_pos.get(int(vj)):
+            continue                        # N(x, vi) < 0 < N(x', vj) impossible
         st, wit, n = lp_bab_pair(weights, biases, lo, hi, pa_idx, values[int(vi)], values[int(vj)],
                                  row_bounds[int(vi)], row_bounds[int(vj)], max(1, node_budget - nodes), deadline,
                                  confirm)
@@ -453,7 +502,11 @@ def _partition_task(mlp, lo, hi, pa_idx, ra_idx, tau, values, pairs, rb, node_bu
         ok = exact.check_pair_constraints(xs[None], xps[None], lo[None], hi[None], pa_idx, ra_idx, tau)
         return bool(ok[0] and exact.is_violation(mlp, xs[None], xps[None])[0])
 
-    return solve_partition(mlp.weights, mlp.biases, lo, hi, pa_idx, values, pairs, rb, node_budget, limit, confirm)
+    def exact_sign(xs):
+        return int(exact.exact_signs(mlp, xs[None])[0])
+
+    return solve_partition(mlp.weights, mlp.biases, lo, hi, pa_idx, values, pairs, rb, node_budget, limit, confirm,
+                           exact_sign)
 
 
 def submit(be, mlp, q, lo: np.ndarray, hi: np.ndarray, values: np.ndarray, pairs: np.ndarray, node_budget: int,

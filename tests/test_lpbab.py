@@ -174,3 +174,42 @@ def test_lp_model_runs_after_other_highs_users():
     lp = lpbab._LP([W0, W1], [b0, b1], np.array([0.0, 0.0]), np.array([3.0, 1.0]), [1], [0.0], [1.0], rb, rb)
     t, cert, v, basis = lp.solve(lp.lb, lp.ub)
     assert v is not None and np.isfinite(cert) and basis is not None
+
+
+@pytest.mark.parametrize("seed", [7, 8])
+def test_lpbab_multivalued_pa_with_sign_pretests(seed):
+    """Race (5 values, 20 ordered pairs): the per-value single-copy sign tests that close whole
+    rows / columns of the pair table keep the verdicts equal to brute force."""
+    from fairify_amd.engine.bab import _pa_table
+    from fairify_amd.smt import lpbab
+
+    pre = presets.get("src/AC-race")
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, 0)[:10]
+    lo, hi = grid.decode(ids)
+    pa = q.pa_idx[0]
+    hi_full = hi.copy()
+    hi = np.minimum(hi, lo + 1)
+    hi[:, pa] = hi_full[:, pa]                     # all 5 race values, <= 2 values elsewhere
+    m = random_mlp(13, [6, 5], seed=seed, bias_scale=0.5)
+    values, pairs = _pa_table(q, lo[:1], hi[:1])
+    assert len(pairs) > 2
+    for k in range(len(ids)):
+        rb = _row_bounds(m, lo[k], hi[k], q, values)
+
+        def confirm(xs, xps):
+            ok = exact.check_pair_constraints(xs[None], xps[None], lo[k:k + 1], hi[k:k + 1], q.pa_idx, q.ra_idx, q.tau)
+            return bool(ok[0] and exact.is_violation(m, xs[None], xps[None])[0])
+
+        def exact_sign(xs):
+            return int(exact.exact_signs(m, xs[None])[0])
+
+        st, wit, nodes = lpbab.solve_partition(m.weights, m.biases, lo[k], hi[k], q.pa_idx, values, pairs, rb,
+                                               4096, 60.0, confirm, exact_sign)
+        pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[k], hi[k])])))
+        zs = [m.logits(np.where(np.arange(m.n_in) == pa, values[v][0], pts)) for v in range(len(values))]
+        truth = any(((zs[i] < 0) & (zs[j] > 0)).any() for i, j in pairs)
+        assert st != "unknown", k
+        assert (st == "sat") == truth, k
+        if st == "sat":
+            assert exact.is_violation(m, np.asarray(wit[0])[None], np.asarray(wit[1])[None])[0]
