@@ -546,9 +546,10 @@ def main() -> None:
             "decided": int(btot[1]), "sat": int(btot[2 + len(STAGES)]), "unsat": int(btot[3 + len(STAGES)]),
             "unsat_by_stage": {name: int(btot[2 + i]) for i, name in enumerate(STAGES) if btot[2 + i]},
             "sat_by_stage": {k: v for k, v in b_sat.items() if v},
-            "note": "untimed; anytime mode: BaB budgets x4 per round, falsifier rounds, HiGHS MILP rounds "
-                    "(a MILP 'unsat' is a floating-point dual bound: recorded, partition left UNKNOWN), "
-                    "heuristic retry last; pct_verified_at_budget_sound excludes heuristic verdicts"}
+            "note": "untimed; anytime mode: falsifier rounds, input-split BaB budgets x4 per round, "
+                    "ReLU-phase BaB, verified-LP rounds (stage 'lp': UNSAT from certified weak-duality "
+                    "bounds; --lp-budget 0 --trust-milp: HiGHS MILP instead), heuristic retry last; "
+                    "pct_verified_at_budget_sound excludes heuristic (and trusted-MILP) verdicts"}
     if args.profile and info.is_main:
         print(timer.report(), file=sys.stderr, flush=True)
     if info.is_main:
