@@ -45,13 +45,20 @@ __device__ void fa_tile_forward(const NetDesc& net, const float* __restrict__ fl
       const int kq = lane >> 4;
       const int j = nt * 16 + (lane & 15);
       const bool jval = j < n_out;
-      const float* arow = bufA + m * S;
+      const float* arow = bufA + m * S + kq;
+      // columns j >= n_out read a valid column instead of a select per step (their accumulators
+      // are never stored); full 4-wide K steps need no k < n_in test (same MFMA order and operands
+      // as the predicated loop: bitwise the same logits and counts), only the tail keeps it
+      const float* wcol = W + (size_t)kq * n_out + (jval ? j : n_out - 1);
+      const int kfull = n_in & ~3;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int k0 = 0; k0 < n_in; k0 += 4) {
-        const int k = k0 + kq;
-        const bool kv = k < n_in;
-        const float av = kv ? arow[k] : 0.f;
-        const float wv = (kv && jval) ? W[k * n_out + j] : 0.f;
+#pragma unroll 4
+      for (int k0 = 0; k0 < kfull; k0 += 4)
+        acc = fa_mfma4(arow[k0], wcol[(size_t)k0 * n_out], acc);
+      if (kfull < n_in) {
+        const bool kv = kfull + kq < n_in;
+        const float av = kv ? arow[kfull] : 0.f;
+        const float wv = kv ? wcol[(size_t)kfull * n_out] : 0.f;
         acc = fa_mfma4(av, wv, acc);
       }
       const float b = jval ? bias[j] : 0.f;
