@@ -327,8 +327,7 @@ extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t 
   args.wstride = ws;
   args.wfloats = wf;
   if (bytes > 64 * 1024)
-    FA_CHECK(hipFuncSetAttribute((const void*)fa_bounds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)bytes));
+    FA_CHECK(fa_raise_lds_once((const void*)fa_bounds_kernel, bytes));
   dim3 grid((args.R + G - 1) / G);
   hipLaunchKernelGGL(fa_bounds_kernel, grid, dim3(FA_THREADS), bytes, stream, net, args);
   return (int)hipGetLastError();

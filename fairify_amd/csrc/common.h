@@ -6,6 +6,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #define FA_MAX_LAYERS 16
 #define FA_THREADS 256
 
@@ -72,3 +76,17 @@ __device__ __forceinline__ f32x4 fa_mfma4(float a, float b, f32x4 c) {
       abort();                                                                   \
     }                                                                            \
   } while (0)
+
+// Raise a kernel's dynamic-LDS limit to `bytes` once per (kernel, bytes), under a lock: the host
+// threads launch concurrently and change no attribute while other threads launch that kernel.
+// Returns the hipFuncSetAttribute error of the first call (hipSuccess afterwards).
+inline hipError_t fa_raise_lds_once(const void* k, size_t bytes) {
+  if (bytes <= 64 * 1024) return hipSuccess;
+  static std::mutex mu;
+  static std::set<std::pair<const void*, size_t>> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count(std::make_pair(k, bytes))) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) done.insert(std::make_pair(k, bytes));
+  return e;
+}

@@ -424,8 +424,8 @@ extern "C" int fa_falsify_launch(const NetDesc& net, FalsifyArgs a, hipStream_t 
   const FalsifyLds L = fa_falsify_lds(a, net.dims[0], cfg.floats);
   const size_t bytes = (size_t)L.floats * sizeof(float);
   if (bytes > 160 * 1024) return 0;
-  if (bytes > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  {
+    const hipError_t e = fa_raise_lds_once((const void*)k, bytes);
     if (e != hipSuccess) return -(int)e;
   }
   hipLaunchKernelGGL(k, dim3((unsigned)a.P), dim3(FA_THREADS), bytes, stream, net, a, cfg);

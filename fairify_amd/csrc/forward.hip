@@ -19,6 +19,9 @@
 // accumulator epilogue (counts reduced across the 4 row-groups of a wave with shuffles, one LDS
 // atomic per column per tile).
 #include "args.h"
+#include "regfwd.h"
+
+#include <stdlib.h>
 
 #define FA_TR 64
 
@@ -114,8 +117,7 @@ extern "C" int fa_forward_launch(const NetDesc& net, FwdArgs a, hipStream_t stre
   a.S = net.max_width | 1;
   size_t bytes = (2 * (size_t)FA_TR * a.S + FA_TR) * sizeof(float);
   if (bytes > 64 * 1024)
-    FA_CHECK(hipFuncSetAttribute((const void*)fa_forward_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)bytes));
+    FA_CHECK(fa_raise_lds_once((const void*)fa_forward_kernel, bytes));
   hipLaunchKernelGGL(fa_forward_kernel, dim3((a.B + FA_TR - 1) / FA_TR), dim3(FA_THREADS), bytes, stream, net, a);
   return (int)hipGetLastError();
 }
@@ -265,18 +267,194 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_finalize_kernel(NetDesc net
     fa_sim_witness(a, n0, p, a.pids[p], key, a.lo + (size_t)p * n0, a.hi + (size_t)p * n0);
 }
 
+// ------------------------------------------------------------------------------------------
+// Register-resident simulation (PA-only queries): the same samples (fa_sample_coord), PA passes,
+// activation counts (at the sampled PA tuple) and first-flip keys as fa_sim_kernel, with 16
+// samples per wave as the MFMA columns (csrc/regfwd.h): W staged once per workgroup in MFMA
+// operand order, activations never leave registers, counts from one ballot per (tile, register)
+// and layer (the 16 lanes of a lane group hold one neuron of the 16 samples).  The K grouping of
+// the MFMA sums differs from the 64-row tile forward, so a logit within fp32 rounding of 0 may
+// flip differently (counts stay within the rounding margins of tests/test_kernels_gpu.py).
+
+// One layer with activation counting: H -> H2 (ReLU outputs); counts neuron j for the samples
+// whose lanes have `match` (the sampled PA tuple is this pass's values[v]); last layer: the logit
+// of sample lane&15 in lanes 0..15, counted when nonzero.
+template <int TM>
+__device__ __forceinline__ float fa_reg_layer_count(const NetDesc& net, const RegNetCfg& cfg, const float* sw_all,
+                                                    int l, int lane, const float (&H)[TM][4], float (&H2)[TM][4],
+                                                    bool match, int* cnt) {
+  const int grp = lane >> 4, col = lane & 15;
+  const int n_in = net.dims[l], n_out = net.dims[l + 1];
+  const int tin = (n_in + 15) >> 4, tout = (n_out + 15) >> 4;
+  const float4* sw = reinterpret_cast<const float4*>(sw_all + cfg.w_lds[l]);
+  const float* sb = sw_all + cfg.b_lds[l];
+  const bool last = l == net.n_layers - 1;
+  const int noff = net.neuron_off[l];
+  float logit = 0.f;
+#pragma unroll
+  for (int jt = 0; jt < TM; ++jt) {
+    if (jt >= tout) break;
+    f32x4 Z = {0.f, 0.f, 0.f, 0.f};
+    const float4* wq = sw + (size_t)jt * tin * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      if (t >= tin) break;
+      const float4 w4 = wq[t * 64];
+      Z = fa_mfma4(w4.x, H[t][0], Z);
+      Z = fa_mfma4(w4.y, H[t][1], Z);
+      Z = fa_mfma4(w4.z, H[t][2], Z);
+      Z = fa_mfma4(w4.w, H[t][3], Z);
+    }
+    if (last) {
+      if (jt == 0) {
+        logit = Z[0] + sb[0];
+        const unsigned long long bm = __ballot(match && grp == 0 && logit != 0.f);
+        if (lane == 0 && bm) atomicAdd(&cnt[noff], __popcll(bm));
+      }
+      continue;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = 16 * jt + 4 * grp + i;
+      const float h = j >= n_out ? 0.f : fmaxf(Z[i] + sb[j], 0.f);
+      H2[jt][i] = h;
+      const unsigned long long bm = __ballot(match && h != 0.f);
+      const int c = __popcll((bm >> (16 * grp)) & 0xFFFFull);
+      if (col == 0 && c) atomicAdd(&cnt[noff + j], c);
+    }
+  }
+  return logit;
+}
+
+template <int TM>
+__global__ void __launch_bounds__(FA_THREADS) fa_sim_reg_kernel(NetDesc net, SimArgs a, RegNetCfg cfg) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 15, grp = lane >> 4;
+  const int n0 = net.dims[0];
+  const int G = a.split;
+  const int p = blockIdx.x / G;
+  const int g = blockIdx.x - p * G;
+  const int V = a.V;
+  const int64_t pid = a.pids[p];
+  float* zs = smem + cfg.floats;              // [64][V] logits of this pass's samples
+  float* s_lo = zs + 64 * V;
+  float* s_hi = s_lo + n0;
+  int* cnt = (int*)(s_hi + n0);               // [n_neurons]
+  int* best = cnt + net.n_neurons;
+  fa_stage_wperm(net, a.flat, smem, tid, FA_THREADS);
+  for (int i = tid; i < n0; i += FA_THREADS) {
+    s_lo[i] = a.lo[(size_t)p * n0 + i];
+    s_hi[i] = a.hi[(size_t)p * n0 + i];
+  }
+  for (int i = tid; i < net.n_neurons; i += FA_THREADS) cnt[i] = 0;
+  if (tid == 0) best[0] = 0x7FFFFFFF;
+  __syncthreads();
+  float Xb[TM][4], HA[TM][4], HB[TM][4];
+  for (int s0 = g * FA_TR; s0 < a.n_samples; s0 += G * FA_TR) {
+    const int s = s0 + wave * 16 + col;
+    const bool sv = s < a.n_samples;
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 16 * t + 4 * grp + i;
+        Xb[t][i] = (k < n0 && sv) ? fa_sample_coord(a.seed, pid, s, k, s_lo[k], s_hi[k]) : 0.f;
+      }
+    for (int v = 0; v < V; ++v) {
+      // counts at the sampled point: the pass whose PA tuple equals the sample's
+      bool match = sv;
+      for (int m = 0; m < a.npa; ++m) {
+        const int d = a.pa_idx[m];
+        match = match && fa_sample_coord(a.seed, pid, s, d, s_lo[d], s_hi[d]) == (float)a.values[v * a.npa + m];
+      }
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 16 * t + 4 * grp + i;
+          float x = Xb[t][i];
+          for (int m = 0; m < a.npa; ++m)
+            if (a.pa_idx[m] == k) x = (float)a.values[v * a.npa + m];
+          HA[t][i] = x;
+        }
+      float z = 0.f;
+      for (int l = 0; l < net.n_layers; ++l) {
+        if (l & 1) z = fa_reg_layer_count<TM>(net, cfg, smem, l, lane, HB, HA, match, cnt);
+        else z = fa_reg_layer_count<TM>(net, cfg, smem, l, lane, HA, HB, match, cnt);
+      }
+      if (grp == 0) zs[(wave * 16 + col) * V + v] = z;   // read back by this same lane only
+    }
+    if (grp == 0 && sv) {
+      const float* zr = zs + (wave * 16 + col) * V;
+      if (a.z0) a.z0[(size_t)p * a.n_samples + s] = zr[0];
+      for (int q = 0; q < a.Pp; ++q) {
+        const float zi = zr[(int)a.pairs[2 * q]], zj = zr[(int)a.pairs[2 * q + 1]];
+        if ((zi < 0.f && zj > 0.f) || (zi > 0.f && zj < 0.f)) {
+          atomicMin(best, s * a.Pp + q);
+          break;                                  // the sample's smallest flipping pair
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int key = best[0];
+  if (G > 1) {
+    for (int i = tid; i < net.n_neurons; i += FA_THREADS)
+      if (cnt[i]) atomicAdd(&a.counts[(size_t)p * net.n_neurons + i], cnt[i]);
+    if (tid == 0 && key != 0x7FFFFFFF) atomicMin(&a.keys[p], key);
+    return;
+  }
+  for (int i = tid; i < net.n_neurons; i += FA_THREADS) a.counts[(size_t)p * net.n_neurons + i] = cnt[i];
+  if (tid == 0) a.found[p] = key != 0x7FFFFFFF;
+  if (key != 0x7FFFFFFF) fa_sim_witness(a, n0, p, pid, key, s_lo, s_hi);
+}
+
+namespace {
+typedef void (*SimRegKernel)(NetDesc, SimArgs, RegNetCfg);
+SimRegKernel select_sim_reg(int TM) {
+  if (TM <= 1) return fa_sim_reg_kernel<1>;
+  if (TM <= 2) return fa_sim_reg_kernel<2>;
+  if (TM <= 4) return fa_sim_reg_kernel<4>;
+  if (TM <= 7) return fa_sim_reg_kernel<7>;
+  return nullptr;
+}
+// A/B switch (FAIRIFY_SIM_REG=0: the 64-row LDS tile kernel for every query)
+bool sim_reg_on() {
+  static const bool v = [] {
+    const char* e = getenv("FAIRIFY_SIM_REG");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+}  // namespace
+
 extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) {
   if (a.P <= 0) return 0;
   if (a.npa > FA_MAX_PA || a.nra > FA_MAX_RA) return -3;
   if ((long long)a.n_samples * a.Pp >= 0x7FFFFFFFLL) return -3;   // flip keys sample * Pp + pair are int
   a.S = net.max_width | 1;
   const int n0 = net.dims[0];
+  if (a.nra == 0 && sim_reg_on()) {
+    const SimRegKernel k = select_sim_reg(fa_regnet_tm(net));
+    RegNetCfg cfg{};
+    if (k && fa_regnet_cfg(net, cfg)) {
+      size_t rb = ((size_t)cfg.floats + 64 * (size_t)a.V + 2 * n0) * sizeof(float) + (net.n_neurons + 4) * sizeof(int);
+      rb = (rb + 15) & ~(size_t)15;
+      const int tiles = (a.n_samples + FA_TR - 1) / FA_TR;
+      if (rb <= 160 * 1024 && a.split >= 1 && (a.split == 1 || (a.keys && a.split <= tiles))) {
+        FA_CHECK(fa_raise_lds_once((const void*)k, rb));
+        hipLaunchKernelGGL(k, dim3((unsigned)a.P * (unsigned)a.split), dim3(FA_THREADS), rb, stream, net, a, cfg);
+        if (a.split > 1) hipLaunchKernelGGL(fa_sim_finalize_kernel, dim3(a.P), dim3(FA_THREADS), 0, stream, net, a);
+        return (int)hipGetLastError();
+      }
+    }
+  }
   size_t floats = 2 * (size_t)FA_TR * a.S + (size_t)FA_TR * n0 + 2 * (size_t)FA_TR * a.V + FA_TR + 2 * n0;
   size_t bytes = floats * sizeof(float) + (net.n_neurons + 4) * sizeof(int) + FA_TR;
   bytes = (bytes + 15) & ~(size_t)15;
   if (bytes > 160 * 1024) return -1;
   if (bytes > 64 * 1024)
-    FA_CHECK(hipFuncSetAttribute((const void*)fa_sim_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    FA_CHECK(fa_raise_lds_once((const void*)fa_sim_kernel, bytes));
   const int tiles = (a.n_samples + FA_TR - 1) / FA_TR;
   if (a.split < 1 || (a.split > 1 && (!a.keys || a.split > tiles))) return -2;
   hipLaunchKernelGGL(fa_sim_kernel, dim3((unsigned)a.P * (unsigned)a.split), dim3(FA_THREADS), bytes, stream, net, a);
@@ -416,8 +594,7 @@ extern "C" int fa_ascent_launch(const NetDesc& net, AscentArgs a, hipStream_t st
   bytes = (bytes + 15) & ~(size_t)15;
   if (bytes > 160 * 1024) return -1;
   if (bytes > 64 * 1024)
-    FA_CHECK(hipFuncSetAttribute((const void*)fa_ascent_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)bytes));
+    FA_CHECK(fa_raise_lds_once((const void*)fa_ascent_kernel, bytes));
   hipLaunchKernelGGL(fa_ascent_kernel, dim3(a.P), dim3(FA_THREADS), bytes, stream, net, a);
   return (int)hipGetLastError();
 }

@@ -277,8 +277,8 @@ extern "C" int fa_agree_launch(const NetDesc& net, const float* flat, int Pm, co
   if (!fa_regnet_cfg(net, cfg)) return -1;
   const size_t bytes = ((size_t)cfg.floats + 2 * net.dims[0] + 4) * sizeof(float) + net.n_hidden + 16;
   if (bytes > 160 * 1024) return 0;
-  if (bytes > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  {
+    const hipError_t e = fa_raise_lds_once((const void*)k, bytes);
     if (e != hipSuccess) return -(int)e;
   }
   hipLaunchKernelGGL(k, dim3((unsigned)Pm), dim3(FA_THREADS), bytes, stream, net, cfg, flat, Pm, rows, lo, hi, pids, dead, S,
