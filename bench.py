@@ -273,7 +273,11 @@ def main() -> None:
         d = [m.n_in] + m.widths
         return float(sum(d[i] * d[i + 1] for i in range(len(d) - 1)))
 
-    node_w = [1.0 + _macs(m) / 256.0 for m in models]
+    # per-node constant (FAIRIFY_NODE_W_C: A/B override).  A c = 10 fit of the per-model BaB time per
+    # node (narrow nets 5.6-17 ns, AC-4 51 ns) did not balance the 8 emulated ranks better than
+    # c = 1: max/mean 1.040 vs 1.022, max 153.8 vs 154.0 ms (profiles/r3/ab/lpt_node_weight.md)
+    node_c = float(os.environ.get("FAIRIFY_NODE_W_C", "1"))
+    node_w = [node_c + _macs(m) / 256.0 for m in models]
     FIXED_COST = 64.0                      # node-equivalents per partition
     ucost = np.array([len(BL.unit_ids(order, j, U)) * FIXED_COST * node_w[k] for k, j in units], dtype=np.float64)
     assigned_cost = []
