@@ -4,7 +4,7 @@
 Builds N random BaB nodes inside partitions of the preset grid, computes their symbolic row
 bounds once, then times ``Backend.pair_certify`` alone.
 
-    python tools/bench_certify.py --models AC-4,AC-8 --nodes 32768
+    python tools/certbench.py --models AC-4,AC-8 --nodes 32768
 """
 from __future__ import annotations
 
