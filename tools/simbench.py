@@ -4,7 +4,7 @@ partitions of every AC model, one stream, median of --reps timed launches after 
 Prints one JSON line per model plus a checksum of the activation counts / flip keys, so two
 builds can be compared for both speed and bitwise-identical results.
 
-    python tools/bench_sim.py --partitions 8192 --reps 5
+    python tools/simbench.py --partitions 8192 --reps 5
 """
 from __future__ import annotations
 
