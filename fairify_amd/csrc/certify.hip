@@ -156,21 +156,36 @@ __device__ __forceinline__ void fa_pair_eval_one(const CertArgs& a, int n, int q
     const float g1 = g_at(1.f);
     if (g1 < best) { best = g1; bt = 1.f; }
   }
-#pragma unroll 1
-  for (int i = 0; i < n0; ++i) {
-    // runtime loop over breakpoints; the register arrays are read through a select chain
-    float ai = 0.f, bi = 0.f;
-    bool s_i = false;
+  if constexpr (NM <= 16) {
+    // unrolled over the register arrays (no select chain per breakpoint); same breakpoints in the
+    // same order as the runtime loop below, so bitwise the same (gmin, t*)
 #pragma unroll
-    for (int k = 0; k < NM; ++k)
-      if (k == i) { ai = ca[k]; bi = cb[k]; s_i = sh[k]; }
-    if (!s_i) continue;
-    const float den = ai - bi;
-    if (den == 0.f) continue;
-    const float t = -bi / den;
-    if (!(t > 0.f && t < 1.f)) continue;
-    const float g = g_at(t);
-    if (g < best) { best = g; bt = t; }
+    for (int i = 0; i < NM; ++i) {
+      if (!sh[i]) continue;                 // uniform: shared flag of dim i (false beyond n0)
+      const float den = ca[i] - cb[i];
+      if (den == 0.f) continue;
+      const float t = -cb[i] / den;
+      if (!(t > 0.f && t < 1.f)) continue;
+      const float g = g_at(t);
+      if (g < best) { best = g; bt = t; }
+    }
+  } else {
+#pragma unroll 1
+    for (int i = 0; i < n0; ++i) {
+      // runtime loop over breakpoints; the register arrays are read through a select chain
+      float ai = 0.f, bi = 0.f;
+      bool s_i = false;
+#pragma unroll
+      for (int k = 0; k < NM; ++k)
+        if (k == i) { ai = ca[k]; bi = cb[k]; s_i = sh[k]; }
+      if (!s_i) continue;
+      const float den = ai - bi;
+      if (den == 0.f) continue;
+      const float t = -bi / den;
+      if (!(t > 0.f && t < 1.f)) continue;
+      const float g = g_at(t);
+      if (g < best) { best = g; bt = t; }
+    }
   }
   gmin = best;
   tstar = bt;
