@@ -44,6 +44,7 @@ extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_
                                 int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open,
                                 EscSteps esc, hipStream_t stream);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
+extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_bab_init_launch(BabInitArgs a, hipStream_t stream);
 extern "C" int fa_bab_finish_launch(int P, const int8_t* status, const int* nodes, const int* open_left, int* out,
                                     hipStream_t stream);
@@ -92,7 +93,7 @@ class BabRuntime {
   BabRuntime(py::handle net, uintptr_t flat, std::vector<int> pa, std::vector<float> values_f,
              std::vector<int64_t> values_i, std::vector<int64_t> pairs, std::vector<int> ra, float tau,
              std::vector<uint8_t> shared, int capacity, int batch_nodes, int cand_cap, double unit, bool crown,
-             int split_target)
+             int split_target, bool refine)
       : net_(fa_net_desc(net)),
         flat_((const float*)flat),
         pa_(std::move(pa)),
@@ -103,6 +104,7 @@ class BabRuntime {
         cand_cap_(cand_cap),
         unit_(unit),
         crown_(crown),
+        refine_(crown && refine),
         split_target_(std::max(2, split_target)) {
     n0_ = net_.dims[0];
     npa_ = (int)pa_.size();
@@ -341,7 +343,7 @@ class BabRuntime {
         sa.cand_buf = cand_buf_.p; sa.cand_count = cnt + 1;
         sa.cand_cap = cand_alloc_;
         ckl(fa_split_launch(sa, st), "split");
-        launches += relaxed_ ? 6 : 5;
+        launches += (relaxed_ ? 6 : 5) + (refine_ ? (relaxed_ ? 2 : 1) : 0);
       }
       ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, nodes_.p, nodes_start_.p, prev_start_.p, cnt,
                            counters_.p + 2 * (slot ^ 1), hcount_, inline_esc ? pbudget_.p : nullptr,
@@ -419,6 +421,13 @@ class BabRuntime {
       b.layer_ub = lay_ub_[slot].p;
     }
     ckl(fa_bounds_launch(net_, b, st), "bounds");
+    // hidden-layer bounds tightened by back-substitution (refine.hip) before the output pass uses
+    // them as relaxation intervals; a network the kernel cannot hold (-1) keeps the forward bounds
+    if (refine_) {
+      const int rc = fa_refine_launch(net_, b, st);
+      if (rc == -1) refine_ = false;
+      else ckl(rc, "refine");
+    }
     // backward output bounds: tighter forms / logit bounds for the certificate.  A network the
     // kernel cannot hold (layer > 256 wide or weights beyond the LDS budget: -1) keeps the
     // forward forms, which are sound on their own.
@@ -554,6 +563,7 @@ class BabRuntime {
   int pool_[2] = {0, 0};
   double unit_;
   bool crown_ = false;
+  bool refine_ = false;
   int split_target_ = 256;
   int n0_ = 0, npa_ = 0, V_ = 0, Pp_ = 0, norient_ = 1;
   bool relaxed_ = false;
@@ -588,11 +598,11 @@ void register_bab(py::module& m) {
   py::class_<BabRuntime>(m, "BabRuntime")
       .def(py::init<py::handle, uintptr_t, std::vector<int>, std::vector<float>, std::vector<int64_t>,
                     std::vector<int64_t>, std::vector<int>, float, std::vector<uint8_t>, int, int, int, double, bool,
-                    int>(),
+                    int, bool>(),
            py::arg("net"), py::arg("flat"), py::arg("pa"), py::arg("values_f"), py::arg("values_i"),
            py::arg("pairs"), py::arg("ra"), py::arg("tau"), py::arg("shared"), py::arg("capacity"),
            py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"), py::arg("crown") = true,
-           py::arg("split_target") = 256)
+           py::arg("split_target") = 256, py::arg("refine") = false)
       .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"),
            py::arg("native_exact") = false, py::arg("budget2") = 0, py::arg("max_w") = 0,

@@ -109,6 +109,7 @@ const NetDesc& fa_net_desc(py::handle h) { return h.cast<const Net&>().d; }
 void register_bab(py::module& m);
 void register_relu(py::module& m);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
+extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 void register_csv(py::module& m);
 
 static void check(int rc, const char* what) {
@@ -199,6 +200,23 @@ PYBIND11_MODULE(_C, m) {
     a.layer_lb = P<float>(layer_lb);
     a.layer_ub = P<float>(layer_ub);
     check(fa_crown_launch(net.d, a, (hipStream_t)stream), "crown");
+  });
+
+  // back-substituted hidden-layer bounds (refine.hip), tightening layer_lb / layer_ub of a preceding
+  // symbolic `bounds` call in place; returns the launch code (0 done, -1 shape not supported)
+  m.def("refine", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t dead_in, int R,
+                     uintptr_t layer_lb, uintptr_t layer_ub, uintptr_t stream) {
+    BoundArgs a{};
+    a.flat = P<const float>(flat);
+    a.lo = P<const float>(lo);
+    a.hi = P<const float>(hi);
+    a.dead_in = P<const uint8_t>(dead_in);
+    a.R = R;
+    a.layer_lb = P<float>(layer_lb);
+    a.layer_ub = P<float>(layer_ub);
+    const int rc = fa_refine_launch(net.d, a, (hipStream_t)stream);
+    if (rc < -1) throw std::runtime_error("refine launch failed, code " + std::to_string(rc));
+    return rc;
   });
 
   m.def("point_bounds", [](const Net& net, uintptr_t flat, uintptr_t x, uintptr_t dead_in, int R, uintptr_t out_lb,
@@ -426,6 +444,10 @@ PYBIND11_MODULE(_C, m) {
     check(fa_trace_marker_launch(tag, P<int>(sink), (hipStream_t)stream), "trace_marker");
   });
   m.def("arch", []() { return std::string("gfx950"); });
+  // raise the dynamic-LDS limit of every registered kernel once (common.h); Backend construction
+  // calls it before any host thread launches.  0 on success.
+  m.def("prepare_lds", [] { return fa_lds_prepare(); });
+  m.def("lds_registered", [] { return (int)fa_lds_registry().size(); });
   register_bab(m);
   register_relu(m);
   // caching allocator of the native runtimes (devmem.h): hipFree / hipHostFree calls reaching the

@@ -326,9 +326,10 @@ extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t 
   args.stride = S;
   args.wstride = ws;
   args.wfloats = wf;
-  if (bytes > 64 * 1024)
-    FA_CHECK(fa_raise_lds_once((const void*)fa_bounds_kernel, bytes));
+  if (!fa_lds_ok(bytes)) return -4;       // fa_lds_prepare() not run (Backend construction)
   dim3 grid((args.R + G - 1) / G);
   hipLaunchKernelGGL(fa_bounds_kernel, grid, dim3(FA_THREADS), bytes, stream, net, args);
   return (int)hipGetLastError();
 }
+
+FA_LDS_REGISTER(FA_LDS_K(fa_bounds_kernel));

@@ -6,9 +6,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <mutex>
-#include <set>
+#include <atomic>
 #include <utility>
+#include <vector>
 
 #define FA_MAX_LAYERS 16
 #define FA_THREADS 256
@@ -77,16 +77,29 @@ __device__ __forceinline__ f32x4 fa_mfma4(float a, float b, f32x4 c) {
     }                                                                            \
   } while (0)
 
-// Raise a kernel's dynamic-LDS limit to `bytes` once per (kernel, bytes), under a lock: the host
-// threads launch concurrently and change no attribute while other threads launch that kernel.
-// Returns the hipFuncSetAttribute error of the first call (hipSuccess afterwards).
-inline hipError_t fa_raise_lds_once(const void* k, size_t bytes) {
-  if (bytes <= 64 * 1024) return hipSuccess;
-  static std::mutex mu;
-  static std::set<std::pair<const void*, size_t>> done;
-  std::lock_guard<std::mutex> g(mu);
-  if (done.count(std::make_pair(k, bytes))) return hipSuccess;
-  const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e == hipSuccess) done.insert(std::make_pair(k, bytes));
-  return e;
+// Dynamic-LDS limits.  Every kernel that may be launched with more than 64 KB of dynamic LDS is
+// registered at library load by a static initialiser (FA_LDS_REGISTER: pushes the host stub's
+// address, no HIP call).  fa_lds_prepare() (csrc/devmem.cpp) raises every registered kernel's limit
+// to the device maximum ONCE, when the first Backend is built (ops/backend.py) -- before any host
+// thread launches -- so no launch path ever changes a function attribute while other threads
+// launch (the round-3 profiled crash had 8 threads racing through per-site hipFuncSetAttribute
+// calls).  Launch paths only ask fa_lds_ok(bytes).
+inline std::vector<const void*>& fa_lds_registry() {
+  static std::vector<const void*> v;
+  return v;
 }
+inline std::atomic<bool>& fa_lds_ready_flag() {
+  static std::atomic<bool> ready{false};
+  return ready;
+}
+struct FaLdsReg {
+  explicit FaLdsReg(const void* k) { fa_lds_registry().push_back(k); }
+};
+#define FA_LDS_CAT2(a, b) a##b
+#define FA_LDS_CAT(a, b) FA_LDS_CAT2(a, b)
+#define FA_LDS_REGISTER(...) \
+  static const FaLdsReg FA_LDS_CAT(fa_lds_reg_, __LINE__)[] = {__VA_ARGS__}
+#define FA_LDS_K(k) FaLdsReg((const void*)(k))
+extern "C" int fa_lds_prepare();
+// may a registered kernel be launched with `bytes` of dynamic LDS?
+inline bool fa_lds_ok(size_t bytes) { return bytes <= 64 * 1024 || fa_lds_ready_flag().load(std::memory_order_acquire); }

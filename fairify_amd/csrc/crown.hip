@@ -518,10 +518,7 @@ int crown_mfma_try(const NetDesc& net, const BoundArgs& a, hipStream_t stream) {
     const auto key = std::make_pair((const void*)k, bytes);
     auto it = occ.find(key);
     if (it == occ.end()) {
-      if (bytes > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        if (e != hipSuccess) return -(int)e;
-      }
+      if (!fa_lds_ok(bytes)) return -4;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, bytes) != hipSuccess || per_cu <= 0) per_cu = 1;
       occ[key] = per_cu;
     } else {
@@ -565,18 +562,12 @@ extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stre
   typedef void (*K)(NetDesc, BoundArgs, int, int);
   K k = G == 4 ? fa_crown_kernel<4> : G == 8 ? fa_crown_kernel<8> : G == 16 ? fa_crown_kernel<16>
       : G == 32 ? fa_crown_kernel<32> : fa_crown_kernel<64>;
-  static std::mutex mu;
-  static size_t raised[7] = {0, 0, 0, 0, 0, 0, 0};
-  const int gi = G == 4 ? 0 : G == 8 ? 1 : G == 16 ? 2 : G == 32 ? 3 : 4;
-  if (bytes > 64 * 1024) {
-    std::lock_guard<std::mutex> g(mu);
-    if (bytes > raised[gi]) {
-      if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
-        return -3;
-      raised[gi] = bytes;
-    }
-  }
+  if (!fa_lds_ok(bytes)) return -3;
   const int blocks = (int)std::min<long long>(((long long)a.R + rows_per_block - 1) / rows_per_block, 256LL * 8);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * FA_CROWN_WAVES), bytes, stream, net, a, nparams, WP);
   return (int)hipGetLastError();
 }
+
+FA_LDS_REGISTER(FA_LDS_K(fa_crown_mfma_kernel<1>), FA_LDS_K(fa_crown_mfma_kernel<2>), FA_LDS_K(fa_crown_mfma_kernel<4>),
+                FA_LDS_K(fa_crown_mfma_kernel<7>), FA_LDS_K(fa_crown_kernel<4>), FA_LDS_K(fa_crown_kernel<8>),
+                FA_LDS_K(fa_crown_kernel<16>), FA_LDS_K(fa_crown_kernel<32>), FA_LDS_K(fa_crown_kernel<64>));

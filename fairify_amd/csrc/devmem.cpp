@@ -1,5 +1,6 @@
 // Caching device / pinned-host allocators of the native runtimes (see devmem.h).
 #include "devmem.h"
+#include "common.h"
 
 #include <algorithm>
 #include <atomic>
@@ -180,3 +181,26 @@ void release_cached() {
 }
 
 }  // namespace fa_mem
+
+// ------------------------------------------------------------------------------------------------
+// Dynamic-LDS registry (common.h): raise every registered kernel's limit to the device maximum
+// once.  Called from Backend construction (bindings: prepare_lds) before host threads launch;
+// magic-static initialisation makes concurrent first calls wait for the one that runs.
+extern "C" int fa_lds_prepare() {
+  static const int rc = [] {
+    int dev = 0, maxb = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&maxb, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || maxb <= 0)
+      maxb = 160 * 1024;
+    for (const void* k : fa_lds_registry()) {
+      hipFuncAttributes at{};
+      if (hipFuncGetAttributes(&at, k) != hipSuccess) return -2;
+      const int dyn = maxb - (int)at.sharedSizeBytes;
+      if (dyn <= 64 * 1024) continue;
+      if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, dyn) != hipSuccess) return -3;
+    }
+    fa_lds_ready_flag().store(true, std::memory_order_release);
+    return 0;
+  }();
+  return rc;
+}

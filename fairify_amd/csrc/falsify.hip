@@ -424,11 +424,11 @@ extern "C" int fa_falsify_launch(const NetDesc& net, FalsifyArgs a, hipStream_t 
   const FalsifyLds L = fa_falsify_lds(a, net.dims[0], cfg.floats);
   const size_t bytes = (size_t)L.floats * sizeof(float);
   if (bytes > 160 * 1024) return 0;
-  {
-    const hipError_t e = fa_raise_lds_once((const void*)k, bytes);
-    if (e != hipSuccess) return -(int)e;
-  }
+  if (!fa_lds_ok(bytes)) return -4;
   hipLaunchKernelGGL(k, dim3((unsigned)a.P), dim3(FA_THREADS), bytes, stream, net, a, cfg);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 1 : -(int)e;
 }
+
+FA_LDS_REGISTER(FA_LDS_K(fa_falsify_kernel<1>), FA_LDS_K(fa_falsify_kernel<2>), FA_LDS_K(fa_falsify_kernel<4>),
+                FA_LDS_K(fa_falsify_kernel<7>));

@@ -116,8 +116,7 @@ extern "C" int fa_forward_launch(const NetDesc& net, FwdArgs a, hipStream_t stre
   if (a.B <= 0) return 0;
   a.S = net.max_width | 1;
   size_t bytes = (2 * (size_t)FA_TR * a.S + FA_TR) * sizeof(float);
-  if (bytes > 64 * 1024)
-    FA_CHECK(fa_raise_lds_once((const void*)fa_forward_kernel, bytes));
+  if (!fa_lds_ok(bytes)) return -4;
   hipLaunchKernelGGL(fa_forward_kernel, dim3((a.B + FA_TR - 1) / FA_TR), dim3(FA_THREADS), bytes, stream, net, a);
   return (int)hipGetLastError();
 }
@@ -442,7 +441,7 @@ extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) 
       rb = (rb + 15) & ~(size_t)15;
       const int tiles = (a.n_samples + FA_TR - 1) / FA_TR;
       if (rb <= 160 * 1024 && a.split >= 1 && (a.split == 1 || (a.keys && a.split <= tiles))) {
-        FA_CHECK(fa_raise_lds_once((const void*)k, rb));
+        if (!fa_lds_ok(rb)) return -4;
         hipLaunchKernelGGL(k, dim3((unsigned)a.P * (unsigned)a.split), dim3(FA_THREADS), rb, stream, net, a, cfg);
         if (a.split > 1) hipLaunchKernelGGL(fa_sim_finalize_kernel, dim3(a.P), dim3(FA_THREADS), 0, stream, net, a);
         return (int)hipGetLastError();
@@ -453,8 +452,7 @@ extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) 
   size_t bytes = floats * sizeof(float) + (net.n_neurons + 4) * sizeof(int) + FA_TR;
   bytes = (bytes + 15) & ~(size_t)15;
   if (bytes > 160 * 1024) return -1;
-  if (bytes > 64 * 1024)
-    FA_CHECK(fa_raise_lds_once((const void*)fa_sim_kernel, bytes));
+  if (!fa_lds_ok(bytes)) return -4;
   const int tiles = (a.n_samples + FA_TR - 1) / FA_TR;
   if (a.split < 1 || (a.split > 1 && (!a.keys || a.split > tiles))) return -2;
   hipLaunchKernelGGL(fa_sim_kernel, dim3((unsigned)a.P * (unsigned)a.split), dim3(FA_THREADS), bytes, stream, net, a);
@@ -593,8 +591,11 @@ extern "C" int fa_ascent_launch(const NetDesc& net, AscentArgs a, hipStream_t st
   size_t bytes = floats * sizeof(float) + ((size_t)a.K + (size_t)a.K * nm + 2) * sizeof(int);
   bytes = (bytes + 15) & ~(size_t)15;
   if (bytes > 160 * 1024) return -1;
-  if (bytes > 64 * 1024)
-    FA_CHECK(fa_raise_lds_once((const void*)fa_ascent_kernel, bytes));
+  if (!fa_lds_ok(bytes)) return -4;
   hipLaunchKernelGGL(fa_ascent_kernel, dim3(a.P), dim3(FA_THREADS), bytes, stream, net, a);
   return (int)hipGetLastError();
 }
+
+FA_LDS_REGISTER(FA_LDS_K(fa_forward_kernel), FA_LDS_K(fa_sim_kernel), FA_LDS_K(fa_ascent_kernel),
+                FA_LDS_K(fa_sim_reg_kernel<1>), FA_LDS_K(fa_sim_reg_kernel<2>), FA_LDS_K(fa_sim_reg_kernel<4>),
+                FA_LDS_K(fa_sim_reg_kernel<7>));

@@ -187,11 +187,7 @@ extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t 
     const auto key = std::make_pair((const void*)k, bytes);
     auto it = occ.find(key);
     if (it == occ.end()) {
-      if (bytes > 64 * 1024) {
-        const hipError_t e =
-            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        if (e != hipSuccess) return -(int)e;
-      }
+      if (!fa_lds_ok(bytes)) return -4;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, FA_THREADS, bytes) != hipSuccess || per_cu <= 0)
         per_cu = 1;
       occ[key] = per_cu;
@@ -207,3 +203,6 @@ extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t 
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 1 : -(int)e;
 }
+
+FA_LDS_REGISTER(FA_LDS_K(fa_point_kernel<1>), FA_LDS_K(fa_point_kernel<2>), FA_LDS_K(fa_point_kernel<4>),
+                FA_LDS_K(fa_point_kernel<7>));

@@ -277,12 +277,12 @@ extern "C" int fa_agree_launch(const NetDesc& net, const float* flat, int Pm, co
   if (!fa_regnet_cfg(net, cfg)) return -1;
   const size_t bytes = ((size_t)cfg.floats + 2 * net.dims[0] + 4) * sizeof(float) + net.n_hidden + 16;
   if (bytes > 160 * 1024) return 0;
-  {
-    const hipError_t e = fa_raise_lds_once((const void*)k, bytes);
-    if (e != hipSuccess) return -(int)e;
-  }
+  if (!fa_lds_ok(bytes)) return -4;
   hipLaunchKernelGGL(k, dim3((unsigned)Pm), dim3(FA_THREADS), bytes, stream, net, cfg, flat, Pm, rows, lo, hi, pids, dead, S,
                      seed, agree);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 1 : -(int)e;
 }
+
+FA_LDS_REGISTER(FA_LDS_K(fa_agree_kernel<1>), FA_LDS_K(fa_agree_kernel<2>), FA_LDS_K(fa_agree_kernel<4>),
+                FA_LDS_K(fa_agree_kernel<7>));

@@ -288,17 +288,7 @@ extern "C" int fa_crown_phase_launch(const NetDesc& net, CrownPhaseArgs a, hipSt
   typedef void (*K)(NetDesc, CrownPhaseArgs, int, int);
   K k = G == 4 ? fa_crown_phase_kernel<4> : G == 8 ? fa_crown_phase_kernel<8> : G == 16 ? fa_crown_phase_kernel<16>
       : G == 32 ? fa_crown_phase_kernel<32> : fa_crown_phase_kernel<64>;
-  if (bytes > 64 * 1024) {
-    static std::mutex mu;
-    static size_t raised[5] = {0, 0, 0, 0, 0};
-    const int gi = G == 4 ? 0 : G == 8 ? 1 : G == 16 ? 2 : G == 32 ? 3 : 4;
-    std::lock_guard<std::mutex> g(mu);
-    if (bytes > raised[gi]) {
-      if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
-        return -3;
-      raised[gi] = bytes;
-    }
-  }
+  if (!fa_lds_ok(bytes)) return -3;
   const int blocks = (int)std::min<long long>(((long long)a.R + rows_per_block - 1) / rows_per_block, 256LL * 8);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * FA_CP_WAVES), bytes, stream, net, a, nparams, WP);
   const hipError_t e = hipGetLastError();
@@ -558,3 +548,7 @@ extern "C" int fa_relu_reset_launch(int* counters, hipStream_t stream) {
   hipLaunchKernelGGL(fa_relu_reset_kernel, dim3(1), dim3(64), 0, stream, counters);
   return (int)hipGetLastError();
 }
+
+FA_LDS_REGISTER(FA_LDS_K(fa_crown_phase_kernel<4>), FA_LDS_K(fa_crown_phase_kernel<8>),
+                FA_LDS_K(fa_crown_phase_kernel<16>), FA_LDS_K(fa_crown_phase_kernel<32>),
+                FA_LDS_K(fa_crown_phase_kernel<64>));

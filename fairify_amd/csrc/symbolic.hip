@@ -873,11 +873,7 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
     const auto key = std::make_pair((const void*)k, bytes);
     auto it = occ.find(key);
     if (it == occ.end()) {
-      if (bytes > 64 * 1024) {
-        const hipError_t e =
-            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        if (e != hipSuccess) return -(int)e;
-      }
+      if (!fa_lds_ok(bytes)) return -4;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, bytes) != hipSuccess || per_cu <= 0)
         per_cu = 1;
       occ[key] = per_cu;
@@ -892,3 +888,9 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 1 : -(int)e;
 }
+
+FA_LDS_REGISTER(FA_LDS_K((sym_ptr<1, 1>())), FA_LDS_K((sym_ptr<1, 1, true>())), FA_LDS_K((sym_ptr<1, 1, true, 2>())),
+                FA_LDS_K((sym_ptr<1, 1, true, 4>())), FA_LDS_K((sym_ptr<1, 2>())), FA_LDS_K((sym_ptr<1, 4>())),
+                FA_LDS_K((sym_ptr<1, 7>())), FA_LDS_K((sym_ptr<1, 10>())), FA_LDS_K((sym_ptr<2, 1>())),
+                FA_LDS_K((sym_ptr<2, 2>())), FA_LDS_K((sym_ptr<2, 4>())), FA_LDS_K((sym_ptr<2, 10>())),
+                FA_LDS_K((sym_ptr<3, 1>())), FA_LDS_K((sym_ptr<3, 2>())));

@@ -50,6 +50,10 @@ class BaBConfig:
     mode: str = "symbolic"
     cand_cap: int = 1 << 17          # candidate pairs confirmed per BFS level (native runtime)
     crown: bool = os.environ.get("FAIRIFY_CROWN", "1") != "0"   # backward output bounds per node
+    # hidden-layer bounds tightened by back-substitution before the output pass (csrc/refine.hip):
+    # "auto" = networks with >= 3 hidden layers of which one is >= 10 wide (AC-7's residue closes
+    # in ~800 nodes instead of > 32 768; on 1-2 hidden layers it equals the forward bounds), "on", "off"
+    refine: str = os.environ.get("FAIRIFY_REFINE", "auto")
     # native runtime branching rule: a partition with w nodes in a BFS level splits each along
     # clamp(log2(split_target / w), 1, 6) dims (per partition: verdicts do not depend on which
     # partitions share a chunk)
@@ -74,6 +78,19 @@ class BaBResult:
     time: float = 0.0
     open_left: Optional[np.ndarray] = None   # [P] open nodes left when an UNKNOWN partition stopped
                                              # (native runtime; the escalation filter's predictor)
+
+
+def refine_on(mode: str, widths) -> bool:
+    """Whether the BaB bounds its nodes with back-substituted hidden-layer bounds (BaBConfig.refine).
+    ``auto``: at least 3 hidden layers and one of them at least 10 wide -- with 1-2 hidden layers the
+    refined bounds equal the forward ones, and on the narrow deep nets (AC-9/10/12, 3-5 wide) the
+    extra pass costs more than it closes (tools/diag_open_nodes.py on the bench residue)."""
+    if mode == "on":
+        return True
+    if mode != "auto":
+        return False
+    hidden = list(widths)[:-1]
+    return len(hidden) >= 3 and max(hidden) >= 10
 
 
 def pa_groups(q: ResolvedQuery, lo: np.ndarray, hi: np.ndarray) -> List[np.ndarray]:
@@ -208,10 +225,11 @@ class BaBSolver:
                 dead_rows = self.dead[bpart].repeat_interleave(V, dim=0)
             with self.tm("bab.bounds"):
                 rlo, rhi = self._rows(blo, bhi, values)
-                res_x = self.be.bounds(rlo, rhi, mode=cfg.mode, dead=dead_rows, crown=cfg.crown)
+                rf = refine_on(self.cfg.refine, self.be.widths)
+                res_x = self.be.bounds(rlo, rhi, mode=cfg.mode, dead=dead_rows, crown=cfg.crown, refine=rf)
                 if self.relaxed:
                     plo, phi = self._rows(bplo, bphi, values)
-                    res_xp = self.be.bounds(plo, phi, mode=cfg.mode, dead=dead_rows, crown=cfg.crown)
+                    res_xp = self.be.bounds(plo, phi, mode=cfg.mode, dead=dead_rows, crown=cfg.crown, refine=rf)
                 else:
                     res_xp = res_x
             with self.tm("bab.certify"):
@@ -348,8 +366,9 @@ class BaBSolver:
         from ..ops.hip import _net
         from .rtpool import checkout
 
+        rf = refine_on(self.cfg.refine, self.be.widths)
         key = (tuple(self.q.pa_idx), tuple(self.q.ra_idx), self.q.tau, values_np.tobytes(), pairs_np.tobytes(),
-               bool(self.cfg.crown), int(self.cfg.split_target))
+               bool(self.cfg.crown), int(self.cfg.split_target), rf)
         shared = np.ones(self.q.n, dtype=np.uint8)
         shared[list(self.q.ra_idx)] = 0
 
@@ -360,7 +379,7 @@ class BaBSolver:
                                     pairs_np.astype(np.int64).reshape(-1).tolist(),
                                     list(self.q.ra_idx) if self.relaxed else [], float(self.q.tau),
                                     shared.tolist(), int(cap), int(self.cfg.batch_nodes), int(self.cfg.cand_cap),
-                                    float(self.be.unit), bool(self.cfg.crown), int(self.cfg.split_target))
+                                    float(self.be.unit), bool(self.cfg.crown), int(self.cfg.split_target), rf)
 
         return checkout(self.be, "_bab_rt", key, max(self.cfg.max_pool, n_run), make)
 

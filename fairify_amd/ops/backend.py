@@ -102,6 +102,13 @@ class Backend:
         probe = torch.empty(0, device=self.device)
         self.hip = use_hip(probe) and dtype == torch.float32
         if self.hip:
+            from . import ext
+
+            # dynamic-LDS limits of every >64 KB kernel, once per process, before any host thread
+            # launches (csrc/common.h registry; no launch path sets a function attribute)
+            rc = ext().prepare_lds()
+            if rc != 0:
+                raise RuntimeError(f"fa_lds_prepare failed ({rc})")
             flat = np.concatenate([np.concatenate([w.reshape(-1), b]) for w, b in zip(mlp.weights, mlp.biases)])
             flat = np.concatenate([flat.astype(np.float32), np.zeros((-len(flat)) % 4, np.float32),
                                    mfma_weight_block(mlp.weights, mlp.biases)])
@@ -136,9 +143,11 @@ class Backend:
     # ----------------------------------------------------------------------------- bounds
     def bounds(self, lo: torch.Tensor, hi: torch.Tensor, mode: str = "symbolic",
                dead: Optional[torch.Tensor] = None, keep_layers: bool = False, fold=(),
-               crown: bool = False, phase: Optional[torch.Tensor] = None) -> ref.BoundResult:
+               crown: bool = False, phase: Optional[torch.Tensor] = None, refine: bool = False) -> ref.BoundResult:
         """``fold``: dims degenerate (lo == hi) in every row — a HIP-kernel layout hint only.
         ``crown``: refine the logit forms/bounds with the backward pass (symbolic mode only).
+        ``refine`` (with ``crown``): first tighten the hidden layers' bounds by back-substitution
+        (ref.crown_refine / csrc/refine.hip), then run the backward output pass on them.
         ``phase``: [R, N_hidden] int8 ReLU phases of the rows' branch regions (-1 / 0 / +1,
         ref.bounds); the result's ``infeasible`` flags rows whose region is empty."""
         lo = lo.to(self.dtype)
@@ -149,9 +158,13 @@ class Backend:
 
             r = hip.bounds(self, lo, hi, mode=mode, dead=dead, keep_layers=keep_layers or crown, fold=fold,
                            phase=phase)
+            if crown and refine:
+                r = hip.refine(self, lo, hi, r, dead)
             return hip.crown(self, lo, hi, r, dead) if crown else r
         r = ref.bounds(self.ws, self.bs, lo, hi, mode=mode, dead=dead, unit=self.unit,
                        keep_layers=keep_layers or crown, phase=phase)
+        if crown and refine:
+            r = ref.crown_refine(self.ws, self.bs, lo, hi, r, dead, unit=self.unit)
         return ref.crown_output(self.ws, self.bs, lo, hi, r, dead, unit=self.unit) if crown else r
 
     def crown_phase(self, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult,

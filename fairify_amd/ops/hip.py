@@ -250,6 +250,30 @@ def crown(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, dead: Op
 
 
 # ------------------------------------------------------------------------------------------------
+def refine(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, dead: Optional[torch.Tensor] = None):
+    """Back-substituted hidden-layer bounds (csrc/refine.hip) tightening ``res.layer_lb/ub`` in place
+    (ref.crown_refine): ``res`` must come from :func:`bounds` with mode='symbolic' and
+    keep_layers=True on the same rows.  Networks the kernel cannot hold keep the forward bounds."""
+    R, n0 = lo.shape
+    if res.lay_lb_full is None:
+        raise ValueError("refine needs symbolic bounds with keep_layers=True (HIP layout)")
+    lo = _c(lo, torch.float32, (R, n0), "lo")
+    hi = _c(hi, torch.float32, (R, n0), "hi")
+    d = None
+    if dead is not None:
+        d = _c(dead, torch.uint8, (R, be.n_hidden), "dead")
+    if R:
+        ext().refine(_net(be), be.flat.data_ptr(), lo.data_ptr(), hi.data_ptr(), _ptr(d), R,
+                     res.lay_lb_full.data_ptr(), res.lay_ub_full.data_ptr(), _stream(lo.device))
+    Nh = be.n_hidden
+    if Nh:
+        res.dead = res.lay_ub_full[:, :Nh] <= 0
+        res.dead_u8 = res.dead.to(torch.uint8)
+        res.active = res.lay_lb_full[:, :Nh] >= 0
+    return res
+
+
+# ------------------------------------------------------------------------------------------------
 def crown_phase(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, phase: Optional[torch.Tensor] = None):
     """ReLU-phase backward bounds (csrc/relu.hip: fa_crown_phase_kernel) on rows bounded by
     :func:`bounds` (symbolic, keep_layers, same ``phase``).  Refines ``res`` (logit bounds, forms)

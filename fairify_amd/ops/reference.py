@@ -367,6 +367,108 @@ def bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Ten
     return res
 
 
+def _backsub(ws, bs, lo: torch.Tensor, hi: torch.Tensor, lbs, ubs, lam: torch.Tensor, c: torch.Tensor, top: int,
+             dead: Optional[torch.Tensor], unit: float):
+    """Back-substitute the linear function ``lam . h_{top-1} + c`` (rows [R, dims[top]]) through the
+    ReLU relaxations of layers top-1 .. 0 down to the input box, with rigorous error terms
+    (csrc/crown.hip, csrc/refine.hip).  Returns (coef [R, n0], const [R], err [R], lower bound [R])
+    with ``lam . h + c >= coef . x + const - err >= low`` on the box for the exact network."""
+    dt = lo.dtype
+    R, n0 = lo.shape
+    L = len(ws)
+    offs = [0]
+    for l in range(L - 1):
+        offs.append(offs[-1] + ws[l].shape[1])
+    mx_in = torch.maximum(lo.abs(), hi.abs())
+    err = torch.zeros(R, dtype=dt, device=lo.device)
+    for l in range(top - 1, -1, -1):
+        W = ws[l].to(dt)
+        b = bs[l].to(dt)
+        n = W.shape[1]
+        lb, ub = lbs[l].to(dt), ubs[l].to(dt)
+        dd = ub <= 0
+        if dead is not None:
+            dd = dd | dead[:, offs[l]:offs[l] + n].bool()
+        act = (lb >= 0) & ~dd
+        unst = ~(dd | act)
+        alpha = (ub > -lb).to(dt)
+        den = torch.where(unst, ub - lb, torch.ones_like(ub))
+        s = torch.where(unst, (ub / den) * (1 + 4 * unit), torch.zeros_like(ub))
+        neg = unst & (lam < 0)
+        slope = torch.where(act, torch.ones_like(ub), torch.where(dd, torch.zeros_like(ub),
+                            torch.where(lam >= 0, alpha, s)))
+        mu = lam * slope
+        t = torch.where(neg, -mu * lb, torch.zeros_like(ub))
+        # only the chord multipliers mu = lambda * s and intercepts t = -mu l are rounded
+        zmax = torch.maximum(lb.abs(), ub.abs())
+        e_rel = torch.where(neg, 3 * unit * (mu.abs() * zmax + t.abs()), torch.zeros_like(ub))
+        g_c = gamma(2 * n + 1, unit)
+        csum = (mu * b[None]).sum(1) + t.sum(1)
+        cmag = c.abs() + (mu * b[None]).abs().sum(1) + t.abs().sum(1)
+        c = c + csum
+        if l > 0:                       # |h| of the layer below: max(0, ub), 0 if forced dead
+            hm = ubs[l - 1].to(dt).clamp(min=0)
+            if dead is not None:
+                hm = torch.where(dead[:, offs[l - 1]:offs[l - 1] + W.shape[0]].bool(), torch.zeros_like(hm), hm)
+        else:
+            hm = mx_in
+        lam = mu @ W.T
+        eps = gamma(n + 1, unit) * (mu.abs() @ W.abs().T)
+        err = err + e_rel.sum(1) + (eps * hm).sum(1) + g_c * cmag
+    a = lam * lo
+    bb = lam * hi
+    conc = torch.minimum(a, bb).sum(1) + c
+    cmg = (lam.abs() * mx_in).sum(1) + c.abs()
+    err = err * (1 + 2 * gamma(2 * sum(int(w.shape[1]) for w in ws) + 4 * L + 4, unit))
+    low = conc - err - gamma(n0 + 1, unit) * cmg - gamma(1, unit) * conc.abs()
+    return lam, c, err, low
+
+
+def crown_refine(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Tensor, hi: torch.Tensor,
+                 res: BoundResult, dead: Optional[torch.Tensor] = None, unit: Optional[float] = None) -> BoundResult:
+    """Tighten the per-neuron pre-activation bounds of hidden layers 1 .. L-2 by back-substitution
+    (csrc/refine.hip, same arithmetic and error terms).
+
+    The forward symbolic pass relaxes every layer with the forms it propagated forward, so on deep
+    networks the intermediate bounds -- and through the relaxation intervals every later bound --
+    degrade with depth.  Here, layer by layer, every neuron z_k[j] = W_k[:, j] . h_{k-1} + b_k[j]
+    is bounded by back-substituting +-W_k[:, j] to the input box through the relaxations of the
+    layers below (CROWN for intermediate neurons), whose intervals are the already refined bounds;
+    each bound is intersected with the forward one.  The output forms are then computed by
+    :func:`crown_output` on the refined intervals.  On the bench residue this closes AC-7's
+    partitions with a median of ~800 nodes where the forward intervals needed > 32 768
+    (tools/diag_open_nodes.py --bound fullcrown, profiles/r4/refine/)."""
+    dt = lo.dtype
+    if unit is None:
+        unit = FP64_UNIT if dt == torch.float64 else FP32_UNIT
+    R, n0 = lo.shape
+    L = len(ws)
+    lbs = [t.clone() for t in res.layer_lb]
+    ubs = [t.clone() for t in res.layer_ub]
+    for k in range(1, L - 1):
+        n_k = ws[k].shape[1]
+        Wt = ws[k].to(dt).T                                       # [n_k, dims[k]]
+        rep = lambda t: t.repeat_interleave(n_k, dim=0)          # noqa: E731  rows x targets
+        rl, rh = rep(lo), rep(hi)
+        lb_r, ub_r = [rep(t.to(dt)) for t in lbs[:k]], [rep(t.to(dt)) for t in ubs[:k]]
+        d_r = rep(dead) if dead is not None else None
+        low = {}
+        for sg in (1.0, -1.0):
+            lam = (sg * Wt)[None].expand(R, -1, -1).reshape(R * n_k, -1).clone()
+            c = (sg * bs[k].to(dt))[None].expand(R, -1).reshape(-1).clone()
+            low[sg] = _backsub(ws, bs, rl, rh, lb_r, ub_r, lam, c, k, d_r, unit)[3].view(R, n_k)
+        lbs[k] = torch.maximum(lbs[k], low[1.0].to(lbs[k].dtype))
+        ubs[k] = torch.minimum(ubs[k], (-low[-1.0]).to(ubs[k].dtype))
+    r = BoundResult(out_lb=res.out_lb, out_ub=res.out_ub, Lc=res.Lc, L0=res.L0, Le=res.Le, Uc=res.Uc, U0=res.U0,
+                    Ue=res.Ue, layer_lb=lbs, layer_ub=ubs)
+    Nh = sum(int(w.shape[1]) for w in ws[:-1])
+    if Nh:
+        r.dead = torch.cat([u <= 0 for u in ubs[:-1]], dim=1)
+        r.active = torch.cat([l >= 0 for l in lbs[:-1]], dim=1)
+    return r
+
+
+
 def crown_output(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Tensor, hi: torch.Tensor,
                  res: BoundResult, dead: Optional[torch.Tensor] = None, unit: Optional[float] = None) -> BoundResult:
     """Backward (CROWN-style) linear bounds of the logit, replacing the forward-symbolic output
@@ -389,57 +491,11 @@ def crown_output(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: tor
         unit = FP64_UNIT if dt == torch.float64 else FP32_UNIT
     R, n0 = lo.shape
     L = len(ws)
-    lbs, ubs = res.layer_lb, res.layer_ub
-    offs = [0]
-    for l in range(L - 1):
-        offs.append(offs[-1] + ws[l].shape[1])
-    mx_in = torch.maximum(lo.abs(), hi.abs())
     out = {}
     for sg in (1.0, -1.0):
         lam = (sg * ws[L - 1][:, 0].to(dt))[None].expand(R, -1).clone()
         c = torch.full((R,), sg * float(bs[L - 1][0]), dtype=dt, device=lo.device)
-        err = torch.zeros(R, dtype=dt, device=lo.device)
-        for l in range(L - 2, -1, -1):
-            W = ws[l].to(dt)
-            b = bs[l].to(dt)
-            n = W.shape[1]
-            lb, ub = lbs[l].to(dt), ubs[l].to(dt)
-            dd = ub <= 0
-            if dead is not None:
-                dd = dd | dead[:, offs[l]:offs[l] + n].bool()
-            act = (lb >= 0) & ~dd
-            unst = ~(dd | act)
-            alpha = (ub > -lb).to(dt)
-            den = torch.where(unst, ub - lb, torch.ones_like(ub))
-            s = torch.where(unst, (ub / den) * (1 + 4 * unit), torch.zeros_like(ub))
-            neg = unst & (lam < 0)
-            slope = torch.where(act, torch.ones_like(ub), torch.where(dd, torch.zeros_like(ub),
-                                torch.where(lam >= 0, alpha, s)))
-            mu = lam * slope
-            t = torch.where(neg, -mu * lb, torch.zeros_like(ub))
-            # only the chord multipliers mu = lambda * s and intercepts t = -mu l are rounded
-            zmax = torch.maximum(lb.abs(), ub.abs())
-            e_rel = torch.where(neg, 3 * unit * (mu.abs() * zmax + t.abs()), torch.zeros_like(ub))
-            g_c = gamma(2 * n + 1, unit)
-            csum = (mu * b[None]).sum(1) + t.sum(1)
-            cmag = c.abs() + (mu * b[None]).abs().sum(1) + t.abs().sum(1)
-            c = c + csum
-            if l > 0:                       # |h| of the layer below: max(0, ub), 0 if forced dead
-                hm = ubs[l - 1].to(dt).clamp(min=0)
-                if dead is not None:
-                    hm = torch.where(dead[:, offs[l - 1]:offs[l - 1] + W.shape[0]].bool(), torch.zeros_like(hm), hm)
-            else:
-                hm = mx_in
-            lam = mu @ W.T
-            eps = gamma(n + 1, unit) * (mu.abs() @ W.abs().T)
-            err = err + e_rel.sum(1) + (eps * hm).sum(1) + g_c * cmag
-        a = lam * lo
-        bb = lam * hi
-        conc = torch.minimum(a, bb).sum(1) + c
-        cmg = (lam.abs() * mx_in).sum(1) + c.abs()
-        err = err * (1 + 2 * gamma(2 * sum(int(w.shape[1]) for w in ws) + 4 * L + 4, unit))
-        low = conc - err - gamma(n0 + 1, unit) * cmg - gamma(1, unit) * conc.abs()
-        out[sg] = (lam, c, err, low)
+        out[sg] = _backsub(ws, bs, lo, hi, res.layer_lb, res.layer_ub, lam, c, L - 1, dead, unit)
     lamL, cL, eL, lowL = out[1.0]
     lamU, cU, eU, lowU = out[-1.0]
     r = BoundResult(out_lb=torch.maximum(res.out_lb, lowL.to(res.out_lb.dtype)),

@@ -4,17 +4,21 @@ Strong-scaling bench step (bench.py): the seeded partition order of every model 
 contiguous units of ``unit_size`` partitions; every unit is verified by exactly one rank, so a
 step's verdict totals do not depend on the assignment (per-partition verdicts are independent
 of which partitions share a chunk: tests/test_determinism_gpu.py, tests/test_bench_launch.py).
-The first step assigns units by a size prior; afterwards every rank reports the wall time of
-the units it ran, the costs are summed over ranks (one ``all_reduce``, RCCL), and the next step
+The first step assigns units by a size prior; afterwards every rank reports the cost of the
+units it ran (BaB node expansions weighted by the model's multiply-adds, plus a fixed cost per
+partition), the costs are summed over ranks (one ``all_reduce``, RCCL), and the next step
 uses a deterministic LPT schedule (longest unit first onto the least loaded rank, ties to the
 lower rank / unit index) -- SURVEY §2.4.2 "work stealing" / §7.5 "heavy-tailed work", with the
 balancing decided once per step instead of by messages between ranks.  The reference is
 sequential (src/AC/Verify-AC.py:78,109).
 
 Host resources: one 8-GPU node runs 8 ranks, each with its own host threads / HIP streams and
-MILP pool; ``rank_cpuset`` gives rank r of a node the r-th contiguous slice of the CPUs the
-launcher may use, ``pin_rank`` applies it before any GPU call, ``host_threads`` sizes the pools
-from that slice.
+MILP pool.  ``gpu_local_cpus`` reads which CPUs are local to rank r's GPU from sysfs (KFD topology
+-> PCI address -> ``local_cpulist``; no HIP call, so it runs before the GPU is touched);
+``rank_cpuset`` splits each GPU-local CPU set evenly among the ranks whose GPUs share it (the
+ranks of one socket), falling back to the r-th contiguous slice of the allowed CPUs when sysfs
+gives nothing usable; ``pin_rank`` applies it before any GPU call, ``host_threads`` sizes the
+pools from that slice.
 """
 from __future__ import annotations
 
@@ -60,26 +64,107 @@ def prior_costs(units: Sequence[Unit], model_weight: Sequence[float], sizes: Dic
 
 
 # ----------------------------------------------------------------------------------- host CPUs
-def rank_cpuset(local_rank: int, local_world: int, cpus: Sequence[int] = None) -> List[int]:
-    """The local_rank-th of local_world contiguous slices of ``cpus`` (default: this process's
-    affinity set), at least one CPU each."""
-    cpus = sorted(os.sched_getaffinity(0)) if cpus is None else sorted(cpus)
-    n = len(cpus)
-    if local_world <= 1 or n == 0:
+def parse_cpulist(text: str) -> List[int]:
+    """sysfs cpulist ("0-31,64-95") -> sorted CPU ids."""
+    out = set()
+    for part in text.strip().split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-", 1)
+            out.update(range(int(a), int(b) + 1))
+        else:
+            out.add(int(part))
+    return sorted(out)
+
+
+def _visible(n: int) -> List[int]:
+    """KFD GPU indices this process sees, in device order (ROCR_VISIBLE_DEVICES, then
+    HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES; integer lists only -- anything else: all)."""
+    idx = list(range(n))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is None or v.strip() == "":
+            continue
+        try:
+            sel = [int(t) for t in v.split(",") if t.strip() != ""]
+        except ValueError:
+            return idx
+        idx = [idx[k] for k in sel if 0 <= k < len(idx)]
+    return idx
+
+
+def gpu_pci_addresses(sysfs: str = "/sys") -> List[str]:
+    """PCI addresses ("dddd:bb:dd.f") of the GPUs in KFD topology order (the order ROCr
+    enumerates them), restricted to the visible devices.  [] when the topology is unreadable."""
+    base = os.path.join(sysfs, "class", "kfd", "kfd", "topology", "nodes")
+    try:
+        nodes = sorted((int(d) for d in os.listdir(base) if d.isdigit()))
+    except OSError:
+        return []
+    addrs = []
+    for nd in nodes:
+        try:
+            with open(os.path.join(base, str(nd), "properties")) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) <= 0:        # CPU node
+            continue
+        loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
+        addrs.append(f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 0x7}")
+    return [addrs[k] for k in _visible(len(addrs))]
+
+
+def gpu_local_cpus(device_index: int, sysfs: str = "/sys") -> List[int]:
+    """CPUs local to GPU ``device_index`` (its PCI device's ``local_cpulist``); [] if unknown."""
+    addrs = gpu_pci_addresses(sysfs)
+    if not addrs:
+        return []
+    addr = addrs[device_index % len(addrs)]
+    try:
+        with open(os.path.join(sysfs, "bus", "pci", "devices", addr, "local_cpulist")) as f:
+            return parse_cpulist(f.read())
+    except (OSError, ValueError):
+        return []
+
+
+def _slice(cpus: Sequence[int], k: int, n: int) -> List[int]:
+    cpus = sorted(cpus)
+    m = len(cpus)
+    if n <= 1 or m == 0:
         return list(cpus)
-    if n < local_world:
-        return [cpus[local_rank % n]]
-    lo = (local_rank * n) // local_world
-    hi = ((local_rank + 1) * n) // local_world
-    return list(cpus[lo:hi])
+    if m < n:
+        return [cpus[k % m]]
+    return list(cpus[(k * m) // n:((k + 1) * m) // n])
+
+
+def rank_cpuset(local_rank: int, local_world: int, cpus: Sequence[int] = None, sysfs: str = "/sys",
+                numa: bool = True) -> List[int]:
+    """This rank's CPUs: with ``numa``, the CPUs local to its GPU (sysfs), split evenly among the
+    ranks of this node whose GPUs report the same local set; otherwise (or when sysfs gives no
+    usable set) the local_rank-th of local_world contiguous slices of ``cpus`` (default: this
+    process's affinity set).  At least one CPU each."""
+    cpus = sorted(os.sched_getaffinity(0)) if cpus is None else sorted(cpus)
+    if local_world <= 1 or not cpus:
+        return list(cpus)
+    if numa:
+        allowed = set(cpus)
+        sets = [tuple(c for c in gpu_local_cpus(r, sysfs) if c in allowed) for r in range(local_world)]
+        if all(sets):
+            peers = [r for r in range(local_world) if sets[r] == sets[local_rank]]
+            return _slice(sets[local_rank], peers.index(local_rank), len(peers))
+    return _slice(cpus, local_rank, local_world)
 
 
 def pin_rank(local_rank: int, local_world: int) -> List[int]:
-    """Restrict this process (and the threads it starts afterwards) to its node slice of CPUs.
-    Call before importing torch / touching the GPU.  FAIRIFY_NO_PIN=1 disables it."""
+    """Restrict this process (and the threads it starts afterwards) to its CPUs (GPU-local when
+    sysfs tells, ``rank_cpuset``).  Call before importing torch / touching the GPU.
+    FAIRIFY_NO_PIN=1 disables it, FAIRIFY_PIN_NUMA=0 uses plain contiguous slices."""
     if os.environ.get("FAIRIFY_NO_PIN") == "1" or local_world <= 1 or not hasattr(os, "sched_setaffinity"):
         return sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
-    mine = rank_cpuset(local_rank, local_world)
+    mine = rank_cpuset(local_rank, local_world, numa=os.environ.get("FAIRIFY_PIN_NUMA", "1") != "0")
     try:
         os.sched_setaffinity(0, set(mine))
     except OSError:

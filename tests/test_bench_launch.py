@@ -40,8 +40,8 @@ def test_self_launch_totals_match_one_rank():
         # LPT's guarantee (mean + largest unit); at 2 ranks the 24 units balance within 10 %.  At 4 / 8
         # ranks a single heavy unit (a partition escalated after the relu stage) dominates 3-6 units
         # per rank, so only the guarantee is asserted there
-        assert dd["balance"] == "lpt" and dd["cost_ratio"] <= (min(dd["cost_bound"], 1.1) if n == 2
-                                                               else dd["cost_bound"]), dd
+        assert dd["balance"] == "lpt" and dd["predicted_cost_ratio"] <= (
+            min(dd["predicted_cost_bound"], 1.1) if n == 2 else dd["predicted_cost_bound"]), dd
     # honest accounting fields add up
     assert one["unsat_sound"] + one["unsat_heuristic"] == one["unsat"]
     assert sum(one["sat_by_stage"].values()) == one["sat"]
@@ -73,6 +73,12 @@ def test_sound_fields_exclude_heuristic_and_milp():
     assert d["unsat_sound"] == d["unsat"] - us["milp"] - us["heuristic"]
     sound = d["sat"] + d["unsat"] - us["milp"] - us["heuristic"] - d["sat_by_stage"]["heuristic"]
     assert abs(d["pct_verified_sound"] - round(100.0 * sound / att, 3)) < 1e-9
+    # the headline value is the SOUND decided rate (heuristic / MILP verdicts excluded); the
+    # all-verdict rate is the secondary field
+    wall = d["ms_per_step"] * d["steps"] / 1000.0
+    assert abs(d["value"] - sound / wall) <= 1e-3 * max(1.0, d["value"]), (d["value"], sound, wall)
+    assert abs(d["decided_per_s_all"] - (d["sat"] + d["unsat"]) / wall) <= 1e-3 * max(1.0, d["decided_per_s_all"])
+    assert d["value"] < d["decided_per_s_all"]
     # default: an untrusted MILP 'unsat' is no verdict (MILP stage: --lp-budget 0) ...
     d2 = _bench(1, ("--models", "AC-8", "--node-budget", "8", "--escalate-budget", "0", "--smt", "milp",
                     "--relu-budget", "0", "--lp-budget", "0"))
@@ -95,7 +101,7 @@ def test_emulated_lpt_shards_cover_the_grid():
     for r in range(4):
         d = _bench(1, ("--emulate-shard", f"{r}/4"))
         dd = d["dist"]
-        assert dd["balance"] == "lpt" and dd["cost_ratio"] <= dd["cost_bound"], dd
+        assert dd["balance"] == "lpt" and dd["predicted_cost_ratio"] <= dd["predicted_cost_bound"], dd
         for k in tot:
             tot[k] += d[k]
     for k in tot:

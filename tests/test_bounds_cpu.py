@@ -131,3 +131,68 @@ def test_output_forms_pointwise_sound(crown):
         assert np.all(z >= Lf - 1e-9), (seed, float((z - Lf).min()))
         assert np.all(z <= Uf + 1e-9), (seed, float((Uf - z).min()))
         assert z.min() >= float(r.out_lb[0]) and z.max() <= float(r.out_ub[0])
+
+
+def _pre_activations(m, x):
+    """Pre-activation of every layer at points x (fp64)."""
+    h = np.asarray(x, dtype=np.float64)
+    out = []
+    for l, (w, b) in enumerate(zip(m.weights, m.biases)):
+        z = h @ w.astype(np.float64) + b.astype(np.float64)
+        out.append(z)
+        h = np.maximum(z, 0)
+    return out
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_refined_layer_bounds_sound_and_tighter(seed):
+    """ref.crown_refine: every lattice point's hidden pre-activations lie inside the refined bounds,
+    which are never looser than the forward ones; the output forms computed on them stay sound."""
+    import itertools
+
+    from fairify_amd.models.mlp import random_mlp
+    from fairify_amd.ops import reference as ref
+    from fairify_amd.ops.backend import Backend
+
+    g = np.random.default_rng(100 + seed)
+    n0 = 13 if seed % 2 else 6
+    hidden = [[64, 32, 16, 8, 4], [10, 10, 10, 10], [16, 16, 16], [8, 8, 8]][seed % 4]
+    m = random_mlp(n0, hidden, seed=seed, bias_scale=0.0 if seed % 3 == 0 else 0.4)
+    be = Backend(m, "cpu")
+    lo = g.integers(0, 5, size=(1, n0))
+    hi = lo.copy()
+    dims = g.choice(n0, size=min(n0, 4), replace=False)
+    hi[0, dims] += g.integers(1, 4, size=dims.size)
+    pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[0], hi[0])])))
+    L_, H_ = torch.tensor(lo, dtype=torch.float32), torch.tensor(hi, dtype=torch.float32)
+    fw = ref.bounds(be.ws, be.bs, L_, H_, mode="symbolic", keep_layers=True, unit=be.unit)
+    rf = ref.crown_refine(be.ws, be.bs, L_, H_, fw, unit=be.unit)
+    z = _pre_activations(m, pts)
+    for k in range(len(hidden)):
+        lb, ub = rf.layer_lb[k][0].double().numpy(), rf.layer_ub[k][0].double().numpy()
+        assert np.all(z[k] >= lb - 1e-9) and np.all(z[k] <= ub + 1e-9), (seed, k)
+        assert np.all(lb >= fw.layer_lb[k][0].double().numpy()) and np.all(ub <= fw.layer_ub[k][0].double().numpy())
+    r = be.bounds(L_, H_, mode="symbolic", crown=True, refine=True)
+    zl = m.logits(pts)
+    Lf = pts @ r.Lc[0].double().numpy() + float(r.L0[0]) - float(r.Le[0])
+    Uf = pts @ r.Uc[0].double().numpy() + float(r.U0[0]) + float(r.Ue[0])
+    assert np.all(zl >= Lf - 1e-9) and np.all(zl <= Uf + 1e-9)
+    assert zl.min() >= float(r.out_lb[0]) and zl.max() <= float(r.out_ub[0])
+
+
+def test_refine_tightens_deep_net():
+    """On the deep AC-7 shape the back-substituted bounds are strictly tighter somewhere."""
+    from fairify_amd.models.mlp import random_mlp
+    from fairify_amd.ops import reference as ref
+    from fairify_amd.ops.backend import Backend
+
+    m = random_mlp(13, [64, 32, 16, 8, 4], seed=7)
+    be = Backend(m, "cpu")
+    g = np.random.default_rng(3)
+    lo = g.integers(0, 30, size=(32, 13)).astype(np.float32)
+    hi = lo + g.integers(0, 10, size=(32, 13)).astype(np.float32)
+    fw = ref.bounds(be.ws, be.bs, torch.from_numpy(lo), torch.from_numpy(hi), mode="symbolic", keep_layers=True)
+    rf = ref.crown_refine(be.ws, be.bs, torch.from_numpy(lo), torch.from_numpy(hi), fw)
+    gain = sum(float((rf.layer_ub[k] - rf.layer_lb[k]).sum()) for k in range(1, 5))
+    base = sum(float((fw.layer_ub[k] - fw.layer_lb[k]).sum()) for k in range(1, 5))
+    assert gain < 0.9 * base

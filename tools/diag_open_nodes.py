@@ -183,6 +183,8 @@ def main():
     ap.add_argument("--bound", default="fwd", choices=["fwd", "crown", "both", "zero", "one", "fwd+zero", "fwd+zero+one",
                                                        "fullcrown", "fwd+fullcrown"])
     ap.add_argument("--split", default="cert", choices=["cert", "strong", "smear"])
+    ap.add_argument("--residue", default=None, help="npz of tools/dump_residue.py: its UNKNOWN ids instead of the order")
+    ap.add_argument("--summary-only", action="store_true")
     args = ap.parse_args()
     from fairify_amd import presets
     from fairify_amd.engine.bab import _pa_table
@@ -195,6 +197,9 @@ def main():
     grid = pre.grid()
     q = pre.resolved()
     order = processing_order(grid, seed=0)[:args.partitions]
+    if args.residue:
+        z = np.load(args.residue)
+        order = z["grid_id"][z["verdict"] == "unknown"][:args.partitions]
     m = get_model(args.model, weights=args.weights, seed=0)
     be = Backend(m, device="cpu")
     lo_np, hi_np = grid.decode(order)
@@ -272,6 +277,10 @@ def main():
     print(f"BaB {time.time() - t0:.1f}s", flush=True)
     open_parts = torch.unique(part)
     print(f"partitions open at budget {args.budget}: {open_parts.numel()} / {P}")
+    closed = np.setdiff1d(np.arange(P), open_parts.numpy())
+    print("nodes of closed partitions:", sorted(nodes[closed].tolist()), "total nodes", int(nodes.sum()))
+    if args.summary_only:
+        return
     # classify the open partitions by sampled logit range (row v = each PA value)
     ws = [w.double() for w in be.ws]; bs_ = [b.double() for b in be.bs]
     def net(x):

@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="src/AC-sex")
-    ap.add_argument("--models", default="AC-8,AC-12,AC-7")
+    ap.add_argument("--models", default="AC-1,AC-2,AC-3,AC-4,AC-5,AC-6,AC-7,AC-8,AC-9,AC-10,AC-11,AC-12")
     ap.add_argument("--limit", type=int, default=4000)
     ap.add_argument("--out", default="gpurun_out/residue")
     args = ap.parse_args()
@@ -42,7 +42,8 @@ def main():
     cfg = VerifyConfig(sim_size=pre.sim_size, chunk=4096, soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
                        node_budget=512, heuristic=False, heuristic_p=pre.heuristic_p, escalate_budget=32768,
                        escalate_max_open=384, smt_backend="none",
-                       escalate_probation=((2048, 768), (4096, 768), (8192, 768), (16384, 1024)))
+                       escalate_probation=((2048, 768), (4096, 768), (8192, 768), (16384, 1024)),
+                       relu_budget=1024, relu_max_width=16, relu_escalate_cap=2048)
     os.makedirs(args.out, exist_ok=True)
     for name in args.models.split(","):
         m = get_model(name, weights="random", seed=0)
