@@ -19,6 +19,7 @@ namespace py = pybind11;
 
 extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream);
 extern "C" int fa_crown_phase_launch(const NetDesc& net, CrownPhaseArgs a, hipStream_t stream);
+extern "C" size_t fa_crown_phase_bytes(const NetDesc& net);
 extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_forward_launch(const NetDesc& net, FwdArgs a, hipStream_t stream);
 extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream);
@@ -182,6 +183,9 @@ PYBIND11_MODULE(_C, m) {
     const int rc = fa_crown_phase_launch(net.d, a, (hipStream_t)stream);
     if (rc != 0) throw std::runtime_error("crown_phase launch failed, code " + std::to_string(rc));
   });
+
+  // does the ReLU-phase backward kernel hold this network (layers <= 256 wide, LDS <= 160 KB)?
+  m.def("relu_fits", [](const Net& net) { return fa_crown_phase_bytes(net.d) > 0; });
 
   // backward output bounds refining forms/out bounds written by a preceding `bounds` call
   m.def("crown", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t dead_in, int R,

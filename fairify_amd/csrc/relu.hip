@@ -270,9 +270,28 @@ __global__ void __launch_bounds__(64 * FA_CP_WAVES) fa_crown_phase_kernel(NetDes
   }
 }
 
+// LDS bytes of fa_crown_phase_kernel for `net`, 0 if it does not fit (a layer wider than 256 or
+// more than 160 KB): checked before a ReluRuntime is built (engine/relu_bab.py), so a network the
+// kernel cannot hold skips the relu stage instead of aborting a level
+extern "C" size_t fa_crown_phase_bytes(const NetDesc& net) {
+  int wmax = 1;
+  for (int l = 0; l <= net.n_layers; ++l) {
+    if (net.dims[l] > 256) return 0;
+    if (l > 0) wmax = std::max(wmax, net.dims[l]);
+  }
+  int G = 4;
+  while (G < wmax && G < 64) G *= 2;
+  const int WP = (std::max(wmax, net.dims[0]) + 3) & ~3;
+  const int nparams = net.b_off[net.n_layers - 1] + net.dims[net.n_layers];
+  const int rows_per_block = FA_CP_WAVES * (64 / G);
+  const size_t bytes = ((size_t)nparams + (size_t)rows_per_block * (5 * WP + 1)) * sizeof(float);
+  return bytes > 160 * 1024 ? 0 : bytes;
+}
+
 // 0 launched, -1 the network does not fit (layer wider than 256 or LDS), < -1 launch error
 extern "C" int fa_crown_phase_launch(const NetDesc& net, CrownPhaseArgs a, hipStream_t stream) {
   if (a.R <= 0) return 0;
+  if (fa_crown_phase_bytes(net) == 0) return -1;
   int wmax = 1;
   for (int l = 0; l <= net.n_layers; ++l) {
     if (net.dims[l] > 256) return -1;
@@ -339,6 +358,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
     const int vA = (int)a.pairs[2 * a.pair[n]], vB = (int)a.pairs[2 * a.pair[n] + 1];
     float ca[NM], cb[NM], xl[NM], xh[NM];
     float fA = 0.f, fB = 0.f;
+    float fmA = 0.f, fmB = 0.f;          // sum |ca_i v_k|: the folded products' rounding magnitude
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       const bool v = i < n0;
@@ -354,13 +374,16 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
         if (i == d) {
           fA += ca[i] * a.values[vA * a.npa + k];
           fB += cb[i] * a.values[vB * a.npa + k];
+          fmA += fabsf(ca[i] * a.values[vA * a.npa + k]);
+          fmB += fabsf(cb[i] * a.values[vB * a.npa + k]);
           ca[i] = cb[i] = 0.f;
           xl[i] = xh[i] = 0.f;
         }
     }
     const float LA0 = a.L0[A] - a.Le[A];
     const float UB0 = a.U0[B] + a.Ue[B];
-    float magA = fabsf(LA0) + fabsf(fA), magB = fabsf(UB0) + fabsf(fB);
+    // with several PA dims the folded sum can cancel: the margin takes the terms' magnitudes
+    float magA = fabsf(LA0) + fmA, magB = fabsf(UB0) + fmB;
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       const float mx = fmaxf(fabsf(xl[i]), fabsf(xh[i]));

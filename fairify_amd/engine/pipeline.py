@@ -263,10 +263,20 @@ def _lp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, budget, limit,
             cex_x[k], cex_xp[k] = pair[0], pair[1]
 
 
+def _lp_available() -> bool:
+    """The verified-LP stage drives HiGHS through SciPy's private ``_highspy._core`` bindings (SciPy
+    >= 1.15); without them the stage is off and the MILP stage runs instead of an aborting worker."""
+    try:
+        from scipy.optimize._highspy import _core  # noqa: F401
+    except ImportError:
+        return False
+    return True
+
+
 def _use_lp(cfg, q) -> bool:
     from ..smt import lpbab  # noqa: F401  (SciPy present: the MILP back-end resolved)
 
-    return cfg.lp_budget > 0 and not cfg.trust_milp and not q.relaxed
+    return cfg.lp_budget > 0 and not cfg.trust_milp and not q.relaxed and _lp_available()
 
 
 def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.ndarray, cfg: VerifyConfig,

@@ -214,8 +214,10 @@ class ReluBaBSolver:
             fa_A = (LAc[:, pa] * values[vA]).sum(1)
             fa_B = (UBc[:, pa] * values[vB]).sum(1)
             mxb = torch.maximum(lo.abs(), hi.abs())
-            MA = (LAc.abs() * mxb * free).sum(1) + (LA0 - LAe).abs() + fa_A.abs()
-            MB = (UBc.abs() * mxb * free).sum(1) + (UB0 + UBe).abs() + fa_B.abs()
+            # rounding margin over the folded PA products' magnitudes (with several PA dims their
+            # sum can cancel below the products' errors)
+            MA = (LAc.abs() * mxb * free).sum(1) + (LA0 - LAe).abs() + (LAc[:, pa] * values[vA]).abs().sum(1)
+            MB = (UBc.abs() * mxb * free).sum(1) + (UB0 + UBe).abs() + (UBc[:, pa] * values[vB]).abs().sum(1)
             g, tstar, xstar = certify_pair(LAc, LA0 - LAe + fa_A, MA, UBc, UB0 + UBe + fa_B, MB, lo, hi, free, be.unit)
             open_ = ~closed & (g > 0)
             # ---- candidate vertex pairs of open nodes: rigorous point bounds, then the exact check
@@ -322,6 +324,15 @@ class ReluBaBSolver:
 
     def _solve_native(self, lo_np, hi_np, mlp_exact, status, values_np, pairs_np, time_budget):
         P, n0 = lo_np.shape
+        from ..ops import ext
+        from ..ops.hip import _net
+
+        if not ext().relu_fits(_net(self.be)):
+            # the phase kernel cannot hold this network (a layer > 256 wide or > 160 KB of LDS):
+            # the stage is skipped, its partitions stay UNKNOWN for the later stages
+            status = status.copy()
+            status[status == RUNNING] = UNKNOWN
+            return status, np.zeros((P, n0), np.int64), np.zeros((P, n0), np.int64), np.zeros(P, np.int64)
         n_root = int((status == RUNNING).sum()) * max(1, pairs_np.shape[0])
         if pairs_np.shape[0] == 0:
             status = status.copy()

@@ -177,3 +177,40 @@ def test_pipeline_relu_stage_and_anytime_rounds():
         X, XP = r.cols["cex_x"][sat], r.cols["cex_xp"][sat]
         assert exact.check_pair_constraints(X, XP, lo, hi, q.pa_idx, q.ra_idx, q.tau).all()
         assert exact.is_violation(m, X, XP).all()
+
+
+def test_relu_bab_two_protected_attributes_matches_bruteforce():
+    """Two PA dims (race, sex): the pair certificate folds both PA coordinates into the constants;
+    its rounding margin takes the folded products' magnitudes (their sum can cancel).  Every PA must
+    differ (src/GC/Verify-GC.py:135-141): verdicts equal enumeration of all (x, x') pairs."""
+    from fairify_amd.spec import ADULT, Query
+
+    q = Query(pa=("race", "sex")).resolve(ADULT)
+    pre = presets.get("src/AC-sex")
+    grid = pre.grid()
+    ids = processing_order(grid, 0)[:24]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 1)
+    ri, si = q.pa_idx
+    for seed in (5, 6):
+        m = random_mlp(13, [6, 6], seed=seed, bias_scale=0.5)
+        res = ReluBaBSolver(Backend(m), q, ReluConfig(node_budget=4096)).solve(lo, hi, m)
+        for k in range(len(ids)):
+            rv = range(int(lo[k, ri]), int(hi[k, ri]) + 1)
+            free = [range(a, b + 1) for a, b in zip(lo[k], hi[k])]
+            pts = np.array(list(itertools.product(*free)))
+            viol = False
+            for r1, r2 in itertools.product(rv, rv):
+                if r1 == r2:
+                    continue
+                for s1 in (0, 1):
+                    x = pts.copy(); x[:, ri] = r1; x[:, si] = s1
+                    xp = pts.copy(); xp[:, ri] = r2; xp[:, si] = 1 - s1
+                    z, zp = m.logits(x), m.logits(xp)
+                    if (((z > 0) & (zp < 0)) | ((z < 0) & (zp > 0))).any():
+                        viol = True
+                        break
+                if viol:
+                    break
+            if res.status[k] != UNKNOWN:
+                assert (res.status[k] == SAT) == viol, (seed, k)
