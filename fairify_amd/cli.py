@@ -39,6 +39,14 @@ def cmd_presets(args):
 
 
 def cmd_verify(args):
+    import os
+
+    from .parallel import balance as BL
+
+    # several ranks per node (torchrun): each takes the CPUs local to its GPU (sysfs NUMA locality,
+    # parallel/balance.py) for its host threads / HIP streams / LP workers, before the GPU is touched
+    BL.pin_rank(int(os.environ.get("LOCAL_RANK", "0")),
+                int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
     from . import presets
     from .engine.pipeline import VerifyConfig
     from .engine.runner import run_preset
@@ -66,7 +74,7 @@ def cmd_verify(args):
                accuracy=not args.no_accuracy, escalate=args.escalate,
                concurrency=args.concurrency or (4 if info.device.type == "cuda" else 1),
                anytime_budget=(args.anytime_budget or cfg.hard_timeout) if args.anytime else None,
-               metrics_csv=True if args.metrics_csv else None)
+               metrics_csv=True if args.metrics_csv else None, balance=args.balance)
     D.destroy(info)
 
 
@@ -191,6 +199,9 @@ def main(argv=None):
                         "--escalate-budget (native BaB; bench default 2048:768,4096:768,8192:768,16384:1024 with --escalate-budget 32768)")
     v.add_argument("--escalate-max-open", type=int, default=0,
                    help="escalate only residue partitions that left <= this many open BaB nodes (0 = all)")
+    v.add_argument("--balance", default="queue", choices=["queue", "strided"],
+                   help="several ranks: claim units of each round from a shared atomic counter (queue, dynamic "
+                        "load balance) or verify fixed strided shares (strided)")
     v.add_argument("--concurrency", type=int, default=0,
                    help="chunks verified at once per rank, one HIP stream each (default 4 on GPU, 1 on CPU)")
     v.add_argument("--smt", default="auto", help="host SMT back-end for the residue: auto | z3py | z3bin | none")

@@ -3,8 +3,13 @@
 Reference flow: ``for model_file in os.listdir(model_dir): for p in p_list: ...`` with one CSV
 append per partition and a per-model hard timeout (src/AC/Verify-AC.py:78-320).  Here:
 
-* the seeded processing order is split into *rounds*; in every round each rank verifies its
-  strided share (``chunk`` partitions) on its own GPU;
+* the seeded processing order is split into *rounds*; in every round the ranks share the round's
+  block of the order through a dynamic unit queue (``balance="queue"``, the default with several
+  ranks): every host thread of every rank claims the next unit of partitions from an atomic counter
+  in the rendezvous store (``store.add``) until the round is exhausted, so a rank that drew
+  expensive partitions simply claims fewer units -- the heavy tail of the BaB (SURVEY §2.4.2 work
+  stealing, §7.5) is balanced without a cost model; ``balance="strided"`` keeps round 1's fixed
+  strided shares;
 * per-partition records are packed into fixed-width rows and ``all_gather``-ed (RCCL) to rank 0,
   which appends them to the reference-format CSV in processing order and checkpoints the set
   of finished positions (``state/<model>.npz``) so ``--resume`` skips them;
@@ -147,6 +152,46 @@ def model_accuracy(mlp, suite: str, seed: int = 0, with_source: bool = False):
     return acc
 
 
+def _claim_fn(info: D.DistInfo):
+    """Atomic unit counter shared by all ranks (the process group's rendezvous store: TCPStore
+    ``add`` is one round trip, thread-safe); single process: a local counter."""
+    if info.initialized:
+        import torch.distributed.distributed_c10d as c10d
+
+        store = c10d._get_default_store()
+        return lambda key: int(store.add(key, 1)) - 1
+    import itertools
+    import threading
+
+    counters: Dict[str, "itertools.count"] = {}
+    lock = threading.Lock()
+
+    def claim(key):
+        with lock:
+            return next(counters.setdefault(key, itertools.count()))
+
+    return claim
+
+
+def queue_unit_size(n_round: int, world: int, workers: int, chunk: int) -> int:
+    """Partitions per claimed unit: about 4 units per host thread of every rank (enough slack for
+    the dynamic queue to even out heavy partitions), never more than a chunk."""
+    return int(max(1, min(chunk, -(-n_round // max(1, 4 * world * workers)))))
+
+
+def _pack_positions(pos: np.ndarray, buf: np.ndarray) -> np.ndarray:
+    """Prefix a rank's wire buffer with the (claimed, hence not recomputable) positions it verified."""
+    pos = np.ascontiguousarray(pos, dtype=np.int64)
+    head = np.array([pos.size], dtype=np.int64)
+    return np.concatenate([head.view(np.uint8), pos.view(np.uint8), np.asarray(buf, dtype=np.uint8).reshape(-1)])
+
+
+def _unpack_positions(b: np.ndarray):
+    n = int(np.frombuffer(b[:8].tobytes(), dtype=np.int64)[0])
+    pos = np.frombuffer(b[8:8 + 8 * n].tobytes(), dtype=np.int64).copy()
+    return pos, b[8 + 8 * n:]
+
+
 def _round_positions(todo: np.ndarray, r: int, per_round: int, world: int) -> List[np.ndarray]:
     """Every rank's positions of round ``r`` (rank k verifies ``todo[k::world]`` in rounds of
     ``per_round``); rank 0 uses this instead of receiving positions over the wire."""
@@ -229,7 +274,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                max_partitions: Optional[int] = None, resume: bool = False, seed: int = 0,
                accuracy: bool = True, verbose: bool = True, escalate: int = 1,
                concurrency: int = 1, anytime_budget: Optional[float] = None,
-               metrics_csv: Optional[bool] = None) -> List[Dict]:
+               metrics_csv: Optional[bool] = None, balance: str = "queue") -> List[Dict]:
     """``escalate`` > 1: every round's UNKNOWN partitions are re-distributed over all ranks and
     retried with ``escalate`` x the node budget (residual work stealing).  ``concurrency`` > 1:
     each rank verifies that many chunks of a round at once, one host thread + HIP stream each
@@ -239,8 +284,13 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
     falsifier rounds over its UNKNOWN residue (VerifyConfig.anytime_seconds).  ``metrics_csv``
     (default: on for the fork's ``experiment/*`` presets): rank 0 also writes the per-partition
     ``synthetic-<dataset>-predicted-<family>-metrics.csv`` of the experiment drivers
-    (src/AC/Verify-AC-experiment-new.py:482-542)."""
+    (src/AC/Verify-AC-experiment-new.py:482-542).  ``balance``: "queue" (several ranks: dynamic
+    unit claiming from the store, see the module docstring) or "strided"."""
     info = info or D.DistInfo()
+    if balance not in ("queue", "strided"):
+        raise ValueError(f"balance must be 'queue' or 'strided', got {balance!r}")
+    queue = balance == "queue" and info.world > 1
+    claim = _claim_fn(info) if queue else None
     grid = preset.grid(seed=seed)
     q = preset.resolved()
     order = processing_order(grid, seed=seed)
@@ -283,12 +333,16 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         stopped = False
         last_note = time.time()
         inflight = None      # (async gather handle, per-rank positions) of the previous round
+        rank_work = [0.0, 0]  # this rank's BaB node expansions and partitions (balance report)
 
         def flush(item):
             handle, rpos, retried = item
             bufs = handle.wait()
             if not info.is_main:
                 return
+            if rpos is None:        # unit queue: every rank's buffer carries its claimed positions
+                split = [_unpack_positions(b) for b in bufs]
+                rpos, bufs = [p for p, _ in split], [b for _, b in split]
             parts = [(p, wire.decode(b, order[p], acc, mlp.n_neurons, cfg.sim_size, q)) for p, b in zip(rpos, bufs)]
             gpos, grecs = wire.merge_rounds(parts)
             if grecs is None:
@@ -314,30 +368,62 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             if elapsed > cfg.hard_timeout:
                 stopped = True
                 break
-            rpos = _round_positions(todo, r, per_round, info.world)
-            pos = rpos[info.rank]
+            rblock = todo[r * per_round * info.world:(r + 1) * per_round * info.world]
+            rpos = None if queue else _round_positions(todo, r, per_round, info.world)
             buf = wire.empty(q)
             codes = np.zeros(0, np.int8)
             rcfg = cfg
             if anytime_budget:
                 # this round's share of the remaining per-model budget (all ranks agree: the
                 # elapsed time is the global max and the round sizes are known everywhere)
-                n_round = sum(len(p) for p in rpos)
+                n_round = len(rblock)
                 n_left = len(todo) - r * per_round * info.world
                 share = max(0.0, (min(anytime_budget, cfg.hard_timeout) - elapsed) * n_round / max(1, n_left))
                 rcfg = replace(cfg, anytime_seconds=0.9 * share)
-            if len(pos):
-                subs = [pos[s:s + cfg.chunk] for s in range(0, len(pos), cfg.chunk)]
-                recs = concat_records(streams.run(
-                    lambda sp: verify_chunk(be, mlp, q, grid, order[sp], rcfg, orig_acc=acc,
-                                            time_budget=cfg.hard_timeout - elapsed, timer=timer), subs))
+
+            def run_ids(sp):
+                return verify_chunk(be, mlp, q, grid, order[sp], rcfg, orig_acc=acc,
+                                    time_budget=cfg.hard_timeout - elapsed, timer=timer)
+
+            recs = None
+            if queue:
+                U = queue_unit_size(len(rblock), info.world, streams.workers, cfg.chunk)
+                n_units = -(-len(rblock) // U)
+                key = f"fairify/units/{preset.name}/{name}/{seed}/{r}"
+
+                def worker(_):
+                    done_units = []
+                    while True:
+                        u = claim(key)
+                        if u >= n_units:
+                            return done_units
+                        sp = rblock[u * U:(u + 1) * U]
+                        done_units.append((u, sp, run_ids(sp)))
+
+                got = sorted((it for lst in streams.run(worker, [None] * streams.workers) for it in lst),
+                             key=lambda it: it[0])
+                pos = np.concatenate([sp for _, sp, _ in got]) if got else np.zeros(0, np.int64)
+                if got:
+                    recs = concat_records([rc for _, _, rc in got])
+            else:
+                pos = rpos[info.rank]
+                if len(pos):
+                    subs = [pos[s:s + cfg.chunk] for s in range(0, len(pos), cfg.chunk)]
+                    recs = concat_records(streams.run(run_ids, subs))
+            if recs is not None:
                 buf = wire.encode(recs, q)
                 codes = wire.verdict_codes(recs)
+                rank_work[0] += float(recs.core["nodes"].sum())
+                rank_work[1] += len(recs)
             retried = None
             if escalate > 1:
                 all_codes = D.all_gather_int8(info, codes)
-                retried = _residual_pass(be, mlp, q, grid, order, np.concatenate(rpos), all_codes, cfg, escalate,
+                all_pos = (D.all_gather_rows(info, np.asarray(pos, np.int64).reshape(-1, 1)).reshape(-1) if queue
+                           else np.concatenate(rpos))
+                retried = _residual_pass(be, mlp, q, grid, order, all_pos, all_codes, cfg, escalate,
                                          acc, info, timer, cfg.hard_timeout - elapsed)
+            if queue:
+                buf = _pack_positions(pos, buf)
             # this round's results travel to rank 0 while the next round computes
             handle = D.gather_bytes(info, buf, async_op=True)
             if inflight is not None:
@@ -363,7 +449,10 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             io.shutdown(wait=True)
         if mwriter is not None:
             mwriter.close()
-        wall = D.all_reduce_max(info, time.time() - t0)
+        rank_busy = time.time() - t0
+        wall = D.all_reduce_max(info, rank_busy)
+        rank_nodes = D.all_gather_floats(info, rank_work[0])
+        rank_parts = D.all_gather_floats(info, float(rank_work[1]))
         if info.is_main:
             tc = {k: (np.concatenate(v) if v else np.zeros(0)) for k, v in table_cols.items()}
             stage_codes = tc.pop("stage").astype(np.int64)
@@ -389,6 +478,9 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             if anytime_budget:
                 row["anytime_budget_s"] = float(anytime_budget)
             row["wire_bytes_per_partition"] = round(wire_bytes[0] / max(1, wire_bytes[1]), 2)
+            row["balance"] = "queue" if queue else ("strided" if info.world > 1 else "none")
+            row["rank_nodes"] = [int(v) for v in rank_nodes]
+            row["rank_partitions"] = [int(v) for v in rank_parts]
             if cfg.keep_masks and mask_parts:
                 from ..report.masks import write_masks
 
