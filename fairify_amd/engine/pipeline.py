@@ -276,7 +276,7 @@ def _lp_available() -> bool:
 def _use_lp(cfg, q) -> bool:
     from ..smt import lpbab  # noqa: F401  (SciPy present: the MILP back-end resolved)
 
-    return cfg.lp_budget > 0 and not cfg.trust_milp and not q.relaxed and _lp_available()
+    return cfg.lp_budget > 0 and not cfg.trust_milp and _lp_available()
 
 
 def verify_chunk(be: Backend, mlp: MLP, q: ResolvedQuery, grid: Grid, ids: np.ndarray, cfg: VerifyConfig,

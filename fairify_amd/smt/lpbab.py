@@ -51,12 +51,21 @@ def _gamma(k: int) -> float:
 
 class _LP:
     """Two-copy LP of one ordered PA pair with exact data.  Variables: [one | x (n0) | PA dims of
-    x' | per copy and layer: h (w_l), a (unstable) | t]; rows two-sided (lo <= A v <= hi)."""
+    x' | RA dims of x' (relaxed queries) | per copy and layer: h (w_l), a (unstable) | t]; rows
+    two-sided (lo <= A v <= hi)."""
 
-    def __init__(self, weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, sign: int = 0):
+    def __init__(self, weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, sign: int = 0,
+                 ra_idx: Sequence[int] = (), tau: float = 0.0, orient: int = 1):
         """``sign`` = 0: the pair LP (maximise t, t <= -N(x, va), t <= N(x', vb)); ``sign`` = -1 / +1:
         ONE copy, maximise t with t <= -N(x, va) / t <= N(x, va) (a certified t <= 0 proves that
-        no point of the box has N(x, va) < 0 / > 0)."""
+        no point of the box has N(x, va) < 0 / > 0).
+
+        Relaxed queries (``ra_idx``, ``tau`` > 0; reference semantics relaxed/BM/Verify-BM.py:53-54,
+        utils/verif_utils.py:879-887): x' has its own integer variable on every RA dim, NOT clipped
+        to the partition box (range [lo - tau, hi + tau]), tied to x by -tau <= x'_r - x_r <= tau;
+        ``bounds_b`` are then the per-layer bounds over that widened box.  ``orient`` = -1: the
+        other orientation, t <= N(x, va), t <= -N(x', vb) (with x' outside the box, swapping the
+        pair does not cover it as it does for PA-only queries)."""
         self.nv = 0
         self.lb: List[float] = []
         self.ub: List[float] = []
@@ -93,6 +102,16 @@ class _LP:
         xpa = var(np.asarray(vb, np.float64), np.asarray(vb, np.float64))
         for k, d in enumerate(pa):
             xb[d] = xpa[k]
+        self.ra = [int(d) for d in ra_idx] if (tau > 0 and not sign) else []
+        self.tau = float(tau)
+        self.xr = np.zeros(0, np.int64)
+        if self.ra:
+            self.xr = var(lo[self.ra].astype(np.float64) - tau, hi[self.ra].astype(np.float64) + tau)
+            for k, d in enumerate(self.ra):
+                xb[d] = self.xr[k]
+                row([self.xr[k], self.x[d]], [1.0, -1.0], -float(tau), float(tau))
+        self.pa = pa
+        self.vb = np.asarray(vb, np.int64)
         self.a_vars: List[Tuple[int, int, int, int, int]] = []   # (a var, h var, copy, layer, neuron)
         self.z_rows = []                                       # (copy, layer, neuron) -> (h, prev, W col, b)
         outs = []
@@ -135,10 +154,12 @@ class _LP:
             + float(np.abs(wb) @ np.maximum(np.asarray(self.ub)[pb_h], 0))
         M = float(np.nextafter(2.0 * M, np.inf))
         self.t = var([-M], [M])[0]
-        if sign <= 0:    # t <= -N(x, va)
-            row(np.concatenate([[self.t], pa_h, [self.one]]), np.concatenate([[1.0], wa, [ba]]), -np.inf, 0.0)
-        if sign >= 0:    # t <= N(x', vb)  (sign mode: N(x, va))
-            row(np.concatenate([[self.t], pb_h, [self.one]]), np.concatenate([[1.0], -wb, [-bb]]), -np.inf, 0.0)
+        o = 1.0 if (sign or orient >= 0) else -1.0
+        if sign <= 0:    # t <= -o N(x, va)
+            row(np.concatenate([[self.t], pa_h, [self.one]]), np.concatenate([[1.0], o * wa, [o * ba]]), -np.inf, 0.0)
+        if sign >= 0:    # t <= o N(x', vb)  (sign mode: N(x, va))
+            row(np.concatenate([[self.t], pb_h, [self.one]]), np.concatenate([[1.0], -o * wb, [-o * bb]]), -np.inf,
+                0.0)
         from scipy.sparse import coo_matrix
 
         self.A = coo_matrix((np.concatenate(rv), (np.concatenate(ri), np.concatenate(rj))),
@@ -152,6 +173,24 @@ class _LP:
         self.c[self.t] = -1.0
         self._h = None          # persistent HiGHS model (warm starts), built on the first solve
         self._h1 = None         # its elastic phase-1 twin (infeasibility certificates)
+        # integer input variables: the non-PA dims of x, then the RA dims of x' -- a node whose
+        # integer variables are all fixed is one lattice pair, decided exactly
+        isx = np.ones(n0, bool)
+        isx[pa] = False
+        self.ivars = np.concatenate([self.x[isx], self.xr]).astype(np.int64)
+
+    def pair(self, v: np.ndarray, lb: np.ndarray, ub: np.ndarray):
+        """Lattice pair (x, x') from a variable vector (rounded into the node's bounds; x'_r also
+        into x_r +- tau), PA dims of x' = vb."""
+        xs = np.clip(np.rint(v[self.x]), lb[self.x], ub[self.x]).astype(np.int64)
+        xps = xs.copy()
+        xps[self.pa] = self.vb
+        for k, d in enumerate(self.ra):
+            j = self.xr[k]
+            lo_ = max(lb[j], xs[d] - self.tau)
+            hi_ = min(ub[j], xs[d] + self.tau)
+            xps[d] = int(np.clip(np.rint(v[j]), lo_, max(lo_, hi_)))
+        return xs, xps
 
     # ------------------------------------------------------------------------------------------
     def _highs(self, elastic: bool):
@@ -331,21 +370,20 @@ def certified_bound_rows(d, A, rlo, rhi, lam, lb, ub) -> float:
     return float(np.nextafter(bound, np.inf)) if math.isfinite(bound) else math.inf
 
 
-def _lp_bab(lp: "_LP", pa, va, node_budget: int, deadline: float, hit) -> Tuple[str, Optional[np.ndarray], int]:
+def _lp_bab(lp: "_LP", pa, va, node_budget: int, deadline: float, hit) -> Tuple[str, Optional[tuple], int]:
     """Best-first LP branch-and-bound over ``lp``: ('closed', None, nodes) when every node closed,
-    ('hit', x, nodes) when ``hit(x)`` (integer x, PA dims = va) accepted a lattice point (a leaf,
-    or the rounded LP optimum of a node whose LP value is > 0), ('unknown', None, nodes) at the node
-    budget / deadline."""
-    isx = np.ones(lp.n0, bool)
-    isx[pa] = False
+    ('hit', (x, x'), nodes) when ``hit(x, x')`` (integers, PA dims = va / vb) accepted a lattice
+    pair (a leaf, or the rounded LP optimum of a node whose LP value is > 0), ('unknown', None,
+    nodes) at the node budget / deadline."""
+    iv = lp.ivars
     tried = set()
 
-    def check(xs) -> bool:
-        key = xs.tobytes()
+    def check(xs, xps) -> bool:
+        key = xs.tobytes() + xps.tobytes()
         if key in tried:
             return False
         tried.add(key)
-        return bool(hit(xs))
+        return bool(hit(xs, xps))
 
     heap = [(0.0, 0, lp.lb.copy(), lp.ub.copy(), None)]   # best-first on the certified bound;
     # each entry carries its parent's simplex basis (a child differs by one bound: ~1 pivot)
@@ -356,21 +394,20 @@ def _lp_bab(lp: "_LP", pa, va, node_budget: int, deadline: float, hit) -> Tuple[
             return "unknown", None, nodes
         _, _, nlb, nub, pbasis = heapq.heappop(heap)
         nodes += 1
-        xl, xh = nlb[lp.x], nub[lp.x]
-        if bool(np.all(xl[isx] == xh[isx])):
-            # a single lattice point: decided exactly (the LP's rounding slack cannot close an
-            # exactly-zero logit, the exact checker can)
-            xs = xl.astype(np.int64)
-            if check(xs):
-                return "hit", xs, nodes
+        if bool(np.all(nlb[iv] == nub[iv])):
+            # a single lattice pair: decided exactly (the LP's rounding slack cannot close an
+            # exactly-zero logit, the exact checker can); the pair constraints are the checker's
+            xs, xps = lp.pair(nlb, nlb, nub)
+            if check(xs, xps):
+                return "hit", (xs, xps), nodes
             continue
         t_lp, cert, v, basis = lp.solve(nlb, nub, pbasis)
         if cert <= 0.0:
             continue
         if t_lp is not None and t_lp > 0:
-            xs = np.clip(np.rint(v[lp.x]), xl, xh).astype(np.int64)
-            if check(xs):
-                return "hit", xs, nodes
+            xs, xps = lp.pair(v, nlb, nub)
+            if check(xs, xps):
+                return "hit", (xs, xps), nodes
         # branch: the unfixed binary whose relaxation the LP optimum exploits most
         best, bi = 0.0, -1
         for i, (a, h, cp, l, j) in enumerate(lp.a_vars if v is not None else ()):
@@ -389,13 +426,14 @@ def _lp_bab(lp: "_LP", pa, va, node_budget: int, deadline: float, hit) -> Tuple[
                 children.append((clb, cub))
         else:
             # the relaxation is not what keeps the node open (or the LP gave no certified answer:
-            # an uncertified 'infeasible'): split the widest input dimension
-            wdt = np.where(isx, xh - xl, -1.0)
-            d = int(np.argmax(wdt))
-            mid = math.floor(0.5 * (xl[d] + xh[d]))
-            for lo_d, hi_d in ((xl[d], mid), (mid + 1, xh[d])):
+            # an uncertified 'infeasible'): split the widest integer input variable (x, or x' on
+            # a relaxed dim)
+            wdt = nub[iv] - nlb[iv]
+            j = int(iv[int(np.argmax(wdt))])
+            mid = math.floor(0.5 * (nlb[j] + nub[j]))
+            for lo_d, hi_d in ((nlb[j], mid), (mid + 1, nub[j])):
                 clb, cub = nlb.copy(), nub.copy()
-                clb[lp.x[d]], cub[lp.x[d]] = lo_d, hi_d
+                clb[j], cub[j] = lo_d, hi_d
                 children.append((clb, cub))
         for clb, cub in children:
             heapq.heappush(heap, (-cert, tick, clb, cub, basis))
@@ -404,24 +442,16 @@ def _lp_bab(lp: "_LP", pa, va, node_budget: int, deadline: float, hit) -> Tuple[
 
 
 def lp_bab_pair(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, node_budget: int, deadline: float,
-                confirm) -> Tuple[str, Optional[tuple], int]:
+                confirm, ra_idx: Sequence[int] = (), tau: float = 0.0, orient: int = 1
+                ) -> Tuple[str, Optional[tuple], int]:
     """LP branch-and-bound of one ordered PA pair (v, v'): ('unsat', None, nodes) when every node
     closed, ('sat', (x, x'), nodes) with an exactly confirmed pair (``confirm(x, x') -> bool``),
-    ('unknown', None, nodes) at the node budget / deadline."""
-    lp = _LP(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b)
-    pa = list(pa_idx)
-    vb_i = np.asarray(vb, np.int64)
-
-    def hit(xs):
-        xps = xs.copy()
-        xps[pa] = vb_i
-        return confirm(xs, xps)
-
-    st, xs, nodes = _lp_bab(lp, pa, va, node_budget, deadline, hit)
+    ('unknown', None, nodes) at the node budget / deadline.  Relaxed queries: ``ra_idx`` / ``tau``
+    (x' free on the RA dims within tau of x, ``bounds_b`` over the widened box)."""
+    lp = _LP(weights, biases, lo, hi, pa_idx, va, vb, bounds_a, bounds_b, ra_idx=ra_idx, tau=tau, orient=orient)
+    st, wit, nodes = _lp_bab(lp, list(pa_idx), va, node_budget, deadline, confirm)
     if st == "hit":
-        xps = xs.copy()
-        xps[pa] = vb_i
-        return "sat", (xs.tolist(), xps.tolist()), nodes
+        return "sat", (wit[0].tolist(), wit[1].tolist()), nodes
     return ("unsat" if st == "closed" else "unknown"), None, nodes
 
 
@@ -431,44 +461,64 @@ def lp_sign_free(weights, biases, lo, hi, pa_idx, va, bounds_a, sign: int, node_
     sign(N(x, va)) == ``sign`` (-1 / +1) -- certified by the same weak-duality bounds, leaves by
     ``exact_sign(x) -> -1 / 0 / +1``."""
     lp = _LP(weights, biases, lo, hi, pa_idx, va, va, bounds_a, bounds_a, sign=sign)
-    st, _, nodes = _lp_bab(lp, list(pa_idx), va, node_budget, deadline, lambda xs: exact_sign(xs) == sign)
+    st, _, nodes = _lp_bab(lp, list(pa_idx), va, node_budget, deadline, lambda xs, xps: exact_sign(xs) == sign)
     return st == "closed", nodes
 
 
 def solve_partition(weights, biases, lo, hi, pa_idx, values, pairs, row_bounds, node_budget: int,
-                    time_limit: float, confirm, exact_sign=None) -> Tuple[str, Optional[tuple], int]:
+                    time_limit: float, confirm, exact_sign=None, ra_idx: Sequence[int] = (), tau: float = 0.0,
+                    row_bounds_p=None) -> Tuple[str, Optional[tuple], int]:
     """Decide one partition over all ordered PA pairs: 'unsat' (every pair's LP-BaB closed),
     'sat' with an exactly confirmed pair (``confirm(x, x') -> bool``), else 'unknown'.
 
     With more than two ordered pairs (a PA of 3+ values: race has 5, i.e. 20 pairs) and
     ``exact_sign(x) -> -1/0/+1`` given, each value first gets two single-copy sign tests: a value
     v whose logit is certainly never < 0 on the box closes every pair (v, .), one whose logit is
-    never > 0 closes every pair (., v) -- 2V half-size searches shared by V(V-1) pairs."""
+    never > 0 closes every pair (., v) -- 2V half-size searches shared by V(V-1) pairs.
+
+    Relaxed queries (``ra_idx``, ``tau`` > 0): x' ranges over the box widened by tau on the RA dims
+    (``row_bounds_p``: per-layer bounds over it); the 'never > 0' test of x' runs on that box."""
     deadline = time.time() + time_limit
     nodes = 0
-    never_neg, never_pos = {}, {}
+    relaxed = tau > 0 and len(ra_idx) > 0
+    rbp = row_bounds_p if (relaxed and row_bounds_p is not None) else row_bounds
+    if relaxed and row_bounds_p is None:
+        raise ValueError("relaxed query: row_bounds_p (bounds over the widened x' box) required")
+    lo_p, hi_p = lo.astype(np.float64).copy(), hi.astype(np.float64).copy()
+    if relaxed:
+        lo_p[list(ra_idx)] -= tau
+        hi_p[list(ra_idx)] += tau
+    # free[(box, sign)][v]: no lattice point of the box (x: "x", widened x' box: "p") has
+    # sign(N(., v)) == sign
+    free = {("x", -1): {}, ("x", 1): {}, ("p", -1): {}, ("p", 1): {}}
     if exact_sign is not None and len(pairs) > 2:
         vals = sorted({int(v) for pr in pairs for v in pr})
-        sb = max(16, node_budget // (8 * len(vals)))
+        tests = [("x", -1), ("p", 1)] + ([("x", 1), ("p", -1)] if relaxed else [])
+        sb = max(16, node_budget // (4 * len(tests) * len(vals)))
         for v in vals:
             def es(xs, v=v):
                 return exact_sign(xs)
-            never_neg[v], n1 = lp_sign_free(weights, biases, lo, hi, pa_idx, values[v], row_bounds[v], -1, sb,
-                                            deadline, es)
-            never_pos[v], n2 = lp_sign_free(weights, biases, lo, hi, pa_idx, values[v], row_bounds[v], +1, sb,
-                                            deadline, es)
-            nodes += n1 + n2
-    for vi, vj in pairs:
-        if never_neg.get(int(vi)) or never_pos.get(int(vj)):
-            continue                        # N(x, vi) < 0 < N(x', vj) impossible
-        st, wit, n = lp_bab_pair(weights, biases, lo, hi, pa_idx, values[int(vi)], values[int(vj)],
-                                 row_bounds[int(vi)], row_bounds[int(vj)], max(1, node_budget - nodes), deadline,
-                                 confirm)
-        nodes += n
-        if st == "sat":
-            return "sat", wit, nodes
-        if st != "unsat":
-            return "unknown", None, nodes
+            for box, sg in tests:
+                bl, bh, rbv = (lo, hi, row_bounds[v]) if box == "x" else (lo_p, hi_p, rbp[v])
+                free[(box, sg)][v], n1 = lp_sign_free(weights, biases, bl, bh, pa_idx, values[v], rbv, sg, sb,
+                                                      deadline, es)
+                nodes += n1
+    # orientation +1: N(x, vi) < 0 < N(x', vj); -1 (relaxed only): N(x, vi) > 0 > N(x', vj)
+    for orient in ((1, -1) if relaxed else (1,)):
+        for vi, vj in pairs:
+            if orient > 0 and (free[("x", -1)].get(int(vi)) or free[("p", 1)].get(int(vj))):
+                continue
+            if orient < 0 and (free[("x", 1)].get(int(vi)) or free[("p", -1)].get(int(vj))):
+                continue
+            st, wit, n = lp_bab_pair(weights, biases, lo, hi, pa_idx, values[int(vi)], values[int(vj)],
+                                     row_bounds[int(vi)], rbp[int(vj)], max(1, node_budget - nodes), deadline,
+                                     confirm, ra_idx=ra_idx if relaxed else (), tau=tau if relaxed else 0.0,
+                                     orient=orient)
+            nodes += n
+            if st == "sat":
+                return "sat", wit, nodes
+            if st != "unsat":
+                return "unknown", None, nodes
     return "unsat", None, nodes
 
 
@@ -498,7 +548,7 @@ def process_pool(workers: int):
         return _PPOOL
 
 
-def _partition_task(mlp, lo, hi, pa_idx, ra_idx, tau, values, pairs, rb, node_budget, limit, deadline):
+def _partition_task(mlp, lo, hi, pa_idx, ra_idx, tau, values, pairs, rb, node_budget, limit, deadline, rbp=None):
     from ..engine import exact
 
     if deadline is not None:
@@ -514,7 +564,7 @@ def _partition_task(mlp, lo, hi, pa_idx, ra_idx, tau, values, pairs, rb, node_bu
         return int(exact.exact_signs(mlp, xs[None])[0])
 
     return solve_partition(mlp.weights, mlp.biases, lo, hi, pa_idx, values, pairs, rb, node_budget, limit, confirm,
-                           exact_sign)
+                           exact_sign, ra_idx=ra_idx, tau=tau, row_bounds_p=rbp)
 
 
 def submit(be, mlp, q, lo: np.ndarray, hi: np.ndarray, values: np.ndarray, pairs: np.ndarray, node_budget: int,
@@ -526,13 +576,15 @@ def submit(be, mlp, q, lo: np.ndarray, hi: np.ndarray, values: np.ndarray, pairs
 
     if len(lo) == 0:
         return []
-    assert not q.relaxed, "lp stage: PA-only queries"
     lbs, ubs = milp.layer_bounds_rows(be, lo, hi, q, values, widen_ra=False)
+    if q.relaxed:         # x' rows: RA dims widened by tau (unclipped, reference semantics)
+        lbp, ubp = milp.layer_bounds_rows(be, lo, hi, q, values, widen_ra=True)
     V = values.shape[0]
     ex = process_pool(workers)
     futs = []
     for k in range(len(lo)):
         rb = {v: ([lb[k, v] for lb in lbs], [ub[k, v] for ub in ubs]) for v in range(V)}
+        rbp = {v: ([lb[k, v] for lb in lbp], [ub[k, v] for ub in ubp]) for v in range(V)} if q.relaxed else None
         futs.append(ex.submit(_partition_task, mlp, lo[k], hi[k], tuple(q.pa_idx), tuple(q.ra_idx), float(q.tau),
-                              values, pairs, rb, int(node_budget), float(time_limit), deadline))
+                              values, pairs, rb, int(node_budget), float(time_limit), deadline, rbp))
     return futs

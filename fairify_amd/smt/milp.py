@@ -304,8 +304,13 @@ def layer_bounds_rows(be, lo: np.ndarray, hi: np.ndarray, q, values: np.ndarray,
         rlo[:, :, ra] -= q.tau
         rhi[:, :, ra] += q.tau
     dev = be.device
+    from ..engine.bab import BaBConfig, refine_on
+
+    # deep nets: hidden-layer bounds tightened by back-substitution (csrc/refine.hip) -- the LP's
+    # triangle relaxation is only as tight as these intervals
+    rf = refine_on(BaBConfig().refine, be.widths)
     res = be.bounds(torch.from_numpy(rlo.reshape(P * V, n)).to(dev), torch.from_numpy(rhi.reshape(P * V, n)).to(dev),
-                    mode="symbolic", keep_layers=True)
+                    mode="symbolic", keep_layers=True, crown=rf, refine=rf)
     # every layer's [lb | ub] rows packed on the device, ONE async copy into pinned host memory on a
     # side stream (the north star's pinned hipMemcpyAsync feed of the host solver) instead of 2L
     # blocking .cpu() copies

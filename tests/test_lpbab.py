@@ -213,3 +213,70 @@ def test_lpbab_multivalued_pa_with_sign_pretests(seed):
         assert (st == "sat") == truth, k
         if st == "sat":
             assert exact.is_violation(m, np.asarray(wit[0])[None], np.asarray(wit[1])[None])[0]
+
+
+def _row_bounds_box(m, lo, hi, q, values):
+    return _row_bounds(m, lo, hi, q, values)
+
+
+@pytest.mark.parametrize("seed,tau,race", [(11, 2, False), (12, 3, False), (13, 2, True)])
+def test_lpbab_relaxed_matches_bruteforce(seed, tau, race):
+    """Relaxed queries (|x_r - x'_r| <= tau on RA = age, x' NOT clipped to the box; reference
+    relaxed/BM/Verify-BM.py:53-54, utils/verif_utils.py:879-887): both orientations, x' bounds over
+    the widened box; verdicts equal enumeration of every (x, x') pair."""
+    from fairify_amd.engine.bab import _pa_table
+    from fairify_amd.smt import lpbab
+    from fairify_amd.spec import ADULT, Query
+
+    q = Query(pa=("race",) if race else ("sex",), ra=("age",), tau=tau).resolve(ADULT)
+    grid = presets.get("src/AC-race" if race else "src/AC-sex").grid()
+    ids = processing_order(grid, 0)[:12]
+    lo, hi = grid.decode(ids)
+    pa, ra = q.pa_idx[0], q.ra_idx[0]
+    keep = hi.copy()
+    hi = np.minimum(hi, lo + 1)
+    if race:
+        hi[:, pa] = np.minimum(keep[:, pa], lo[:, pa] + 2)      # 3 race values: 6 ordered pairs
+    m = random_mlp(13, [6, 5], seed=seed, bias_scale=0.5)
+    decided = 0
+    for k in range(len(ids)):
+        values, pairs = _pa_table(q, lo[k:k + 1], hi[k:k + 1])
+        rb = _row_bounds(m, lo[k], hi[k], q, values)
+        lw, hw = lo[k].copy(), hi[k].copy()
+        lw[ra] -= tau
+        hw[ra] += tau
+        rbp = _row_bounds(m, lw, hw, q, values)
+
+        def confirm(xs, xps):
+            ok = exact.check_pair_constraints(xs[None], xps[None], lo[k:k + 1], hi[k:k + 1], q.pa_idx, q.ra_idx, q.tau)
+            return bool(ok[0] and exact.is_violation(m, xs[None], xps[None])[0])
+
+        def exact_sign(xs):
+            return int(exact.exact_signs(m, xs[None])[0])
+
+        st, wit, nodes = lpbab.solve_partition(m.weights, m.biases, lo[k], hi[k], q.pa_idx, values, pairs, rb,
+                                               8192, 60.0, confirm, exact_sign, ra_idx=q.ra_idx, tau=float(tau),
+                                               row_bounds_p=rbp)
+        pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[k], hi[k])])))
+        truth = False
+        for vi, vj in pairs:
+            x = pts.copy()
+            x[:, pa] = values[vi][0]
+            z = m.logits(x)
+            for d in range(-tau, tau + 1):
+                xp = x.copy()
+                xp[:, pa] = values[vj][0]
+                xp[:, ra] += d
+                zp = m.logits(xp)
+                if (((z < 0) & (zp > 0)) | ((z > 0) & (zp < 0))).any():
+                    truth = True
+                    break
+            if truth:
+                break
+        if st == "sat":
+            assert truth, k
+            assert confirm(np.asarray(wit[0]), np.asarray(wit[1]))
+        elif st == "unsat":
+            assert not truth, k
+        decided += st != "unknown"
+    assert decided == len(ids)
