@@ -121,6 +121,13 @@ struct FalsifyArgs {
   float* wit_x;             // [P, n0]
   float* wit_xp;            // [P, n0]
   int8_t* how;              // [P] 0 none, 1 sampling, 2 boundary walk, 3 local search
+  // relaxed queries (nra > 0, tau > 0): x' = x with PA value v' and x'_r = x_r + d_r on the RA dims,
+  // d_r in [-tau, tau] (unclipped, reference semantics); a sample's offsets come from the hash
+  // stream dseed, the local search also moves them; both orientations of every pair count
+  int nra;
+  int ra_idx[FA_MAX_RA];
+  int tau;
+  uint32_t dseed;
 };
 
 struct SimArgs {

@@ -318,8 +318,9 @@ PYBIND11_MODULE(_C, m) {
                       int n_samples, int n_local, uint32_t seed, int V, const std::vector<int>& pa, uintptr_t values,
                       int Pp, uintptr_t pairs, int walk_k, int walk_steps, int K, int iters,
                       const std::vector<int>& free_dims, uintptr_t found, uintptr_t wit_x, uintptr_t wit_xp,
-                      uintptr_t how, uintptr_t stream) {
-    if (pa.size() > FA_MAX_PA || free_dims.size() > 64) throw std::invalid_argument("too many PA/free dims");
+                      uintptr_t how, uintptr_t stream, const std::vector<int>& ra, int tau, uint32_t dseed) {
+    if (pa.size() > FA_MAX_PA || free_dims.size() > 64 || ra.size() > FA_MAX_RA)
+      throw std::invalid_argument("too many PA/RA/free dims");
     FalsifyArgs a{};
     a.flat = P<const float>(flat);
     a.lo = P<const float>(lo);
@@ -339,6 +340,10 @@ PYBIND11_MODULE(_C, m) {
     a.wit_x = P<float>(wit_x);
     a.wit_xp = P<float>(wit_xp);
     a.how = P<int8_t>(how);
+    a.nra = tau > 0 ? (int)ra.size() : 0;
+    for (int i = 0; i < a.nra; ++i) a.ra_idx[i] = ra[i];
+    a.tau = tau;
+    a.dseed = dseed;
     const int rc = fa_falsify_launch(net.d, a, (hipStream_t)stream);
     if (rc == 0) return false;
     if (rc < 0) check(-rc, "falsify");

@@ -16,6 +16,12 @@
 //      first n_local, +-1 moves on every free dimension, all rounds inside the kernel
 //      (engine/falsify.py:_local_search, same moves and acceptance rule as fa_ascent_kernel).
 //
+// Relaxed queries (|x_r - x'_r| <= tau on the RA dims, x' unclipped): every point carries its RA
+// offsets d (sample: hash stream dseed, like engine/falsify.py; local search: +-1 moves clamped to
+// [-tau, tau]); a point is evaluated as V rows of x and V rows of x', and a pair (v, v') counts in
+// both orientations, N(x, v) < 0 < N(x', v') or N(x, v) > 0 > N(x', v').  The boundary walk probes
+// x' = x (d = 0, always admissible).
+//
 // Only the witness is reported; the pipeline confirms it exactly (engine/exact.py).
 #include <hip/hip_runtime.h>
 
@@ -26,8 +32,10 @@
 namespace {
 
 struct FalsifyLds {
-  int z0, fm, fq, zs, slo, shi, wa, wb, tlo, thi, wok, widx, sval, X, F, Q, marg, margq, misc, floats;
+  int z0, fm, fq, zs, slo, shi, wa, wb, tlo, thi, wok, widx, sval, X, F, Q, marg, margq, misc, DK, floats;
 };
+
+__host__ __device__ inline bool fa_fals_relaxed(const FalsifyArgs& a) { return a.nra > 0 && a.tau > 0; }
 
 // Offsets (floats) of the kernel's LDS arrays after the staged weights; identical on host/device.
 __host__ __device__ inline FalsifyLds fa_falsify_lds(const FalsifyArgs& a, int n0, int wfloats) {
@@ -35,12 +43,14 @@ __host__ __device__ inline FalsifyLds fa_falsify_lds(const FalsifyArgs& a, int n
   const int nl = a.n_local < a.n_samples ? a.n_local : a.n_samples;
   const int kw = a.walk_k < a.n_samples ? a.walk_k : a.n_samples;
   const int K = a.K < nl ? a.K : nl;
-  const int nm = 2 * a.nfree;
+  const bool rx = fa_fals_relaxed(a);
+  const int nm = 2 * a.nfree + (rx ? 2 * a.nra : 0);
+  const int RV = rx ? 2 * a.V : a.V;              // rows per point: x (and x') per PA value
   int o = wfloats;
   L.z0 = o; o += a.n_samples;
   L.fm = o; o += nl;
   L.fq = o; o += nl;
-  const int zs1 = 4 * 16 * a.V, zs2 = K * nm * a.V, zs3 = kw * a.V;
+  const int zs1 = 4 * 16 * RV, zs2 = K * nm * RV, zs3 = kw * a.V;
   int zs = zs1 > zs2 ? zs1 : zs2;
   zs = zs > zs3 ? zs : zs3;
   L.zs = o; o += zs;
@@ -58,6 +68,7 @@ __host__ __device__ inline FalsifyLds fa_falsify_lds(const FalsifyArgs& a, int n
   L.Q = o; o += K;
   L.marg = o; o += K * nm;
   L.margq = o; o += K * nm;
+  L.DK = o; o += rx ? K * a.nra : 0;
   L.misc = o; o += 8;
   L.floats = (o + 3) & ~3;
   return L;
@@ -74,6 +85,39 @@ __device__ __forceinline__ int fa_pa_slot(const FalsifyArgs& a, int d) {
   for (int m = 0; m < a.npa; ++m)
     if (a.pa_idx[m] == d) r = m;
   return r;
+}
+
+// RA dim d -> index into the RA list, or -1 (relaxed queries only)
+__device__ __forceinline__ int fa_ra_slot(const FalsifyArgs& a, int d) {
+  int r = -1;
+  for (int m = 0; m < a.nra; ++m)
+    if (a.ra_idx[m] == d) r = m;
+  return r;
+}
+
+// sample s's offset on RA slot m: uniform in [-tau, tau] (engine/falsify.py: rng_u32(dseed, pid, s,
+// ra_idx[m]) % (2 tau + 1) - tau)
+__device__ __forceinline__ float fa_roff(const FalsifyArgs& a, int64_t pid, int s, int m) {
+  return (float)(fa_rng(a.dseed, pid, s, a.ra_idx[m]) % (uint32_t)(2 * a.tau + 1)) - (float)a.tau;
+}
+
+// best margin over the pairs of one point from its row logits zr (x rows [0, V), x' rows [V, 2V)
+// when relaxed): returns max over pairs (and orientations) of min(-N(x, v), N(x', v')) /
+// min(N(x, v), -N(x', v')); *gq = the pair index, *flip = first strictly violating pair or -1
+__device__ __forceinline__ float fa_pair_margin(const FalsifyArgs& a, const float* zr, bool rx, int* gq, int* flip) {
+  float g = -INFINITY;
+  int q0 = 0, fk = -1;
+  for (int q = 0; q < a.Pp; ++q) {
+    const float zi = zr[(int)a.pairs[2 * q]];
+    const float zj = zr[(rx ? a.V : 0) + (int)a.pairs[2 * q + 1]];
+    float mg = fminf(-zi, zj);
+    if (rx) mg = fmaxf(mg, fminf(zi, -zj));
+    if (mg > g) { g = mg; q0 = q; }
+    if (fk < 0 && ((zi < 0.f && zj > 0.f) || (zi > 0.f && zj < 0.f))) fk = q;
+  }
+  *gq = q0;
+  *flip = fk;
+  return g;
 }
 
 // wave-wide (value, index) selection: the largest value (sign = +1) or the smallest (sign = -1),
@@ -129,6 +173,8 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
   int* misc = (int*)(smem + L.misc);        // [0] best flip key, [1] hit, [2] hit j, [3] hit q, [4] change
   const int nl = min(a.n_local, a.n_samples);
   const int V = a.V, Pp = a.Pp;
+  const bool rx = fa_fals_relaxed(a);
+  const int RV = rx ? 2 * V : V;
   fa_stage_wperm(net, a.flat, smem, tid, FA_THREADS);
   for (int i = tid; i < n0; i += FA_THREADS) {
     s_lo[i] = a.lo[(size_t)p * n0 + i];
@@ -152,34 +198,35 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
         const int k = 16 * t + 4 * grp + i;
         Xb[t][i] = (k < n0 && sv) ? fa_coord(a.seed, pid, s, k, s_lo[k], s_hi[k]) : 0.f;
       }
-    for (int v = 0; v < V; ++v) {
+    for (int v2 = 0; v2 < RV; ++v2) {
+      const int v = v2 < V ? v2 : v2 - V;
+      const bool xp = v2 >= V;                   // an x' row (relaxed): RA dims shifted
 #pragma unroll
       for (int t = 0; t < TM; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int k = 16 * t + 4 * grp + i;
           const int m = k < n0 ? fa_pa_slot(a, k) : -1;
-          HA[t][i] = m >= 0 ? (float)a.values[v * a.npa + m] : Xb[t][i];
+          float val = m >= 0 ? (float)a.values[v * a.npa + m] : Xb[t][i];
+          if (xp && k < n0 && sv) {
+            const int r = fa_ra_slot(a, k);
+            if (r >= 0) val += fa_roff(a, pid, s, r);
+          }
+          HA[t][i] = val;
         }
       const float z = fa_reg_forward<TM>(net, cfg, smem, lane, HA, HB);
-      if (grp == 0) zs[(wave * 16 + col) * V + v] = z;   // read back by this same lane only
+      if (grp == 0) zs[(wave * 16 + col) * RV + v2] = z;   // read back by this same lane only
     }
     if (grp == 0 && sv) {
-      const float* zr = zs + (wave * 16 + col) * V;
+      const float* zr = zs + (wave * 16 + col) * RV;
       z0[s] = zr[0];
-      float g = -INFINITY;
-      int gq = 0, fk = INT_MAX;
-      for (int q = 0; q < Pp; ++q) {
-        const float zi = zr[(int)a.pairs[2 * q]], zj = zr[(int)a.pairs[2 * q + 1]];
-        const float mg = fminf(-zi, zj);
-        if (mg > g) { g = mg; gq = q; }
-        if (fk == INT_MAX && ((zi < 0.f && zj > 0.f) || (zi > 0.f && zj < 0.f))) fk = s * Pp + q;
-      }
+      int gq = 0, fq0 = -1;
+      const float g = fa_pair_margin(a, zr, rx, &gq, &fq0);
       if (s < nl) {
         fm[s] = g;
         fq[s] = gq;
       }
-      if (fk != INT_MAX) atomicMin(&misc[0], fk);
+      if (fq0 >= 0) atomicMin(&misc[0], s * Pp + fq0);
     }
     __syncthreads();
     if (misc[0] != INT_MAX) break;                 // uniform
@@ -191,8 +238,9 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
     for (int d = tid; d < n0; d += FA_THREADS) {
       const float base = fa_coord(a.seed, pid, s, d, s_lo[d], s_hi[d]);
       const int m = fa_pa_slot(a, d);
+      const int r = rx ? fa_ra_slot(a, d) : -1;
       a.wit_x[(size_t)p * n0 + d] = m >= 0 ? (float)a.values[vi * a.npa + m] : base;
-      a.wit_xp[(size_t)p * n0 + d] = m >= 0 ? (float)a.values[vj * a.npa + m] : base;
+      a.wit_xp[(size_t)p * n0 + d] = m >= 0 ? (float)a.values[vj * a.npa + m] : base + (r >= 0 ? fa_roff(a, pid, s, r) : 0.f);
     }
     if (tid == 0) {
       a.found[p] = 1;
@@ -292,13 +340,15 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
   }
   // ================= phase 3: coordinate ascent from the K best-margin samples
   const int K = min(a.K, nl);
-  const int nm = 2 * a.nfree;
+  const int nmf = 2 * a.nfree;                   // +-1 on the free dims, then (relaxed) +-1 on the offsets
+  const int nm = nmf + (rx ? 2 * a.nra : 0);
   if (K > 0 && nm > 0 && a.iters > 0) {
     float* X = smem + L.X;
     float* F = smem + L.F;
     int* Q = (int*)(smem + L.Q);
     float* marg = smem + L.marg;
     int* margq = (int*)(smem + L.margq);
+    float* DK = smem + L.DK;                     // [K, nra] RA offsets of the starts (relaxed)
     int* sidx = (int*)(smem + L.widx);           // the walk is over: reuse its selection slots
     if (wave == 0) fa_select_extremes(fm, nl, K, 1.f, sidx, smem + L.sval, lane);
     __syncthreads();
@@ -306,12 +356,17 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
       const int j = e / n0, d = e - j * n0;
       X[e] = fa_coord(a.seed, pid, sidx[j], d, s_lo[d], s_hi[d]);
     }
+    if (rx)
+      for (int e = tid; e < K * a.nra; e += FA_THREADS) {
+        const int j = e / a.nra, m = e - j * a.nra;
+        DK[e] = fa_roff(a, pid, sidx[j], m);
+      }
     for (int j = tid; j < K; j += FA_THREADS) {
       F[j] = fm[sidx[j]];
       Q[j] = fq[sidx[j]];
     }
     __syncthreads();
-    const int per = nm * V, total = K * per;
+    const int per = nm * RV, total = K * per;
     for (int it = 0; it < a.iters; ++it) {
       if (tid == 0) {
         int h = 0;
@@ -324,8 +379,12 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
       for (int g0 = wave * 16; g0 < total; g0 += 64) {
         const int r = g0 + col;
         const bool rv = r < total;
-        const int v = rv ? r % V : 0, mv = rv ? (r / V) % nm : 0, s = rv ? r / per : 0;
-        const int fd = a.free_idx[mv >> 1];
+        const int v2 = rv ? r % RV : 0, mv = rv ? (r / RV) % nm : 0, s = rv ? r / per : 0;
+        const int v = v2 < V ? v2 : v2 - V;
+        const bool xpr = v2 >= V;
+        const int fd = mv < nmf ? a.free_idx[mv >> 1] : -1;
+        const int rm = mv < nmf ? -1 : (mv - nmf) >> 1;   // RA offset moved by this move
+        const float step = (mv & 1) ? 1.f : -1.f;
 #pragma unroll
         for (int t = 0; t < TM; ++t)
 #pragma unroll
@@ -334,7 +393,15 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
             float val = 0.f;
             if (rv && k < n0) {
               val = X[s * n0 + k];
-              if (k == fd) val = fminf(fmaxf(val + ((mv & 1) ? 1.f : -1.f), s_lo[k]), s_hi[k]);
+              if (k == fd) val = fminf(fmaxf(val + step, s_lo[k]), s_hi[k]);
+              if (xpr) {
+                const int ro = fa_ra_slot(a, k);
+                if (ro >= 0) {
+                  float dd = DK[s * a.nra + ro];
+                  if (ro == rm) dd = fminf(fmaxf(dd + step, -(float)a.tau), (float)a.tau);
+                  val += dd;
+                }
+              }
               const int m = fa_pa_slot(a, k);
               if (m >= 0) val = (float)a.values[v * a.npa + m];
             }
@@ -345,14 +412,8 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
       }
       __syncthreads();
       for (int i = tid; i < K * nm; i += FA_THREADS) {   // best pair per (start, move); first on ties
-        const float* z = zs + (size_t)i * V;
-        float g = -INFINITY;
-        int gq = 0;
-        for (int q = 0; q < Pp; ++q) {
-          const float m = fminf(-z[a.pairs[2 * q]], z[a.pairs[2 * q + 1]]);
-          if (m > g) { g = m; gq = q; }
-        }
-        marg[i] = g;
+        int gq = 0, fl = -1;
+        marg[i] = fa_pair_margin(a, zs + (size_t)i * RV, rx, &gq, &fl);
         margq[i] = gq;
       }
       __syncthreads();
@@ -362,8 +423,14 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
         for (int mv = 0; mv < nm; ++mv)
           if (marg[s * nm + mv] > g) { g = marg[s * nm + mv]; gm = mv; }
         if (g > F[s]) {
-          const int d = a.free_idx[gm >> 1];
-          X[s * n0 + d] = fminf(fmaxf(X[s * n0 + d] + ((gm & 1) ? 1.f : -1.f), s_lo[d]), s_hi[d]);
+          const float step = (gm & 1) ? 1.f : -1.f;
+          if (gm < nmf) {
+            const int d = a.free_idx[gm >> 1];
+            X[s * n0 + d] = fminf(fmaxf(X[s * n0 + d] + step, s_lo[d]), s_hi[d]);
+          } else {
+            float& dd = DK[s * a.nra + ((gm - nmf) >> 1)];
+            dd = fminf(fmaxf(dd + step, -(float)a.tau), (float)a.tau);
+          }
           F[s] = g;
           Q[s] = margq[s * nm + gm];
           misc[4] = 1;
@@ -382,9 +449,10 @@ __global__ void __launch_bounds__(FA_THREADS) fa_falsify_kernel(NetDesc net, Fal
       const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];
       for (int d = tid; d < n0; d += FA_THREADS) {
         const int m = fa_pa_slot(a, d);
+        const int ro = rx ? fa_ra_slot(a, d) : -1;
         const float x = X[sh * n0 + d];
         a.wit_x[(size_t)p * n0 + d] = m >= 0 ? (float)a.values[vi * a.npa + m] : x;
-        a.wit_xp[(size_t)p * n0 + d] = m >= 0 ? (float)a.values[vj * a.npa + m] : x;
+        a.wit_xp[(size_t)p * n0 + d] = m >= 0 ? (float)a.values[vj * a.npa + m] : x + (ro >= 0 ? DK[sh * a.nra + ro] : 0.f);
       }
       if (tid == 0) {
         a.found[p] = 1;
@@ -414,7 +482,7 @@ FalsifyKernel select_falsify(int TM) {
 extern "C" int fa_falsify_launch(const NetDesc& net, FalsifyArgs a, hipStream_t stream) {
   if (a.P <= 0) return 1;
   if (a.npa > FA_MAX_PA || a.nfree > 64 || a.V <= 0 || a.Pp <= 0 || a.n_samples <= 0 || a.K < 0 ||
-      a.walk_k < 0 || a.n_local < 0)
+      a.walk_k < 0 || a.n_local < 0 || a.nra < 0 || a.nra > FA_MAX_RA || a.tau < 0)
     return -3;
   if ((long long)a.n_samples * a.Pp >= INT_MAX) return -3;   // flip keys sample * Pp + pair are int
   FalsifyKernel k = select_falsify(fa_regnet_tm(net));

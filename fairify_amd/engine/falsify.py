@@ -14,10 +14,11 @@ the LP-optimal vertex candidates of the BaB miss them.  For those partitions onl
 3. from the ``k_starts`` best points, coordinate ascent on the integer lattice: every ±1 move
    of a non-protected feature (and of the relaxed offset x'_r - x_r within [-tau, tau]) is
    evaluated in one batched forward, the best improving move is taken, ``iters`` rounds.
-   On the HIP path (non-relaxed queries) all three steps -- heavy sampling, the boundary walk of
+   On the HIP path all three steps -- heavy sampling, the boundary walk of
    :func:`engine.sim.boundary_walk` and the ascent -- run in ONE ``fa_falsify_kernel`` launch
    (``csrc/falsify.hip``, register-resident MFMA forward); each partition stops at its first hit.
-   Relaxed queries keep the simulation kernel + PyTorch walk + ``fa_ascent_kernel`` path.
+   Relaxed queries run in the same launch: every sample carries its RA offsets (the hash stream
+   below), the ascent moves them too, and both orientations of a pair count.
 
 Hits are only *candidates*: the pipeline confirms them with the exact checker
 (:mod:`fairify_amd.engine.exact`) before a partition becomes SAT.
@@ -73,12 +74,12 @@ def residual_falsify(be: Backend, q: ResolvedQuery, lo: torch.Tensor, hi: torch.
     ``n_local`` materialised samples of the partitions still without a witness."""
     P, n = lo.shape
     dev = lo.device
-    if be.hip and P and not q.relaxed and os.environ.get("FAIRIFY_FUSED_FALSIFY", "1") != "0":
+    if be.hip and P and os.environ.get("FAIRIFY_FUSED_FALSIFY", "1") != "0":
         from ..ops import hip
 
         free = [d for d in range(n) if d not in set(q.pa_idx)]
         out = hip.falsify(be, q, lo, hi, pids, values, pairs, (seed ^ 0x6A09E667) & 0xFFFFFFFF, n_samples, n_local,
-                          16, 12, k_starts, iters, free)
+                          16, 12, k_starts, iters, free, dseed=(seed ^ 0x3C6EF372) & 0xFFFFFFFF)
         if out is not None:
             return FalsifyResult(out[0], out[1], out[2], how=out[3])
     if be.hip and P:

@@ -440,15 +440,14 @@ def ascent(be, q, lo, hi, x0, f0, q0, iters, values, pairs, free_dims):
 
 
 def falsify(be, q, lo, hi, pids, values, pairs, seed, n_samples, n_local, walk_k, walk_steps, k_starts, iters,
-            free_dims):
-    """Fused residual falsifier (``csrc/falsify.hip``), non-relaxed queries: heavy sampling,
-    boundary walk, lattice coordinate ascent in one launch.  Returns ``(found [P] bool,
-    wit_x [P, n0], wit_xp [P, n0], how [P] int8)`` or ``None`` when the network shape is not
-    supported by the kernel (the caller keeps the PyTorch path)."""
+            free_dims, dseed: int = 0):
+    """Fused residual falsifier (``csrc/falsify.hip``): heavy sampling, boundary walk, lattice
+    coordinate ascent in one launch.  Relaxed queries: x' carries RA offsets in [-tau, tau] (hash
+    stream ``dseed`` per sample, moved by the ascent), both orientations of every pair count.
+    Returns ``(found [P] bool, wit_x [P, n0], wit_xp [P, n0], how [P] int8)`` or ``None`` when the
+    network shape is not supported by the kernel (the caller keeps the PyTorch path)."""
     P, n0 = lo.shape
     dev = lo.device
-    if q.relaxed:
-        raise ValueError("fused falsifier: non-relaxed queries only")
     lo_c = _c(lo, torch.float32, (P, n0), "lo")
     hi_c = _c(hi, torch.float32, (P, n0), "hi")
     pids_c = _c(pids, torch.int64, (P,), "pids")
@@ -468,7 +467,8 @@ def falsify(be, q, lo, hi, pids, values, pairs, seed, n_samples, n_local, walk_k
                        int(n_samples), int(n_local), int(seed) & 0xFFFFFFFF, V, list(q.pa_idx), values_c.data_ptr(),
                        Pp, pairs_c.data_ptr(), int(walk_k), int(walk_steps), int(k_starts), int(iters),
                        [int(d) for d in free_dims], found.data_ptr(), wx.data_ptr(), wxp.data_ptr(), how.data_ptr(),
-                       _stream(dev))
+                       _stream(dev), list(q.ra_idx) if q.relaxed else [], int(q.tau) if q.relaxed else 0,
+                       int(dseed) & 0xFFFFFFFF)
     if not ok:
         return None
     return found.bool(), wx, wxp, how

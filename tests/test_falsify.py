@@ -148,3 +148,40 @@ def test_fused_falsifier_matches_sim_and_is_sound(cuda, monkeypatch, model):
         amb = ((lb <= 0) & (ub >= 0)).view(4, len(bad)).any(dim=0).cpu().numpy()
         assert amb.all(), f"{int((~amb).sum())} sampling-phase mismatches outside the rounding margin"
     assert f.sum() >= 0.98 * legacy.found.cpu().numpy().sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("preset,model", [("relaxed/BM", "BM-1"), ("relaxed/BM", "BM-8"), ("relaxed/AC", "AC-3")])
+def test_fused_falsifier_relaxed_is_sound_and_matches_torch(cuda, monkeypatch, preset, model):
+    """Relaxed queries through fa_falsify_kernel (x' offsets on the RA dims, both orientations):
+    every witness satisfies the pair constraints (|x_r - x'_r| <= tau, x' unclipped) and flips the
+    exact network, and the kernel decides at least 95 % of what the PyTorch local search decides."""
+    from fairify_amd import presets
+    from fairify_amd.engine import falsify as F
+    from fairify_amd.engine.bab import _pa_table
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.partition import processing_order
+
+    pre = presets.get(preset)
+    grid, q = pre.grid(), pre.resolved()
+    assert q.relaxed
+    ids = processing_order(grid, seed=0)[:512]
+    lo_np, hi_np = grid.decode(ids)
+    m = get_model(model, weights="random", seed=0)
+    be = Backend(m, cuda)
+    v_np, p_np = _pa_table(q, lo_np, hi_np)
+    values, pairs = torch.from_numpy(v_np).to(cuda), torch.from_numpy(p_np).to(cuda)
+    lo, hi = torch.from_numpy(lo_np).to(cuda).float(), torch.from_numpy(hi_np).to(cuda).float()
+    pids = torch.from_numpy(ids).to(cuda)
+    fused = F.residual_falsify(be, q, lo, hi, pids, values, pairs, 0, n_samples=1024, k_starts=16, iters=12)
+    assert fused.how is not None, "fused kernel did not run"
+    f = fused.found.cpu().numpy()
+    idx = np.nonzero(f)[0]
+    assert idx.size > 0
+    X = fused.wit_x.cpu().numpy()[idx].round().astype(np.int64)
+    XP = fused.wit_xp.cpu().numpy()[idx].round().astype(np.int64)
+    assert exact.check_pair_constraints(X, XP, lo_np[idx], hi_np[idx], q.pa_idx, q.ra_idx, q.tau).all()
+    assert exact.is_violation(m, X, XP).all()
+    monkeypatch.setenv("FAIRIFY_FUSED_FALSIFY", "0")
+    legacy = F.residual_falsify(be, q, lo, hi, pids, values, pairs, 0, n_samples=1024, k_starts=16, iters=12)
+    assert f.sum() >= 0.95 * legacy.found.cpu().numpy().sum()
