@@ -267,13 +267,15 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_finalize_kernel(NetDesc net
 }
 
 // ------------------------------------------------------------------------------------------
-// Register-resident simulation (PA-only queries): the same samples (fa_sample_coord), PA passes,
+// Register-resident simulation: the same samples (fa_sample_coord), PA passes,
 // activation counts (at the sampled PA tuple) and first-flip keys as fa_sim_kernel, with 16
 // samples per wave as the MFMA columns (csrc/regfwd.h): W staged once per workgroup in MFMA
 // operand order, activations never leave registers, counts from one ballot per (tile, register)
 // and layer (the 16 lanes of a lane group hold one neuron of the 16 samples).  The K grouping of
 // the MFMA sums differs from the 64-row tile forward, so a logit within fp32 rounding of 0 may
 // flip differently (counts stay within the rounding margins of tests/test_kernels_gpu.py).
+// Relaxed queries add V passes of x' rows (fa_sim_kernel's offsets: x'_r = x_r + d, d uniform in
+// [-tau, tau] from the seed ^ 0x2545F491 stream, unclipped), which are not counted.
 
 // One layer with activation counting: H -> H2 (ReLU outputs); counts neuron j for the samples
 // whose lanes have `match` (the sampled PA tuple is this pass's values[v]); last layer: the logit
@@ -334,9 +336,12 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_reg_kernel(NetDesc net, Sim
   const int p = blockIdx.x / G;
   const int g = blockIdx.x - p * G;
   const int V = a.V;
+  const bool rx = a.nra > 0;
+  const int RV = rx ? 2 * V : V;              // x rows, then (relaxed) x' rows per PA value
+  const uint32_t seed_ra = a.seed ^ 0x2545F491u;
   const int64_t pid = a.pids[p];
-  float* zs = smem + cfg.floats;              // [64][V] logits of this pass's samples
-  float* s_lo = zs + 64 * V;
+  float* zs = smem + cfg.floats;              // [64][RV] logits of this pass's samples
+  float* s_lo = zs + 64 * RV;
   float* s_hi = s_lo + n0;
   int* cnt = (int*)(s_hi + n0);               // [n_neurons]
   int* best = cnt + net.n_neurons;
@@ -359,9 +364,11 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_reg_kernel(NetDesc net, Sim
         const int k = 16 * t + 4 * grp + i;
         Xb[t][i] = (k < n0 && sv) ? fa_sample_coord(a.seed, pid, s, k, s_lo[k], s_hi[k]) : 0.f;
       }
-    for (int v = 0; v < V; ++v) {
-      // counts at the sampled point: the pass whose PA tuple equals the sample's
-      bool match = sv;
+    for (int v2 = 0; v2 < RV; ++v2) {
+      const int v = v2 < V ? v2 : v2 - V;
+      const bool xp = v2 >= V;
+      // counts at the sampled point: the x pass whose PA tuple equals the sample's
+      bool match = sv && !xp;
       for (int m = 0; m < a.npa; ++m) {
         const int d = a.pa_idx[m];
         match = match && fa_sample_coord(a.seed, pid, s, d, s_lo[d], s_hi[d]) == (float)a.values[v * a.npa + m];
@@ -374,6 +381,9 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_reg_kernel(NetDesc net, Sim
           float x = Xb[t][i];
           for (int m = 0; m < a.npa; ++m)
             if (a.pa_idx[m] == k) x = (float)a.values[v * a.npa + m];
+          if (xp && sv)
+            for (int m = 0; m < a.nra; ++m)
+              if (a.ra_idx[m] == k) x += (float)(fa_rng(seed_ra, pid, s, k) % (uint32_t)(2 * a.tau + 1)) - (float)a.tau;
           HA[t][i] = x;
         }
       float z = 0.f;
@@ -381,13 +391,13 @@ __global__ void __launch_bounds__(FA_THREADS) fa_sim_reg_kernel(NetDesc net, Sim
         if (l & 1) z = fa_reg_layer_count<TM>(net, cfg, smem, l, lane, HB, HA, match, cnt);
         else z = fa_reg_layer_count<TM>(net, cfg, smem, l, lane, HA, HB, match, cnt);
       }
-      if (grp == 0) zs[(wave * 16 + col) * V + v] = z;   // read back by this same lane only
+      if (grp == 0) zs[(wave * 16 + col) * RV + v2] = z;   // read back by this same lane only
     }
     if (grp == 0 && sv) {
-      const float* zr = zs + (wave * 16 + col) * V;
+      const float* zr = zs + (wave * 16 + col) * RV;
       if (a.z0) a.z0[(size_t)p * a.n_samples + s] = zr[0];
       for (int q = 0; q < a.Pp; ++q) {
-        const float zi = zr[(int)a.pairs[2 * q]], zj = zr[(int)a.pairs[2 * q + 1]];
+        const float zi = zr[(int)a.pairs[2 * q]], zj = zr[(rx ? V : 0) + (int)a.pairs[2 * q + 1]];
         if ((zi < 0.f && zj > 0.f) || (zi > 0.f && zj < 0.f)) {
           atomicMin(best, s * a.Pp + q);
           break;                                  // the sample's smallest flipping pair
@@ -433,11 +443,12 @@ extern "C" int fa_sim_launch(const NetDesc& net, SimArgs a, hipStream_t stream) 
   if ((long long)a.n_samples * a.Pp >= 0x7FFFFFFFLL) return -3;   // flip keys sample * Pp + pair are int
   a.S = net.max_width | 1;
   const int n0 = net.dims[0];
-  if (a.nra == 0 && sim_reg_on()) {
+  if (sim_reg_on()) {
     const SimRegKernel k = select_sim_reg(fa_regnet_tm(net));
     RegNetCfg cfg{};
     if (k && fa_regnet_cfg(net, cfg)) {
-      size_t rb = ((size_t)cfg.floats + 64 * (size_t)a.V + 2 * n0) * sizeof(float) + (net.n_neurons + 4) * sizeof(int);
+      const size_t RV = a.nra > 0 ? 2 * (size_t)a.V : (size_t)a.V;
+      size_t rb = ((size_t)cfg.floats + 64 * RV + 2 * n0) * sizeof(float) + (net.n_neurons + 4) * sizeof(int);
       rb = (rb + 15) & ~(size_t)15;
       const int tiles = (a.n_samples + FA_TR - 1) / FA_TR;
       if (rb <= 160 * 1024 && a.split >= 1 && (a.split == 1 || (a.keys && a.split <= tiles))) {

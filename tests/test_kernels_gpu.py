@@ -225,3 +225,39 @@ def test_certify_matches_reference(cuda):
     assert bool(((a.score - b.score.cpu()).abs() <= tol).all())
     differ = a.open_ != b.open_.cpu()
     assert bool((a.score[differ].abs() <= tol[differ]).all())
+
+
+@pytest.mark.parametrize("model", ["AC-3", "AC-7"])
+def test_sim_reg_kernel_relaxed_matches_tile_kernel(cuda, monkeypatch, model):
+    """Relaxed queries on the register-resident simulation kernel (x' rows with the tile kernel's RA
+    offsets): activation counts equal the 64-row tile kernel's up to rounding-ambiguous samples
+    (compared in total), every witness is an exact violation within the pair constraints, and the
+    found sets agree on >= 99 % of the partitions."""
+    from fairify_amd.engine import exact
+    from fairify_amd.engine.sim import simulate
+    from fairify_amd.partition import Grid
+
+    q = Query(("sex",), ("age",), 5).resolve(ADULT)
+    grid = Grid.reference(ADULT, 10)
+    ids = np.arange(0, 16000, 37)[:256]
+    lo, hi = grid.decode(ids)
+    values = torch.from_numpy(q.pa_values(lo[0], hi[0])).to(cuda)
+    pairs = torch.from_numpy(q.pa_pairs(values.cpu().numpy())).to(cuda)
+    m = get_model(model, weights="random", seed=0)
+    gpu = Backend(m, cuda)
+    lo_t, hi_t = torch.from_numpy(lo).float().to(cuda), torch.from_numpy(hi).float().to(cuda)
+    pid = torch.from_numpy(ids).to(cuda)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("FAIRIFY_SIM_REG", flag)
+        out[flag] = simulate(gpu, q, lo_t, hi_t, pid, 1000, 3, values, pairs, 0, 0)
+    a, b = out["1"], out["0"]
+    ca, cb = a.counts.cpu().numpy().astype(np.int64), b.counts.cpu().numpy().astype(np.int64)
+    assert np.abs(ca - cb).sum() <= 1e-3 * max(1, cb.sum())
+    fa, fb = a.found.cpu().numpy(), b.found.cpu().numpy()
+    assert (fa == fb).mean() >= 0.99
+    idx = np.nonzero(fa)[0]
+    X = a.wit_x.cpu().numpy()[idx].round().astype(np.int64)
+    XP = a.wit_xp.cpu().numpy()[idx].round().astype(np.int64)
+    assert exact.check_pair_constraints(X, XP, lo[idx], hi[idx], q.pa_idx, q.ra_idx, q.tau).all()
+    assert exact.is_violation(m, X, XP).all()
