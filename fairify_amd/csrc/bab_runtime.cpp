@@ -45,6 +45,7 @@ extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_
                                 EscSteps esc, hipStream_t stream);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
+extern "C" int fa_backward_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_bab_init_launch(BabInitArgs a, hipStream_t stream);
 extern "C" int fa_bab_finish_launch(int P, const int8_t* status, const int* nodes, const int* open_left, int* out,
                                     hipStream_t stream);
@@ -93,7 +94,7 @@ class BabRuntime {
   BabRuntime(py::handle net, uintptr_t flat, std::vector<int> pa, std::vector<float> values_f,
              std::vector<int64_t> values_i, std::vector<int64_t> pairs, std::vector<int> ra, float tau,
              std::vector<uint8_t> shared, int capacity, int batch_nodes, int cand_cap, double unit, bool crown,
-             int split_target, bool refine)
+             int split_target, int refine)
       : net_(fa_net_desc(net)),
         flat_((const float*)flat),
         pa_(std::move(pa)),
@@ -104,7 +105,7 @@ class BabRuntime {
         cand_cap_(cand_cap),
         unit_(unit),
         crown_(crown),
-        refine_(crown && refine),
+        refine_(crown ? refine : 0),
         split_target_(std::max(2, split_target)) {
     n0_ = net_.dims[0];
     npa_ = (int)pa_.size();
@@ -343,7 +344,7 @@ class BabRuntime {
         sa.cand_buf = cand_buf_.p; sa.cand_count = cnt + 1;
         sa.cand_cap = cand_alloc_;
         ckl(fa_split_launch(sa, st), "split");
-        launches += (relaxed_ ? 6 : 5) + (refine_ ? (relaxed_ ? 2 : 1) : 0);
+        launches += (relaxed_ ? 2 : 1) * (refine_ == 2 ? 1 : (refine_ == 1 ? 3 : 2)) + 3;
       }
       ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, nodes_.p, nodes_start_.p, prev_start_.p, cnt,
                            counters_.p + 2 * (slot ^ 1), hcount_, inline_esc ? pbudget_.p : nullptr,
@@ -416,6 +417,15 @@ class BabRuntime {
     }
     b.skip_status = status_.p;     // skip nodes of partitions decided / stopped earlier
     b.skip_part = part;
+    if (refine_ == 2) {
+      // backward-only bounding (refine.hip mode FULL): one launch computes every hidden layer's
+      // bounds and the logit's forms, no forward pass and no output pass; -1: the network does not
+      // fit, fall back to forward + refine + output pass
+      const int rc = fa_backward_launch(net_, b, st);
+      if (rc == 0) return;
+      if (rc != -1) ckl(rc, "backward");
+      refine_ = 1;
+    }
     if (crown_) {
       b.layer_lb = lay_lb_[slot].p;
       b.layer_ub = lay_ub_[slot].p;
@@ -423,9 +433,9 @@ class BabRuntime {
     ckl(fa_bounds_launch(net_, b, st), "bounds");
     // hidden-layer bounds tightened by back-substitution (refine.hip) before the output pass uses
     // them as relaxation intervals; a network the kernel cannot hold (-1) keeps the forward bounds
-    if (refine_) {
+    if (refine_ == 1) {
       const int rc = fa_refine_launch(net_, b, st);
-      if (rc == -1) refine_ = false;
+      if (rc == -1) refine_ = 0;
       else ckl(rc, "refine");
     }
     // backward output bounds: tighter forms / logit bounds for the certificate.  A network the
@@ -563,7 +573,7 @@ class BabRuntime {
   int pool_[2] = {0, 0};
   double unit_;
   bool crown_ = false;
-  bool refine_ = false;
+  int refine_ = 0;          // 0 forward + output pass, 1 + refine between them, 2 backward only
   int split_target_ = 256;
   int n0_ = 0, npa_ = 0, V_ = 0, Pp_ = 0, norient_ = 1;
   bool relaxed_ = false;
@@ -598,11 +608,11 @@ void register_bab(py::module& m) {
   py::class_<BabRuntime>(m, "BabRuntime")
       .def(py::init<py::handle, uintptr_t, std::vector<int>, std::vector<float>, std::vector<int64_t>,
                     std::vector<int64_t>, std::vector<int>, float, std::vector<uint8_t>, int, int, int, double, bool,
-                    int, bool>(),
+                    int, int>(),
            py::arg("net"), py::arg("flat"), py::arg("pa"), py::arg("values_f"), py::arg("values_i"),
            py::arg("pairs"), py::arg("ra"), py::arg("tau"), py::arg("shared"), py::arg("capacity"),
            py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"), py::arg("crown") = true,
-           py::arg("split_target") = 256, py::arg("refine") = false)
+           py::arg("split_target") = 256, py::arg("refine") = 0)
       .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"),
            py::arg("native_exact") = false, py::arg("budget2") = 0, py::arg("max_w") = 0,

@@ -32,12 +32,17 @@
 
 #include "args.h"
 
+// Mode FULL (fa_backward_launch): no forward pass at all -- layer 0 from the box, every hidden layer
+// by back-substitution, then the logit's forms and bounds (the work of crown.hip) in the same
+// launch: one kernel instead of forward symbolic + refine + output pass (ops/reference.py:
+// backward_bounds).  Mode REFINE (fa_refine_launch): tighten the forward pass's hidden-layer bounds.
 struct RefineCfg {
   int w_lds[FA_MAX_LAYERS];   // LDS float offset of layer l's W in backward operand order
   int b_lds[FA_MAX_LAYERS];
   int slab;                   // LDS float offset of the row slabs: G x [lb (N) | ub (N)]
   int G;                      // box-rows per workgroup
   int floats;
+  int full;                   // 1: mode FULL
 };
 
 __device__ __forceinline__ float fa_rgam(int k, float u) {
@@ -50,8 +55,9 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int L = net.n_layers;
-  // ---- stage W_l (l < L-1) in backward operand order + the biases
-  for (int l = 0; l < L - 1; ++l) {
+  const int LW = cfg.full ? L : L - 1;          // layers whose W is staged (FULL: the logit's too)
+  // ---- stage W_l (l < LW) in backward operand order + the biases
+  for (int l = 0; l < LW; ++l) {
     const int nin = net.dims[l], nout = net.dims[l + 1];
     const int tin = (nin + 15) >> 4, tout = (nout + 15) >> 4;
     const float* W = a.flat + net.w_off[l];
@@ -90,15 +96,17 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
       any = (st == 3 || st == 4);
     }
     if (!any) continue;   // uniform across the workgroup (same loads everywhere)
-    // ---- load the rows' forward bounds
+    // ---- load the rows' forward bounds (FULL: no forward pass, start from the whole line)
     for (int e = tid; e < G * N; e += 256) {
       const int g = e / N, k = e - g * N;
       const int r = min(rb + g, a.R - 1);
-      slab[g * 2 * N + k] = a.layer_lb[(size_t)r * N + k];
-      slab[g * 2 * N + N + k] = a.layer_ub[(size_t)r * N + k];
+      slab[g * 2 * N + k] = cfg.full ? -INFINITY : a.layer_lb[(size_t)r * N + k];
+      slab[g * 2 * N + N + k] = cfg.full ? INFINITY : a.layer_ub[(size_t)r * N + k];
     }
     __syncthreads();
-    for (int k = 1; k < L - 1; ++k) {
+    const int k0 = cfg.full ? 0 : 1, k1 = cfg.full ? L : L - 1;
+    for (int k = k0; k < k1; ++k) {
+      const bool logit = k == L - 1;               // FULL only: the output forms
       const int nk = net.dims[k + 1];
       const int ktop = net.dims[k];                  // width of h_{k-1}
       const int offk = net.neuron_off[k];
@@ -239,7 +247,29 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
         mp += __shfl_xor(mp, 16); mp += __shfl_xor(mp, 32);
         const float conc = cp + c;
         const float cmg = mp + fabsf(c);
-        const float low = conc - err * (1.f + 2.f * gK) - g0 * cmg - g1 * fabsf(conc);
+        const float errK = err * (1.f + 2.f * gK);
+        const float low = conc - errK - g0 * cmg - g1 * fabsf(conc);
+        bool wr = rvalid;
+        if (logit && wr && a.skip_status) {       // forms of decided partitions' rows: not needed
+          const int8_t st = a.skip_status[a.skip_part[node]];
+          wr = (st == 3 || st == 4);
+        }
+        if (logit && wr) {
+          // the logit's back-substituted forms: s = 0 lower (L), s = 1 upper (U = -form)
+#pragma unroll
+          for (int t = 0; t < TM; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int in = 16 * t + 4 * grp + i;
+              if (in >= n0) continue;
+              if (s) a.Uc[(size_t)r * n0 + in] = -lam[t][i];
+              else a.Lc[(size_t)r * n0 + in] = lam[t][i];
+            }
+          if (grp == 0) {
+            if (s) { a.U0[r] = -c; a.Ue[r] = errK; a.out_ub[r] = -low; }
+            else { a.L0[r] = c; a.Le[r] = errK; a.out_lb[r] = low; }
+          }
+        }
         // lane group 0 of each column writes (the 4 groups hold the same column value)
         if (rvalid && grp == 0) {
           float* dst = slab + g * 2 * N + (s ? N : 0) + offk + j;
@@ -248,9 +278,11 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
       }
       __syncthreads();
     }
-    // ---- write the refined hidden-layer bounds back (rows of running partitions only)
-    const int lo_n = net.neuron_off[1 < L - 1 ? 1 : 0];
-    const int hi_n = net.n_hidden;
+    // ---- write the refined hidden-layer bounds back (rows of running partitions only; FULL: only
+    // when the caller wants them -- the BaB does not)
+    if (cfg.full && !a.layer_lb) continue;
+    const int lo_n = cfg.full ? 0 : net.neuron_off[1 < L - 1 ? 1 : 0];
+    const int hi_n = cfg.full ? N : net.n_hidden;
     const int span = hi_n - lo_n;
     if (span > 0)
       for (int e = tid; e < G * span; e += 256) {
@@ -292,24 +324,22 @@ int refine_cus() {
 }
 }  // namespace
 
-// 0 launched (or nothing to refine: fewer than two hidden layers), -1 shape not supported (a layer
-// wider than 160 or the weights beyond the LDS budget: the caller keeps the forward bounds, which
-// are sound), < -1 error.  Needs a.layer_lb / a.layer_ub [R, n_neurons] from the forward pass.
-extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream) {
+namespace {
+int backward_launch(const NetDesc& net, const BoundArgs& a, int full, hipStream_t stream) {
   const int L = net.n_layers;
-  if (a.R <= 0 || L < 3) return 0;
-  if (!a.layer_lb || !a.layer_ub) return -2;
   int TM = 1;
   for (int l = 0; l < L; ++l) TM = std::max(TM, (net.dims[l] + 15) / 16);
   const RefineKernel k = select_refine(TM);
   if (!k) return -1;
   RefineCfg cfg{};
+  cfg.full = full;
+  const int LW = full ? L : L - 1;
   int offs = 0;
-  for (int l = 0; l < L - 1; ++l) {
+  for (int l = 0; l < LW; ++l) {
     cfg.w_lds[l] = offs;
     offs += ((net.dims[l] + 15) / 16) * ((net.dims[l + 1] + 15) / 16) * 256;
   }
-  for (int l = 0; l < L - 1; ++l) {
+  for (int l = 0; l < LW; ++l) {
     cfg.b_lds[l] = offs;
     offs += net.dims[l + 1];
   }
@@ -345,6 +375,25 @@ extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t str
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), bytes, stream, net, a, cfg);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e - 10;
+}
+}  // namespace
+
+// 0 launched (or nothing to refine: fewer than two hidden layers), -1 shape not supported (a layer
+// wider than 160 or the weights beyond the LDS budget: the caller keeps the forward bounds, which
+// are sound), < -1 error.  Needs a.layer_lb / a.layer_ub [R, n_neurons] from the forward pass.
+extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream) {
+  if (a.R <= 0 || net.n_layers < 3) return 0;
+  if (!a.layer_lb || !a.layer_ub) return -2;
+  return backward_launch(net, a, 0, stream);
+}
+
+// Mode FULL: out_lb / out_ub and the logit's forms (Lc, L0, Le, Uc, U0, Ue) of every row without a
+// forward pass; layer_lb / layer_ub [R, n_neurons] written when given.  0 launched, -1 shape not
+// supported (the caller runs the forward pass instead), < -1 error.
+extern "C" int fa_backward_launch(const NetDesc& net, BoundArgs a, hipStream_t stream) {
+  if (a.R <= 0) return 0;
+  if (!a.out_lb || !a.out_ub || !a.Lc || !a.L0 || !a.Le || !a.Uc || !a.U0 || !a.Ue) return -2;
+  return backward_launch(net, a, 1, stream);
 }
 
 FA_LDS_REGISTER(FA_LDS_K(fa_refine_kernel<1>), FA_LDS_K(fa_refine_kernel<2>), FA_LDS_K(fa_refine_kernel<4>),

@@ -80,17 +80,26 @@ class BaBResult:
                                              # (native runtime; the escalation filter's predictor)
 
 
-def refine_on(mode: str, widths) -> bool:
-    """Whether the BaB bounds its nodes with back-substituted hidden-layer bounds (BaBConfig.refine).
-    ``auto``: at least 3 hidden layers and one of them at least 10 wide -- with 1-2 hidden layers the
-    refined bounds equal the forward ones, and on the narrow deep nets (AC-9/10/12, 3-5 wide) the
-    extra pass costs more than it closes (tools/diag_open_nodes.py on the bench residue)."""
-    if mode == "on":
-        return True
+def refine_level(mode: str, widths) -> int:
+    """How the BaB bounds its nodes (BaBConfig.refine): 0 forward symbolic + backward output pass,
+    1 with back-substituted hidden-layer bounds between them (csrc/refine.hip), 2 back-substitution
+    alone (one launch, no forward pass).  ``auto``: level 1 for networks with at least 3 hidden
+    layers, one of them at least 10 wide -- with 1-2 hidden layers the refined bounds equal the
+    forward ones, and on the narrow deep nets (AC-9/10/12, 3-5 wide) the extra pass costs more than
+    it closes (tools/diag_open_nodes.py on the bench residue)."""
+    if mode in ("on", "refine"):
+        return 1
+    if mode == "full":
+        return 2
     if mode != "auto":
-        return False
+        return 0
     hidden = list(widths)[:-1]
-    return len(hidden) >= 3 and max(hidden) >= 10
+    return 1 if (len(hidden) >= 3 and max(hidden) >= 10) else 0
+
+
+def refine_on(mode: str, widths) -> bool:
+    """Hidden-layer bounds tightened by back-substitution (any level > 0 of :func:`refine_level`)."""
+    return refine_level(mode, widths) > 0
 
 
 def pa_groups(q: ResolvedQuery, lo: np.ndarray, hi: np.ndarray) -> List[np.ndarray]:
@@ -366,7 +375,7 @@ class BaBSolver:
         from ..ops.hip import _net
         from .rtpool import checkout
 
-        rf = refine_on(self.cfg.refine, self.be.widths)
+        rf = refine_level(self.cfg.refine, self.be.widths)
         key = (tuple(self.q.pa_idx), tuple(self.q.ra_idx), self.q.tau, values_np.tobytes(), pairs_np.tobytes(),
                bool(self.cfg.crown), int(self.cfg.split_target), rf)
         shared = np.ones(self.q.n, dtype=np.uint8)

@@ -152,6 +152,17 @@ class Backend:
         ref.bounds); the result's ``infeasible`` flags rows whose region is empty."""
         lo = lo.to(self.dtype)
         hi = hi.to(self.dtype)
+        if mode == "backward":
+            # every bound by back-substitution alone (ref.backward_bounds / csrc/refine.hip FULL)
+            if self.hip:
+                from . import hip
+
+                r = hip.backward_bounds(self, lo, hi, dead)
+                if r is not None:
+                    return r
+                mode, crown, refine = "symbolic", True, True
+            else:
+                return ref.backward_bounds(self.ws, self.bs, lo, hi, dead, unit=self.unit)
         crown = crown and mode == "symbolic"
         if self.hip:
             from . import hip

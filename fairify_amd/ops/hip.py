@@ -274,6 +274,46 @@ def refine(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, dead: O
 
 
 # ------------------------------------------------------------------------------------------------
+def backward_bounds(be, lo: torch.Tensor, hi: torch.Tensor, dead: Optional[torch.Tensor] = None,
+                    keep_layers: bool = True) -> Optional[ref.BoundResult]:
+    """Every neuron's bounds and the logit's forms by back-substitution alone (csrc/refine.hip mode
+    FULL, ref.backward_bounds).  ``None`` when the network does not fit the kernel."""
+    R, n0 = lo.shape
+    dev = lo.device
+    lo = _c(lo, torch.float32, (R, n0), "lo")
+    hi = _c(hi, torch.float32, (R, n0), "hi")
+    f32 = dict(dtype=torch.float32, device=dev)
+    res = ref.BoundResult(out_lb=torch.empty(R, **f32), out_ub=torch.empty(R, **f32),
+                          Lc=torch.empty(R, n0, **f32), L0=torch.empty(R, **f32), Le=torch.empty(R, **f32),
+                          Uc=torch.empty(R, n0, **f32), U0=torch.empty(R, **f32), Ue=torch.empty(R, **f32))
+    N = be.mlp.n_neurons
+    lay_lb = torch.empty(R, N, **f32) if keep_layers else None
+    lay_ub = torch.empty(R, N, **f32) if keep_layers else None
+    d = None
+    if dead is not None:
+        d = _c(dead, torch.uint8, (R, be.n_hidden), "dead")
+    if R:
+        rc = ext().backward_bounds(_net(be), be.flat.data_ptr(), lo.data_ptr(), hi.data_ptr(), _ptr(d), R,
+                                   res.out_lb.data_ptr(), res.out_ub.data_ptr(), res.Lc.data_ptr(), res.L0.data_ptr(),
+                                   res.Le.data_ptr(), res.Uc.data_ptr(), res.U0.data_ptr(), res.Ue.data_ptr(),
+                                   _ptr(lay_lb), _ptr(lay_ub), _stream(dev))
+        if rc == -1:
+            return None
+    if keep_layers:
+        widths = be.mlp.widths
+        offs = [0]
+        for w in widths:
+            offs.append(offs[-1] + w)
+        res.layer_lb = [lay_lb[:, offs[i]:offs[i + 1]] for i in range(len(widths))]
+        res.layer_ub = [lay_ub[:, offs[i]:offs[i + 1]] for i in range(len(widths))]
+        res.lay_lb_full, res.lay_ub_full = lay_lb, lay_ub
+        Nh = be.n_hidden
+        res.dead = lay_ub[:, :Nh] <= 0
+        res.active = lay_lb[:, :Nh] >= 0
+    return res
+
+
+# ------------------------------------------------------------------------------------------------
 def crown_phase(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, phase: Optional[torch.Tensor] = None):
     """ReLU-phase backward bounds (csrc/relu.hip: fa_crown_phase_kernel) on rows bounded by
     :func:`bounds` (symbolic, keep_layers, same ``phase``).  Refines ``res`` (logit bounds, forms)

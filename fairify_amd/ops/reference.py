@@ -469,6 +469,48 @@ def crown_refine(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: tor
 
 
 
+def backward_bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Tensor, hi: torch.Tensor,
+                    dead: Optional[torch.Tensor] = None, unit: Optional[float] = None) -> BoundResult:
+    """Bounds of every neuron and the logit's linear forms by back-substitution alone (csrc/refine.hip,
+    mode FULL): layer 0 from the box, each hidden layer k by back-substituting +-W_k[:, j] through the
+    relaxations of the layers below, the logit's forms likewise -- no forward symbolic pass.  On the
+    deep nets the forward intervals add nothing to these (the refined bounds close the same AC-7
+    residue with or without them, tools/diag_open_nodes.py --bound fullcrown vs crown_refine), so the
+    BaB bounds them with this one pass instead of forward + refine + output (3 launches -> 1)."""
+    dt = lo.dtype
+    if unit is None:
+        unit = FP64_UNIT if dt == torch.float64 else FP32_UNIT
+    R, n0 = lo.shape
+    L = len(ws)
+    lbs, ubs = [], []
+    for k in range(L - 1):
+        n_k = ws[k].shape[1]
+        Wt = ws[k].to(dt).T
+        rep = lambda t: t.repeat_interleave(n_k, dim=0)          # noqa: E731
+        rl, rh = rep(lo), rep(hi)
+        lb_r, ub_r = [rep(t) for t in lbs], [rep(t) for t in ubs]
+        d_r = rep(dead) if dead is not None else None
+        low = {}
+        for sg in (1.0, -1.0):
+            lam = (sg * Wt)[None].expand(R, -1, -1).reshape(R * n_k, -1).clone()
+            c = (sg * bs[k].to(dt))[None].expand(R, -1).reshape(-1).clone()
+            low[sg] = _backsub(ws, bs, rl, rh, lb_r, ub_r, lam, c, k, d_r, unit)[3].view(R, n_k)
+        lbs.append(low[1.0])
+        ubs.append(-low[-1.0])
+    inf = torch.full((R,), float("inf"), dtype=dt, device=lo.device)
+    base = BoundResult(out_lb=-inf, out_ub=inf, Lc=torch.zeros(R, n0, dtype=dt, device=lo.device),
+                       L0=torch.zeros(R, dtype=dt, device=lo.device), Le=inf.clone(),
+                       Uc=torch.zeros(R, n0, dtype=dt, device=lo.device), U0=torch.zeros(R, dtype=dt, device=lo.device),
+                       Ue=inf.clone(), layer_lb=lbs + [-inf[:, None]], layer_ub=ubs + [inf[:, None]])
+    r = crown_output(ws, bs, lo, hi, base, dead, unit=unit)
+    r.layer_lb = lbs + [r.out_lb[:, None]]
+    r.layer_ub = ubs + [r.out_ub[:, None]]
+    if lbs:
+        r.dead = torch.cat([u <= 0 for u in ubs], dim=1)
+        r.active = torch.cat([l >= 0 for l in lbs], dim=1)
+    return r
+
+
 def crown_output(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Tensor, hi: torch.Tensor,
                  res: BoundResult, dead: Optional[torch.Tensor] = None, unit: Optional[float] = None) -> BoundResult:
     """Backward (CROWN-style) linear bounds of the logit, replacing the forward-symbolic output

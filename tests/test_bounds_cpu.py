@@ -196,3 +196,37 @@ def test_refine_tightens_deep_net():
     gain = sum(float((rf.layer_ub[k] - rf.layer_lb[k]).sum()) for k in range(1, 5))
     base = sum(float((fw.layer_ub[k] - fw.layer_lb[k]).sum()) for k in range(1, 5))
     assert gain < 0.9 * base
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_backward_bounds_sound(seed):
+    """ref.backward_bounds (no forward pass): sound on every lattice point (hidden pre-activations,
+    forms, logit bounds).  (Not always as tight as forward + refine + output pass: the forward forms
+    sometimes win at the output.)"""
+    import itertools
+
+    from fairify_amd.models.mlp import random_mlp
+    from fairify_amd.ops import reference as ref
+    from fairify_amd.ops.backend import Backend
+
+    g = np.random.default_rng(200 + seed)
+    n0 = 13 if seed % 2 else 6
+    hidden = [[64, 32, 16, 8, 4], [10, 10, 10, 10], [16, 16, 16]][seed % 3]
+    m = random_mlp(n0, hidden, seed=seed, bias_scale=0.0 if seed % 3 == 0 else 0.4)
+    be = Backend(m, "cpu")
+    lo = g.integers(0, 5, size=(1, n0))
+    hi = lo.copy()
+    dims = g.choice(n0, size=min(n0, 4), replace=False)
+    hi[0, dims] += g.integers(1, 4, size=dims.size)
+    pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[0], hi[0])])))
+    L_, H_ = torch.tensor(lo, dtype=torch.float32), torch.tensor(hi, dtype=torch.float32)
+    r = ref.backward_bounds(be.ws, be.bs, L_, H_, unit=be.unit)
+    z = _pre_activations(m, pts)
+    for k in range(len(hidden)):
+        assert np.all(z[k] >= r.layer_lb[k][0].double().numpy() - 1e-9)
+        assert np.all(z[k] <= r.layer_ub[k][0].double().numpy() + 1e-9)
+    zl = m.logits(pts)
+    Lf = pts @ r.Lc[0].double().numpy() + float(r.L0[0]) - float(r.Le[0])
+    Uf = pts @ r.Uc[0].double().numpy() + float(r.U0[0]) + float(r.Ue[0])
+    assert np.all(zl >= Lf - 1e-9) and np.all(zl <= Uf + 1e-9)
+    assert zl.min() >= float(r.out_lb[0]) and zl.max() <= float(r.out_ub[0])

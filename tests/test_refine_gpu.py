@@ -137,3 +137,64 @@ def test_refine_cuts_bab_nodes_on_ac7(cuda):
         out[mode] = (int(np.isin(r.status, (SAT, UNSAT)).sum()), int(r.nodes.sum()))
     assert out["on"][0] >= out["off"][0], out
     assert out["on"][1] < out["off"][1], out
+
+
+@pytest.mark.parametrize("n0,hidden", SHAPES)
+def test_backward_kernel_matches_reference_and_is_sound(cuda, n0, hidden):
+    """Mode FULL (one launch, no forward pass) vs ref.backward_bounds in fp64 with fp32 error terms;
+    sound against sampled lattice points (hidden pre-activations, logit forms, logit bounds)."""
+    m = random_mlp(n0, hidden, seed=21 + n0 + len(hidden), bias_scale=0.3)
+    lo, hi = _boxes(n0, 203, 7)
+    gpu = Backend(m, cuda)
+    rg = gpu.bounds(lo.to(cuda), hi.to(cuda), mode="backward")
+    ws = [w.double() for w in Backend(m, "cpu").ws]
+    bs = [b.double() for b in Backend(m, "cpu").bs]
+    rr = ref.backward_bounds(ws, bs, lo.double(), hi.double(), unit=ref.FP32_UNIT)
+    for k in range(len(hidden)):
+        scale = float((rr.layer_ub[k] - rr.layer_lb[k]).abs().max() + rr.layer_ub[k].abs().max() + 1e-3)
+        assert torch.allclose(rg.layer_lb[k].cpu().double(), rr.layer_lb[k], rtol=1e-4, atol=1e-4 * scale), k
+        assert torch.allclose(rg.layer_ub[k].cpu().double(), rr.layer_ub[k], rtol=1e-4, atol=1e-4 * scale), k
+    scale = float((rr.out_ub - rr.out_lb).abs().max() + rr.out_ub.abs().max() + 1e-3)
+    assert torch.allclose(rg.out_lb.cpu().double(), rr.out_lb, rtol=1e-4, atol=1e-4 * scale)
+    assert torch.allclose(rg.out_ub.cpu().double(), rr.out_ub, rtol=1e-4, atol=1e-4 * scale)
+    g = np.random.default_rng(5)
+    X = (lo[:, None, :] + torch.from_numpy(g.random((lo.shape[0], 64, n0))).float()
+         * (hi - lo + 1)[:, None, :]).floor().clamp(max=hi[:, None, :]).numpy().astype(np.float64)
+    h = X
+    for k, (w, b) in enumerate(zip(m.weights[:-1], m.biases[:-1])):
+        z = h @ w.astype(np.float64) + b.astype(np.float64)
+        assert np.all(z >= rg.layer_lb[k].double().cpu().numpy()[:, None, :] - 1e-9)
+        assert np.all(z <= rg.layer_ub[k].double().cpu().numpy()[:, None, :] + 1e-9)
+        h = np.maximum(z, 0)
+    zl = m.logits(X.reshape(-1, n0)).reshape(X.shape[0], -1)
+    Lf = np.einsum("rsn,rn->rs", X, rg.Lc.double().cpu().numpy()) + (rg.L0 - rg.Le).double().cpu().numpy()[:, None]
+    Uf = np.einsum("rsn,rn->rs", X, rg.Uc.double().cpu().numpy()) + (rg.U0 + rg.Ue).double().cpu().numpy()[:, None]
+    assert np.all(zl >= Lf - 1e-9) and np.all(zl <= Uf + 1e-9)
+    assert np.all(zl >= rg.out_lb.double().cpu().numpy()[:, None]) and np.all(zl <= rg.out_ub.double().cpu().numpy()[:, None])
+
+
+@pytest.mark.parametrize("name", ["AC-7", "AC-4"])
+def test_backward_native_bab_matches_bruteforce(cuda, name):
+    """The native BaB bounding with back-substitution alone (BaBConfig.refine='full') decides like
+    exhaustive enumeration."""
+    from fairify_amd import presets
+    from fairify_amd.engine.bab import SAT, UNSAT, BaBConfig, BaBSolver
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.partition import processing_order
+
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    m = get_model(name, weights="random", seed=2)
+    be = Backend(m, cuda)
+    ids = processing_order(grid, 0)[:96]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 1)
+    res = BaBSolver(be, q, BaBConfig(node_budget=4096, refine="full")).solve(lo, hi, m)
+    pa = q.pa_idx[0]
+    for k in range(len(ids)):
+        pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[k], hi[k])])))
+        z0 = m.logits(np.where(np.arange(m.n_in) == pa, 0, pts))
+        z1 = m.logits(np.where(np.arange(m.n_in) == pa, 1, pts))
+        viol = bool((((z0 > 0) & (z1 < 0)) | ((z0 < 0) & (z1 > 0))).any())
+        assert res.status[k] in (SAT, UNSAT), k
+        assert (res.status[k] == SAT) == viol, k
