@@ -68,6 +68,16 @@ struct SymBox {
   }
 };
 
+// Row rotation of the epilogue's staging tile: form column c of tile row rho (0..31: 16 U rows, 16
+// L rows) sits at rho * TS + c + (rho >> 3).  The spill / reload (lanes of one 32-lane half write
+// or read 2 rows that share rho >> 3, 16 consecutive columns each) stay conflict-free as with the
+// plain layout (TS = 4 mod 8), and the per-lane row walk of the epilogue -- 32 lanes on 32
+// different rows, the compiler splits it into ds_read2_b32 / ds_write2_b32 pairs (banks mod 32) --
+// no longer hits the 8-row period of the 20-float stride: rows rho and rho + 8 land 1 bank apart
+// instead of on the same bank (4-way conflicts, 1.7-1.9 conflict cycles per LDS instruction in
+// profiles/r3/pmc/README.md).  Columns stay below TS: c <= 16 NT - 1, shift <= 3, TS = 16 NT + 4.
+__device__ __forceinline__ int fa_trot(int rho) { return rho >> 3; }
+
 // per-wave LDS slab: tile staging T[2 blocks][16 neurons][TS] + box values [2 PG boxes][3][48]
 // (+ packed mode: the boxes' input ranges [2 PG][lo 16 | hi 16] for the on-the-fly layer-0 operands)
 template <int NT, int PG = 1>
@@ -161,16 +171,18 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
   const int n_out_t = net.dims[l + 1];
   const bool nl_act = PG > 1 ? r < a.R : (16 * jt < n_out_t && (!second || v2));
   const int ob = (lane >> 4) & 1;
-  float* Trow = T + tsub * SymSlab<NT>::TILE1 + (ob * 16 + col) * TS;
-    // ---------------- spill both tiles: T[tile][block][neuron][column]
+  // this lane's row (tile row ob * 16 + col of tile tsub), rotated (fa_trot)
+  float* Trow = T + tsub * SymSlab<NT>::TILE1 + (ob * 16 + col) * TS + fa_trot(ob * 16 + col);
+    // ---------------- spill both tiles: T[tile][block][neuron][column] (rotated rows)
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          T[u * SymSlab<NT>::TILE1 + (4 * grp + i) * TS + ct * 16 + col] = U[u][ct][i];
-          T[u * SymSlab<NT>::TILE1 + (16 + 4 * grp + i) * TS + ct * 16 + col] = Lq[u][ct][i];
+          const int ru = 4 * grp + i, rl = 16 + 4 * grp + i;
+          T[u * SymSlab<NT>::TILE1 + ru * TS + fa_trot(ru) + ct * 16 + col] = U[u][ct][i];
+          T[u * SymSlab<NT>::TILE1 + rl * TS + fa_trot(rl) + ct * 16 + col] = Lq[u][ct][i];
         }
     __builtin_amdgcn_wave_barrier();
     // ---------------- one lane per (tile, neuron, block): bounds, relaxation, new form row
@@ -178,10 +190,7 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
     const bool jv = j < n_out;
     float v[16 * NT];
 #pragma unroll
-    for (int q = 0; q < 4 * NT; ++q) {
-      const float4 x = reinterpret_cast<const float4*>(Trow)[q];
-      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
-    }
+    for (int c = 0; c < 16 * NT; ++c) v[c] = Trow[c];
     const float b = jv ? sb[PG > 1 ? col : j] : 0.f;       // packed biases: 16 per layer, box g at g * PS
     // concretisation of the coefficient part over the box in centre/radius form:
     //   min / max = Σ v mid -+ Σ |v| rad,  magnitude Σ |v| m  (m >= |mid| + rad)
@@ -287,8 +296,7 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
     for (int c = 4; c < 16 * NT; ++c) v[c] *= s;
     if (nl_act) {
 #pragma unroll
-      for (int q = 0; q < 4 * NT; ++q)
-        reinterpret_cast<float4*>(Trow)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      for (int c = 0; c < 16 * NT; ++c) Trow[c] = v[c];
     }
     __builtin_amdgcn_wave_barrier();
     // ---------------- reload both tiles in MFMA operand layout: next layer's B
@@ -298,8 +306,9 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
       for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float xu = T[u * SymSlab<NT>::TILE1 + (4 * grp + i) * TS + ct * 16 + col];
-          const float xl = T[u * SymSlab<NT>::TILE1 + (16 + 4 * grp + i) * TS + ct * 16 + col];
+          const int ru = 4 * grp + i, rl = 16 + 4 * grp + i;
+          const float xu = T[u * SymSlab<NT>::TILE1 + ru * TS + fa_trot(ru) + ct * 16 + col];
+          const float xl = T[u * SymSlab<NT>::TILE1 + rl * TS + fa_trot(rl) + ct * 16 + col];
           nu[u][ct][i] = CR ? 0.5f * (xu + xl) : xu;     // C/R: centre / radius operands
           nlo[u][ct][i] = CR ? 0.5f * (xu - xl) : xl;
         }
@@ -337,7 +346,6 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
   // neuron lane role in the epilogue: lanes 0-15 = U block, 16-31 = L block of neuron (lane & 15)
   const bool nl_act = lane < 32;
   const int ob = (lane >> 4) & 1;
-  float* Trow = T + (ob * 16 + col) * TS;
 #ifndef FA_SYM_TIMING_NO_EPILOGUE
   if (PG > 1 && l == 0) {
     // packed layer 0: group u accumulates its PG boxes, box g through tile g of the packed W_0
