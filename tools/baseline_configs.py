@@ -1,0 +1,135 @@
+#!/usr/bin/env python
+"""One-HEAD re-measurement of every BASELINE.json config, sound verdicts only.
+
+    python tools/baseline_configs.py --group tablev  --out gpurun_out/r4/base --head <sha>
+    python tools/baseline_configs.py --group stress  --out ...
+    python tools/baseline_configs.py --group relaxed --out ...
+    python tools/baseline_configs.py --group targeted --out ...
+    python tools/baseline_configs.py --report gpurun_out/r4/base > profiles/r4/baseline_configs.md
+
+Groups (BASELINE.json ``configs``; reference constants per SURVEY §2.5):
+
+* ``tablev``   -- Table V of the paper with the reference's TRAINED weights: src/AC-sex, src/AC-race,
+                  src/BM-age, src/GC-sex, src/GC-age, every model, anytime mode (the reference spends up
+                  to its hard timeout per model, src/AC/Verify-AC.py:318-320; here ``--anytime-budget``
+                  seconds per model);
+* ``stress``   -- stress/AC, stress/BM, stress/GC full grids (3.29 M / 1.0 M / 18 009 partitions);
+* ``relaxed``  -- relaxed/AC, relaxed/BM, relaxed/GC (|x_r - x'_r| <= tau, x' unclipped);
+* ``targeted`` -- targeted/* and targeted2/* (domain overrides).
+
+Every preset runs every model of the preset (trained weights where the zoo has them, else the
+preset's random-init shape), with the heuristic retry OFF: every UNSAT is a proof and every SAT an
+exactly confirmed pair.  Each run writes ``<out>/<preset>/summary.json`` (per-model Table-V rows
+with ``Cov_sound%``, ``UNSAT_heuristic``, wall time) and the HEAD sha; the
+report turns all of them into one markdown table.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+GROUPS = {
+    "tablev": ["src/AC-sex", "src/AC-race", "src/BM-age", "src/GC-sex", "src/GC-age"],
+    "stress": ["stress/AC", "stress/BM", "stress/GC"],
+    "relaxed": ["relaxed/AC", "relaxed/BM", "relaxed/GC"],
+    "targeted": ["targeted/AC", "targeted/BM", "targeted/GC", "targeted2/AC", "targeted2/BM", "targeted2/GC"],
+}
+
+
+def run_group(args) -> None:
+    import torch
+
+    from fairify_amd import presets
+    from fairify_amd.engine.pipeline import VerifyConfig
+    from fairify_amd.engine.runner import run_preset
+    from fairify_amd.models.zoo import has_weights
+    from fairify_amd.parallel import dist as D
+
+    info = D.init("cuda" if torch.cuda.device_count() else "cpu")
+    names = GROUPS[args.group] if args.group in GROUPS else args.group.split(",")
+    for name in names:
+        pre = presets.get(name)
+        models = list(pre.models) if not args.models else args.models.split(",")
+        out = os.path.join(args.out, name.replace("/", "_"))
+        os.makedirs(out, exist_ok=True)
+        anytime = args.anytime_budget if (args.group == "tablev" or args.anytime_budget > 0 and args.all_anytime) else 0
+        cfg = VerifyConfig(sim_size=pre.sim_size, soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
+                           heuristic=False, heuristic_p=pre.heuristic_p, node_budget=512, escalate_budget=32768,
+                           escalate_max_open=384,
+                           escalate_probation=((2048, 768), (4096, 768), (8192, 768), (16384, 1024)),
+                           relu_budget=1024, relu_escalate_cap=2048, smt_backend="auto", chunk=8192)
+        t0 = time.time()
+        weights = {m: ("zoo" if has_weights(m) else "random") for m in models}
+        rows = []
+        for m in models:
+            r = run_preset(pre, models=[m], weights=weights[m], out_dir=os.path.join(out, m), cfg=cfg, info=info,
+                           seed=0, accuracy=False, verbose=False, concurrency=4,
+                           anytime_budget=anytime or None, max_partitions=args.max_partitions)
+            for row in r:
+                row["weights"] = weights[m]
+                rows.append(row)
+                print(f"[{name}] {m} ({weights[m]}): {row['SAT']} sat / {row['UNSAT']} unsat / {row['UNK']} unk "
+                      f"of {row['#P']}, Cov_sound {row.get('Cov_sound%')} %, {row.get('wall_s')} s",
+                      flush=True)
+        with open(os.path.join(out, "summary.json"), "w") as f:
+            json.dump({"preset": name, "models": rows, "head": args.head, "wall_s": round(time.time() - t0, 2),
+                       "anytime_budget_s": anytime, "heuristic": False}, f, indent=2)
+        print(f"[{name}] done in {time.time() - t0:.1f}s", flush=True)
+    D.destroy(info)
+
+
+def report(root: str) -> None:
+    rows = []
+    heads = set()
+    for path in sorted(glob.glob(os.path.join(root, "*", "summary.json"))):
+        s = json.load(open(path))
+        heads.add(s.get("head"))
+        for r in s["models"]:
+            rows.append((s["preset"], s.get("anytime_budget_s", 0), r))
+    print(f"# BASELINE configs at one HEAD ({', '.join(sorted(h or '?' for h in heads))}), sound verdicts only\n")
+    print("`tools/baseline_configs.py` on 1x MI355X; heuristic retry off (every UNSAT a proof, every SAT an exactly "
+          "confirmed pair).  Cov_sound% = (SAT + sound UNSAT) / grid.\n")
+    print("| preset | model | weights | grid | SAT | UNSAT | UNK | Cov_sound % | UNSAT_heuristic | anytime s | wall s | "
+          "partitions/s |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
+    tot = {}
+    for preset, any_s, r in rows:
+        print(f"| {preset} | {r['model']} | {r.get('weights', '?')} | {r['Grid']} | {r['SAT']} | {r['UNSAT']} | "
+              f"{r['UNK']} | {r.get('Cov_sound%')} | {r.get('UNSAT_heuristic', 0)} | {any_s or '-'} | "
+              f"{r.get('wall_s', '?')} | {r.get('partitions_per_s', '?')} |")
+        t = tot.setdefault(preset, [0, 0, 0, 0.0])
+        t[0] += r["Grid"]
+        t[1] += r["SAT"] + r.get("UNSAT_sound", r["UNSAT"])
+        t[2] += r.get("UNSAT_heuristic", 0)
+        t[3] += float(r.get("wall_s", 0) or 0)
+    print("\n| preset | grid (all models) | sound decided | Cov_sound % | UNSAT_heuristic | wall s |")
+    print("|---|---|---|---|---|---|")
+    for preset, (g, d, h, w) in tot.items():
+        print(f"| {preset} | {g} | {d} | {100.0 * d / max(1, g):.3f} | {h} | {w:.1f} |")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--group", default=None)
+    ap.add_argument("--models", default=None)
+    ap.add_argument("--out", default="gpurun_out/r4/base")
+    ap.add_argument("--head", default=os.environ.get("FAIRIFY_HEAD", ""))
+    ap.add_argument("--anytime-budget", type=float, default=120.0, help="tablev: seconds per model")
+    ap.add_argument("--all-anytime", action="store_true", help="anytime mode for the other groups too")
+    ap.add_argument("--max-partitions", type=int, default=None, help="CPU rehearsal: first N of each grid")
+    ap.add_argument("--report", default=None)
+    args = ap.parse_args()
+    if args.report:
+        report(args.report)
+    else:
+        run_group(args)
+
+
+if __name__ == "__main__":
+    main()
