@@ -46,6 +46,7 @@ extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_backward_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
+extern "C" int fa_refine_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_bab_init_launch(BabInitArgs a, hipStream_t stream);
 extern "C" int fa_bab_finish_launch(int P, const int8_t* status, const int* nodes, const int* open_left, int* out,
                                     hipStream_t stream);
@@ -344,7 +345,7 @@ class BabRuntime {
         sa.cand_buf = cand_buf_.p; sa.cand_count = cnt + 1;
         sa.cand_cap = cand_alloc_;
         ckl(fa_split_launch(sa, st), "split");
-        launches += (relaxed_ ? 2 : 1) * (refine_ == 2 ? 1 : (refine_ == 1 ? 3 : 2)) + 3;
+        launches += (relaxed_ ? 2 : 1) * (refine_ == 2 ? 1 : 2) + 3;   // bounding launches + certify, points, split
       }
       ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, nodes_.p, nodes_start_.p, prev_start_.p, cnt,
                            counters_.p + 2 * (slot ^ 1), hcount_, inline_esc ? pbudget_.p : nullptr,
@@ -434,9 +435,11 @@ class BabRuntime {
     // hidden-layer bounds tightened by back-substitution (refine.hip) before the output pass uses
     // them as relaxation intervals; a network the kernel cannot hold (-1) keeps the forward bounds
     if (refine_ == 1) {
-      const int rc = fa_refine_launch(net_, b, st);
-      if (rc == -1) refine_ = 0;
-      else ckl(rc, "refine");
+      // refined hidden-layer bounds and the logit's backward pass in one launch
+      const int rc = fa_refine_crown_launch(net_, b, st);
+      if (rc == 0) return;
+      if (rc != -1) ckl(rc, "refine");
+      refine_ = 0;
     }
     // backward output bounds: tighter forms / logit bounds for the certificate.  A network the
     // kernel cannot hold (layer > 256 wide or weights beyond the LDS budget: -1) keeps the

@@ -112,6 +112,7 @@ void register_relu(py::module& m);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_backward_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
+extern "C" int fa_refine_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 void register_csv(py::module& m);
 
 static void check(int rc, const char* what) {
@@ -221,6 +222,27 @@ PYBIND11_MODULE(_C, m) {
     a.layer_ub = P<float>(layer_ub);
     const int rc = fa_refine_launch(net.d, a, (hipStream_t)stream);
     if (rc < -1) throw std::runtime_error("refine launch failed, code " + std::to_string(rc));
+    return rc;
+  });
+
+  // refined hidden-layer bounds + the logit's backward pass in one launch (what the BaB runtime runs
+  // for BaBConfig.refine level 1), tightening a preceding symbolic `bounds` call in place
+  m.def("refine_crown", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t dead_in, int R,
+                           uintptr_t out_lb, uintptr_t out_ub, uintptr_t Lc, uintptr_t L0, uintptr_t Le, uintptr_t Uc,
+                           uintptr_t U0, uintptr_t Ue, uintptr_t layer_lb, uintptr_t layer_ub, uintptr_t stream) {
+    BoundArgs a{};
+    a.flat = P<const float>(flat);
+    a.lo = P<const float>(lo);
+    a.hi = P<const float>(hi);
+    a.dead_in = P<const uint8_t>(dead_in);
+    a.R = R;
+    a.out_lb = P<float>(out_lb); a.out_ub = P<float>(out_ub);
+    a.Lc = P<float>(Lc); a.L0 = P<float>(L0); a.Le = P<float>(Le);
+    a.Uc = P<float>(Uc); a.U0 = P<float>(U0); a.Ue = P<float>(Ue);
+    a.layer_lb = P<float>(layer_lb);
+    a.layer_ub = P<float>(layer_ub);
+    const int rc = fa_refine_crown_launch(net.d, a, (hipStream_t)stream);
+    if (rc < -1) throw std::runtime_error("refine_crown launch failed, code " + std::to_string(rc));
     return rc;
   });
 

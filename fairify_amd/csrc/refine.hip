@@ -43,6 +43,8 @@ struct RefineCfg {
   int G;                      // box-rows per workgroup
   int floats;
   int full;                   // 1: mode FULL
+  int logit;                  // REFINE mode: also the logit's backward forms (the work of crown.hip),
+                              // kept where tighter than the forward ones (FULL: always)
 };
 
 __device__ __forceinline__ float fa_rgam(int k, float u) {
@@ -55,7 +57,7 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int L = net.n_layers;
-  const int LW = cfg.full ? L : L - 1;          // layers whose W is staged (FULL: the logit's too)
+  const int LW = (cfg.full || cfg.logit) ? L : L - 1;   // layers whose W is staged (+ the logit's)
   // ---- stage W_l (l < LW) in backward operand order + the biases
   for (int l = 0; l < LW; ++l) {
     const int nin = net.dims[l], nout = net.dims[l + 1];
@@ -104,9 +106,9 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
       slab[g * 2 * N + N + k] = cfg.full ? INFINITY : a.layer_ub[(size_t)r * N + k];
     }
     __syncthreads();
-    const int k0 = cfg.full ? 0 : 1, k1 = cfg.full ? L : L - 1;
+    const int k0 = cfg.full ? 0 : 1, k1 = (cfg.full || cfg.logit) ? L : L - 1;
     for (int k = k0; k < k1; ++k) {
-      const bool logit = k == L - 1;               // FULL only: the output forms
+      const bool logit = k == L - 1;               // the output forms (FULL, or REFINE + logit)
       const int nk = net.dims[k + 1];
       const int ktop = net.dims[k];                  // width of h_{k-1}
       const int offk = net.neuron_off[k];
@@ -254,6 +256,11 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
           const int8_t st = a.skip_status[a.skip_part[node]];
           wr = (st == 3 || st == 4);
         }
+        if (logit && wr && !cfg.full) {
+          // REFINE + logit: replace the forward forms only where the backward ones concretise
+          // tighter (both are sound; crown.hip's rule)
+          wr = s ? (-low <= a.out_ub[r]) : (low >= a.out_lb[r]);
+        }
         if (logit && wr) {
           // the logit's back-substituted forms: s = 0 lower (L), s = 1 upper (U = -form)
 #pragma unroll
@@ -325,7 +332,7 @@ int refine_cus() {
 }  // namespace
 
 namespace {
-int backward_launch(const NetDesc& net, const BoundArgs& a, int full, hipStream_t stream) {
+int backward_launch(const NetDesc& net, const BoundArgs& a, int full, int logit, hipStream_t stream) {
   const int L = net.n_layers;
   int TM = 1;
   for (int l = 0; l < L; ++l) TM = std::max(TM, (net.dims[l] + 15) / 16);
@@ -333,7 +340,8 @@ int backward_launch(const NetDesc& net, const BoundArgs& a, int full, hipStream_
   if (!k) return -1;
   RefineCfg cfg{};
   cfg.full = full;
-  const int LW = full ? L : L - 1;
+  cfg.logit = logit;
+  const int LW = (full || logit) ? L : L - 1;
   int offs = 0;
   for (int l = 0; l < LW; ++l) {
     cfg.w_lds[l] = offs;
@@ -384,7 +392,16 @@ int backward_launch(const NetDesc& net, const BoundArgs& a, int full, hipStream_
 extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream) {
   if (a.R <= 0 || net.n_layers < 3) return 0;
   if (!a.layer_lb || !a.layer_ub) return -2;
-  return backward_launch(net, a, 0, stream);
+  return backward_launch(net, a, 0, 0, stream);
+}
+
+// REFINE + the logit's backward pass in the same launch (replaces fa_refine_launch + fa_crown_launch):
+// out_lb / out_ub and the forms of a preceding forward pass are tightened in place.
+extern "C" int fa_refine_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream) {
+  if (a.R <= 0) return 0;
+  if (net.n_layers < 3) return -1;
+  if (!a.layer_lb || !a.layer_ub || !a.out_lb || !a.Lc || !a.Uc) return -2;
+  return backward_launch(net, a, 0, 1, stream);
 }
 
 // Mode FULL: out_lb / out_ub and the logit's forms (Lc, L0, Le, Uc, U0, Ue) of every row without a
@@ -393,7 +410,7 @@ extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t str
 extern "C" int fa_backward_launch(const NetDesc& net, BoundArgs a, hipStream_t stream) {
   if (a.R <= 0) return 0;
   if (!a.out_lb || !a.out_ub || !a.Lc || !a.L0 || !a.Le || !a.Uc || !a.U0 || !a.Ue) return -2;
-  return backward_launch(net, a, 1, stream);
+  return backward_launch(net, a, 1, 1, stream);
 }
 
 FA_LDS_REGISTER(FA_LDS_K(fa_refine_kernel<1>), FA_LDS_K(fa_refine_kernel<2>), FA_LDS_K(fa_refine_kernel<4>),

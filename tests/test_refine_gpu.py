@@ -198,3 +198,26 @@ def test_backward_native_bab_matches_bruteforce(cuda, name):
         viol = bool((((z0 > 0) & (z1 < 0)) | ((z0 < 0) & (z1 > 0))).any())
         assert res.status[k] in (SAT, UNSAT), k
         assert (res.status[k] == SAT) == viol, k
+
+
+@pytest.mark.parametrize("n0,hidden", [(13, [64, 32, 16, 8, 4]), (13, [10, 10, 10, 10]), (16, [150, 100, 50])])
+def test_fused_refine_crown_equals_refine_then_crown(cuda, n0, hidden):
+    """The runtime's one-launch refine + logit pass (refine_crown) gives the forms and logit bounds
+    of the two launches it replaces (refine, then crown.hip), to rounding-order differences."""
+    from fairify_amd.ops import ext
+    from fairify_amd.ops import hip as H
+
+    m = random_mlp(n0, hidden, seed=31 + len(hidden), bias_scale=0.3)
+    lo, hi = _boxes(n0, 257, 11)
+    gpu = Backend(m, cuda)
+    L_, H_ = lo.to(cuda), hi.to(cuda)
+    two = gpu.bounds(L_, H_, mode="symbolic", crown=True, refine=True)
+    one = gpu.bounds(L_, H_, mode="symbolic", keep_layers=True)
+    ext().refine_crown(H._net(gpu), gpu.flat.data_ptr(), L_.contiguous().data_ptr(), H_.contiguous().data_ptr(), 0,
+                       L_.shape[0], one.out_lb.data_ptr(), one.out_ub.data_ptr(), one.Lc.data_ptr(), one.L0.data_ptr(),
+                       one.Le.data_ptr(), one.Uc.data_ptr(), one.U0.data_ptr(), one.Ue.data_ptr(),
+                       one.lay_lb_full.data_ptr(), one.lay_ub_full.data_ptr(), H._stream(cuda))
+    torch.cuda.synchronize()
+    scale = float((two.out_ub - two.out_lb).abs().max().cpu() + two.out_ub.abs().max().cpu() + 1e-3)
+    assert torch.allclose(one.out_lb, two.out_lb, rtol=1e-4, atol=1e-4 * scale)
+    assert torch.allclose(one.out_ub, two.out_ub, rtol=1e-4, atol=1e-4 * scale)
