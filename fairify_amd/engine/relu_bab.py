@@ -61,9 +61,21 @@ class ReluConfig:
 
 
 def supported(q: ResolvedQuery) -> bool:
-    """Relaxed queries (|x_r - x'_r| <= tau, x' unclipped) need a second input box per node; the
-    ReLU-phase stage covers the PA-only queries."""
-    return not q.relaxed
+    """PA-only and relaxed queries (|x_r - x'_r| <= tau on the RA dims, x' unclipped: the nodes then
+    carry a second box for the x' RA coordinates, and the second orientation runs on the negated
+    network; see :meth:`ReluBaBSolver.solve`)."""
+    return True
+
+
+def negated(mlp: MLP) -> MLP:
+    """The network with its logit negated (last layer's weights and bias): N_A > 0 > N_B on ``mlp``
+    is N_A < 0 < N_B on the result -- the second orientation of a relaxed query, where x' may leave
+    the box so swapping the pair does not cover it."""
+    ws = [w.copy() for w in mlp.weights]
+    bs = [b.copy() for b in mlp.biases]
+    ws[-1] = -ws[-1]
+    bs[-1] = -bs[-1]
+    return MLP(ws, bs, name=mlp.name + "-neg")
 
 
 def certify_pair(LA_c, LA_0, MA, UB_c, UB_0, MB, lo, hi, free, unit):
@@ -96,6 +108,40 @@ def certify_pair(LA_c, LA_0, MA, UB_c, UB_0, MB, lo, hi, free, unit):
     return gmin, tstar, xstar
 
 
+def certify_pair_relaxed(LA_c, LA_0, MA, UB_c, UB_0, MB, lo, hi, plo, phi, shared, ra, unit):
+    """:func:`certify_pair` for relaxed queries: copy A reads x, copy B reads x with the RA dims
+    replaced by x' (their own box [plo, phi]).  Shared dims (``shared``: non-PA, non-RA) couple the
+    copies as before; on an RA dim the two maxima are taken separately (x_r in [lo, hi], x'_r in
+    [plo, phi]) -- the tie |x_r - x'_r| <= tau is dropped, which only loosens the bound.  Returns
+    (g*, t*, x*, x'* on the RA dims)."""
+    N, n0 = lo.shape
+    dt = lo.dtype
+    A = -LA_c
+    B = UB_c
+    As, Bs = A * shared, B * shared
+    den = As - Bs
+    tb = torch.where(den.abs() > 0, -Bs / torch.where(den.abs() > 0, den, torch.ones_like(den)),
+                     torch.full_like(den, -1.0)).clamp(-1.0, 2.0)
+    ts = torch.cat([torch.zeros(N, 1, dtype=dt, device=lo.device), torch.ones(N, 1, dtype=dt, device=lo.device),
+                    tb], dim=1).clamp(0.0, 1.0)                                   # [N, T]
+    t = ts[:, :, None]
+    cs = t * As[:, None, :] + (1 - t) * Bs[:, None, :]
+    val = torch.maximum(cs * lo[:, None, :], cs * hi[:, None, :]).sum(-1)
+    ar = A[:, ra][:, None, :] * t                                                 # [N, T, nra]
+    br = B[:, ra][:, None, :] * (1 - t)
+    val = val + torch.maximum(ar * lo[:, None, ra], ar * hi[:, None, ra]).sum(-1) \
+        + torch.maximum(br * plo[:, None, :], br * phi[:, None, :]).sum(-1)
+    g = val + ts * LA_0[:, None].neg() + (1 - ts) * UB_0[:, None]
+    g = g + ref.gamma(2 * n0 + 4, unit) * (ts * MA[:, None] + (1 - ts) * MB[:, None]) + 8 * unit * (MA + MB)[:, None]
+    gmin, targ = g.min(dim=1)
+    tstar = ts.gather(1, targ[:, None])[:, 0]
+    c = tstar[:, None] * A + (1 - tstar[:, None]) * B
+    xstar = torch.where(c > 0, hi, lo)
+    xstar[:, ra] = torch.where(A[:, ra] > 0, hi[:, ra], lo[:, ra])
+    xpstar = torch.where(B[:, ra] > 0, phi, plo)
+    return gmin, tstar, xstar, xpstar
+
+
 def _pick_form(res_c, res_0, res_e, fw_low, cr):
     """Per row, the tighter of the forward form (res_c, res_0, res_e; its bound fw_low) and the
     backward input form ``cr`` = (coef, const, err, low)."""
@@ -115,12 +161,39 @@ class ReluBaBSolver:
 
     def solve(self, lo_np: np.ndarray, hi_np: np.ndarray, mlp_exact: MLP,
               init_status: Optional[np.ndarray] = None) -> BaBResult:
+        """Relaxed queries: orientation N(x, v) < 0 < N(x', v') on this backend's network, then, on the
+        partitions it closed, N(x, v) > 0 > N(x', v') as the first orientation of the NEGATED network
+        (:func:`negated`); a partition is UNSAT when both close, SAT when either finds a pair (always
+        confirmed exactly on ``mlp_exact``, whose violation test is orientation-free)."""
         t0 = time.time()
         P, n = lo_np.shape
         status = np.full(P, RUNNING, dtype=np.int8) if init_status is None else init_status.astype(np.int8).copy()
         if not supported(self.q):
             status[status == RUNNING] = UNKNOWN
             return BaBResult(status, np.zeros((P, n), np.int64), np.zeros((P, n), np.int64), np.zeros(P, np.int64))
+        if self.q.relaxed and not getattr(self, "_second", False):
+            r1 = self._solve_groups_all(lo_np, hi_np, mlp_exact, status, t0)
+            closed = (r1.status == UNSAT) & (status == RUNNING)
+            if not closed.any():
+                return r1
+            neg = ReluBaBSolver(Backend(negated(self.be.mlp), device=self.dev), self.q,
+                                ReluConfig(node_budget=self.cfg.node_budget, batch_nodes=self.cfg.batch_nodes,
+                                           time_budget=max(0.0, self.cfg.time_budget - (time.time() - t0)),
+                                           max_pool=self.cfg.max_pool), timer=self.tm)
+            neg._second = True
+            st2 = np.where(closed, RUNNING, UNKNOWN).astype(np.int8)
+            r2 = neg.solve(lo_np, hi_np, mlp_exact, init_status=st2)
+            out = r1.status.copy()
+            out[closed] = r2.status[closed]                 # UNSAT only if the second closed too
+            cx, cxp = r1.cex_x.copy(), r1.cex_xp.copy()
+            s2 = closed & (r2.status == SAT)
+            cx[s2], cxp[s2] = r2.cex_x[s2], r2.cex_xp[s2]
+            return BaBResult(out, cx, cxp, r1.nodes + r2.nodes, 0, time.time() - t0)
+        return self._solve_groups_all(lo_np, hi_np, mlp_exact, status, t0)
+
+    def _solve_groups_all(self, lo_np, hi_np, mlp_exact, status, t0) -> BaBResult:
+        P, n = lo_np.shape
+        status = status.copy()
         groups = pa_groups(self.q, lo_np, hi_np)
         cex_x = np.zeros((P, n), dtype=np.int64)
         cex_xp = np.zeros((P, n), dtype=np.int64)
@@ -134,7 +207,9 @@ class ReluBaBSolver:
     # ------------------------------------------------------------------------------------------
     def _solve_group(self, lo_np, hi_np, mlp_exact, status, time_budget):
         values_np, pairs_np = _pa_table(self.q, lo_np, hi_np)
-        if self.be.hip and os.environ.get("FAIRIFY_TORCH_BAB") != "1":
+        # relaxed queries: the torch path (with the HIP bound kernels on the GPU); the native level
+        # kernels carry one box per node
+        if self.be.hip and not self.q.relaxed and os.environ.get("FAIRIFY_TORCH_BAB") != "1":
             return self._solve_native(lo_np, hi_np, mlp_exact, status, values_np, pairs_np, time_budget)
         return self._solve_torch(lo_np, hi_np, mlp_exact, status, values_np, pairs_np, time_budget)
 
@@ -158,11 +233,19 @@ class ReluBaBSolver:
         pairs = torch.from_numpy(pairs_np).to(dev)
         free = torch.ones(n0, dtype=dt, device=dev)
         free[pa] = 0
+        relaxed = q.relaxed
+        ra = list(q.ra_idx) if relaxed else []
+        tau = float(q.tau)
+        shared = free.clone()
+        shared[ra] = 0
         # one root per (partition, ordered pair)
         part = torch.from_numpy(np.repeat(run, Pp)).to(dev)
         pair = torch.arange(Pp, device=dev).repeat(len(run))
         lo = torch.from_numpy(lo_np).to(dev, dt)[part]
         hi = torch.from_numpy(hi_np).to(dev, dt)[part]
+        # relaxed: the x' coordinates of the RA dims, unclipped, [lo - tau, hi + tau]
+        plo = (lo[:, ra] - tau) if relaxed else torch.zeros(len(part), 0, dtype=dt, device=dev)
+        phi = (hi[:, ra] + tau) if relaxed else torch.zeros(len(part), 0, dtype=dt, device=dev)
         phase = torch.zeros(len(part), 2, Nh, dtype=torch.int8, device=dev)
         levels = 0
         timed_out = False
@@ -173,8 +256,11 @@ class ReluBaBSolver:
             levels += 1
             N = part.numel()
             alive = torch.from_numpy(status == RUNNING).to(dev)[part]
+            if relaxed:      # x_r and x'_r boxes more than tau apart: no admissible pair, node closed
+                alive &= ~((plo > hi[:, ra] + tau) | (phi < lo[:, ra] - tau)).any(dim=1)
             if not bool(alive.all()):
                 part, pair, lo, hi, phase = part[alive], pair[alive], lo[alive], hi[alive], phase[alive]
+                plo, phi = plo[alive], phi[alive]
                 N = part.numel()
                 if N == 0:
                     break
@@ -185,6 +271,9 @@ class ReluBaBSolver:
             rv = torch.stack([vA, vB], dim=1).reshape(-1)
             rlo[:, pa] = values[rv]
             rhi[:, pa] = values[rv]
+            if relaxed:          # copy B reads x' on the RA dims
+                rlo[1::2, ra] = plo
+                rhi[1::2, ra] = phi
             rph = phase.reshape(2 * N, Nh)
             with self.tm("relu.bounds"):
                 res = be.bounds(rlo, rhi, mode="symbolic", keep_layers=True, phase=rph)
@@ -214,11 +303,21 @@ class ReluBaBSolver:
             fa_A = (LAc[:, pa] * values[vA]).sum(1)
             fa_B = (UBc[:, pa] * values[vB]).sum(1)
             mxb = torch.maximum(lo.abs(), hi.abs())
+            mxb_b = mxb.clone()
+            if relaxed:
+                mxb_b[:, ra] = torch.maximum(plo.abs(), phi.abs())
             # rounding margin over the folded PA products' magnitudes (with several PA dims their
             # sum can cancel below the products' errors)
             MA = (LAc.abs() * mxb * free).sum(1) + (LA0 - LAe).abs() + (LAc[:, pa] * values[vA]).abs().sum(1)
-            MB = (UBc.abs() * mxb * free).sum(1) + (UB0 + UBe).abs() + (UBc[:, pa] * values[vB]).abs().sum(1)
-            g, tstar, xstar = certify_pair(LAc, LA0 - LAe + fa_A, MA, UBc, UB0 + UBe + fa_B, MB, lo, hi, free, be.unit)
+            MB = (UBc.abs() * mxb_b * free).sum(1) + (UB0 + UBe).abs() + (UBc[:, pa] * values[vB]).abs().sum(1)
+            xpstar = None
+            if relaxed:
+                LAcf, UBcf = LAc * free, UBc * free
+                g, tstar, xstar, xpstar = certify_pair_relaxed(LAcf, LA0 - LAe + fa_A, MA, UBcf, UB0 + UBe + fa_B, MB,
+                                                               lo, hi, plo, phi, shared, ra, be.unit)
+            else:
+                g, tstar, xstar = certify_pair(LAc, LA0 - LAe + fa_A, MA, UBc, UB0 + UBe + fa_B, MB, lo, hi, free,
+                                               be.unit)
             open_ = ~closed & (g > 0)
             # ---- candidate vertex pairs of open nodes: rigorous point bounds, then the exact check
             oi = torch.nonzero(open_).flatten()
@@ -227,6 +326,8 @@ class ReluBaBSolver:
                 xb = xstar[oi].clone()
                 xa[:, pa] = values[vA[oi]]
                 xb[:, pa] = values[vB[oi]]
+                if relaxed:      # x'_r: its vertex, pulled into [x_r - tau, x_r + tau]
+                    xb[:, ra] = torch.minimum(torch.maximum(xpstar[oi], xa[:, ra] - tau), xa[:, ra] + tau)
                 with self.tm("relu.cand"):
                     alb, _ = be.point_bounds(xa)
                     _, bub = be.point_bounds(xb)
@@ -234,8 +335,11 @@ class ReluBaBSolver:
                 ci = oi[poss]
                 if ci.numel():
                     self._confirm(ci, xa[poss], xb[poss], part, status, cex_x, cex_xp, mlp_exact, lo_np, hi_np)
-            # ---- leaves: the non-PA box is a single lattice point -> decided exactly above
+            # ---- leaves: the non-PA box (and the x' RA box) is a single lattice point -> decided
+            # exactly above
             width = ((hi - lo) * free).amax(dim=1)
+            if relaxed:
+                width = torch.maximum(width, (phi - plo).amax(dim=1))
             leaf = open_ & (width == 0)
             run_t = torch.from_numpy(status == RUNNING).to(dev)[part]
             grow = open_ & ~leaf & run_t
@@ -265,26 +369,44 @@ class ReluBaBSolver:
             cp[torch.arange(2 * k, device=dev), r2, n2] = torch.cat([torch.full((k,), -1, dtype=torch.int8, device=dev),
                                                                      torch.ones(k, dtype=torch.int8, device=dev)])
             # input split along the dim of largest |coefficient| x width of the certificate at t*
+            # (relaxed: the x' RA dims compete as extra columns, scored by copy B's coefficient)
             ii = gi[~relu]
             c_t = tstar[ii, None] * (-LAc[ii]) + (1 - tstar[ii, None]) * UBc[ii]
+            if relaxed:
+                c_t[:, ra] = tstar[ii, None] * LAc[ii][:, ra]
             w = (hi[ii] - lo[ii]) * free
             sc = torch.where(w > 0, c_t.abs() * w + 1e-9 * w, torch.full_like(w, -1.0))
+            if relaxed:
+                wp = phi[ii] - plo[ii]
+                cp_ = (1 - tstar[ii, None]) * UBc[ii][:, ra]
+                sc = torch.cat([sc, torch.where(wp > 0, cp_.abs() * wp + 1e-9 * wp, torch.full_like(wp, -1.0))], dim=1)
             d = sc.argmax(dim=1)
-            mid = torch.floor((lo[ii, d] + hi[ii, d]) / 2)
-            lo1, hi1, lo2, hi2 = lo[ii].clone(), hi[ii].clone(), lo[ii].clone(), hi[ii].clone()
             ar = torch.arange(ii.numel(), device=dev)
-            hi1[ar, d] = mid
-            lo2[ar, d] = mid + 1
+            lo1, hi1, lo2, hi2 = lo[ii].clone(), hi[ii].clone(), lo[ii].clone(), hi[ii].clone()
+            plo1, phi1, plo2, phi2 = plo[ii].clone(), phi[ii].clone(), plo[ii].clone(), phi[ii].clone()
+            onx = d < n0
+            if bool(onx.any()):
+                a_, d_ = ar[onx], d[onx]
+                mid = torch.floor((lo[ii][a_, d_] + hi[ii][a_, d_]) / 2)
+                hi1[a_, d_] = mid
+                lo2[a_, d_] = mid + 1
+            if relaxed and bool((~onx).any()):
+                a_, d_ = ar[~onx], d[~onx] - n0
+                mid = torch.floor((plo[ii][a_, d_] + phi[ii][a_, d_]) / 2)
+                phi1[a_, d_] = mid
+                plo2[a_, d_] = mid + 1
             part = torch.cat([part[ri], part[ri], part[ii], part[ii]])
             pair = torch.cat([pair[ri], pair[ri], pair[ii], pair[ii]])
             lo_n = torch.cat([lo[ri], lo[ri], lo1, lo2])
             hi_n = torch.cat([hi[ri], hi[ri], hi1, hi2])
+            plo = torch.cat([plo[ri], plo[ri], plo1, plo2])
+            phi = torch.cat([phi[ri], phi[ri], phi1, phi2])
             phase = torch.cat([cp, phase[ii], phase[ii]])
             lo, hi = lo_n, hi_n
             if part.numel() > cfg.max_pool:
                 lost = torch.unique(part[cfg.max_pool:]).cpu().numpy()
                 status[lost[status[lost] == RUNNING]] = UNKNOWN
-                part, pair, lo, hi, phase = (t[:cfg.max_pool] for t in (part, pair, lo, hi, phase))
+                part, pair, lo, hi, phase, plo, phi = (t[:cfg.max_pool] for t in (part, pair, lo, hi, phase, plo, phi))
         left = set(part.cpu().numpy().tolist()) if (timed_out and part.numel()) else set()
         for p in np.nonzero(status == RUNNING)[0]:
             status[p] = UNKNOWN if p in left else UNSAT
