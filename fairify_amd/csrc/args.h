@@ -192,6 +192,17 @@ struct CertArgs {
   int skip_closed;
   const int8_t* status;
   const int* part;
+  // input-split scores from the first layer ("smear", non-relaxed queries): dim i scores
+  // width_i * sum over the node's rows of sum_{j unstable in layer 0} |W0[i, j]| instead of the
+  // certificate's |coefficient| x width -- a first-layer-dominated net (AC-4 / AC-5 / AC-7: 64-100
+  // wide) closes its residue in 30-50 % fewer nodes (tools/diag_open_nodes.py --split smear); the
+  // narrow deep nets keep the certificate scores (smear costs them nodes)
+  int smear;
+  const float* lay_lb;                            // [Nn*V, lay_N] row bounds (layer 0 first)
+  const float* lay_ub;
+  int lay_N;
+  const float* W0;                                // [n0, n1] first layer (Keras layout)
+  int n1;
 };
 
 // Branch step: close / flag / split the nodes of one sub-batch into the next BFS level.

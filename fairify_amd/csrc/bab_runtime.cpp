@@ -95,7 +95,7 @@ class BabRuntime {
   BabRuntime(py::handle net, uintptr_t flat, std::vector<int> pa, std::vector<float> values_f,
              std::vector<int64_t> values_i, std::vector<int64_t> pairs, std::vector<int> ra, float tau,
              std::vector<uint8_t> shared, int capacity, int batch_nodes, int cand_cap, double unit, bool crown,
-             int split_target, int refine)
+             int split_target, int refine, bool smear)
       : net_(fa_net_desc(net)),
         flat_((const float*)flat),
         pa_(std::move(pa)),
@@ -107,6 +107,7 @@ class BabRuntime {
         unit_(unit),
         crown_(crown),
         refine_(crown ? refine : 0),
+        smear_(smear),
         split_target_(std::max(2, split_target)) {
     n0_ = net_.dims[0];
     npa_ = (int)pa_.size();
@@ -132,7 +133,7 @@ class BabRuntime {
       Uc_[s].ensure(R * n0_);
       L0_[s].ensure(R); Le_[s].ensure(R); U0_[s].ensure(R); Ue_[s].ensure(R);
       olb_[s].ensure(R); oub_[s].ensure(R);
-      if (crown_) {
+      if (crown_ || smear_) {
         lay_lb_[s].ensure(R * net_.n_neurons);
         lay_ub_[s].ensure(R * net_.n_neurons);
       }
@@ -309,6 +310,11 @@ class BabRuntime {
         c.cand_v = cv_.p; c.cand_o = co_.p;
         c.scores = scores_.p; c.leaf = leaf_.p;
         if (cert_skip_closed()) { c.skip_closed = 1; c.status = status_.p; c.part = bpart; }
+        if (smear_ && !relaxed_) {
+          c.smear = 1;
+          c.lay_lb = lay_lb_[0].p; c.lay_ub = lay_ub_[0].p; c.lay_N = net_.n_neurons;
+          c.W0 = flat_ + net_.w_off[0]; c.n1 = net_.dims[1];
+        }
         ckl(fa_certify_launch(c, st), "certify");
         // rigorous interval evaluation of the candidate pairs (rows: x then x')
         BoundArgs b{};
@@ -421,13 +427,15 @@ class BabRuntime {
     if (refine_ == 2) {
       // backward-only bounding (refine.hip mode FULL): one launch computes every hidden layer's
       // bounds and the logit's forms, no forward pass and no output pass; -1: the network does not
-      // fit, fall back to forward + refine + output pass
+      // fit, fall back to forward + refine + output pass (layer bounds written only for the smear
+      // split scores)
+      if (smear_) { b.layer_lb = lay_lb_[slot].p; b.layer_ub = lay_ub_[slot].p; }
       const int rc = fa_backward_launch(net_, b, st);
       if (rc == 0) return;
       if (rc != -1) ckl(rc, "backward");
       refine_ = 1;
     }
-    if (crown_) {
+    if (crown_ || smear_) {
       b.layer_lb = lay_lb_[slot].p;
       b.layer_ub = lay_ub_[slot].p;
     }
@@ -577,6 +585,7 @@ class BabRuntime {
   double unit_;
   bool crown_ = false;
   int refine_ = 0;          // 0 forward + output pass, 1 + refine between them, 2 backward only
+  bool smear_ = false;      // first-layer smear split scores (CertArgs.smear)
   int split_target_ = 256;
   int n0_ = 0, npa_ = 0, V_ = 0, Pp_ = 0, norient_ = 1;
   bool relaxed_ = false;
@@ -611,11 +620,11 @@ void register_bab(py::module& m) {
   py::class_<BabRuntime>(m, "BabRuntime")
       .def(py::init<py::handle, uintptr_t, std::vector<int>, std::vector<float>, std::vector<int64_t>,
                     std::vector<int64_t>, std::vector<int>, float, std::vector<uint8_t>, int, int, int, double, bool,
-                    int, int>(),
+                    int, int, bool>(),
            py::arg("net"), py::arg("flat"), py::arg("pa"), py::arg("values_f"), py::arg("values_i"),
            py::arg("pairs"), py::arg("ra"), py::arg("tau"), py::arg("shared"), py::arg("capacity"),
            py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"), py::arg("crown") = true,
-           py::arg("split_target") = 256, py::arg("refine") = 0)
+           py::arg("split_target") = 256, py::arg("refine") = 0, py::arg("smear") = false)
       .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"),
            py::arg("native_exact") = false, py::arg("budget2") = 0, py::arg("max_w") = 0,

@@ -13,6 +13,8 @@
 //                       maximises the objective (PA values set, relaxed features clipped to tau).
 #include "args.h"
 
+#define FA_SMEAR_MAXN 32   // input dims the smear scores cover (every zoo suite: <= 30)
+
 // Folded form of one row: coefficient i (0 on PA dims), constant (incl. err sign and PA terms),
 // |PA contribution| for the rounding margin.
 struct Form {
@@ -310,6 +312,34 @@ __device__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t
     }
     if (sco) sco[n0 + i] = sxp;
     if (sxp > bs) { bs = sxp; bd = n0 + i; }
+  }
+  if (a.smear && sco && a.nra == 0 && n0 <= FA_SMEAR_MAXN) {
+    // first-layer smear: sum over the node's rows of |W0[i, j]| over layer-0 neurons j that are
+    // unstable on the row's box, times the width of dim i
+    float acc[FA_SMEAR_MAXN];
+#pragma unroll
+    for (int i = 0; i < FA_SMEAR_MAXN; ++i) acc[i] = 0.f;
+    for (int v = 0; v < a.V; ++v) {
+      const float* lb = a.lay_lb + ((size_t)n * a.V + v) * a.lay_N;
+      const float* ub = a.lay_ub + ((size_t)n * a.V + v) * a.lay_N;
+      for (int j = 0; j < a.n1; ++j) {
+        if (!(lb[j] < 0.f && ub[j] > 0.f)) continue;
+#pragma unroll
+        for (int i = 0; i < FA_SMEAR_MAXN; ++i)
+          if (i < n0) acc[i] += fabsf(a.W0[(size_t)i * a.n1 + j]);
+      }
+    }
+    bs = -1.f;
+    bd = 0;
+#pragma unroll
+    for (int i = 0; i < FA_SMEAR_MAXN; ++i) {
+      if (i >= n0) break;
+      const float wx = xh[i] - xl[i];
+      float sx = acc[i] * wx + 1e-9f * wx;
+      if (fa_is_pa(a, i) || wx <= 0.f) sx = -1.f;
+      sco[i] = sx;
+      if (sx > bs) { bs = sx; bd = i; }
+    }
   }
   // candidate pair: PA values of the chosen pair, relaxed features within tau of x (and in x' box)
   const int vi = (int)a.pairs[2 * q], vj = (int)a.pairs[2 * q + 1];

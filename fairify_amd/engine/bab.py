@@ -54,6 +54,10 @@ class BaBConfig:
     # "auto" = networks with >= 3 hidden layers of which one is >= 10 wide (AC-7's residue closes
     # in ~800 nodes instead of > 32 768; on 1-2 hidden layers it equals the forward bounds), "on", "off"
     refine: str = os.environ.get("FAIRIFY_REFINE", "auto")
+    # native runtime input-split scores: "auto" = first-layer smear (CertArgs.smear) for networks
+    # whose first hidden layer is >= 32 wide (AC-2/3/4/5/7; the narrow deep nets keep the
+    # certificate scores), "on", "off"
+    smear: str = os.environ.get("FAIRIFY_SMEAR", "auto")
     # native runtime branching rule: a partition with w nodes in a BFS level splits each along
     # clamp(log2(split_target / w), 1, 6) dims (per partition: verdicts do not depend on which
     # partitions share a chunk)
@@ -95,6 +99,15 @@ def refine_level(mode: str, widths) -> int:
         return 0
     hidden = list(widths)[:-1]
     return 1 if (len(hidden) >= 3 and max(hidden) >= 10) else 0
+
+
+def smear_on(mode: str, widths) -> bool:
+    """First-layer smear split scores in the native runtime (BaBConfig.smear)."""
+    if mode == "on":
+        return True
+    if mode != "auto":
+        return False
+    return len(widths) >= 2 and int(widths[0]) >= 32
 
 
 def refine_on(mode: str, widths) -> bool:
@@ -376,8 +389,9 @@ class BaBSolver:
         from .rtpool import checkout
 
         rf = refine_level(self.cfg.refine, self.be.widths)
+        sm = smear_on(self.cfg.smear, self.be.widths)
         key = (tuple(self.q.pa_idx), tuple(self.q.ra_idx), self.q.tau, values_np.tobytes(), pairs_np.tobytes(),
-               bool(self.cfg.crown), int(self.cfg.split_target), rf)
+               bool(self.cfg.crown), int(self.cfg.split_target), rf, sm)
         shared = np.ones(self.q.n, dtype=np.uint8)
         shared[list(self.q.ra_idx)] = 0
 
@@ -388,7 +402,7 @@ class BaBSolver:
                                     pairs_np.astype(np.int64).reshape(-1).tolist(),
                                     list(self.q.ra_idx) if self.relaxed else [], float(self.q.tau),
                                     shared.tolist(), int(cap), int(self.cfg.batch_nodes), int(self.cfg.cand_cap),
-                                    float(self.be.unit), bool(self.cfg.crown), int(self.cfg.split_target), rf)
+                                    float(self.be.unit), bool(self.cfg.crown), int(self.cfg.split_target), rf, sm)
 
         return checkout(self.be, "_bab_rt", key, max(self.cfg.max_pool, n_run), make)
 
