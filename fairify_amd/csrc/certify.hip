@@ -32,10 +32,14 @@ __device__ __forceinline__ bool fa_is_pa(const CertArgs& a, int d) {
 __device__ __forceinline__ Form fa_fold(const CertArgs& a, const float* C, float c0, int v) {
   Form f;
   f.c = C;
-  float contrib = 0.f;
-  for (int k = 0; k < a.npa; ++k) contrib += C[a.pa_idx[k]] * (float)a.values[v * a.npa + k];
+  float contrib = 0.f, cmag = 0.f;
+  for (int k = 0; k < a.npa; ++k) {
+    const float t = C[a.pa_idx[k]] * (float)a.values[v * a.npa + k];
+    contrib += t;
+    cmag += fabsf(t);          // the products' magnitudes: with several PA dims the sum can cancel
+  }
   f.c0 = c0 + contrib;
-  f.fmag = fabsf(contrib);
+  f.fmag = cmag;
   return f;
 }
 

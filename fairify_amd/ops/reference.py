@@ -747,9 +747,11 @@ def pair_certify(res_x: BoundResult, res_xp: BoundResult, xlo: torch.Tensor, xhi
     def fold(C, c0):
         # PA coordinates are fixed per row: move their terms into the constant
         C = C.view(Nn, V, n0).clone()
-        contrib = (C[:, :, pa] * vals[None]).sum(-1)
+        terms = C[:, :, pa] * vals[None]
+        contrib = terms.sum(-1)
         C[:, :, pa] = 0
-        return C, c0.view(Nn, V) + contrib, contrib.abs()
+        # rounding margin over the products' magnitudes (several PA dims can cancel in the sum)
+        return C, c0.view(Nn, V) + contrib, terms.abs().sum(-1)
 
     Lc, L0, fL = fold(res_x.Lc, res_x.L0 - res_x.Le)      # lower form minus its error
     Uc, U0, fU = fold(res_x.Uc, res_x.U0 + res_x.Ue)
