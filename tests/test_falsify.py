@@ -177,11 +177,11 @@ def test_fused_falsifier_relaxed_is_sound_and_matches_torch(cuda, monkeypatch, p
     assert fused.how is not None, "fused kernel did not run"
     f = fused.found.cpu().numpy()
     idx = np.nonzero(f)[0]
-    assert idx.size > 0
     X = fused.wit_x.cpu().numpy()[idx].round().astype(np.int64)
     XP = fused.wit_xp.cpu().numpy()[idx].round().astype(np.int64)
     assert exact.check_pair_constraints(X, XP, lo_np[idx], hi_np[idx], q.pa_idx, q.ra_idx, q.tau).all()
     assert exact.is_violation(m, X, XP).all()
     monkeypatch.setenv("FAIRIFY_FUSED_FALSIFY", "0")
     legacy = F.residual_falsify(be, q, lo, hi, pids, values, pairs, 0, n_samples=1024, k_starts=16, iters=12)
-    assert f.sum() >= 0.95 * legacy.found.cpu().numpy().sum()
+    n_leg = int(legacy.found.cpu().numpy().sum())
+    assert f.sum() >= 0.95 * n_leg and (n_leg == 0 or idx.size > 0), (int(f.sum()), n_leg)
