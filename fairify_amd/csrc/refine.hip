@@ -21,7 +21,10 @@
 // concretises its form at its row's box and tightens the slab (max of lower, min of upper bounds:
 // both are rigorous); a workgroup barrier separates the layers; the slab goes back to global memory
 // at the end.  Columns of one tile may belong to different rows (narrow layers pack several rows
-// per tile).
+// per tile).  Only UNSTABLE neurons get columns (compacted per layer with an LDS counter): a stable
+// neuron's relaxation is exact, so its interval only enters rounding terms.  Each neuron's
+// relaxation (slopes, offset, rounding magnitude) is computed once per row when its layer is final
+// (fa_refine_records), not per column and layer; the rows' boxes are staged in LDS.
 #include <hip/hip_runtime.h>
 
 #include <stdlib.h>
@@ -40,6 +43,11 @@ struct RefineCfg {
   int w_lds[FA_MAX_LAYERS];   // LDS float offset of layer l's W in backward operand order
   int b_lds[FA_MAX_LAYERS];
   int slab;                   // LDS float offset of the row slabs: G x [lb (N) | ub (N)]
+  int rec;                    // G x n_hidden float4 relaxation records (fa_refine_records)
+  int hm;                     // G x n_hidden: max(ub, 0) of live neurons (the GEMM rounding terms)
+  int box;                    // G x [xl (n0) | xh (n0)], protected attributes fixed
+  int list;                   // G x max width ints: the current layer's columns
+  int rrun;                   // G running-row flags + the column counter
   int G;                      // box-rows per workgroup
   int floats;
   int full;                   // 1: mode FULL
@@ -50,6 +58,48 @@ struct RefineCfg {
 __device__ __forceinline__ float fa_rgam(int k, float u) {
   const float ku = (float)(k + 2) * u;
   return ku / (1.f - ku) * (1.f + 4.f * u);
+}
+
+__device__ __forceinline__ const uint8_t* fa_refine_dmask(const NetDesc& net, const BoundArgs& a, int r) {
+  if (a.dead_in) return a.dead_in + (size_t)r * net.n_hidden;
+  if (a.dead_part) {
+    const int node = a.V > 0 ? r / a.V : r;
+    return a.dead_part + (size_t)a.node_part[a.part_mod ? node % a.part_mod : node] * net.n_hidden;
+  }
+  return nullptr;
+}
+
+// the +-1 multiplier of a hidden neuron's relaxation, per (row, neuron) once its bounds are final:
+// x = slope for a multiplier >= 0, y = slope for one < 0, z = lb (unstable only: the upper
+// relaxation's offset), w = max(|lb|, |ub|) (unstable only: the offset's rounding term).  Stable
+// neurons get slopes 1/1 or 0/0 and z = w = 0, so the column loop needs no branches and no
+// division (ops/reference.py:_backsub, same values).
+__device__ __forceinline__ void fa_refine_records(const NetDesc& net, const BoundArgs& a, const RefineCfg& cfg,
+                                                  int l, int rb, float* smem) {
+  const int N = net.n_neurons, NH = net.n_hidden;
+  const int n = net.dims[l + 1], off = net.neuron_off[l];
+  const float u = net.unit;
+  const float* slab = smem + cfg.slab;
+  float4* rec = reinterpret_cast<float4*>(smem + cfg.rec);
+  float* hmx = smem + cfg.hm;
+  for (int e = threadIdx.x; e < cfg.G * n; e += blockDim.x) {
+    const int g = e / n, jj = e - g * n, h = off + jj;
+    const float lb = slab[g * 2 * N + h], ub = slab[g * 2 * N + N + h];
+    bool dd = ub <= 0.f;
+    const uint8_t* dm = fa_refine_dmask(net, a, min(rb + g, a.R - 1));
+    if (dm && dm[h]) dd = true;
+    const bool act = !dd && lb >= 0.f;
+    const bool unst = !dd && !act;
+    const float alpha = ub > -lb ? 1.f : 0.f;
+    const float sl = unst ? (ub / (ub - lb)) * (1.f + 4.f * u) : 0.f;
+    float4 q;
+    q.x = act ? 1.f : (dd ? 0.f : alpha);
+    q.y = act ? 1.f : (dd ? 0.f : sl);
+    q.z = unst ? lb : 0.f;
+    q.w = unst ? fmaxf(fabsf(lb), fabsf(ub)) : 0.f;
+    rec[g * NH + h] = q;
+    hmx[g * NH + h] = dd ? 0.f : fmaxf(ub, 0.f);
+  }
 }
 
 template <int TM>
@@ -76,10 +126,15 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
   const int lane = tid & 63, col = lane & 15, grp = lane >> 4;
   const int wave = tid >> 6;
   const int n0 = net.dims[0];
-  const int N = net.n_neurons;
+  const int N = net.n_neurons, NH = net.n_hidden;
   const float u = net.unit;
   const int G = cfg.G;
   float* slab = smem + cfg.slab;
+  const float4* rec = reinterpret_cast<const float4*>(smem + cfg.rec);
+  const float* hmx = smem + cfg.hm;
+  float* box = smem + cfg.box;
+  int* list = reinterpret_cast<int*>(smem + cfg.list);
+  int* rrun = reinterpret_cast<int*>(smem + cfg.rrun);   // G running flags, then the column counter
   int K = 4 * L + 4;
   for (int l = 0; l < L; ++l) K += 2 * net.dims[l + 1];
   const float gK = fa_rgam(K, u);
@@ -87,62 +142,95 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
   const float g1 = fa_rgam(1, u);
   for (int rb = blockIdx.x * G; rb < a.R; rb += gridDim.x * G) {
     __syncthreads();   // previous block's slab fully written back
-    // ---- block-uniform skip: every row of the block invalid or of a decided partition
-    bool any = false;
-    for (int g = 0; g < G && !any; ++g) {
-      const int r = rb + g;
-      if (r >= a.R) break;
-      if (!a.skip_status) { any = true; break; }
-      const int node = a.V > 0 ? r / a.V : r;
-      const int8_t st = a.skip_status[a.skip_part[node]];
-      any = (st == 3 || st == 4);
+    // ---- rows of running partitions (the others get no columns); skip the block if none
+    if (tid < G) {
+      const int r = rb + tid;
+      int run = r < a.R;
+      if (run && a.skip_status) {
+        const int node = a.V > 0 ? r / a.V : r;
+        const int8_t st = a.skip_status[a.skip_part[node]];
+        run = (st == 3 || st == 4);
+      }
+      rrun[tid] = run;
     }
-    if (!any) continue;   // uniform across the workgroup (same loads everywhere)
-    // ---- load the rows' forward bounds (FULL: no forward pass, start from the whole line)
+    __syncthreads();
+    bool any = false;
+    for (int g = 0; g < G; ++g) any |= rrun[g] != 0;
+    if (!any) continue;   // uniform across the workgroup (same LDS values everywhere)
+    // ---- the rows' forward bounds (FULL: no forward pass, start from the whole line) and boxes
+    // (protected attributes fixed to the row's values)
     for (int e = tid; e < G * N; e += 256) {
       const int g = e / N, k = e - g * N;
       const int r = min(rb + g, a.R - 1);
       slab[g * 2 * N + k] = cfg.full ? -INFINITY : a.layer_lb[(size_t)r * N + k];
       slab[g * 2 * N + N + k] = cfg.full ? INFINITY : a.layer_ub[(size_t)r * N + k];
     }
+    for (int e = tid; e < G * n0; e += 256) {
+      const int g = e / n0, d = e - g * n0;
+      const int r = min(rb + g, a.R - 1);
+      const int node = a.V > 0 ? r / a.V : r;
+      const int v = a.V > 0 ? r - node * a.V : 0;
+      float xl = a.lo[(size_t)node * n0 + d], xh = a.hi[(size_t)node * n0 + d];
+      if (a.V > 0)
+        for (int q = 0; q < a.npa; ++q)
+          if (a.pa_idx[q] == d) xl = xh = a.values[v * a.npa + q];
+      box[g * 2 * n0 + d] = xl;
+      box[g * 2 * n0 + n0 + d] = xh;
+    }
     __syncthreads();
+    if (!cfg.full && L > 1) fa_refine_records(net, a, cfg, 0, rb, smem);   // layer 0 is final
     const int k0 = cfg.full ? 0 : 1, k1 = (cfg.full || cfg.logit) ? L : L - 1;
     for (int k = k0; k < k1; ++k) {
       const bool logit = k == L - 1;               // the output forms (FULL, or REFINE + logit)
       const int nk = net.dims[k + 1];
       const int ktop = net.dims[k];                  // width of h_{k-1}
       const int offk = net.neuron_off[k];
-      const int nv = G * 2 * nk;
+      const int tk = (nk + 15) >> 4;                 // output tiles of W_k (staged layout)
+      const float* wk = smem + cfg.w_lds[k];
+      // ---- the columns of this layer: both bounds of every UNSTABLE neuron of a running row (a
+      // stable neuron's relaxation is exact whatever its interval, so tightening it buys nothing);
+      // the logit: every running row
+      if (tid == 0) rrun[G] = 0;
+      __syncthreads();
+      for (int e = tid; e < G * nk; e += 256) {
+        const int g = e / nk, j = e - g * nk;
+        bool take = rrun[g] != 0;
+        if (take && !logit) {
+          const float lb = slab[g * 2 * N + offk + j], ub = slab[g * 2 * N + N + offk + j];
+          const uint8_t* dm = fa_refine_dmask(net, a, rb + g);
+          take = lb < 0.f && ub > 0.f && !(dm && dm[offk + j]);
+        }
+        if (take) list[atomicAdd(&rrun[G], 1)] = e;
+      }
+      __syncthreads();
+      const int nv = 2 * rrun[G];
       const int ntile = (nv + 15) >> 4;
-      const float* Wk = a.flat + net.w_off[k];
       for (int tile = wave; tile < ntile; tile += 4) {
         const int idx0 = tile * 16 + col;
         const bool vvalid = idx0 < nv;
         const int idx = vvalid ? idx0 : nv - 1;
-        const int g = idx / (2 * nk);
-        const int rem = idx - g * 2 * nk;
-        const int s = rem / nk;
-        const int j = rem - s * nk;
-        const int r0 = rb + g;
-        const bool rvalid = vvalid && r0 < a.R;
-        const int r = min(r0, a.R - 1);
+        const int e = list[idx >> 1];
+        const int s = idx & 1;
+        const int g = e / nk;
+        const int j = e - g * nk;
+        const int r = rb + g;
         const int node = a.V > 0 ? r / a.V : r;
-        const int v = a.V > 0 ? r - node * a.V : 0;
-        const uint8_t* dmask = nullptr;
-        if (a.dead_in) dmask = a.dead_in + (size_t)r * net.n_hidden;
-        else if (a.dead_part)
-          dmask = a.dead_part + (size_t)a.node_part[a.part_mod ? node % a.part_mod : node] * net.n_hidden;
-        const float* lbr = slab + g * 2 * N;
-        const float* ubr = lbr + N;
+        const float4* recg = rec + g * NH;
+        const float* hmg = hmx + g * NH;
+        const float* bl = box + g * 2 * n0;
         const float sgn = s ? -1.f : 1.f;
+        // lam = +-W_k[:, j] from the staged copy: element (in, j) of layer k's operand order
         float lam[TM][4];
+        {
+          const int jb = ((j >> 4) * 64 + 16 * ((j & 15) >> 2)) * 4 + (j & 3);
 #pragma unroll
-        for (int t = 0; t < TM; ++t)
+          for (int t = 0; t < TM; ++t)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int in = 16 * t + 4 * grp + i;
-            lam[t][i] = in < ktop ? sgn * Wk[(size_t)in * nk + j] : 0.f;
-          }
+            for (int i = 0; i < 4; ++i) {
+              const int in = 16 * t + 4 * grp + i;
+              lam[t][i] = in < ktop ? sgn * wk[jb + (t * tk * 64 + 4 * grp + i) * 4] : 0.f;
+            }
+        }
         float c = sgn * smem[cfg.b_lds[k] + j];
         float err = 0.f;
         for (int l = k - 1; l >= 0; --l) {
@@ -154,29 +242,24 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
           float mu[TM][4];
           float cs = 0.f, cm = 0.f, er = 0.f;
 #pragma unroll
-          for (int t = 0; t < TM; ++t)
+          for (int t = 0; t < TM; ++t) {
+            if (t >= tout) break;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int jj = 16 * t + 4 * grp + i;
-              const bool jv = t < tout && jj < n;
-              const float lb = jv ? lbr[off + jj] : 0.f, ub = jv ? ubr[off + jj] : 0.f;
-              const bool dd = !jv || ub <= 0.f || (dmask && dmask[off + jj]);
-              const bool act = !dd && lb >= 0.f;
-              const bool unst = !dd && !act;
-              const float alpha = ub > -lb ? 1.f : 0.f;
-              const float sl = unst ? (ub / (ub - lb)) * (1.f + 4.f * u) : 0.f;
-              const float zmax = fmaxf(fabsf(lb), fabsf(ub));
+              const bool jv = jj < n;
+              const float4 q = jv ? recg[off + jj] : make_float4(0.f, 0.f, 0.f, 0.f);
               const float bj = jv ? b[jj] : 0.f;
               const float lm = lam[t][i];
-              const float slope = act ? 1.f : (dd ? 0.f : (lm >= 0.f ? alpha : sl));
-              const float m = lm * slope;
-              const bool neg = unst && lm < 0.f;
-              const float tt = neg ? -m * lb : 0.f;
+              const bool neg = lm < 0.f;
+              const float m = lm * (neg ? q.y : q.x);
+              const float tt = neg ? -m * q.z : 0.f;
               mu[t][i] = m;
               cs += m * bj + tt;
               cm += fabsf(m * bj) + fabsf(tt);
-              if (neg) er += 3.f * u * (fabsf(m) * zmax + fabsf(tt));
+              er += neg ? 3.f * u * (fabsf(m) * q.w + fabsf(tt)) : 0.f;
             }
+          }
           const float4* wb = reinterpret_cast<const float4*>(smem + cfg.w_lds[l]);
           const float gn = fa_rgam(2 * n + 1, u);
 #pragma unroll
@@ -199,17 +282,8 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
               const int in = 16 * ot + 4 * grp + i;
               float hm = 0.f;
               if (in < nin) {
-                if (l > 0) {
-                  const int po = net.neuron_off[l - 1];
-                  hm = fmaxf(ubr[po + in], 0.f);
-                  if (dmask && dmask[po + in]) hm = 0.f;
-                } else {
-                  float xl = a.lo[(size_t)node * n0 + in], xh = a.hi[(size_t)node * n0 + in];
-                  if (a.V > 0)
-                    for (int q = 0; q < a.npa; ++q)
-                      if (a.pa_idx[q] == in) xl = xh = a.values[v * a.npa + q];
-                  hm = fmaxf(fabsf(xl), fabsf(xh));
-                }
+                if (l > 0) hm = hmg[net.neuron_off[l - 1] + in];
+                else hm = fmaxf(fabsf(bl[in]), fabsf(bl[n0 + in]));
               }
               lam[ot][i] = in < nin ? Z[i] : 0.f;
               er += gn * Q[i] * hm;
@@ -237,10 +311,7 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
           for (int i = 0; i < 4; ++i) {
             const int in = 16 * t + 4 * grp + i;
             if (in >= n0) continue;
-            float xl = a.lo[(size_t)node * n0 + in], xh = a.hi[(size_t)node * n0 + in];
-            if (a.V > 0)
-              for (int q = 0; q < a.npa; ++q)
-                if (a.pa_idx[q] == in) xl = xh = a.values[v * a.npa + q];
+            const float xl = bl[in], xh = bl[n0 + in];
             const float lm = lam[t][i];
             cp += fminf(lm * xl, lm * xh);
             mp += fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
@@ -251,11 +322,7 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
         const float cmg = mp + fabsf(c);
         const float errK = err * (1.f + 2.f * gK);
         const float low = conc - errK - g0 * cmg - g1 * fabsf(conc);
-        bool wr = rvalid;
-        if (logit && wr && a.skip_status) {       // forms of decided partitions' rows: not needed
-          const int8_t st = a.skip_status[a.skip_part[node]];
-          wr = (st == 3 || st == 4);
-        }
+        bool wr = vvalid;
         if (logit && wr && !cfg.full) {
           // REFINE + logit: replace the forward forms only where the backward ones concretise
           // tighter (both are sound; crown.hip's rule)
@@ -278,12 +345,13 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
           }
         }
         // lane group 0 of each column writes (the 4 groups hold the same column value)
-        if (rvalid && grp == 0) {
+        if (vvalid && grp == 0) {
           float* dst = slab + g * 2 * N + (s ? N : 0) + offk + j;
           *dst = s ? fminf(*dst, -low) : fmaxf(*dst, low);
         }
       }
       __syncthreads();
+      if (k < L - 1) fa_refine_records(net, a, cfg, k, rb, smem);   // layer k is final now
     }
     // ---- write the refined hidden-layer bounds back (rows of running partitions only; FULL: only
     // when the caller wants them -- the BaB does not)
@@ -294,13 +362,8 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
     if (span > 0)
       for (int e = tid; e < G * span; e += 256) {
         const int g = e / span, k = lo_n + (e - (e / span) * span);
+        if (!rrun[g]) continue;
         const int r = rb + g;
-        if (r >= a.R) continue;
-        if (a.skip_status) {
-          const int node = a.V > 0 ? r / a.V : r;
-          const int8_t st = a.skip_status[a.skip_part[node]];
-          if (!(st == 3 || st == 4)) continue;
-        }
         a.layer_lb[(size_t)r * N + k] = slab[g * 2 * N + k];
         a.layer_ub[(size_t)r * N + k] = slab[g * 2 * N + N + k];
       }
@@ -351,17 +414,32 @@ int backward_launch(const NetDesc& net, const BoundArgs& a, int full, int logit,
     cfg.b_lds[l] = offs;
     offs += net.dims[l + 1];
   }
-  cfg.slab = (offs + 3) & ~3;
-  const int N = net.n_neurons;
-  // rows per workgroup: 16 when the slab fits next to the weights in 64 KB (2+ workgroups per CU),
+  const int base = (offs + 3) & ~3;
+  const int N = net.n_neurons, NH = net.n_hidden, n0 = net.dims[0];
+  int maxw = 1;
+  for (int l = 1; l <= L; ++l) maxw = std::max(maxw, net.dims[l]);
+  // per-row LDS: slab 2N, records 4 NH (16-byte aligned first), hm NH, box 2 n0, columns maxw
+  auto layout = [&](int g) {
+    cfg.rec = base;
+    cfg.slab = cfg.rec + g * 4 * NH;
+    cfg.hm = cfg.slab + g * 2 * N;
+    cfg.box = cfg.hm + g * NH;
+    cfg.list = cfg.box + g * 2 * n0;
+    cfg.rrun = cfg.list + g * maxw;
+    return (size_t)(cfg.rrun + g + 1) * sizeof(float);
+  };
+  // rows per workgroup: 16 while two workgroups fit a CU's 160 KB (the VGPR budget allows two),
   // fewer for the widest nets, at least 1 within the 160 KB LDS
+  static const size_t cap_bytes = [] {
+    const char* e = getenv("FAIRIFY_REFINE_LDS_KB");   // A/B of the rows-per-workgroup rule
+    return (size_t)(e ? atoi(e) : 80) * 1024;
+  }();
   int G = 16;
-  auto bytes_for = [&](int g) { return ((size_t)cfg.slab + (size_t)g * 2 * N) * sizeof(float); };
-  while (G > 1 && bytes_for(G) > 64 * 1024) G /= 2;
-  if (bytes_for(G) > 160 * 1024) return -1;
+  while (G > 1 && layout(G) > cap_bytes) G /= 2;
+  if (layout(G) > 160 * 1024) return -1;
   cfg.G = G;
-  cfg.floats = cfg.slab + G * 2 * N;
-  const size_t bytes = bytes_for(G);
+  const size_t bytes = layout(G);
+  cfg.floats = (int)(bytes / sizeof(float));
   if (!fa_lds_ok(bytes)) return -4;
   static std::mutex mu;
   static std::map<std::pair<const void*, size_t>, int> occ;

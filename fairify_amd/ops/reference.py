@@ -457,8 +457,14 @@ def crown_refine(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: tor
             lam = (sg * Wt)[None].expand(R, -1, -1).reshape(R * n_k, -1).clone()
             c = (sg * bs[k].to(dt))[None].expand(R, -1).reshape(-1).clone()
             low[sg] = _backsub(ws, bs, rl, rh, lb_r, ub_r, lam, c, k, d_r, unit)[3].view(R, n_k)
-        lbs[k] = torch.maximum(lbs[k], low[1.0].to(lbs[k].dtype))
-        ubs[k] = torch.minimum(ubs[k], (-low[-1.0]).to(ubs[k].dtype))
+        # only unstable neurons are refined (the kernel's column list): a stable neuron's relaxation
+        # is exact, its interval only enters rounding terms
+        unst = (lbs[k] < 0) & (ubs[k] > 0)
+        if dead is not None:
+            off = sum(int(w.shape[1]) for w in ws[:k])
+            unst = unst & ~dead[:, off:off + n_k].bool()
+        lbs[k] = torch.where(unst, torch.maximum(lbs[k], low[1.0].to(lbs[k].dtype)), lbs[k])
+        ubs[k] = torch.where(unst, torch.minimum(ubs[k], (-low[-1.0]).to(ubs[k].dtype)), ubs[k])
     r = BoundResult(out_lb=res.out_lb, out_ub=res.out_ub, Lc=res.Lc, L0=res.L0, Le=res.Le, Uc=res.Uc, U0=res.U0,
                     Ue=res.Ue, layer_lb=lbs, layer_ub=ubs)
     Nh = sum(int(w.shape[1]) for w in ws[:-1])
