@@ -201,7 +201,9 @@ struct CertArgs {
   const float* lay_lb;                            // [Nn*V, lay_N] row bounds (layer 0 first)
   const float* lay_ub;
   int lay_N;
-  const float* W0;                                // [n0, n1] first layer (Keras layout)
+  const float* W0T;                               // [n1, 16 or 32] |W0| transposed, zero padded
+                                                  // (the row stride is the kernel's NM: n0 <= 16
+                                                  // -> 16, else 32)
   int n1;
 };
 

@@ -104,7 +104,9 @@ __device__ __forceinline__ int fa_wave_incl_scan(int v, int lane) {
   return v;
 }
 
-// One wave64 per node, FA_SPLIT_NPW nodes per wave, FA_SPLIT_NB nodes per workgroup, three phases:
+// One wave64 per node, npw (1..FA_SPLIT_NPW) nodes per wave, FA_SPLIT_WAVES * npw nodes per
+// workgroup (npw shrinks for small levels: a wave walks its nodes one after another, so at a 1/8
+// shard's small levels 8 nodes per wave made the kernel 8 dependent node latencies long), three phases:
 //   A  each wave plans its nodes: split dims by wave arg-max reductions, feasible children by a
 //      ballot (lane c = child c), candidate counts by ballots over the leaf's PA pairs;
 //   B  wave 0 scans the block's child / candidate counts and reserves both ranges with ONE
@@ -119,7 +121,7 @@ __device__ __forceinline__ int fa_wave_incl_scan(int v, int lane) {
 #define FA_SPLIT_WAVES 8
 #define FA_SPLIT_NPW 8
 #define FA_SPLIT_NB (FA_SPLIT_WAVES * FA_SPLIT_NPW)
-__global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs a) {
+__global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs a, int npw) {
   __shared__ FaSplitPlan plan[FA_SPLIT_NB];
   __shared__ int child_off[FA_SPLIT_NB], cand_off[FA_SPLIT_NB];
   // per-node scalars of the block's 64 nodes, fetched once by 64 threads in parallel: each wave
@@ -133,9 +135,11 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
   const int wave = threadIdx.x >> 6;
   const int n0 = a.n0;
   const int npair = a.norient * a.Pp;
-  if (threadIdx.x < FA_SPLIT_NB) {
+  const int nb = FA_SPLIT_WAVES * npw;             // nodes of this workgroup (<= FA_SPLIT_NB)
+  if (threadIdx.x >= nb && threadIdx.x < FA_SPLIT_NB) plan[threadIdx.x] = FaSplitPlan{0ull, 0ull, 0, 0, 0, 0, -1};
+  if (threadIdx.x < nb) {
     const int t = threadIdx.x;
-    const int n = blockIdx.x * FA_SPLIT_NB + t;
+    const int n = blockIdx.x * nb + t;
     uint8_t op = 0;
     int p = 0;
     if (n < a.Nn) {
@@ -158,9 +162,9 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
   }
   __syncthreads();
   // ---------------- phase A: plan
-  for (int i = 0; i < FA_SPLIT_NPW; ++i) {
-    const int loc = wave * FA_SPLIT_NPW + i;
-    const int n = blockIdx.x * FA_SPLIT_NB + loc;
+  for (int i = 0; i < npw; ++i) {
+    const int loc = wave * npw + i;
+    const int n = blockIdx.x * nb + loc;
     FaSplitPlan pl{0ull, 0ull, 0, 0, 0, 0, -1};
     do {
       if (n >= a.Nn || !s_open[loc]) break;                // wave-uniform
@@ -269,9 +273,9 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
   }
   __syncthreads();
   // ---------------- phase C: write candidates and children
-  for (int i = 0; i < FA_SPLIT_NPW; ++i) {
-    const int loc = wave * FA_SPLIT_NPW + i;
-    const int n = blockIdx.x * FA_SPLIT_NB + loc;
+  for (int i = 0; i < npw; ++i) {
+    const int loc = wave * npw + i;
+    const int n = blockIdx.x * nb + loc;
     const FaSplitPlan pl = plan[loc];
     if (pl.ncand == 0 && pl.nchild == 0) continue;         // wave-uniform (LDS broadcast)
     const int p = s_part[loc];
@@ -463,8 +467,11 @@ __global__ void fa_set_status_kernel(const int* idx, int n, int8_t* status, int8
 extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream) {
   if (a.Nn <= 0) return 0;
   if (a.nra > FA_MAX_RA || a.npa > FA_CMAX_PA || a.n0 > 64) return -3;
-  hipLaunchKernelGGL(fa_split_kernel, dim3((a.Nn + FA_SPLIT_NB - 1) / FA_SPLIT_NB), dim3(64 * FA_SPLIT_WAVES),
-                     0, stream, a);
+  // nodes per wave: 8 while that still makes >= 1024 workgroups (4 per CU), fewer for small levels
+  int npw = FA_SPLIT_NPW;
+  while (npw > 1 && (a.Nn + FA_SPLIT_WAVES * npw - 1) / (FA_SPLIT_WAVES * npw) < 1024) npw >>= 1;
+  const int nb = FA_SPLIT_WAVES * npw;
+  hipLaunchKernelGGL(fa_split_kernel, dim3((a.Nn + nb - 1) / nb), dim3(64 * FA_SPLIT_WAVES), 0, stream, a, npw);
   return (int)hipGetLastError();
 }
 

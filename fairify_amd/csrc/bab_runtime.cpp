@@ -173,6 +173,17 @@ class BabRuntime {
     if (relaxed_)
       for (int k : ra_) exact_.is_ra[k] = 1;
     exact_.tau = tau_;
+    // |W0| transposed for the smear split scores: row j = neuron j's |W0[:, j]|, zero padded to the
+    // certify kernel's register width NM (16 or 32 input dims), so a neuron is NM/4 float4 loads
+    if (smear_ && n0_ > 32) smear_ = false;
+    if (smear_) {
+      const int nm = n0_ <= 16 ? 16 : 32, n1 = net_.dims[1];
+      std::vector<float> wt((size_t)n1 * nm, 0.f);
+      for (int j = 0; j < n1; ++j)
+        for (int i = 0; i < n0_; ++i) wt[(size_t)j * nm + i] = std::fabs(hf[(size_t)net_.w_off[0] + (size_t)i * n1 + j]);
+      w0t_.ensure(wt.size());
+      ck(hipMemcpy(w0t_.p, wt.data(), wt.size() * sizeof(float), hipMemcpyHostToDevice), "cp w0t");
+    }
   }
 
   py::tuple solve(py::array_t<float, py::array::c_style | py::array::forcecast> lo,
@@ -313,7 +324,7 @@ class BabRuntime {
         if (smear_ && !relaxed_) {
           c.smear = 1;
           c.lay_lb = lay_lb_[0].p; c.lay_ub = lay_ub_[0].p; c.lay_N = net_.n_neurons;
-          c.W0 = flat_ + net_.w_off[0]; c.n1 = net_.dims[1];
+          c.W0T = w0t_.p; c.n1 = net_.dims[1];
         }
         ckl(fa_certify_launch(c, st), "certify");
         // rigorous interval evaluation of the candidate pairs (rows: x then x')
@@ -589,7 +600,7 @@ class BabRuntime {
   int split_target_ = 256;
   int n0_ = 0, npa_ = 0, V_ = 0, Pp_ = 0, norient_ = 1;
   bool relaxed_ = false;
-  DevBuf<float> vals_f_;
+  DevBuf<float> vals_f_, w0t_;
   DevBuf<int64_t> vals_i_, pairs_;
   DevBuf<uint8_t> shared_;
   DevBuf<float> lo_[2], hi_[2], plo_[2], phi_[2];

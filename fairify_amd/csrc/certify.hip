@@ -13,8 +13,6 @@
 //                       maximises the objective (PA values set, relaxed features clipped to tau).
 #include "args.h"
 
-#define FA_SMEAR_MAXN 32   // input dims the smear scores cover (every zoo suite: <= 30)
-
 // Folded form of one row: coefficient i (0 on PA dims), constant (incl. err sign and PA terms),
 // |PA contribution| for the rounding margin.
 struct Form {
@@ -145,7 +143,7 @@ __device__ __forceinline__ void fa_pair_eval_one(const CertArgs& a, int n, int q
   }
   const float A0 = sA * A.c0, B0 = sB * B.c0;
   const float marg0 = 8.f * a.unit * (magA + magB);
-  auto g_at = [&](float t) {
+  auto g_at = [&](float t) __attribute__((always_inline)) {
     float val = 0.f;
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
@@ -211,8 +209,10 @@ __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_eval_kernel(CertArgs 
 }
 
 // most violating pair (bq, its g = bg, its t*) of node n -> open flag, split scores, candidate
-__device__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t);
+template <int NM>
+__device__ __forceinline__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t);
 
+template <int NM>
 __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_pick_kernel(CertArgs a) {
   const int n = blockIdx.x * FA_CERT_THREADS + threadIdx.x;
   if (n >= a.Nn) return;
@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(FA_CERT_THREADS) fa_pair_pick_kernel(CertArgs 
     if (g != g) g = INFINITY;     // a non-finite certificate value never closes a node
     if (g > bg) { bg = g; bq = qq; }
   }
-  fa_pick_node(a, n, bg, bq, a.tstar[(size_t)n * Q + bq]);
+  fa_pick_node<NM>(a, n, bg, bq, a.tstar[(size_t)n * Q + bq]);
 }
 
 // Eval + pick fused for nodes with at most FA_CERT_FUSE_Q (pair, orientation) entries: a group
@@ -255,10 +255,16 @@ fa_pair_fused_kernel(CertArgs a, int QG) {
     const int q2 = __shfl_xor(bq, o);
     if (g2 > g || (g2 == g && q2 < bq)) { g = g2; t = t2; bq = q2; }
   }
-  if (n < a.Nn && qq == 0) fa_pick_node(a, n, g, bq == 0x7fffffff ? 0 : bq, t);
+  if (n < a.Nn && qq == 0) fa_pick_node<NM>(a, n, g, bq == 0x7fffffff ? 0 : bq, t);
 }
 
-__device__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t) {
+// Register-resident pick (NM >= n0, compile-time): the pair's coefficients and the node's boxes
+// are loaded once with independent loads, every per-dimension loop is unrolled.  A node's pick is
+// one lane's serial work, so at a small BFS level (a 1/8 shard) its memory round trips ARE the
+// kernel's duration: the per-dimension loads of the old runtime loops and the smear's one
+// neuron-at-a-time loads cost ~100 us per launch (profiles/r4/emu/).
+template <int NM>
+__device__ __forceinline__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t) {
   if (a.skip_closed && !(bg > 0.f)) {
     a.open[n] = 0;
     a.score[n] = bg;
@@ -270,77 +276,122 @@ __device__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t
   float sA, sB;
   fa_pair_forms(a, n, q, o, A, sA, B, sB);
   const int n0 = a.n0;
-  const float* xl = a.xlo + (size_t)n * n0;
-  const float* xh = a.xhi + (size_t)n * n0;
-  const float* pl = a.xplo + (size_t)n * n0;
-  const float* ph = a.xphi + (size_t)n * n0;
+  const float* xlp = a.xlo + (size_t)n * n0;
+  const float* xhp = a.xhi + (size_t)n * n0;
+  const float* plp = a.xplo + (size_t)n * n0;
+  const float* php = a.xphi + (size_t)n * n0;
   float* cxo = a.cand_x + (size_t)n * n0;
   float* cpo = a.cand_xp + (size_t)n * n0;
   float* sco = a.scores ? a.scores + (size_t)n * 2 * n0 : nullptr;
+  float ai[NM], bi[NM], xl[NM], xh[NM], pl[NM], ph[NM];
+  unsigned pam = 0u, shm = 0u;   // protected / shared dims (bit masks: bool arrays stay in scratch)
+  for (int k = 0; k < a.npa; ++k) pam |= 1u << a.pa_idx[k];
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    const bool v = i < n0;
+    if (v && a.shared[i]) shm |= 1u << i;
+    const bool p = (pam >> i) & 1u;
+    ai[i] = (v && !p) ? sA * A.c[i] : 0.f;
+    bi[i] = (v && !p) ? sB * B.c[i] : 0.f;
+    xl[i] = v ? xlp[i] : 0.f;
+    xh[i] = v ? xhp[i] : 0.f;
+    pl[i] = v ? plp[i] : 0.f;
+    ph[i] = v ? php[i] : 0.f;
+  }
   float bs = -1.f;
   int bd = 0;
   bool leaf = true;
-  for (int i = 0; i < n0; ++i) {
-    const bool pa = fa_is_pa(a, i);
-    const float ai = pa ? 0.f : sA * A.c[i];
-    const float bi = pa ? 0.f : sB * B.c[i];
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    if (i >= n0) continue;
     const float wx = xh[i] - xl[i];
-    const float cs = t * ai + (1.f - t) * bi;
+    const float cs = t * ai[i] + (1.f - t) * bi[i];
     float sx, cx;
-    if (a.shared[i]) {
+    if (((shm >> i) & 1u)) {
       sx = fabsf(cs) * wx;
       cx = cs > 0.f ? xh[i] : xl[i];
     } else {
-      sx = fabsf(t * ai) * wx;
-      cx = (t * ai > 0.f) ? xh[i] : xl[i];
+      sx = fabsf(t * ai[i]) * wx;
+      cx = (t * ai[i] > 0.f) ? xh[i] : xl[i];
     }
     sx += 1e-9f * wx;
-    if (pa || wx <= 0.f) sx = -1.f;
-    if (!pa && wx > 0.f) leaf = false;
+    if (((pam >> i) & 1u) || wx <= 0.f) sx = -1.f;
+    if (!((pam >> i) & 1u) && wx > 0.f) leaf = false;
     if (sx > bs) { bs = sx; bd = i; }
     if (sco) sco[i] = sx;
-    float cxp = cx;
-    if (!a.shared[i]) cxp = ((1.f - t) * bi > 0.f) ? ph[i] : pl[i];
     cxo[i] = cx;
-    cpo[i] = cxp;
+    cpo[i] = ((shm >> i) & 1u) ? cx : (((1.f - t) * bi[i] > 0.f) ? ph[i] : pl[i]);
   }
-  for (int i = 0; i < n0; ++i) {
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    if (i >= n0) continue;
     float sxp = -1.f;
-    if (!a.shared[i] && !fa_is_pa(a, i)) {
-      const float bi = sB * B.c[i];
+    if (!((shm >> i) & 1u) && !((pam >> i) & 1u)) {
       const float wxp = ph[i] - pl[i];
       if (wxp > 0.f) {
-        sxp = fabsf((1.f - t) * bi) * wxp + 1e-9f * wxp;
+        sxp = fabsf((1.f - t) * bi[i]) * wxp + 1e-9f * wxp;
         leaf = false;
       }
     }
     if (sco) sco[n0 + i] = sxp;
     if (sxp > bs) { bs = sxp; bd = n0 + i; }
   }
-  if (a.smear && sco && a.nra == 0 && n0 <= FA_SMEAR_MAXN) {
+  if (a.smear && sco && a.nra == 0 && n0 <= NM) {
     // first-layer smear: sum over the node's rows of |W0[i, j]| over layer-0 neurons j that are
-    // unstable on the row's box, times the width of dim i
-    float acc[FA_SMEAR_MAXN];
+    // unstable on the row's box, times the width of dim i.  The unstable set comes 32 neurons at a
+    // time from independent loads into a bit mask; the |W0| rows (transposed, NM wide) of two
+    // unstable neurons are fetched together; accumulation in ascending j as before.
+    float acc[NM];
 #pragma unroll
-    for (int i = 0; i < FA_SMEAR_MAXN; ++i) acc[i] = 0.f;
+    for (int i = 0; i < NM; ++i) acc[i] = 0.f;
     for (int v = 0; v < a.V; ++v) {
       const float* lb = a.lay_lb + ((size_t)n * a.V + v) * a.lay_N;
       const float* ub = a.lay_ub + ((size_t)n * a.V + v) * a.lay_N;
-      for (int j = 0; j < a.n1; ++j) {
-        if (!(lb[j] < 0.f && ub[j] > 0.f)) continue;
+      for (int j0 = 0; j0 < a.n1; j0 += 32) {
+        unsigned msk = 0u;
 #pragma unroll
-        for (int i = 0; i < FA_SMEAR_MAXN; ++i)
-          if (i < n0) acc[i] += fabsf(a.W0[(size_t)i * a.n1 + j]);
+        for (int k = 0; k < 32; ++k) {
+          const int j = j0 + k;
+          const bool jv = j < a.n1;
+          const float l = jv ? lb[j] : 0.f, u = jv ? ub[j] : 0.f;
+          if (l < 0.f && u > 0.f) msk |= 1u << k;
+        }
+        while (msk) {
+          int jj[2];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            jj[k] = msk ? j0 + __builtin_ctz(msk) : -1;
+            msk &= msk - 1u;
+          }
+          float4 w[2][NM / 4];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const float4* wr = reinterpret_cast<const float4*>(a.W0T + (size_t)(jj[k] < 0 ? 0 : jj[k]) * NM);
+#pragma unroll
+            for (int i4 = 0; i4 < NM / 4; ++i4) w[k][i4] = wr[i4];
+          }
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            if (jj[k] < 0) break;
+#pragma unroll
+            for (int i4 = 0; i4 < NM / 4; ++i4) {
+              acc[4 * i4] += w[k][i4].x;
+              acc[4 * i4 + 1] += w[k][i4].y;
+              acc[4 * i4 + 2] += w[k][i4].z;
+              acc[4 * i4 + 3] += w[k][i4].w;
+            }
+          }
+        }
       }
     }
     bs = -1.f;
     bd = 0;
 #pragma unroll
-    for (int i = 0; i < FA_SMEAR_MAXN; ++i) {
-      if (i >= n0) break;
+    for (int i = 0; i < NM; ++i) {
+      if (i >= n0) continue;
       const float wx = xh[i] - xl[i];
       float sx = acc[i] * wx + 1e-9f * wx;
-      if (fa_is_pa(a, i) || wx <= 0.f) sx = -1.f;
+      if (((pam >> i) & 1u) || wx <= 0.f) sx = -1.f;
       sco[i] = sx;
       if (sx > bs) { bs = sx; bd = i; }
     }
@@ -353,8 +404,8 @@ __device__ void fa_pick_node(const CertArgs& a, int n, float bg, int bq, float t
   }
   for (int k = 0; k < a.nra; ++k) {
     const int r = a.ra_idx[k];
-    float v = fminf(fmaxf(cpo[r], cxo[r] - a.tau), cxo[r] + a.tau);
-    cpo[r] = fminf(fmaxf(v, pl[r]), ph[r]);
+    const float v = fminf(fmaxf(cpo[r], cxo[r] - a.tau), cxo[r] + a.tau);
+    cpo[r] = fminf(fmaxf(v, plp[r]), php[r]);
   }
   a.open[n] = bg > 0.f ? 1 : 0;
   a.score[n] = bg;
@@ -386,7 +437,8 @@ extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream) {
   if (a.n0 <= 16) hipLaunchKernelGGL(fa_pair_eval_kernel<16>, ge, dim3(FA_CERT_THREADS), 0, stream, a);
   else if (a.n0 <= 32) hipLaunchKernelGGL(fa_pair_eval_kernel<32>, ge, dim3(FA_CERT_THREADS), 0, stream, a);
   else return -4;
-  hipLaunchKernelGGL(fa_pair_pick_kernel, dim3((a.Nn + FA_CERT_THREADS - 1) / FA_CERT_THREADS),
-                     dim3(FA_CERT_THREADS), 0, stream, a);
+  const dim3 gp((a.Nn + FA_CERT_THREADS - 1) / FA_CERT_THREADS);
+  if (a.n0 <= 16) hipLaunchKernelGGL(fa_pair_pick_kernel<16>, gp, dim3(FA_CERT_THREADS), 0, stream, a);
+  else hipLaunchKernelGGL(fa_pair_pick_kernel<32>, gp, dim3(FA_CERT_THREADS), 0, stream, a);
   return (int)hipGetLastError();
 }

@@ -38,11 +38,16 @@ if cur_e is not None:
     busy += cur_e - cur_s
 tot = defaultdict(int)
 cnt = defaultdict(int)
+durs = defaultdict(list)
 for s, e, k in iv:
     tot[k.split("(")[0][:48]] += e - s
     cnt[k.split("(")[0][:48]] += 1
+    durs[k.split("(")[0][:48]].append(e - s)
 what = "timed window" if window else "span"
 print(f"{what} {span/1e9:.3f}s  busy(union) {busy/1e9:.3f}s  ({100*busy/max(1, span):.1f}%)  kernels {len(iv)}  "
       f"sum of kernel time {sum(tot.values())/1e9:.3f}s")
+print(f"  {'kernel':50s} {'total':>9s}  {'launches':>7s}  {'p50 us':>8s}  {'p90 us':>8s}")
 for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:14]:
-    print(f"  {k:50s} {v/1e9:8.3f}s  {cnt[k]:7d}")
+    d = sorted(durs[k])
+    p50, p90 = d[len(d) // 2] / 1e3, d[min(len(d) - 1, (9 * len(d)) // 10)] / 1e3
+    print(f"  {k:50s} {v/1e9:8.3f}s  {cnt[k]:7d}  {p50:8.1f}  {p90:8.1f}")
