@@ -207,6 +207,27 @@ struct CertArgs {
   int n1;
 };
 
+// Level end (fa_settle): per-partition state for the next level, level counters to the host.
+// Run by its own launch, or fused into the level's last split launch (P > 0 there).
+struct SettleArgs {
+  int P;                                  // partitions (0: not fused into this split launch)
+  int8_t* status;
+  int* lvl_open;
+  int* part_open;
+  const int* part_nodes;
+  int* nodes_start;
+  int* prev_start;
+  const int* counters_cur;                // this level's (children, candidates)
+  int* counters_next;                     // the next level's slot (cleared)
+  int* host_counts;                       // pinned host words
+  int* pbudget;
+  uint8_t* prob;
+  int budget2;
+  int max_open;
+  EscSteps esc;
+  int* done;                              // fused: workgroups finished (the last one settles, resets it)
+};
+
 // Branch step: close / flag / split the nodes of one sub-batch into the next BFS level.
 struct SplitArgs {
   int Nn, n0, relaxed, nra, V, Pp, norient;
@@ -250,6 +271,7 @@ struct SplitArgs {
                                           //   partition id (int bits), one D2H per level
   int* cand_count;
   int cand_cap;
+  SettleArgs settle;                      // fused level end (settle.P > 0: last sub-batch of the level)
 };
 
 // BaB solve start (fa_bab_init_kernel): staged host block -> per-partition state + root pool.

@@ -76,6 +76,42 @@ __device__ __forceinline__ void fa_wave_argmax(float& s, int& d) {
   }
 }
 
+__device__ __forceinline__ void fa_settle_counters(const SettleArgs& s) {
+  // level counters straight into pinned host memory (no blit per level), next slot cleared; the
+  // counters were accumulated by device atomics (L2): read them the same way
+  const int c0 = __hip_atomic_load(&s.counters_cur[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int c1 = __hip_atomic_load(&s.counters_cur[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&s.host_counts[0], c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&s.host_counts[1], c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  s.counters_next[0] = 0;
+  s.counters_next[1] = 0;
+}
+
+__device__ __forceinline__ void fa_settle_part(const SettleArgs& s, int p) {
+  const int8_t st = s.status[p];
+  if (st == ST_STOPPING) {
+    s.status[p] = ST_UNKNOWN;
+    if (s.part_open) s.part_open[p] = s.lvl_open[p];
+  } else if (s.prob && s.prob[p] && st == ST_RUNNING) {
+    // stepped escalation: budget -> esc.budget[0] -> ... -> budget2; at each step's probation
+    // level the frontier must be at most max_open (first step) / esc.open[k-1] (step k)
+    const int cur = s.pbudget[p];
+    int k = 0;
+    while (k < s.esc.n && s.esc.budget[k] <= cur) ++k;
+    const int thr = k == 0 ? s.max_open : s.esc.open[k - 1];
+    if (s.lvl_open[p] <= thr) {
+      s.pbudget[p] = k < s.esc.n ? s.esc.budget[k] : s.budget2;
+    } else {
+      s.status[p] = ST_UNKNOWN;
+      if (s.part_open) s.part_open[p] = s.lvl_open[p];
+    }
+  }
+  if (s.prob) s.prob[p] = 0;
+  s.lvl_open[p] = 0;
+  s.prev_start[p] = s.nodes_start[p];
+  s.nodes_start[p] = s.part_nodes[p];     // the next level's budget reference
+}
+
 // Per-node plan of the split kernel (phase A -> phase C through LDS).
 struct FaSplitPlan {
   unsigned long long fmask;   // feasible children (bit c = child c)
@@ -363,6 +399,22 @@ __global__ void __launch_bounds__(64 * FA_SPLIT_WAVES) fa_split_kernel(SplitArgs
       }
     }
   }
+  // ---------------- fused level end (the level's last sub-batch): the last workgroup to finish
+  // settles every partition -- one launch per level less.  Release this workgroup's writes, count
+  // it done; the last one acquires everything (the fence invalidates its L1) and settles.
+  if (a.settle.P > 0) {
+    __shared__ int s_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(a.settle.done, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (s_last) {
+      __threadfence();
+      if (threadIdx.x == 0) fa_settle_counters(a.settle);
+      for (int p = threadIdx.x; p < a.settle.P; p += blockDim.x) fa_settle_part(a.settle, p);
+      if (threadIdx.x == 0) *a.settle.done = 0;   // ready for the next fused launch (stream order)
+    }
+  }
 }
 
 // Solve start, one launch: per-partition state from the staged host block [status int8 x P,
@@ -398,7 +450,7 @@ __global__ void fa_bab_init_kernel(BabInitArgs a) {
       a.xphi[e] = r ? hi[e] + a.tau : hi[e];
     }
   }
-  if (tid < 4) a.counters[tid] = 0;
+  if (tid < 5) a.counters[tid] = 0;   // two level-counter slots + the fused settle's workgroup counter
 }
 
 // Solve end, one launch: status / nodes / open_left packed into one int block (one D2H copy).
@@ -423,40 +475,10 @@ __global__ void fa_mark_unknown_kernel(const int* part, int n, int8_t* status) {
 // of the two-pass schedule, same selection rule (profiles/escalate_sweep/), without restarting
 // from the root; otherwise it ends UNKNOWN with open_left = those nodes, exactly like the
 // first pass.  Its surplus children are skipped by the bound kernels (status filter).
-__global__ void fa_settle_kernel(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
-                                 int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
-                                 int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open,
-                                 EscSteps esc) {
+__global__ void fa_settle_kernel(SettleArgs s) {
   const int p = blockIdx.x * FA_THREADS + threadIdx.x;
-  if (p == 0) {
-    // level counters straight into pinned host memory (no blit per level), next slot cleared
-    __hip_atomic_store(&host_counts[0], counters_cur[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&host_counts[1], counters_cur[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    counters_next[0] = 0;
-    counters_next[1] = 0;
-  }
-  if (p >= P) return;
-  if (status[p] == ST_STOPPING) {
-    status[p] = ST_UNKNOWN;
-    if (part_open) part_open[p] = lvl_open[p];
-  } else if (prob && prob[p] && status[p] == ST_RUNNING) {
-    // stepped escalation: budget -> esc.budget[0] -> ... -> budget2; at each step's probation
-    // level the frontier must be at most max_open (first step) / esc.open[k-1] (step k)
-    const int cur = pbudget[p];
-    int k = 0;
-    while (k < esc.n && esc.budget[k] <= cur) ++k;
-    const int thr = k == 0 ? max_open : esc.open[k - 1];
-    if (lvl_open[p] <= thr) {
-      pbudget[p] = k < esc.n ? esc.budget[k] : budget2;
-    } else {
-      status[p] = ST_UNKNOWN;
-      if (part_open) part_open[p] = lvl_open[p];
-    }
-  }
-  if (prob) prob[p] = 0;
-  lvl_open[p] = 0;
-  prev_start[p] = nodes_start[p];
-  nodes_start[p] = part_nodes[p];     // the next level's budget reference
+  if (p == 0) fa_settle_counters(s);
+  if (p < s.P) fa_settle_part(s, p);
 }
 
 __global__ void fa_set_status_kernel(const int* idx, int n, int8_t* status, int8_t v) {
@@ -489,14 +511,9 @@ extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_
   return (int)hipGetLastError();
 }
 
-extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
-                                int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
-                                int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open,
-                                EscSteps esc, hipStream_t stream) {
-  const int n = P > 0 ? P : 1;
-  hipLaunchKernelGGL(fa_settle_kernel, dim3((n + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, P,
-                     status, lvl_open, part_open, part_nodes, nodes_start, prev_start, counters_cur, counters_next,
-                     host_counts, pbudget, prob, budget2, max_open, esc);
+extern "C" int fa_settle_launch(SettleArgs s, hipStream_t stream) {
+  const int n = s.P > 0 ? s.P : 1;
+  hipLaunchKernelGGL(fa_settle_kernel, dim3((n + FA_THREADS - 1) / FA_THREADS), dim3(FA_THREADS), 0, stream, s);
   return (int)hipGetLastError();
 }
 

@@ -39,10 +39,7 @@ extern "C" int fa_certify_launch(CertArgs a, hipStream_t stream);
 extern "C" int fa_split_launch(SplitArgs a, hipStream_t stream);
 extern "C" int fa_mark_unknown_launch(const int* part, int n, int8_t* status, hipStream_t stream);
 extern "C" int fa_set_status_launch(const int* idx, int n, int8_t* status, int8_t v, hipStream_t stream);
-extern "C" int fa_settle_launch(int P, int8_t* status, int* lvl_open, int* part_open, const int* part_nodes,
-                                int* nodes_start, int* prev_start, const int* counters_cur, int* counters_next,
-                                int* host_counts, int* pbudget, uint8_t* prob, int budget2, int max_open,
-                                EscSteps esc, hipStream_t stream);
+extern "C" int fa_settle_launch(SettleArgs s, hipStream_t stream);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_backward_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
@@ -79,6 +76,16 @@ bool cert_skip_closed() {
   static const bool v = [] {
     const char* e = getenv("FAIRIFY_CERT_SKIP_CLOSED");
     return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// A/B switch of the level end fused into the last split launch (FAIRIFY_FUSE_SETTLE=1: fused;
+// default its own launch -- BaBConfig.fuse_settle sets it per solve)
+bool fuse_settle() {
+  static const bool v = [] {
+    const char* e = getenv("FAIRIFY_FUSE_SETTLE");
+    return e && e[0] == '1';
   }();
   return v;
 }
@@ -152,7 +159,8 @@ class BabRuntime {
     pe_lb_.ensure(2 * (size_t)batch_);
     pe_ub_.ensure(2 * (size_t)batch_);
     ensure_cand(cand_cap_);
-    counters_.ensure(4);   // two slots of (children, candidates), alternating per level
+    counters_.ensure(5);   // two slots of (children, candidates), alternating per level, + the
+                           // fused settle's workgroup counter
     // fine-grained (coherent) pinned words: the settle kernel writes the level counters here
     hcount_buf_.ensure(2 * sizeof(int));
     hcount_ = reinterpret_cast<int*>(hcount_buf_.p);
@@ -185,6 +193,8 @@ class BabRuntime {
       ck(hipMemcpy(w0t_.p, wt.data(), wt.size() * sizeof(float), hipMemcpyHostToDevice), "cp w0t");
     }
   }
+
+  void set_fuse_settle(bool v) { fuse_settle_ = v; }
 
   py::tuple solve(py::array_t<float, py::array::c_style | py::array::forcecast> lo,
                   py::array_t<float, py::array::c_style | py::array::forcecast> hi,
@@ -290,6 +300,16 @@ class BabRuntime {
       // candidate buffer for the whole level (one per inner node, every PA pair of a leaf): a
       // capped buffer would drop candidates depending on which partitions share the chunk
       ensure_cand(std::min<long long>((long long)n_in * std::max(1, Pp_ * norient_), FA_CAND_MAX));
+      // level end: its own launch, or (fuse_settle_) fused into the level's last split launch
+      // whose last workgroup settles
+      SettleArgs se{};
+      se.P = P; se.status = status_.p; se.lvl_open = lvl_open_.p; se.part_open = open_left_.p;
+      se.part_nodes = nodes_.p; se.nodes_start = nodes_start_.p; se.prev_start = prev_start_.p;
+      se.counters_cur = cnt; se.counters_next = counters_.p + 2 * (slot ^ 1); se.host_counts = hcount_;
+      se.pbudget = inline_esc ? pbudget_.p : nullptr; se.prob = inline_esc ? prob_.p : nullptr;
+      se.budget2 = budget2; se.max_open = max_w; se.esc = esc;
+      se.done = counters_.p + 4;
+      bool settled = false;
       for (int s = 0; s < n_in; s += batch_) {
         const int nb = std::min(batch_, n_in - s);
         const float* blo = lo_[cur].p + (size_t)s * n0_;
@@ -361,13 +381,17 @@ class BabRuntime {
         sa.opart = part_[nxt].p; sa.count_out = cnt; sa.cap = pool_[nxt];
         sa.cand_buf = cand_buf_.p; sa.cand_count = cnt + 1;
         sa.cand_cap = cand_alloc_;
+        if (s + nb >= n_in && fuse_settle_) {
+          sa.settle = se;
+          settled = true;
+        }
         ckl(fa_split_launch(sa, st), "split");
         launches += (relaxed_ ? 2 : 1) * (refine_ == 2 ? 1 : 2) + 3;   // bounding launches + certify, points, split
       }
-      ckl(fa_settle_launch(P, status_.p, lvl_open_.p, open_left_.p, nodes_.p, nodes_start_.p, prev_start_.p, cnt,
-                           counters_.p + 2 * (slot ^ 1), hcount_, inline_esc ? pbudget_.p : nullptr,
-                           inline_esc ? prob_.p : nullptr, budget2, max_w, esc, st),
-          "settle");
+      if (!settled) {
+        ckl(fa_settle_launch(se, st), "settle");
+        ++launches;
+      }
       ck(hipStreamSynchronize(st), "sync");
       slot ^= 1;
       total_nodes += n_in;
@@ -597,6 +621,7 @@ class BabRuntime {
   bool crown_ = false;
   int refine_ = 0;          // 0 forward + output pass, 1 + refine between them, 2 backward only
   bool smear_ = false;      // first-layer smear split scores (CertArgs.smear)
+  bool fuse_settle_ = fuse_settle();   // level end in the last split launch (BaBConfig.fuse_settle)
   int split_target_ = 256;
   int n0_ = 0, npa_ = 0, V_ = 0, Pp_ = 0, norient_ = 1;
   bool relaxed_ = false;
@@ -636,6 +661,7 @@ void register_bab(py::module& m) {
            py::arg("pairs"), py::arg("ra"), py::arg("tau"), py::arg("shared"), py::arg("capacity"),
            py::arg("batch_nodes"), py::arg("cand_cap"), py::arg("unit"), py::arg("crown") = true,
            py::arg("split_target") = 256, py::arg("refine") = 0, py::arg("smear") = false)
+      .def("set_fuse_settle", &BabRuntime::set_fuse_settle, py::arg("on"))
       .def("solve", &BabRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("dead_part"), py::arg("confirm"), py::arg("stream"),
            py::arg("native_exact") = false, py::arg("budget2") = 0, py::arg("max_w") = 0,

@@ -58,6 +58,12 @@ class BaBConfig:
     # whose first hidden layer is >= 32 wide (AC-2/3/4/5/7; the narrow deep nets keep the
     # certificate scores), "on", "off"
     smear: str = os.environ.get("FAIRIFY_SMEAR", "auto")
+    # native runtime: the level end (fa_settle) runs in the level's last split launch (its last
+    # workgroup) instead of its own launch.  Off: the device-scope release fence every workgroup
+    # needs before counting itself done writes back the XCD's L2 (the level's children pool), and
+    # cost more than the launch it saves (N=1 944 -> 1 011 ms/step, 1/8 shard 141 -> 169 ms,
+    # profiles/r4/ab_fuse_settle.md)
+    fuse_settle: bool = os.environ.get("FAIRIFY_FUSE_SETTLE", "0") == "1"
     # native runtime branching rule: a partition with w nodes in a BFS level splits each along
     # clamp(log2(split_target / w), 1, 6) dims (per partition: verdicts do not depend on which
     # partitions share a chunk)
@@ -432,6 +438,7 @@ class BaBSolver:
             dead_ptr = self._dead_u8.data_ptr()
         stream = torch.cuda.current_stream(self.dev).cuda_stream
         with self.tm("bab.native"), self._runtime(values_np, pairs_np, n_run) as rt:
+            rt.set_fuse_settle(bool(self.cfg.fuse_settle))
             st, cx, cxp, nodes, stats = rt.solve(lo_np.astype(np.float32), hi_np.astype(np.float32), status,
                                                   int(self.cfg.node_budget), float(self.cfg.time_budget), dead_ptr,
                                                   confirm, stream, exact_models is None,

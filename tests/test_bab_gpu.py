@@ -118,3 +118,26 @@ def test_escalation_steps_only_stop_earlier(cuda, name):
     assert np.array_equal(steps.status[dec], one.status[dec])
     assert not np.any(dec & (one.status == 0))
     assert (one.status != 0).sum() >= dec.sum()
+
+
+@pytest.mark.parametrize("name", ["AC-7", "AC-12", "AC-4"])
+def test_fused_settle_matches_separate_launch(cuda, name):
+    """The level end fused into the last split launch (its last workgroup settles every partition,
+    csrc/bab.hip fa_split_kernel tail) gives exactly the per-partition verdicts and node counts of
+    the separate fa_settle_kernel launch, inline escalation steps included."""
+    from fairify_amd import presets
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.partition import processing_order
+
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    lo, hi = grid.decode(processing_order(grid, 0)[:1024])
+    m = get_model(name, weights="random", seed=0)
+    be = Backend(m, cuda)
+    base = dict(node_budget=512, escalate_budget=8192, escalate_max_w=384, escalate_steps=((2048, 768), (4096, 1024)))
+    out = {}
+    for fused in (False, True):
+        r = BaBSolver(be, q, BaBConfig(**base, fuse_settle=fused)).solve(lo, hi, m)
+        out[fused] = r
+    assert np.array_equal(out[True].status, out[False].status)
+    assert np.array_equal(out[True].nodes, out[False].nodes)
