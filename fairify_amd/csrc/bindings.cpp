@@ -211,7 +211,7 @@ PYBIND11_MODULE(_C, m) {
   // back-substituted hidden-layer bounds (refine.hip), tightening layer_lb / layer_ub of a preceding
   // symbolic `bounds` call in place; returns the launch code (0 done, -1 shape not supported)
   m.def("refine", [](const Net& net, uintptr_t flat, uintptr_t lo, uintptr_t hi, uintptr_t dead_in, int R,
-                     uintptr_t layer_lb, uintptr_t layer_ub, uintptr_t stream) {
+                     uintptr_t layer_lb, uintptr_t layer_ub, uintptr_t stream, uintptr_t phase, uintptr_t infeas) {
     BoundArgs a{};
     a.flat = P<const float>(flat);
     a.lo = P<const float>(lo);
@@ -220,10 +220,13 @@ PYBIND11_MODULE(_C, m) {
     a.R = R;
     a.layer_lb = P<float>(layer_lb);
     a.layer_ub = P<float>(layer_ub);
+    a.phase_in = P<const int8_t>(phase);   // ReLU-phase rows [R, n_hidden] (+1 / -1 fixed, 0 free)
+    a.infeas = P<uint8_t>(infeas);         // [R] set to 1 where a refined bound contradicts a phase
     const int rc = fa_refine_launch(net.d, a, (hipStream_t)stream);
     if (rc < -1) throw std::runtime_error("refine launch failed, code " + std::to_string(rc));
     return rc;
-  });
+  }, py::arg("net"), py::arg("flat"), py::arg("lo"), py::arg("hi"), py::arg("dead_in"), py::arg("R"),
+     py::arg("layer_lb"), py::arg("layer_ub"), py::arg("stream"), py::arg("phase") = 0, py::arg("infeas") = 0);
 
   // refined hidden-layer bounds + the logit's backward pass in one launch (what the BaB runtime runs
   // for BaBConfig.refine level 1), tightening a preceding symbolic `bounds` call in place

@@ -84,11 +84,16 @@ __device__ __forceinline__ void fa_refine_records(const NetDesc& net, const Boun
   float* hmx = smem + cfg.hm;
   for (int e = threadIdx.x; e < cfg.G * n; e += blockDim.x) {
     const int g = e / n, jj = e - g * n, h = off + jj;
-    const float lb = slab[g * 2 * N + h], ub = slab[g * 2 * N + N + h];
-    bool dd = ub <= 0.f;
-    const uint8_t* dm = fa_refine_dmask(net, a, min(rb + g, a.R - 1));
+    const int r = min(rb + g, a.R - 1);
+    const int ph = a.phase_in ? (int)a.phase_in[(size_t)r * NH + h] : 0;
+    // a fixed phase (ReLU-phase BaB rows) holds on the node's region: fixed active -> exact identity
+    // (lb >= 0 there), fixed inactive -> exactly 0
+    const float lb = ph > 0 ? fmaxf(slab[g * 2 * N + h], 0.f) : slab[g * 2 * N + h];
+    const float ub = ph < 0 ? fminf(slab[g * 2 * N + N + h], 0.f) : slab[g * 2 * N + N + h];
+    bool dd = ub <= 0.f || ph < 0;
+    const uint8_t* dm = fa_refine_dmask(net, a, r);
     if (dm && dm[h]) dd = true;
-    const bool act = !dd && lb >= 0.f;
+    const bool act = !dd && (lb >= 0.f || ph > 0);
     const bool unst = !dd && !act;
     const float alpha = ub > -lb ? 1.f : 0.f;
     const float sl = unst ? (ub / (ub - lb)) * (1.f + 4.f * u) : 0.f;
@@ -198,7 +203,10 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
         if (take && !logit) {
           const float lb = slab[g * 2 * N + offk + j], ub = slab[g * 2 * N + N + offk + j];
           const uint8_t* dm = fa_refine_dmask(net, a, rb + g);
-          take = lb < 0.f && ub > 0.f && !(dm && dm[offk + j]);
+          // phase-fixed neurons too: a refined bound that contradicts the phase proves the node's
+          // region empty (a.infeas)
+          const bool fixed = a.phase_in && a.phase_in[(size_t)(rb + g) * NH + offk + j] != 0;
+          take = ((lb < 0.f && ub > 0.f) || fixed) && !(dm && dm[offk + j]);
         }
         if (take) list[atomicAdd(&rrun[G], 1)] = e;
       }
@@ -348,6 +356,10 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
         if (vvalid && grp == 0) {
           float* dst = slab + g * 2 * N + (s ? N : 0) + offk + j;
           *dst = s ? fminf(*dst, -low) : fmaxf(*dst, low);
+          if (!logit && a.phase_in && a.infeas) {
+            const int ph = a.phase_in[(size_t)r * NH + offk + j];
+            if ((ph > 0 && s && -low < 0.f) || (ph < 0 && !s && low > 0.f)) a.infeas[r] = 1;
+          }
         }
       }
       __syncthreads();

@@ -27,6 +27,7 @@ namespace py = pybind11;
 extern "C" int fa_bounds_launch(const NetDesc& net, BoundArgs args, hipStream_t stream);
 extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_crown_phase_launch(const NetDesc& net, CrownPhaseArgs a, hipStream_t stream);
+extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_relu_rows_launch(ReluLevelArgs a, hipStream_t stream);
 extern "C" int fa_relu_cert_launch(ReluLevelArgs a, hipStream_t stream);
 extern "C" int fa_relu_split_launch(ReluLevelArgs a, hipStream_t stream);
@@ -58,9 +59,9 @@ float rgamma(int k, double unit) {
 class ReluRuntime {
  public:
   ReluRuntime(py::handle net, uintptr_t flat, std::vector<int> pa, std::vector<float> values_f,
-              std::vector<int64_t> pairs, int capacity, int batch_nodes, double unit)
+              std::vector<int64_t> pairs, int capacity, int batch_nodes, double unit, int refine)
       : net_(fa_net_desc(net)), flat_((const float*)flat), pa_(std::move(pa)), cap_(capacity), batch_(batch_nodes),
-        unit_(unit) {
+        unit_(unit), refine_(refine) {
     n0_ = net_.dims[0];
     nh_ = net_.n_hidden;
     npa_ = (int)pa_.size();
@@ -259,6 +260,13 @@ class ReluRuntime {
     b.phase_in = a.phase;           // node-major [n][2][nh] = row-major [2n + side][nh]
     b.infeas = infeas_.p;
     rckl(fa_bounds_launch(net_, b, st), "relu bounds");
+    // hidden-layer bounds by back-substitution with the rows' fixed phases (refine.hip): tighter
+    // relaxation intervals for the backward pass, and empty regions detected (infeas)
+    if (refine_) {
+      const int rc = fa_refine_launch(net_, b, st);
+      if (rc == -1) refine_ = 0;
+      else rckl(rc, "relu refine");
+    }
     CrownPhaseArgs c{};
     c.flat = flat_; c.lo = rlo_.p; c.hi = rhi_.p; c.R = R; c.phase = a.phase;
     c.layer_lb = lay_lb_.p; c.layer_ub = lay_ub_.p; c.infeas = infeas_.p;
@@ -375,6 +383,7 @@ class ReluRuntime {
   std::vector<int> pa_;
   int cap_, batch_;
   double unit_;
+  int refine_ = 0;          // phase-aware back-substituted hidden-layer bounds (ReluConfig.refine)
   int n0_ = 0, nh_ = 0, npa_ = 0, V_ = 0, Pp_ = 0;
   int pool_[2] = {0, 0};
   int cand_alloc_ = 0;
@@ -402,9 +411,9 @@ class ReluRuntime {
 void register_relu(py::module& m) {
   py::class_<ReluRuntime>(m, "ReluRuntime")
       .def(py::init<py::handle, uintptr_t, std::vector<int>, std::vector<float>, std::vector<int64_t>, int, int,
-                    double>(),
+                    double, int>(),
            py::arg("net"), py::arg("flat"), py::arg("pa"), py::arg("values_f"), py::arg("pairs"),
-           py::arg("capacity"), py::arg("batch_nodes"), py::arg("unit"))
+           py::arg("capacity"), py::arg("batch_nodes"), py::arg("unit"), py::arg("refine") = 0)
       .def("solve", &ReluRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("confirm"), py::arg("stream"));
 }

@@ -58,6 +58,10 @@ class ReluConfig:
     batch_nodes: int = 32768         # nodes bounded per sub-batch (torch path: per level)
     time_budget: float = 1e9         # wall-clock seconds for the whole call
     max_pool: int = 1 << 22          # live nodes (more: the partitions losing nodes end UNKNOWN)
+    # native runtime: hidden-layer bounds of every node tightened by back-substitution with its
+    # fixed phases (csrc/refine.hip; a refined bound contradicting a fixed phase proves the node's
+    # region empty) -- same "auto" rule as BaBConfig.refine
+    refine: str = os.environ.get("FAIRIFY_RELU_REFINE", "auto")
 
 
 def supported(q: ResolvedQuery) -> bool:
@@ -434,13 +438,16 @@ class ReluBaBSolver:
         from ..ops.hip import _net
         from .rtpool import checkout
 
-        key = (tuple(self.q.pa_idx), values_np.tobytes(), pairs_np.tobytes(), int(self.cfg.batch_nodes))
+        from .bab import refine_level
+
+        rf = min(1, refine_level(self.cfg.refine, self.be.widths))
+        key = (tuple(self.q.pa_idx), values_np.tobytes(), pairs_np.tobytes(), int(self.cfg.batch_nodes), rf)
 
         def make(cap):
             return ext().ReluRuntime(_net(self.be), self.be.flat.data_ptr(), list(self.q.pa_idx),
                                      values_np.astype(np.float32).reshape(-1).tolist(),
                                      pairs_np.astype(np.int64).reshape(-1).tolist(), int(cap),
-                                     int(self.cfg.batch_nodes), float(self.be.unit))
+                                     int(self.cfg.batch_nodes), float(self.be.unit), rf)
 
         return checkout(self.be, "_relu_rt", key, max(self.cfg.max_pool, 2 * n_root), make)
 

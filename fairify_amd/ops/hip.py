@@ -250,10 +250,14 @@ def crown(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, dead: Op
 
 
 # ------------------------------------------------------------------------------------------------
-def refine(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, dead: Optional[torch.Tensor] = None):
+def refine(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, dead: Optional[torch.Tensor] = None,
+           phase: Optional[torch.Tensor] = None):
     """Back-substituted hidden-layer bounds (csrc/refine.hip) tightening ``res.layer_lb/ub`` in place
     (ref.crown_refine): ``res`` must come from :func:`bounds` with mode='symbolic' and
-    keep_layers=True on the same rows.  Networks the kernel cannot hold keep the forward bounds."""
+    keep_layers=True on the same rows.  Networks the kernel cannot hold keep the forward bounds.
+    ``phase`` [R, n_hidden] int8 (ReLU-phase rows: +1 active / -1 inactive fixed, 0 free): the
+    bounds hold on the region where the fixed phases hold, and ``res.infeasible`` [R] also marks rows
+    whose refined bounds contradict a fixed phase (empty region)."""
     R, n0 = lo.shape
     if res.lay_lb_full is None:
         raise ValueError("refine needs symbolic bounds with keep_layers=True (HIP layout)")
@@ -262,9 +266,14 @@ def refine(be, lo: torch.Tensor, hi: torch.Tensor, res: ref.BoundResult, dead: O
     d = None
     if dead is not None:
         d = _c(dead, torch.uint8, (R, be.n_hidden), "dead")
+    ph = _c(phase, torch.int8, (R, be.n_hidden), "phase") if phase is not None else None
+    infeas = torch.zeros(R, dtype=torch.uint8, device=lo.device) if phase is not None else None
     if R:
         ext().refine(_net(be), be.flat.data_ptr(), lo.data_ptr(), hi.data_ptr(), _ptr(d), R,
-                     res.lay_lb_full.data_ptr(), res.lay_ub_full.data_ptr(), _stream(lo.device))
+                     res.lay_lb_full.data_ptr(), res.lay_ub_full.data_ptr(), _stream(lo.device), _ptr(ph),
+                     _ptr(infeas))
+    if infeas is not None:
+        res.infeasible = infeas.bool() if res.infeasible is None else (res.infeasible | infeas.bool())
     Nh = be.n_hidden
     if Nh:
         res.dead = res.lay_ub_full[:, :Nh] <= 0

@@ -232,3 +232,56 @@ def test_fused_refine_crown_equals_refine_then_crown(cuda, n0, hidden):
     scale = float((two.out_ub - two.out_lb).abs().max().cpu() + two.out_ub.abs().max().cpu() + 1e-3)
     assert torch.allclose(one.out_lb, two.out_lb, rtol=1e-4, atol=1e-4 * scale)
     assert torch.allclose(one.out_ub, two.out_ub, rtol=1e-4, atol=1e-4 * scale)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_phase_refine_sound_and_infeasibility_exact(cuda, seed):
+    """Phase-aware refinement (ReLU-phase BaB rows): on every lattice point of the box whose
+    activation pattern satisfies the row's fixed phases, each hidden pre-activation lies in the
+    refined bounds; a row flagged infeasible has no such point."""
+    from fairify_amd.ops import hip as H
+
+    torch.manual_seed(seed)
+    n0, hidden = 5, [12, 10, 8]
+    m = random_mlp(n0, hidden, seed=seed)
+    be = Backend(m, cuda)
+    g = torch.Generator().manual_seed(seed)
+    R = 48
+    lo = torch.randint(0, 3, (R, n0), generator=g).float()
+    hi = lo + torch.randint(0, 3, (R, n0), generator=g).float()
+    Nh = sum(hidden)
+    phase = torch.zeros(R, Nh, dtype=torch.int8)
+    for r in range(R):          # fix a few neurons per row, either phase
+        idx = torch.randperm(Nh, generator=g)[:4]
+        phase[r, idx] = (torch.randint(0, 2, (4,), generator=g) * 2 - 1).to(torch.int8)
+    lo_d, hi_d, ph_d = lo.to(cuda), hi.to(cuda), phase.to(cuda)
+    res = H.bounds(be, lo_d, hi_d, mode="symbolic", keep_layers=True, phase=ph_d)
+    res = H.refine(be, lo_d, hi_d, res, phase=ph_d)
+    llb, lub = res.lay_lb_full.cpu().double(), res.lay_ub_full.cpu().double()
+    infeas = res.infeasible.cpu()
+    cpu = Backend(m, "cpu")
+    W = [w.double() for w in cpu.ws]
+    B = [b.double() for b in cpu.bs]
+    n_feas_rows = 0
+    for r in range(R):
+        pts = torch.tensor(list(itertools.product(*[range(int(a), int(b) + 1) for a, b in zip(lo[r], hi[r])])),
+                           dtype=torch.float64)
+        h, zs = pts, []
+        for l in range(len(hidden)):
+            z = h @ W[l] + B[l]
+            zs.append(z)
+            h = torch.relu(z)
+        Z = torch.cat(zs, 1)                                     # [pts, Nh]
+        ph = phase[r].double()
+        ok = torch.all(((ph > 0) & (Z < 0)).logical_not() & ((ph < 0) & (Z > 0)).logical_not(), dim=1)
+        if infeas[r]:
+            assert not ok.any(), r
+            continue
+        if not ok.any():
+            continue
+        n_feas_rows += 1
+        Zf = Z[ok]
+        tol = 1e-5 * (1 + Zf.abs())
+        assert torch.all(Zf >= llb[r, :Nh] - tol), r
+        assert torch.all(Zf <= lub[r, :Nh] + tol), r
+    assert n_feas_rows > 0

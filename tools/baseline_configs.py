@@ -58,6 +58,8 @@ def run_group(args) -> None:
         models = list(pre.models) if not args.models else args.models.split(",")
         out = os.path.join(args.out, name.replace("/", "_"))
         os.makedirs(out, exist_ok=True)
+        # per-partition CSVs (MBs per model) go to scratch: gpurun copies back <= 64 MiB of gpurun_out
+        scratch = os.path.join(args.scratch, name.replace("/", "_"))
         anytime = args.anytime_budget if (args.group == "tablev" or args.anytime_budget > 0 and args.all_anytime) else 0
         cfg = VerifyConfig(sim_size=pre.sim_size, soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
                            heuristic=False, heuristic_p=pre.heuristic_p, node_budget=512, escalate_budget=32768,
@@ -68,7 +70,7 @@ def run_group(args) -> None:
         weights = {m: ("zoo" if has_weights(m) else "random") for m in models}
         rows = []
         for m in models:
-            r = run_preset(pre, models=[m], weights=weights[m], out_dir=os.path.join(out, m), cfg=cfg, info=info,
+            r = run_preset(pre, models=[m], weights=weights[m], out_dir=os.path.join(scratch, m), cfg=cfg, info=info,
                            seed=0, accuracy=False, verbose=False, concurrency=4,
                            anytime_budget=anytime or None, max_partitions=args.max_partitions)
             for row in r:
@@ -124,6 +126,8 @@ def main():
     ap.add_argument("--all-anytime", action="store_true", help="anytime mode for the other groups too")
     ap.add_argument("--max-partitions", type=int, default=None, help="CPU rehearsal: first N of each grid")
     ap.add_argument("--report", default=None)
+    ap.add_argument("--scratch", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "fairify_base"),
+                    help="per-partition CSVs (not copied back)")
     args = ap.parse_args()
     if args.report:
         report(args.report)
