@@ -92,6 +92,11 @@ class VerifyConfig:
     anytime_pool: int = 1 << 24          # live BaB nodes per group: group size = pool / budget
     anytime_max_samples: int = 16384
     anytime_milp_seconds: float = 1.0    # first MILP round's per-partition limit (x growth per round)
+    # a GPU stage (input-split / ReLU-phase BaB) whose anytime round decides less than this fraction
+    # of the partitions it attempted is not run in later rounds: its next budget (x growth) would
+    # spend the remaining time where it does not converge (trained AC-7: 1.6 G input-split nodes in
+    # 110 s for 424 proofs) -- the other stages get it
+    anytime_min_yield: float = 0.01
     relu_budget: int = 2048              # ReLU-phase BaB (stage "relu", engine/relu_bab.py) on the
                                          # input-split residue: nodes per partition (0 = off)
     relu_max_width: int = 16             # ... only for networks whose hidden layers are at most this
@@ -599,6 +604,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         lp_budget = max(1, cfg.lp_budget // 16)                     # x growth per round
         relu_any = _relu_supported(q)
         r_budget = max(cfg.relu_budget, 1) if relu_on else 64      # x growth before the first round
+        bab_live, relu_live = True, True                          # stages still yielding
         with tm("anytime"):
             while True:
                 unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
@@ -626,14 +632,17 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                 # (c) deeper sound BaB, in groups that fit the node pool
                 e_budget *= cfg.anytime_growth
                 if e_budget > cfg.anytime_max_budget:
-                    break
+                    bab_live = False
+                if not (bab_live or (relu_any and cfg.relu_budget > 0 and relu_live) or use_milp):
+                    break                                       # nothing left that can still decide
                 unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
                 if _VERBOSE_ANYTIME:
                     print(f"[anytime] {mlp.name} round {anytime_rounds}: {unk.size} unknown after falsify "
                           f"({n_samp} samples), BaB budget {e_budget}, {deadline - time.time():.1f}s left",
                           flush=True)
                 G = max(1, cfg.anytime_pool // e_budget)
-                for g0 in range(0, unk.size, G):
+                n_try = n_dec = 0
+                for g0 in range(0, unk.size if bab_live else 0, G):
                     left = deadline - time.time()
                     if left <= 0:
                         break
@@ -642,6 +651,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                                                          time_budget=left, max_pool=cfg.anytime_pool), timer=tm)
                     ares = asolver.solve(lo_np[grp], hi_np[grp], mlp)
                     dec_a = np.isin(ares.status, (SAT, UNSAT))
+                    n_try += grp.size
+                    n_dec += int(dec_a.sum())
                     hit = grp[dec_a]
                     status[hit] = ares.status[dec_a]
                     stage[hit] = "bab"
@@ -649,12 +660,15 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                     cex_x[grp[sa]] = ares.cex_x[sa]
                     cex_xp[grp[sa]] = ares.cex_xp[sa]
                     nodes[grp] += ares.nodes
+                if bab_live and n_try and n_dec < cfg.anytime_min_yield * n_try:
+                    bab_live = False
                 # (d) ReLU-phase BaB with a growing budget, any layer width (the anytime budget pays
                 # for the wide nets too; it re-proves partitions the MILP only claims)
-                if relu_any and cfg.relu_budget > 0:
+                if relu_any and cfg.relu_budget > 0 and relu_live:
                     r_budget *= cfg.anytime_growth
                     unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
                     left = deadline - time.time()
+                    r_try = r_dec = 0
                     if unk.size and left > 0:
                         from .relu_bab import ReluBaBSolver, ReluConfig
 
@@ -669,12 +683,16 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                             with tm("relu"):
                                 rr = rs.solve(lo_np[grp], hi_np[grp], mlp)
                             dec_r = np.isin(rr.status, (SAT, UNSAT))
+                            r_try += grp.size
+                            r_dec += int(dec_r.sum())
                             status[grp[dec_r]] = rr.status[dec_r]
                             stage[grp[dec_r]] = "relu"
                             sr = rr.status == SAT
                             cex_x[grp[sr]] = rr.cex_x[sr]
                             cex_xp[grp[sr]] = rr.cex_xp[sr]
                             nodes[grp] += rr.nodes
+                    if r_try and r_dec < cfg.anytime_min_yield * r_try:
+                        relu_live = False
                 # (e) verified-LP branch-and-bound with a growing node budget (sound UNSAT), or
                 # -- trust_milp / lp_budget 0 -- the HiGHS MILP with a growing time limit.  Last in the
                 # round: host LPs cost ~10-30 ms per node (AC-7: 341 variables), the GPU stages above
