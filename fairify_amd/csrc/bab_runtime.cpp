@@ -379,7 +379,7 @@ class BabRuntime {
         sa.oxlo = lo_[nxt].p; sa.oxhi = hi_[nxt].p;
         sa.oxplo = relaxed_ ? plo_[nxt].p : nullptr; sa.oxphi = relaxed_ ? phi_[nxt].p : nullptr;
         sa.opart = part_[nxt].p; sa.count_out = cnt; sa.cap = pool_[nxt];
-        sa.cand_buf = cand_buf_.p; sa.cand_count = cnt + 1;
+        sa.cand_buf = reinterpret_cast<float*>(cand_host_.p); sa.cand_count = cnt + 1;
         sa.cand_cap = cand_alloc_;
         if (s + nb >= n_in && fuse_settle_) {
           sa.settle = se;
@@ -518,7 +518,7 @@ class BabRuntime {
     long long n = std::max<long long>(cand_alloc_, 1 << 16);
     while (n < need) n *= 2;
     n = std::min<long long>(n, FA_CAND_MAX);
-    cand_buf_.ensure((size_t)n * (2 * n0_ + 1));
+    cand_host_.ensure((size_t)n * (2 * n0_ + 1) * sizeof(float));
     cand_alloc_ = (int)n;
   }
 
@@ -526,14 +526,12 @@ class BabRuntime {
   void confirm_candidates(int n_cand, py::object& confirm, std::vector<char>& got, std::vector<int64_t>& cex_x,
                           std::vector<int64_t>& cex_xp, hipStream_t st) {
     const size_t rec = (size_t)2 * n0_ + 1;             // x, x', partition id (int bits)
-    hcand_.ensure((size_t)n_cand * rec * sizeof(float));
-    ck(hipMemcpyAsync(hcand_.p, cand_buf_.p, (size_t)n_cand * rec * sizeof(float), hipMemcpyDeviceToHost, st),
-       "cp cand");
-    ck(hipStreamSynchronize(st), "sync");
+    // the split kernel wrote the records straight into pinned host memory, and the level-end
+    // synchronisation retired it: no copy, no second round trip per level
     std::vector<float> buf((size_t)n_cand * 2 * n0_);
     std::vector<int> parts(n_cand);
     {
-      const float* hc = reinterpret_cast<const float*>(hcand_.p);
+      const float* hc = reinterpret_cast<const float*>(cand_host_.p);
       for (int i = 0; i < n_cand; ++i) {
         std::memcpy(buf.data() + (size_t)i * 2 * n0_, hc + (size_t)i * rec, sizeof(float) * 2 * n0_);
         std::memcpy(&parts[i], hc + (size_t)i * rec + 2 * n0_, sizeof(int));
@@ -631,7 +629,7 @@ class BabRuntime {
   DevBuf<float> lo_[2], hi_[2], plo_[2], phi_[2];
   DevBuf<int> part_[2];
   DevBuf<float> Lc_[2], Uc_[2], L0_[2], Le_[2], U0_[2], Ue_[2], olb_[2], oub_[2], lay_lb_[2], lay_ub_[2];
-  DevBuf<float> gmin_, tstar_, score_, cand_, scores_, pe_lb_, pe_ub_, cand_buf_;
+  DevBuf<float> gmin_, tstar_, score_, cand_, scores_, pe_lb_, pe_ub_;
   DevBuf<uint8_t> open_, leaf_;
   DevBuf<int64_t> split_, cv_, co_;
   DevBuf<int> counters_, nodes_, idx_, open_left_, lvl_open_, nodes_start_, prev_start_, out_, pbudget_;
@@ -649,7 +647,11 @@ class BabRuntime {
   // it to another runtime).  Round 1 enqueued pageable H2D copies and then rewrote the source
   // vector in place (relaxed x' boxes); with 8 host threads that raced the runtime's staging of
   // pageable copies.
-  fa_mem::HostBuf hstage_, hout_, hcand_, hidx_;
+  fa_mem::HostBuf hstage_, hout_, hidx_;
+  // candidate records [cand_alloc_][2 n0 + 1], written by fa_split_kernel into coherent pinned host
+  // memory and read by confirm_candidates after the level-end synchronisation; the next level's
+  // split (launched after the confirmation returns) is the next writer
+  fa_mem::HostBuf cand_host_{true};
 };
 
 void register_bab(py::module& m) {

@@ -243,7 +243,7 @@ class ReluRuntime {
     a.status = status_.p; a.part_nodes = nodes_.p; a.nodes_start = nodes_start_.p; a.budget = budget;
     a.opart = part_[nxt].p; a.opair = pair_[nxt].p; a.oxlo = lo_[nxt].p; a.oxhi = hi_[nxt].p;
     a.ophase = phase_[nxt].p; a.count_out = counters_.p; a.cap = pool_[nxt];
-    a.cand_buf = cand_.p; a.cand_count = counters_.p + 1; a.cand_cap = cand_alloc_;
+    a.cand_buf = reinterpret_cast<float*>(cand_host_.p); a.cand_count = counters_.p + 1; a.cand_cap = cand_alloc_;
     a.unit = (float)unit_;
     a.gmarg = rgamma(2 * n0_ + 4, unit_);
     rckl(fa_relu_rows_launch(a, st), "relu rows");
@@ -307,7 +307,7 @@ class ReluRuntime {
     long long n = std::max<long long>(cand_alloc_, 1 << 14);
     while (n < need) n *= 2;
     n = std::min<long long>(n, 1LL << 24);
-    cand_.ensure((size_t)n * (2 * n0_ + 1));
+    cand_host_.ensure((size_t)n * (2 * n0_ + 1) * sizeof(float));
     cand_alloc_ = (int)n;
   }
 
@@ -315,10 +315,8 @@ class ReluRuntime {
   void confirm_candidates(int n_cand, py::object& confirm, std::vector<char>& got, std::vector<int64_t>& cex_x,
                           std::vector<int64_t>& cex_xp, hipStream_t st) {
     const size_t rec = (size_t)2 * n0_ + 1;
-    hcand_.ensure((size_t)n_cand * rec * sizeof(float));
-    rck(hipMemcpyAsync(hcand_.p, cand_.p, (size_t)n_cand * rec * sizeof(float), hipMemcpyDeviceToHost, st), "cp cand");
-    rck(hipStreamSynchronize(st), "sync");
-    const float* hc = reinterpret_cast<const float*>(hcand_.p);
+    // written by the split kernel into pinned host memory, retired by the level-end sync
+    const float* hc = reinterpret_cast<const float*>(cand_host_.p);
     std::vector<float> buf((size_t)n_cand * 2 * n0_);
     std::vector<int> parts(n_cand);
     for (int i = 0; i < n_cand; ++i) {
@@ -395,8 +393,7 @@ class ReluRuntime {
   RBuf<int> part_[2], pair_[2];
   RBuf<float> lo_[2], hi_[2];
   RBuf<int8_t> phase_[2];
-  RBuf<float> rlo_, rhi_, olb_, oub_, Lc_, Uc_, L0_, Le_, U0_, Ue_, lay_lb_, lay_ub_, score_, cpts_, pe_lb_, pe_ub_,
-      cand_;
+  RBuf<float> rlo_, rhi_, olb_, oub_, Lc_, Uc_, L0_, Le_, U0_, Ue_, lay_lb_, lay_ub_, score_, cpts_, pe_lb_, pe_ub_;
   RBuf<int> rpart_, split_, choice_, idim_, counters_, nodes_, nodes_start_, idx_;
   RBuf<uint8_t> infeas_, open_;
   RBuf<int8_t> status_;
@@ -405,7 +402,8 @@ class ReluRuntime {
   int* hcount_ = nullptr;
   // pinned staging; same buffer-lifetime rule as BabRuntime (released / regrown only after the
   // stream synchronisation that retires its last copy)
-  fa_mem::HostBuf hstage_, hout_, hcand_, hidx_;
+  fa_mem::HostBuf hstage_, hout_, hidx_;
+  fa_mem::HostBuf cand_host_{true};   // candidate records (coherent pinned, written by the split kernel)
 };
 
 void register_relu(py::module& m) {
