@@ -60,8 +60,11 @@ class ReluConfig:
     max_pool: int = 1 << 22          # live nodes (more: the partitions losing nodes end UNKNOWN)
     # native runtime: hidden-layer bounds of every node tightened by back-substitution with its
     # fixed phases (csrc/refine.hip; a refined bound contradicting a fixed phase proves the node's
-    # region empty) -- same "auto" rule as BaBConfig.refine
-    refine: str = os.environ.get("FAIRIFY_RELU_REFINE", "auto")
+    # region empty); "auto" = BaBConfig.refine's rule.  Default off: on the bench (AC-11 is the
+    # only refine-eligible net the stage runs on) it decided 3 partitions per step fewer at +3-8 %
+    # step time, and on the trained AC-7 residue it closed none either way
+    # (profiles/r4/relu_refine.md)
+    refine: str = os.environ.get("FAIRIFY_RELU_REFINE", "off")
 
 
 def supported(q: ResolvedQuery) -> bool:
