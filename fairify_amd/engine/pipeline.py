@@ -660,6 +660,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                     cex_x[grp[sa]] = ares.cex_x[sa]
                     cex_xp[grp[sa]] = ares.cex_xp[sa]
                     nodes[grp] += ares.nodes
+                    if n_try >= 256 and n_dec < cfg.anytime_min_yield * n_try:
+                        break                                   # not converging: stop the round early
                 if bab_live and n_try and n_dec < cfg.anytime_min_yield * n_try:
                     bab_live = False
                 # (d) ReLU-phase BaB with a growing budget, any layer width (the anytime budget pays
@@ -691,6 +693,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                             cex_x[grp[sr]] = rr.cex_x[sr]
                             cex_xp[grp[sr]] = rr.cex_xp[sr]
                             nodes[grp] += rr.nodes
+                            if r_try >= 256 and r_dec < cfg.anytime_min_yield * r_try:
+                                break
                     if r_try and r_dec < cfg.anytime_min_yield * r_try:
                         relu_live = False
                 # (e) verified-LP branch-and-bound with a growing node budget (sound UNSAT), or
