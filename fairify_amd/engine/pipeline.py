@@ -251,16 +251,30 @@ def _lp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, budget, limit,
     """Verified-LP branch-and-bound (smt/lpbab.py) on the partitions ``unk``: HiGHS solves, a
     rigorous weak-duality bound from its multipliers closes nodes, lattice points and LP optima
     are checked exactly.  UNSAT and SAT verdicts are both sound (stage ``lp``)."""
+    pending = _lp_submit(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, budget, limit, workers, deadline)
+    _lp_collect(mlp, pending, budget, status, stage, cex_x, cex_xp)
+
+
+def _lp_submit(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, budget, limit, workers, deadline=None):
+    """Start the verified-LP searches of ``unk`` in the worker processes; returns [(k, future)]."""
     from ..smt import lpbab
 
     futs = lpbab.submit(be, mlp, q, lo_np[unk], hi_np[unk], values_np, pairs_np, budget, limit, workers=workers,
                         deadline=deadline)
+    return list(zip(unk, futs))
+
+
+def _lp_collect(mlp, pending, budget, status, stage, cex_x, cex_xp):
+    """Wait for the LP searches of :func:`_lp_submit`; a partition another stage decided meanwhile
+    keeps that verdict (both are sound)."""
     t_note = time.time()
-    for i, (k, f) in enumerate(zip(unk, futs)):
+    for i, (k, f) in enumerate(pending):
         verdict, pair, _ = f.result()
         if _VERBOSE_ANYTIME and time.time() - t_note > 30.0:
             t_note = time.time()
-            print(f"[lp] {mlp.name}: {i + 1}/{len(unk)} partitions, budget {budget}", flush=True)
+            print(f"[lp] {mlp.name}: {i + 1}/{len(pending)} partitions, budget {budget}", flush=True)
+        if status[k] != UNKNOWN:
+            continue
         if verdict == "unsat":
             status[k], stage[k] = UNSAT, "lp"
         elif verdict == "sat" and pair is not None:
@@ -611,6 +625,16 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                 if not unk.size or time.time() >= deadline:
                     break
                 anytime_rounds += 1
+                # (e, started first) verified-LP branch-and-bound on the host workers with a growing
+                # node budget, CONCURRENT with this round's GPU stages (collected at the round's end):
+                # on a residue the GPU stages do not converge on (trained AC-7) the round costs
+                # max(GPU, LP) instead of their sum
+                lp_pending = None
+                if use_milp and _use_lp(cfg, q):
+                    left = deadline - time.time()
+                    with tm("lp.submit"):
+                        lp_pending = _lp_submit(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, lp_budget,
+                                                min(milp_limit * 4, left), cfg.smt_workers, deadline=deadline)
                 # (a) fresh samples + boundary walk + local search, new seed every round
                 n_samp = min(n_samp * cfg.anytime_growth, cfg.anytime_max_samples)
                 ut = torch.from_numpy(unk).to(dev)
@@ -697,18 +721,11 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                                 break
                     if r_try and r_dec < cfg.anytime_min_yield * r_try:
                         relu_live = False
-                # (e) verified-LP branch-and-bound with a growing node budget (sound UNSAT), or
-                # -- trust_milp / lp_budget 0 -- the HiGHS MILP with a growing time limit.  Last in the
-                # round: host LPs cost ~10-30 ms per node (AC-7: 341 variables), the GPU stages above
-                # decide most of the residue first
-                if use_milp and _use_lp(cfg, q):
-                    unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
-                    left = deadline - time.time()
-                    if unk.size and left > 0:
-                        with tm("lp"):
-                            _lp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, lp_budget,
-                                      min(milp_limit * 4, left), cfg.smt_workers, status, stage, cex_x, cex_xp,
-                                      deadline=deadline)
+                # (e) collect the verified-LP searches started with the round (sound UNSAT and SAT),
+                # or -- trust_milp / lp_budget 0 -- the HiGHS MILP with a growing time limit
+                if lp_pending is not None:
+                    with tm("lp"):
+                        _lp_collect(mlp, lp_pending, lp_budget, status, stage, cex_x, cex_xp)
                     lp_budget *= cfg.anytime_growth
                     milp_limit *= cfg.anytime_growth
                 elif use_milp:

@@ -256,3 +256,31 @@ def test_relu_bab_relaxed_matches_bruteforce(seed, tau):
             assert not truth, k
         decided += res.status[k] != UNKNOWN
     assert decided >= 0.9 * len(ids)
+
+
+def test_anytime_lp_overlaps_gpu_stages_and_agrees():
+    """Anytime mode with the verified LP: the LP searches start with each round and run in the host
+    workers while the BaB / relu stages work on the same residue; a partition decided by both keeps
+    one verdict, LP verdicts agree with the plain input-split ones, and LP SAT pairs are exact."""
+    from fairify_amd.engine import exact
+    from fairify_amd.engine.pipeline import VerifyConfig, _lp_available, verify_chunk
+
+    if not _lp_available():
+        pytest.skip("SciPy HiGHS bindings not available")
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    m = get_model("AC-8", weights="random", seed=0)
+    ids = processing_order(grid, 0)[:48]
+    be = Backend(m)
+    base = dict(sim_size=200, node_budget=32, heuristic=False, relu_budget=0)
+    off = verify_chunk(be, m, q, grid, ids, VerifyConfig(smt_backend="none", **base))
+    r = verify_chunk(be, m, q, grid, ids, VerifyConfig(smt_backend="auto", anytime_seconds=20, lp_budget=256,
+                                                       smt_workers=2, **base))
+    assert (r.cols["verdict"] != "unknown").sum() >= (off.cols["verdict"] != "unknown").sum()
+    both = (off.cols["verdict"] != "unknown") & (r.cols["verdict"] != "unknown")
+    assert (off.cols["verdict"][both] == r.cols["verdict"][both]).all()
+    sat = np.nonzero(r.cols["verdict"] == "sat")[0]
+    lo, hi = grid.decode(ids[sat])
+    X, XP = r.cols["cex_x"][sat], r.cols["cex_xp"][sat]
+    assert exact.check_pair_constraints(X, XP, lo, hi, q.pa_idx, q.ra_idx, q.tau).all()
+    assert exact.is_violation(m, X, XP).all()
