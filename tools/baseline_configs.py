@@ -53,6 +53,18 @@ def run_group(args) -> None:
 
     info = D.init("cuda" if torch.cuda.device_count() else "cpu")
     names = GROUPS[args.group] if args.group in GROUPS else args.group.split(",")
+    # heartbeat: a stress model (3.29 M partitions) runs for minutes without a per-model line, and a
+    # silent GPU command is taken to be hung
+    import threading
+
+    cur = {"what": "start", "t": time.time()}
+
+    def beat():
+        while True:
+            time.sleep(60)
+            print(f"[hb] {cur['what']} {time.time() - cur['t']:.0f}s", flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
     for name in names:
         pre = presets.get(name)
         models = list(pre.models) if not args.models else args.models.split(",")
@@ -70,6 +82,7 @@ def run_group(args) -> None:
         weights = {m: ("zoo" if has_weights(m) else "random") for m in models}
         rows = []
         for m in models:
+            cur["what"], cur["t"] = f"{name} {m}", time.time()
             r = run_preset(pre, models=[m], weights=weights[m], out_dir=os.path.join(scratch, m), cfg=cfg, info=info,
                            seed=0, accuracy=False, verbose=False, concurrency=4,
                            anytime_budget=anytime or None, max_partitions=args.max_partitions)
