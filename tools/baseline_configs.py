@@ -73,11 +73,16 @@ def run_group(args) -> None:
         # per-partition CSVs (MBs per model) go to scratch: gpurun copies back <= 64 MiB of gpurun_out
         scratch = os.path.join(args.scratch, name.replace("/", "_"))
         anytime = args.anytime_budget if (args.group == "tablev" or args.anytime_budget > 0 and args.all_anytime) else 0
+        # the large grids (stress / relaxed / targeted: 0.2-3.3 M partitions per model) run the GPU
+        # stages only (--smt none) with a shorter escalation; Table V adds the host LP (anytime)
+        big = args.group != "tablev" and not args.all_anytime
         cfg = VerifyConfig(sim_size=pre.sim_size, soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
-                           heuristic=False, heuristic_p=pre.heuristic_p, node_budget=512, escalate_budget=32768,
-                           escalate_max_open=384,
-                           escalate_probation=((2048, 768), (4096, 768), (8192, 768), (16384, 1024)),
-                           relu_budget=1024, relu_escalate_cap=2048, smt_backend="auto", chunk=8192)
+                           heuristic=False, heuristic_p=pre.heuristic_p, node_budget=512,
+                           escalate_budget=8192 if big else 32768, escalate_max_open=384,
+                           escalate_probation=((2048, 768), (4096, 768)) if big else
+                           ((2048, 768), (4096, 768), (8192, 768), (16384, 1024)),
+                           relu_budget=1024, relu_escalate_cap=2048, smt_backend=args.smt or ("none" if big else "auto"),
+                           chunk=8192)
         t0 = time.time()
         weights = {m: ("zoo" if has_weights(m) else "random") for m in models}
         rows = []
@@ -92,9 +97,11 @@ def run_group(args) -> None:
                 print(f"[{name}] {m} ({weights[m]}): {row['SAT']} sat / {row['UNSAT']} unsat / {row['UNK']} unk "
                       f"of {row['#P']}, Cov_sound {row.get('Cov_sound%')} %, {row.get('wall_s')} s",
                       flush=True)
-        with open(os.path.join(out, "summary.json"), "w") as f:
-            json.dump({"preset": name, "models": rows, "head": args.head, "wall_s": round(time.time() - t0, 2),
-                       "anytime_budget_s": anytime, "heuristic": False}, f, indent=2)
+            # after every model: a run cut by its time limit keeps the finished models
+            with open(os.path.join(out, "summary.json"), "w") as f:
+                json.dump({"preset": name, "models": rows, "head": args.head, "wall_s": round(time.time() - t0, 2),
+                           "anytime_budget_s": anytime, "heuristic": False, "smt": cfg.smt_backend,
+                           "escalate_budget": cfg.escalate_budget}, f, indent=2)
         print(f"[{name}] done in {time.time() - t0:.1f}s", flush=True)
     D.destroy(info)
 
@@ -139,6 +146,7 @@ def main():
     ap.add_argument("--all-anytime", action="store_true", help="anytime mode for the other groups too")
     ap.add_argument("--max-partitions", type=int, default=None, help="CPU rehearsal: first N of each grid")
     ap.add_argument("--report", default=None)
+    ap.add_argument("--smt", default=None, help="host back-end (default: auto for tablev, none for the big grids)")
     ap.add_argument("--scratch", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "fairify_base"),
                     help="per-partition CSVs (not copied back)")
     args = ap.parse_args()
