@@ -183,8 +183,13 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
       box[g * 2 * n0 + n0 + d] = xh;
     }
     __syncthreads();
-    if (!cfg.full && L > 1) fa_refine_records(net, a, cfg, 0, rb, smem);   // layer 0 is final
-    const int k0 = cfg.full ? 0 : 1, k1 = (cfg.full || cfg.logit) ? L : L - 1;
+    // REFINE starts at hidden layer 2: back-substituting a layer-1 neuron through layer 0 picks, per
+    // weight sign, the same relaxation of h_0 the forward pass already combined (W+ U + W- L), so
+    // its bounds only move by rounding (<= 4e-4 of the width, ops/reference.py:crown_refine) --
+    // that layer was ~30 % of the kernel's column work on AC-7
+    const int k0 = cfg.full ? 0 : 2, k1 = (cfg.full || cfg.logit) ? L : L - 1;
+    if (!cfg.full)
+      for (int l = 0; l < k0 && l < L - 1; ++l) fa_refine_records(net, a, cfg, l, rb, smem);   // final
     for (int k = k0; k < k1; ++k) {
       const bool logit = k == L - 1;               // the output forms (FULL, or REFINE + logit)
       const int nk = net.dims[k + 1];
@@ -480,7 +485,7 @@ int backward_launch(const NetDesc& net, const BoundArgs& a, int full, int logit,
 // wider than 160 or the weights beyond the LDS budget: the caller keeps the forward bounds, which
 // are sound), < -1 error.  Needs a.layer_lb / a.layer_ub [R, n_neurons] from the forward pass.
 extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream) {
-  if (a.R <= 0 || net.n_layers < 3) return 0;
+  if (a.R <= 0 || net.n_layers < 4) return 0;   // refines hidden layers 2 .. L-2
   if (!a.layer_lb || !a.layer_ub) return -2;
   return backward_launch(net, a, 0, 0, stream);
 }

@@ -426,7 +426,7 @@ def _backsub(ws, bs, lo: torch.Tensor, hi: torch.Tensor, lbs, ubs, lam: torch.Te
 
 def crown_refine(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: torch.Tensor, hi: torch.Tensor,
                  res: BoundResult, dead: Optional[torch.Tensor] = None, unit: Optional[float] = None) -> BoundResult:
-    """Tighten the per-neuron pre-activation bounds of hidden layers 1 .. L-2 by back-substitution
+    """Tighten the per-neuron pre-activation bounds of hidden layers 2 .. L-2 by back-substitution
     (csrc/refine.hip, same arithmetic and error terms).
 
     The forward symbolic pass relaxes every layer with the forms it propagated forward, so on deep
@@ -445,7 +445,9 @@ def crown_refine(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: tor
     L = len(ws)
     lbs = [t.clone() for t in res.layer_lb]
     ubs = [t.clone() for t in res.layer_ub]
-    for k in range(1, L - 1):
+    # from hidden layer 2 on (the kernel's rule): a layer-1 neuron back-substituted through layer 0
+    # gets the forward pass's own relaxation choice per weight sign -- the same bounds up to rounding
+    for k in range(2, L - 1):
         n_k = ws[k].shape[1]
         Wt = ws[k].to(dt).T                                       # [n_k, dims[k]]
         rep = lambda t: t.repeat_interleave(n_k, dim=0)          # noqa: E731  rows x targets
