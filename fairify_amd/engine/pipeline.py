@@ -75,7 +75,9 @@ class VerifyConfig:
     residual_iters: int = 12             # coordinate-ascent rounds
     smt_backend: str = "auto"            # exact host solver on the BaB residue: auto (Z3 if installed,
                                          # else the HiGHS MILP back-end) | z3py | z3bin | milp | none
-    smt_workers: int = field(default_factory=lambda: _host_workers(12))
+    # host solver processes (LP / MILP / SMT); FAIRIFY_SMT_WORKERS overrides the CPU-share rule
+    smt_workers: int = field(default_factory=lambda: int(os.environ.get("FAIRIFY_SMT_WORKERS", "0"))
+                             or _host_workers(12))
                                          # host solver threads: this rank's CPUs (its node slice when
                                          # several ranks share a node, parallel/balance.py), at most 12
     smt_timeout: Optional[float] = None  # per query; defaults to soft_timeout
@@ -615,7 +617,10 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
 
             use_milp = smt_solver.resolve(cfg.smt_backend) == "milp"
         milp_limit = cfg.anytime_milp_seconds
-        lp_budget = max(1, cfg.lp_budget // 16)                     # x growth per round
+        # x growth per round; the first round at budget / 4: trained AC-7's UNSAT partitions need
+        # 100-5 000 LP nodes (profiles/r4/lp_tree_sizes_ac7_trained.jsonl), and every round restarts
+        # its searches from the root
+        lp_budget = max(1, cfg.lp_budget // 4)
         relu_any = _relu_supported(q)
         r_budget = max(cfg.relu_budget, 1) if relu_on else 64      # x growth before the first round
         bab_live, relu_live = True, True                          # stages still yielding
