@@ -42,6 +42,10 @@ struct BoundArgs {
   // STOPPING are skipped (nothing written; the split kernel ignores those nodes)
   const int8_t* skip_status;
   const int* skip_part;
+  // refine.hip (REFINE + logit, single-PA BaB rows, V > 1): the node's forward logit bounds
+  // already exclude every ordered pair of its V rows (out_lb[i] >= 0 or out_ub[j] <= 0 for all
+  // i != j -- the certificate's sign shortcut closes it): its rows are not refined
+  int skip_signdef;
   // point kernel in the BaB level: point r is the candidate x (r < open_mod) or x' of node
   // r % open_mod; tiles whose 16 points all belong to closed nodes (open == 0, the certificate
   // excluded every pair) are skipped -- the split kernel reads point bounds of open nodes only

@@ -90,6 +90,15 @@ bool fuse_settle() {
   return v;
 }
 
+// A/B switch: refine skips nodes its forward bounds already close (FAIRIFY_REFINE_SKIP_SIGNDEF=0: off)
+bool skip_signdef() {
+  static const bool v = [] {
+    const char* e = getenv("FAIRIFY_REFINE_SKIP_SIGNDEF");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 float gamma_up(int k, double unit) {
   const double ku = (k + 2) * unit;
   return std::nextafter((float)(ku / (1.0 - ku)), INFINITY);
@@ -478,7 +487,9 @@ class BabRuntime {
     // hidden-layer bounds tightened by back-substitution (refine.hip) before the output pass uses
     // them as relaxation intervals; a network the kernel cannot hold (-1) keeps the forward bounds
     if (refine_ == 1) {
-      // refined hidden-layer bounds and the logit's backward pass in one launch
+      // refined hidden-layer bounds and the logit's backward pass in one launch; nodes whose
+      // forward bounds already exclude every ordered pair (single PA: Pp = V (V - 1)) are skipped
+      b.skip_signdef = (!relaxed_ && npa_ == 1 && Pp_ == V_ * (V_ - 1) && skip_signdef()) ? 1 : 0;
       const int rc = fa_refine_crown_launch(net_, b, st);
       if (rc == 0) return;
       if (rc != -1) ckl(rc, "refine");

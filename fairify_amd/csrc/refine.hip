@@ -156,6 +156,15 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
         const int8_t st = a.skip_status[a.skip_part[node]];
         run = (st == 3 || st == 4);
       }
+      if (run && a.skip_signdef && cfg.logit && !cfg.full && a.V > 1) {
+        // the forward bounds already close the node (sign shortcut over all ordered pairs)
+        const int base = (r / a.V) * a.V;
+        bool closed = true;
+        for (int i = 0; i < a.V && closed; ++i)
+          for (int j = 0; j < a.V; ++j)
+            if (i != j && !(a.out_lb[base + i] >= 0.f || a.out_ub[base + j] <= 0.f)) { closed = false; break; }
+        if (closed) run = 0;
+      }
       rrun[tid] = run;
     }
     __syncthreads();
