@@ -168,7 +168,8 @@ def _mem_delta(a, b):
         return None
     return {"driver_frees": b["driver_frees"] - a["driver_frees"], "dev_mallocs": b["dev_mallocs"] - a["dev_mallocs"],
             "dev_cache_hits": b["dev_hits"] - a["dev_hits"], "host_mallocs": b["host_mallocs"] - a["host_mallocs"],
-            "dev_gb": round((b["dev_live_bytes"] + b["dev_cached_bytes"]) / 2 ** 30, 3)}
+            "dev_gb": round((b["dev_live_bytes"] + b["dev_cached_bytes"]) / 2 ** 30, 3),
+            "host_pinned_gb": round((b.get("host_live_bytes", 0) + b.get("host_cached_bytes", 0)) / 2 ** 30, 3)}
 
 
 def main() -> None:
