@@ -101,6 +101,11 @@ class VerifyConfig:
     # spend the remaining time where it does not converge (trained AC-7: 1.6 G input-split nodes in
     # 110 s for 424 proofs) -- the other stages get it
     anytime_min_yield: float = 0.01
+    # the first anytime round's verified-LP node budget is lp_budget / this (x growth per round);
+    # 0 = by the PA table: a binary PA (2 ordered pairs) starts at 1/4 -- many cheap attempts first
+    # (trained AC-7/sex at 120 s: 78.8 % vs 72.8 % at the full budget) --, a multi-valued PA at the
+    # full budget, where the per-value sign tests need it (AC-7/race: 99.8 % vs 87.8 %)
+    anytime_lp_div: int = int(os.environ.get("FAIRIFY_ANYTIME_LP_DIV", "0"))
     relu_budget: int = 2048              # ReLU-phase BaB (stage "relu", engine/relu_bab.py) on the
                                          # input-split residue: nodes per partition (0 = off)
     relu_max_width: int = 16             # ... only for networks whose hidden layers are at most this
@@ -622,7 +627,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         # x growth per round; the first round at budget / 4: trained AC-7's UNSAT partitions need
         # 100-5 000 LP nodes (profiles/r4/lp_tree_sizes_ac7_trained.jsonl), and every round restarts
         # its searches from the root
-        lp_budget = max(1, cfg.lp_budget // 4)
+        lp_div = cfg.anytime_lp_div or (1 if len(pairs_np) > 2 else 4)
+        lp_budget = max(1, cfg.lp_budget // lp_div)
         relu_any = _relu_supported(q)
         r_budget = max(cfg.relu_budget, 1) if relu_on else 64      # x growth before the first round
         bab_live, relu_live = True, True                          # stages still yielding
