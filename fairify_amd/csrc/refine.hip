@@ -102,8 +102,8 @@ __device__ __forceinline__ void fa_refine_records(const NetDesc& net, const Boun
     q.y = act ? 1.f : (dd ? 0.f : sl);
     q.z = unst ? lb : 0.f;
     q.w = unst ? fmaxf(fabsf(lb), fabsf(ub)) : 0.f;
-    rec[g * NH + h] = q;
-    hmx[g * NH + h] = dd ? 0.f : fmaxf(ub, 0.f);
+    rec[g * (NH + 1) + h] = q;
+    hmx[g * (NH + 1) + h] = dd ? 0.f : fmaxf(ub, 0.f);
   }
 }
 
@@ -237,8 +237,11 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
         const int j = e - g * nk;
         const int r = rb + g;
         const int node = a.V > 0 ? r / a.V : r;
-        const float4* recg = rec + g * NH;
-        const float* hmg = hmx + g * NH;
+        // row strides NH + 1: the lanes of a column tile read the same neuron of up to 16 rows, and
+        // an NH-float4 stride put those rows 4 ways on the same LDS banks (PMC: ~1 conflict cycle
+        // per LDS instruction, profiles/r4/pmc/final_pmc.md)
+        const float4* recg = rec + g * (NH + 1);
+        const float* hmg = hmx + g * (NH + 1);
         const float* bl = box + g * 2 * n0;
         const float sgn = s ? -1.f : 1.f;
         // lam = +-W_k[:, j] from the staged copy: element (in, j) of layer k's operand order
@@ -444,12 +447,12 @@ int backward_launch(const NetDesc& net, const BoundArgs& a, int full, int logit,
   const int N = net.n_neurons, NH = net.n_hidden, n0 = net.dims[0];
   int maxw = 1;
   for (int l = 1; l <= L; ++l) maxw = std::max(maxw, net.dims[l]);
-  // per-row LDS: slab 2N, records 4 NH (16-byte aligned first), hm NH, box 2 n0, columns maxw
+  // per-row LDS: records 4 (NH + 1) (16-byte aligned, first), slab 2N, hm NH + 1, box 2 n0, columns maxw
   auto layout = [&](int g) {
     cfg.rec = base;
-    cfg.slab = cfg.rec + g * 4 * NH;
+    cfg.slab = cfg.rec + g * 4 * (NH + 1);
     cfg.hm = cfg.slab + g * 2 * N;
-    cfg.box = cfg.hm + g * NH;
+    cfg.box = cfg.hm + g * (NH + 1);
     cfg.list = cfg.box + g * 2 * n0;
     cfg.rrun = cfg.list + g * maxw;
     return (size_t)(cfg.rrun + g + 1) * sizeof(float);
