@@ -10,15 +10,21 @@ ranks (strong scaling: total work fixed).  Weights are random-init (glorot-unifo
 seed) per BASELINE.json; ``--weights zoo`` uses the reference's trained weights instead.
 
 value  = SOUNDLY decided partitions per second, whole job: SAT pairs confirmed exactly on the
-         original network + UNSAT from rigorous proofs (stages bab / relu / alpha / lp / smt).
+         original network + UNSAT from rigorous proofs (stages bab / relu / beta / lp / smt).
          Heuristic-retry UNSAT (the reference's unsound retry, src/AC/Verify-AC.py:173-212), a
          trusted MILP's floating-point UNSAT and heuristic SAT pairs that do not flip the
          original network are excluded; the all-verdict rate the reference would count is the
          secondary field ``decided_per_s_all``.
 vs_baseline = value / 0.02497 decided partitions/s, the reference's AC/sex aggregate from
 Table V (553 decided in sum(#P x Total) = 22 144 s).  That reference number is on
-its TRAINED weights; this bench runs random-init weights of the same shapes (BASELINE.json), so
-``vs_baseline_trained`` reports the trained-weight Table-V comparison of profiles/r4/ beside it.
+its TRAINED weights; this bench runs random-init weights of the same shapes (BASELINE.json).  The
+trained-weight Table-V comparison is a separate run (tools/baseline_configs.py, README), not a
+field of this line.
+
+JSON keys (rank 0 prints one line; tests/test_bench_launch.py checks every one is present):
+metric, value, unit, n_gpus, steps, warmup, ms_per_step, higher_is_better, scaling, vs_baseline,
+dtype, data, config, decided_per_s_all, pct_verified, pct_verified_sound, partitions_per_s, sat,
+unsat, unknown, unsat_sound, unsat_heuristic, sat_by_stage, unsat_by_stage, dist, baseline.
 
 Multi-GPU: one process per GPU, ``torch.distributed`` backend ``nccl`` (= RCCL over xGMI).
 
@@ -49,7 +55,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_DECIDED_PER_S = 553.0 / 22143.5
 METRIC = "% partitions verified + partitions/sec on AC suite at 1/2/4/8 MI355X"
-STAGES = ("sim", "bab", "relu", "lp", "falsify", "smt", "milp", "heuristic", "heuristic-confirmed")
+STAGES = ("sim", "bab", "relu", "beta", "lp", "falsify", "smt", "milp", "heuristic", "heuristic-confirmed")
 UNSOUND_UNSAT = ("heuristic", "milp")     # engine/stages.py: UNSAT verdicts that are not proofs
 
 

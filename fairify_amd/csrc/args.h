@@ -379,3 +379,35 @@ struct ReluLevelArgs {
   float unit;
   float gmarg;              // gamma(2 n0 + 4)
 };
+
+// beta-CROWN level of the ReLU-phase BaB (csrc/beta.hip, ops/beta.py:level_ref): one wave per node
+struct BetaArgs {
+  const float* flat;        // network (NetDesc layout)
+  const float* wt;          // per layer W_l transposed ([out][in] row-major, at net.w_off[l])
+  int R;
+  int npa;
+  int pa_idx[FA_MAX_PA];
+  const float* lo;          // [R, n0] node boxes (PA dims ignored)
+  const float* hi;
+  const float* va;          // [R, npa] PA values of copy A / copy B
+  const float* vb;
+  const float* LBA;         // [R, NH] partition pre-activation bounds (unclamped) of copy A / B
+  const float* UBA;
+  const float* LBB;
+  const float* UBB;
+  const int8_t* phA;        // [R, NH] phases -1 / 0 / +1
+  const int8_t* phB;
+  float* par;               // [R, 4, NH] alpha_A, alpha_B, beta_A, beta_B: in = start, out = best
+  float* t;                 // [R] in/out
+  float* scratch;           // [R, 12, NH] current params, Adam m, Adam v
+  int iters;
+  float lr_a, lr_b, lr_t, decay;
+  int lookahead;            // candidates per score of the filtered branching (0: best gap score)
+  int beta_pos;             // project beta >= 0 (1) or keep it free-signed (0)
+  int wpb;                  // waves per workgroup
+  int wt_lds;               // 1: transposed weights staged in LDS too
+  double* bound;            // [R] rigorous lower bound of t N(x,va) - (1-t) N(x,vb) (+inf: empty region)
+  int* split;               // [R] >= 0 neuron (A: j, B: NH + j), -1-d input dim d, -(n0+1) leaf
+  float* xstar;             // [R, n0] concretising vertex
+  float* binit;             // [R, 2] split multiplier of the (inactive, active) child
+};

@@ -1,0 +1,689 @@
+// beta-CROWN bounding of ReLU-phase BaB nodes on gfx950 (stage "beta"; semantics:
+// fairify_amd/ops/beta.py:level_ref, which the GPU tests compare this kernel against).
+//
+// The reference decides a partition with Z3, whose simplex case-splits each ReLU
+// If(z >= 0, z, 0) (utils/verif_utils.py:525-528; src/AC/Verify-AC.py:146-158): inside a case
+// split the phase is a linear constraint on the region.  Per node (box, ordered PA pair (va, vb),
+// phases of both network copies) this kernel maximises the Lagrangian lower bound of
+//     f_t(x) = t N(x, va) - (1 - t) N(x, vb)        (f_t >= 0 on the region: no violating pair)
+// over the lower slopes alpha (unstable neurons), the split multipliers beta (fixed neurons) and t
+// by projected Adam in fp32, then re-evaluates the bound at the best parameters in fp64 with
+// rigorous rounding terms, picks the branching neuron by a filtered look-ahead and returns the
+// concretising vertex (the host screens / confirms it as a candidate pair).
+//
+// Mapping: ONE wave64 per node, lanes over the neurons of a layer (widths <= 64 take one lane
+// each; wider layers loop).  Per layer the backward step is lam_{l-1} = W_l mu_l: lane i of the
+// previous layer sums over the w_l multipliers, read as LDS broadcasts, against the transposed
+// weights (consecutive across lanes: no bank conflicts); the forward step of the linearised
+// network reads W_l row-major the same way.  The weights are staged once per workgroup (the
+// transposed copy too when it fits), the per-node bounds / records live in a per-wave LDS slab,
+// the optimiser state (current parameters, Adam moments) in a global scratch row per node that
+// stays L2-resident while the wave runs.  The network is a handful of KB and every node runs
+// ~100 dependent passes through it, so the kernel is latency / issue bound: MFMA would need 16
+// nodes sharing one multiplier layout, which their per-node relaxation choices do not allow.
+#include <float.h>
+
+#include "args.h"
+
+namespace {
+
+constexpr double U64 = 1.1102230246251565e-16;   // 2^-53
+
+__device__ __forceinline__ double g64(int k) {    // Higham gamma_k in fp64, padded like ref.gamma
+  const double ku = (k + 2) * U64;
+  return ku / (1.0 - ku);
+}
+
+__device__ __forceinline__ void wsync() {
+  // lanes of ONE wave exchange data through LDS: DS instructions of a wave execute in order, so a
+  // compiler-level barrier with wave-scope fences is enough (no workgroup barrier: waves are independent)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T>
+__device__ __forceinline__ T tabs(T v) {
+  return v < (T)0 ? -v : v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wsum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// wave arg-max (first index on ties); returns the winning value, index in *idx
+__device__ __forceinline__ float wargmax(float v, int i, int* idx) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(v, o, 64);
+    const int i2 = __shfl_xor(i, o, 64);
+    if (v2 > v || (v2 == v && i2 < i)) {
+      v = v2;
+      i = i2;
+    }
+  }
+  *idx = i;
+  return v;
+}
+
+struct Slab {            // per-wave LDS workspace
+  float* lb[2];          // phase-clamped pre-activation bounds [NH] per copy
+  float* ub[2];
+  float* lam[2];         // multiplier on h_j of the last backward pass [NH]
+  float* z[2];           // linearised pre-activations at x* [NH]
+  float* sc;             // branching scores [2 NH]
+  int8_t* kd[2];         // relaxation kind of the last backward pass (0 off, 1 identity, 2 alpha, 3 chord)
+  int8_t* ph[2];         // phases
+  double* b0;            // broadcast buffers [mw] (fp32 passes use them as float arrays)
+  double* b1;
+  double* cf[2];         // input coefficients of the rigorous pass [n0]
+  double* hm[2];         // |input| maxima per copy [n0]
+  float* cft;            // input coefficients of a look-ahead pass [n0]
+  float* xs;             // concretising vertex [n0]
+};
+
+struct Node {            // per-node constants (wave-uniform)
+  const float* lo;
+  const float* hi;
+  float va[FA_MAX_PA];
+  float vb[FA_MAX_PA];
+  unsigned long long pamask;
+};
+
+// Backward pass of copy `c` (objective scale * logit).  T = float: an optimisation step (no
+// rounding terms); T = double with RIG: the rigorous bound (every rounding charged to *err).
+// REC: record lam / kind per neuron (the gradient and the scores read them).  ovr >= 0: look-ahead
+// child -- neuron ovr of this copy gets phase ovs (its multiplier 0).  Leaves the input
+// coefficients in `coef` (LDS, n0) and returns the constant.
+template <typename T, bool RIG, bool REC, bool WTL>
+__device__ T bwd(const NetDesc& nd, const float* Wf, const float* Wt, const Slab& S, int c, T scale,
+                 const float* __restrict__ al, const float* __restrict__ be, int ovr, int ovs, T* coef, T* err,
+                 int* infeas) {
+  const int lane = threadIdx.x & 63;
+  const int L = nd.n_layers;
+  const int NH = nd.n_hidden;
+  T* b0 = reinterpret_cast<T*>(S.b0);
+  T* b1 = reinterpret_cast<T*>(S.b1);
+  const float* lbv = S.lb[c];
+  const float* ubv = S.ub[c];
+  T cpart = 0, mpart = 0, epart = 0;
+  int bad = 0;
+  {
+    const int w = nd.dims[L - 1];
+    const float* wo = Wf + nd.w_off[L - 1];
+    const int off = nd.neuron_off[L - 2];
+    for (int j = lane; j < w; j += 64) {
+      const T lam = scale * (T)wo[j];
+      b0[j] = lam;
+      if (RIG) epart += (T)U64 * tabs(lam) * (T)fmaxf(ubv[off + j], 0.f);
+    }
+    if (lane == 0) {
+      const T c0 = scale * (T)Wf[nd.b_off[L - 1]];
+      cpart += c0;
+      if (RIG) mpart += tabs(c0);
+    }
+  }
+  wsync();
+  for (int l = L - 2; l >= 0; --l) {
+    const int w = nd.dims[l + 1];
+    const int win = nd.dims[l];
+    const int off = nd.neuron_off[l];
+    const float* bias = Wf + nd.b_off[l];
+    for (int j = lane; j < w; j += 64) {
+      const int k = off + j;
+      const T lam = b0[j];
+      float lbj = lbv[k], ubj = ubv[k];
+      int p = S.ph[c][k];
+      T bet = (T)be[k];
+      if (k == ovr) {
+        p = ovs;
+        bet = 0;
+        if (p > 0) lbj = fmaxf(lbj, 0.f);
+        if (p < 0) ubj = fminf(ubj, 0.f);
+        if (lbj > ubj) bad = 1;
+      }
+      if (p == 0) bet = 0;
+      const bool dead = ubj <= 0.f || p < 0;
+      const bool act = !dead && (lbj >= 0.f || p > 0);
+      T base = 0, kap = 0;
+      int kind = 0;
+      if (act) {
+        base = lam;
+        kind = 1;
+      } else if (!dead) {
+        if (lam >= 0) {
+          base = lam * (T)al[k];
+          kind = 2;
+        } else {
+          T s = (T)ubj / ((T)ubj - (T)lbj);
+          if (RIG) s *= (T)(1.0 + 4.0 * U64);         // rounded up: a steeper chord stays above relu
+          base = lam * s;
+          kap = -base * (T)lbj;
+          kind = 3;
+        }
+      }
+      const T mu = base - bet * (T)p;
+      // a negative multiplier of a fixed neuron takes the interval side of its region
+      const T kb = (p != 0 && bet < 0) ? bet * (T)p * (T)(p > 0 ? ubj : lbj) : (T)0;
+      const T mb = mu * (T)bias[j];
+      cpart += mb + kap + kb;
+      if (RIG) {
+        const T zmax = (T)fmaxf(fabsf(lbj), fabsf(ubj));
+        T e = 0;
+        if (kind == 2) e += (T)g64(1) * tabs(base) * zmax;
+        if (kind == 3) e += (T)(3.0 * U64) * ((T)2 * tabs(base) * zmax + tabs(kap));
+        if (p != 0) e += (T)g64(1) * (tabs(mu) * zmax + tabs(kb));
+        epart += e;
+        mpart += tabs(mb) + tabs(kap) + tabs(kb);
+      }
+      b1[j] = mu;
+      if (REC) {
+        S.lam[c][k] = (float)lam;
+        S.kd[c][k] = (int8_t)kind;
+      }
+    }
+    wsync();
+    const float* wt = Wt + nd.w_off[l];
+    for (int i = lane; i < win; i += 64) {
+      T acc = 0, aab = 0;
+      for (int j = 0; j < w; ++j) {
+        const T wv = (T)wt[j * win + i];
+        const T m = b1[j];
+        acc += wv * m;
+        if (RIG) aab += tabs(wv) * tabs(m);
+      }
+      b0[i] = acc;
+      if (RIG) {
+        const T hmx = l > 0 ? (T)fmaxf(ubv[nd.neuron_off[l - 1] + i], 0.f) : (T)S.hm[c][i];
+        epart += (T)g64(w) * aab * hmx;
+      }
+    }
+    wsync();
+  }
+  for (int i = lane; i < nd.dims[0]; i += 64) coef[i] = b0[i];
+  wsync();
+  if (RIG) *err = wsum(epart) + (T)g64(2 * NH + 8) * wsum(mpart);
+  if (infeas) *infeas = __any(bad) ? 1 : 0;
+  return wsum(cpart);
+}
+
+// Concretisation of the coupled input form over the node box (PA dims: va / vb); writes x* to
+// S.xs.  RIG: returns the bound less every rounding term (errA + errB passed in).
+template <typename T, bool RIG>
+__device__ T conc(const NetDesc& nd, const Slab& S, const Node& N, const T* cA, const T* cB, T kA, T kB, T eAB) {
+  const int lane = threadIdx.x & 63;
+  const int n0 = nd.dims[0];
+  T part = 0, mag = 0, emag = 0;
+  for (int i = lane; i < n0; i += 64) {
+    const float lo = N.lo[i], hi = N.hi[i];
+    if ((N.pamask >> i) & 1ull) {
+      // this PA dim's position in the value list
+      int q = __popcll(N.pamask & ((1ull << i) - 1ull));
+      const T ta = cA[i] * (T)N.va[q];
+      const T tb = cB[i] * (T)N.vb[q];
+      part += ta + tb;
+      if (RIG) mag += tabs(ta) + tabs(tb);
+      S.xs[i] = lo;
+    } else {
+      const T cf = cA[i] + cB[i];
+      const float x = cf >= 0 ? lo : hi;
+      const T tm = cf * (T)x;
+      part += tm;
+      if (RIG) {
+        mag += tabs(tm);
+        emag += tabs(cf) * (T)fmaxf(fabsf(lo), fabsf(hi));
+      }
+      S.xs[i] = x;
+    }
+  }
+  T B = wsum(part) + kA + kB;
+  if (RIG) {
+    const T m = wsum(mag) + tabs(kA) + tabs(kB);
+    const T econ = (T)U64 * wsum(emag) + (T)g64(n0 + 8) * m;
+    B -= (eAB + econ) * (T)(1.0 + 1e-6);
+  }
+  wsync();
+  return B;
+}
+
+// Linearised network of copy c at S.xs (PA dims = v): records z per neuron, returns the logit.
+template <typename T>
+__device__ T fwd(const NetDesc& nd, const float* Wf, const Slab& S, const Node& N, int c, const float* v,
+                 const float* __restrict__ al) {
+  const int lane = threadIdx.x & 63;
+  const int L = nd.n_layers;
+  const int n0 = nd.dims[0];
+  T* h0 = reinterpret_cast<T*>(S.b0);
+  T* h1 = reinterpret_cast<T*>(S.b1);
+  for (int i = lane; i < n0; i += 64) {
+    T x = (T)S.xs[i];
+    if ((N.pamask >> i) & 1ull) x = (T)v[__popcll(N.pamask & ((1ull << i) - 1ull))];
+    h0[i] = x;
+  }
+  wsync();
+  for (int l = 0; l < L - 1; ++l) {
+    const int w = nd.dims[l + 1];
+    const int win = nd.dims[l];
+    const int off = nd.neuron_off[l];
+    const float* W = Wf + nd.w_off[l];
+    const float* bias = Wf + nd.b_off[l];
+    for (int j = lane; j < w; j += 64) {
+      T z = (T)bias[j];
+      for (int i = 0; i < win; ++i) z += (T)W[i * w + j] * h0[i];
+      const int k = off + j;
+      S.z[c][k] = (float)z;
+      const int kind = S.kd[c][k];
+      T h = 0;
+      if (kind == 1) h = z;
+      else if (kind == 2) h = (T)al[k] * z;
+      else if (kind == 3) {
+        const T lbj = (T)S.lb[c][k], ubj = (T)S.ub[c][k];
+        h = ubj / (ubj - lbj) * (z - lbj);
+      }
+      h1[j] = h;
+    }
+    wsync();
+    T* tmp = h0;
+    h0 = h1;
+    h1 = tmp;
+  }
+  const int w = nd.dims[L - 1];
+  const float* wo = Wf + nd.w_off[L - 1];
+  T part = 0;
+  for (int j = lane; j < w; j += 64) part += (T)wo[j] * h0[j];
+  const T out = wsum(part) + (T)Wf[nd.b_off[L - 1]];
+  wsync();
+  return out;
+}
+
+template <bool WTL>
+__global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
+  extern __shared__ float smem[];
+  const int L = nd.n_layers;
+  const int NH = nd.n_hidden;
+  const int n0 = nd.dims[0];
+  const int mw = nd.max_width;
+  const int tot = nd.b_off[L - 1] + nd.dims[L];
+  const int tot4 = (tot + 3) & ~3;
+  float* Wf = smem;
+  float* Wtl = smem + tot4;
+  for (int k = threadIdx.x; k < tot; k += blockDim.x) {
+    Wf[k] = a.flat[k];
+    if (WTL) Wtl[k] = a.wt[k];
+  }
+  __syncthreads();
+  const float* Wt = WTL ? (const float*)Wtl : a.wt;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * a.wpb + wave;
+  if (r >= a.R) return;
+
+  // ---- per-wave slab
+  const int NHp = (NH + 3) & ~3;
+  const int n0p = (n0 + 3) & ~3;
+  const int mwp = (mw + 3) & ~3;
+  const int slab = 11 * NHp + 4 * mwp + 10 * n0p + 32;
+  float* base = smem + tot4 * (WTL ? 2 : 1) + wave * slab;
+  Slab S;
+  S.lb[0] = base; S.ub[0] = base + NHp; S.lb[1] = base + 2 * NHp; S.ub[1] = base + 3 * NHp;
+  S.lam[0] = base + 4 * NHp; S.lam[1] = base + 5 * NHp;
+  S.z[0] = base + 6 * NHp; S.z[1] = base + 7 * NHp;
+  S.sc = base + 8 * NHp;                                  // 2 NHp
+  int8_t* bytes = reinterpret_cast<int8_t*>(base + 10 * NHp);
+  S.kd[0] = bytes; S.kd[1] = bytes + NHp; S.ph[0] = bytes + 2 * NHp; S.ph[1] = bytes + 3 * NHp;
+  double* dbase = reinterpret_cast<double*>(base + 11 * NHp);  // 11 NHp is a multiple of 4: 16-B aligned
+  S.b0 = dbase; S.b1 = dbase + mwp;
+  S.cf[0] = dbase + 2 * mwp; S.cf[1] = S.cf[0] + n0p; S.hm[0] = S.cf[1] + n0p; S.hm[1] = S.hm[0] + n0p;
+  S.cft = reinterpret_cast<float*>(S.hm[1] + n0p);
+  S.xs = S.cft + n0p;
+  int* cand = reinterpret_cast<int*>(S.xs + n0p);      // look-ahead candidates [32]
+
+  Node N;
+  N.lo = a.lo + (size_t)r * n0;
+  N.hi = a.hi + (size_t)r * n0;
+  N.pamask = 0;
+  for (int q = 0; q < a.npa; ++q) {
+    N.va[q] = a.va[(size_t)r * a.npa + q];
+    N.vb[q] = a.vb[(size_t)r * a.npa + q];
+    N.pamask |= 1ull << a.pa_idx[q];
+  }
+  // PA indices must be listed in increasing order for the popcount lookup (checked on the host)
+
+  // ---- phase-clamped bounds, phases, |input| maxima
+  int bad = 0;
+  {
+    const float* LB[2] = {a.LBA + (size_t)r * NH, a.LBB + (size_t)r * NH};
+    const float* UB[2] = {a.UBA + (size_t)r * NH, a.UBB + (size_t)r * NH};
+    const int8_t* PH[2] = {a.phA + (size_t)r * NH, a.phB + (size_t)r * NH};
+    for (int c = 0; c < 2; ++c)
+      for (int k = lane; k < NH; k += 64) {
+        const int p = PH[c][k];
+        float lb = LB[c][k], ub = UB[c][k];
+        if (p > 0) lb = fmaxf(lb, 0.f);
+        if (p < 0) ub = fminf(ub, 0.f);
+        if (lb > ub) bad = 1;
+        S.lb[c][k] = lb;
+        S.ub[c][k] = ub;
+        S.ph[c][k] = (int8_t)p;
+      }
+    for (int i = lane; i < n0; i += 64) {
+      const double m = fmax(fabs((double)N.lo[i]), fabs((double)N.hi[i]));
+      if ((N.pamask >> i) & 1ull) {
+        const int q = __popcll(N.pamask & ((1ull << i) - 1ull));
+        S.hm[0][i] = fabs((double)N.va[q]);
+        S.hm[1][i] = fabs((double)N.vb[q]);
+      } else {
+        S.hm[0][i] = m;
+        S.hm[1][i] = m;
+      }
+    }
+  }
+  wsync();
+  float* par = a.par + (size_t)r * 4 * NH;          // alpha_A, alpha_B, beta_A, beta_B (best)
+  float* cur = a.scratch + (size_t)r * 12 * NH;     // current
+  float* mom = cur + 4 * NH;
+  float* vel = cur + 8 * NH;
+  if (__any(bad)) {
+    if (lane == 0) {
+      a.bound[r] = __builtin_inf();
+      a.split[r] = -(n0 + 1);
+      a.binit[2 * r] = 0.f;
+      a.binit[2 * r + 1] = 0.f;
+    }
+    for (int i = lane; i < n0; i += 64) a.xstar[(size_t)r * n0 + i] = N.lo[i];
+    return;
+  }
+  // every neuron's state is touched by the SAME lane everywhere (lane j of its layer), so no
+  // lane reads a global word another lane of the wave wrote
+  for (int l = 0; l < L - 1; ++l)
+    for (int j = lane; j < nd.dims[l + 1]; j += 64)
+      for (int q = 0; q < 4; ++q) {
+        const int k = q * NH + nd.neuron_off[l] + j;
+        cur[k] = par[k];
+        mom[k] = 0.f;
+        vel[k] = 0.f;
+      }
+  float tc = a.t[r], tbest = tc, mt = 0.f, vt = 0.f;
+  float best = -FLT_MAX;
+  float* cA = reinterpret_cast<float*>(S.cf[0]);   // fp32 passes borrow the rigorous arrays
+  float* cB = reinterpret_cast<float*>(S.cf[1]);
+  const float b1c = 0.9f, b2c = 0.999f;
+  float p1 = 1.f, p2 = 1.f, dk = 1.f;
+  for (int it = 0; it < a.iters; ++it) {
+    const float kA = bwd<float, false, true, WTL>(nd, Wf, Wt, S, 0, tc, cur, cur + 2 * NH, -1, 0, cA, nullptr,
+                                                  nullptr);
+    const float kB = bwd<float, false, true, WTL>(nd, Wf, Wt, S, 1, -(1.f - tc), cur + NH, cur + 3 * NH, -1, 0, cB,
+                                                  nullptr, nullptr);
+    const float Bv = conc<float, false>(nd, S, N, cA, cB, kA, kB, 0.f);
+    if (Bv > best) {
+      best = Bv;
+      tbest = tc;
+      for (int l = 0; l < L - 1; ++l)
+        for (int j = lane; j < nd.dims[l + 1]; j += 64)
+          for (int q = 0; q < 4; ++q) par[q * NH + nd.neuron_off[l] + j] = cur[q * NH + nd.neuron_off[l] + j];
+    }
+    if (best > 0.f) break;
+    const float oA = fwd<float>(nd, Wf, S, N, 0, N.va, cur);
+    const float oB = fwd<float>(nd, Wf, S, N, 1, N.vb, cur + NH);
+    // Adam (bias-corrected), gradient ascent, projected
+    p1 *= b1c;
+    p2 *= b2c;
+    const float c1 = 1.f - p1, c2 = 1.f - p2;
+    for (int c = 0; c < 2; ++c)
+      for (int l = 0; l < L - 1; ++l)
+      for (int j = lane; j < nd.dims[l + 1]; j += 64) {
+        const int k = nd.neuron_off[l] + j;
+        const float z = S.z[c][k];
+        const int kind = S.kd[c][k];
+        const int p = S.ph[c][k];
+        // alpha
+        {
+          const float g = kind == 2 ? S.lam[c][k] * z : 0.f;
+          float* x = cur + c * NH + k;
+          float* m = mom + c * NH + k;
+          float* v = vel + c * NH + k;
+          const float mm = b1c * *m + (1.f - b1c) * g;
+          const float vv = b2c * *v + (1.f - b2c) * g * g;
+          *m = mm;
+          *v = vv;
+          *x = fminf(fmaxf(*x + a.lr_a * dk * (mm / c1) / (sqrtf(vv / c2) + 1e-8f), 0.f), 1.f);
+        }
+        // beta
+        {
+          float* x = cur + (2 + c) * NH + k;
+          float g = 0.f;
+          if (p != 0) {
+            const float e = *x < 0.f ? (p > 0 ? S.ub[c][k] : S.lb[c][k]) : 0.f;
+            g = -(float)p * (z - e);
+          }
+          float* m = mom + (2 + c) * NH + k;
+          float* v = vel + (2 + c) * NH + k;
+          const float mm = b1c * *m + (1.f - b1c) * g;
+          const float vv = b2c * *v + (1.f - b2c) * g * g;
+          *m = mm;
+          *v = vv;
+          float nx = *x + a.lr_b * dk * (mm / c1) / (sqrtf(vv / c2) + 1e-8f);
+          if (a.beta_pos) nx = fmaxf(nx, 0.f);
+          *x = nx;
+        }
+      }
+    {
+      const float g = oA + oB;
+      mt = b1c * mt + (1.f - b1c) * g;
+      vt = b2c * vt + (1.f - b2c) * g * g;
+      tc = fminf(fmaxf(tc + a.lr_t * dk * (mt / c1) / (sqrtf(vt / c2) + 1e-8f), 0.f), 1.f);
+    }
+    dk *= a.decay;
+    wsync();
+  }
+  if (lane == 0) a.t[r] = a.iters > 0 ? tbest : tc;
+  const float tf = a.iters > 0 ? tbest : tc;
+
+  // ---- rigorous fp64 bound at the kept parameters
+  double eA = 0, eB = 0;
+  const double kA = bwd<double, true, true, WTL>(nd, Wf, Wt, S, 0, (double)tf, par, par + 2 * NH, -1, 0, S.cf[0],
+                                                 &eA, nullptr);
+  const double kB = bwd<double, true, true, WTL>(nd, Wf, Wt, S, 1, -(1.0 - (double)tf), par + NH, par + 3 * NH, -1,
+                                                 0, S.cf[1], &eB, nullptr);
+  const double Bd = conc<double, true>(nd, S, N, S.cf[0], S.cf[1], kA, kB, eA + eB);
+  (void)fwd<double>(nd, Wf, S, N, 0, N.va, par);
+  (void)fwd<double>(nd, Wf, S, N, 1, N.vb, par + NH);
+
+  // ---- branching scores: |lam| x relaxation gap at x* of unfixed unstable neurons
+  for (int c = 0; c < 2; ++c)
+    for (int k = lane; k < NH; k += 64) {
+      const int kind = S.kd[c][k];
+      float s = 0.f;
+      if (kind >= 2 && S.ph[c][k] == 0) {
+        const float z = S.z[c][k];
+        const float rz = fmaxf(z, 0.f);
+        float gap;
+        if (kind == 2) gap = rz - par[c * NH + k] * z;
+        else {
+          const float lbj = S.lb[c][k], ubj = S.ub[c][k];
+          gap = ubj / (ubj - lbj) * (z - lbj) - rz;
+        }
+        s = fabsf(S.lam[c][k]) * fabsf(gap);
+      }
+      S.sc[c * NH + k] = s;
+    }
+  wsync();
+  int j0;
+  float mx;
+  {
+    float v = -1.f;
+    int iv = 0x7fffffff;
+    for (int k = lane; k < 2 * NH; k += 64)
+      if (S.sc[k] > v) {
+        v = S.sc[k];
+        iv = k;
+      }
+    mx = wargmax(v, iv, &j0);
+  }
+  int jsel = j0;
+  if (a.lookahead > 0 && mx > 0.f) {
+    // filtered look-ahead: top-K by gap score, then top-K by chord intercept; each candidate's two
+    // children are bounded at this node's parameters (new multiplier 0), the best worse child wins
+    const int K = a.lookahead < 16 ? a.lookahead : 16;
+    int nc = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass == 1) {
+        for (int c = 0; c < 2; ++c)
+          for (int k = lane; k < NH; k += 64) {
+            float s = 0.f;
+            if (S.kd[c][k] == 3 && S.ph[c][k] == 0) {
+              const float lbj = S.lb[c][k], ubj = S.ub[c][k];
+              s = fabsf(S.lam[c][k] * ubj / (ubj - lbj) * lbj);
+            }
+            S.sc[c * NH + k] = s;
+          }
+        wsync();
+      }
+      for (int q = 0; q < K; ++q) {
+        float v = -1.f;
+        int iv = 0x7fffffff;
+        for (int k = lane; k < 2 * NH; k += 64)
+          if (S.sc[k] > v) {
+            v = S.sc[k];
+            iv = k;
+          }
+        int jq;
+        const float vq = wargmax(v, iv, &jq);
+        if (!(vq > 0.f)) break;
+        if (lane == 0) {
+          cand[nc] = jq;
+          S.sc[jq] = -1.f;
+        }
+        ++nc;
+        wsync();
+      }
+    }
+    float bw = -FLT_MAX;
+    int bj = -1;
+    float* cA32 = S.cft;
+    for (int q = 0; q < nc; ++q) {
+      const int jq = cand[q];
+      const int c = jq >= NH ? 1 : 0;
+      const int k = jq - c * NH;
+      float worst = FLT_MAX;
+      for (int sg = -1; sg <= 1; sg += 2) {
+        int inf = 0;
+        const float kc = bwd<float, false, false, WTL>(nd, Wf, Wt, S, c, c == 0 ? tf : -(1.f - tf), par + c * NH,
+                                                       par + (2 + c) * NH, k, sg, cA32, nullptr, &inf);
+        float part = 0.f;
+        for (int i = lane; i < n0; i += 64) {
+          const float other = (float)S.cf[1 - c][i];
+          if ((N.pamask >> i) & 1ull) {
+            const int qq = __popcll(N.pamask & ((1ull << i) - 1ull));
+            part += cA32[i] * (c == 0 ? N.va[qq] : N.vb[qq]) + other * (c == 0 ? N.vb[qq] : N.va[qq]);
+          } else {
+            const float cf = cA32[i] + other;
+            part += cf * (cf >= 0.f ? N.lo[i] : N.hi[i]);
+          }
+        }
+        float Bc = wsum(part) + kc + (float)(c == 0 ? kB : kA);
+        if (inf) Bc = FLT_MAX;
+        worst = fminf(worst, Bc);
+        wsync();
+      }
+      if (worst > bw) {
+        bw = worst;
+        bj = jq;
+      }
+    }
+    if (bj >= 0) jsel = bj;
+  }
+  // ---- outputs
+  if (lane == 0) {
+    a.bound[r] = Bd;
+    float b_in = 0.f, b_ac = 0.f;
+    int sp;
+    if (mx > 0.f) {
+      sp = jsel;
+      const int c = jsel >= NH ? 1 : 0;
+      const int k = jsel - c * NH;
+      const float lam = S.lam[c][k];
+      const int kind = S.kd[c][k];
+      float slope = 0.f;
+      if (kind == 2) slope = par[c * NH + k];
+      else if (kind == 3) slope = S.ub[c][k] / (S.ub[c][k] - S.lb[c][k]);
+      b_in = lam * slope;
+      b_ac = lam * (1.f - slope);
+    } else {
+      // input split: |coefficient| x width over the non-PA dims; none left: a lattice leaf
+      float bv = -1.f;
+      int bd = -1;
+      for (int i = 0; i < n0; ++i) {
+        if ((N.pamask >> i) & 1ull) continue;
+        const float wd = N.hi[i] - N.lo[i];
+        if (!(wd > 0.f)) continue;
+        const float s = (float)fabs(S.cf[0][i] + S.cf[1][i]) * wd + 1e-9f * wd;
+        if (s > bv) {
+          bv = s;
+          bd = i;
+        }
+      }
+      sp = bd >= 0 ? -1 - bd : -(n0 + 1);
+    }
+    a.split[r] = sp;
+    a.binit[2 * r] = b_in;
+    a.binit[2 * r + 1] = b_ac;
+  }
+  for (int i = lane; i < n0; i += 64) a.xstar[(size_t)r * n0 + i] = S.xs[i];
+}
+
+FA_LDS_REGISTER(FA_LDS_K(fa_beta_kernel<true>), FA_LDS_K(fa_beta_kernel<false>));
+
+}  // namespace
+
+extern "C" size_t fa_beta_slab_floats(const NetDesc& nd) {
+  const int NHp = (nd.n_hidden + 3) & ~3;
+  const int n0p = (nd.dims[0] + 3) & ~3;
+  const int mwp = (nd.max_width + 3) & ~3;
+  return (size_t)(11 * NHp + 4 * mwp + 10 * n0p + 32);
+}
+
+// Launch configuration: waves per workgroup and whether the transposed weights fit in LDS next to
+// the forward copy, chosen for two workgroups per CU (<= 80 KB) when possible.  Returns 0 on
+// success, -1 when the network cannot run here (inputs > 64, no hidden layer, too many PA dims,
+// the weights alone over the LDS budget).
+extern "C" int fa_beta_config(const NetDesc& nd, int* wpb, int* wtl, size_t* bytes) {
+  if (nd.dims[0] > 64 || nd.n_layers < 2 || nd.n_hidden <= 0) return -1;
+  const int L = nd.n_layers;
+  const size_t tot = (size_t)nd.b_off[L - 1] + nd.dims[L];
+  const size_t tot4 = (tot + 3) & ~(size_t)3;
+  const size_t slab = fa_beta_slab_floats(nd) * 4;
+  const size_t caps[2] = {80 * 1024, 160 * 1024 - 1024};
+  for (size_t cap : caps)
+    for (int w : {8, 4, 2, 1})
+      for (int t : {1, 0}) {
+        const size_t b = tot4 * 4 * (t ? 2 : 1) + w * slab;
+        if (b <= cap) {
+          *wpb = w;
+          *wtl = t;
+          *bytes = b;
+          return 0;
+        }
+      }
+  return -1;
+}
+
+extern "C" int fa_beta_launch(const NetDesc& nd, BetaArgs a, hipStream_t stream) {
+  if (a.R <= 0) return 0;
+  int wpb = 0, wtl = 0;
+  size_t bytes = 0;
+  if (fa_beta_config(nd, &wpb, &wtl, &bytes) != 0) return -1;
+  if (!fa_lds_ok(bytes)) return -2;
+  a.wpb = wpb;
+  a.wt_lds = wtl;
+  const dim3 grid((a.R + wpb - 1) / wpb);
+  const dim3 block(64 * wpb);
+  if (wtl)
+    hipLaunchKernelGGL(fa_beta_kernel<true>, grid, block, bytes, stream, nd, a);
+  else
+    hipLaunchKernelGGL(fa_beta_kernel<false>, grid, block, bytes, stream, nd, a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

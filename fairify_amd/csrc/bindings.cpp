@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include <cmath>
+#include <cstring>
 #include <cstdint>
 #include <stdexcept>
 #include <vector>
@@ -38,6 +39,8 @@ extern "C" int fa_agree_launch(const NetDesc& net, const float* flat, int Pm, co
 extern "C" int fa_decode_launch(const DecodeDesc& d, const int64_t* ids, int P, const float* chunk_lo,
                                 const float* chunk_hi, float* lo, float* hi, hipStream_t stream);
 extern "C" int fa_trace_marker_launch(int tag, int* sink, hipStream_t stream);
+extern "C" int fa_beta_launch(const NetDesc& nd, BetaArgs a, hipStream_t stream);
+extern "C" int fa_beta_config(const NetDesc& nd, int* wpb, int* wtl, size_t* bytes);
 extern "C" int fa_knn_launch(const float* X, int n, int d, int k, int* idx, float* dist, hipStream_t stream);
 extern "C" int fa_actdiff_launch(const NetDesc& net, const float* flat, const float* x, const float* xp, int npairs,
                                  float* sum_out, hipStream_t stream);
@@ -499,6 +502,53 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("trace_marker", [](int tag, uintptr_t sink, uintptr_t stream) {
     check(fa_trace_marker_launch(tag, P<int>(sink), (hipStream_t)stream), "trace_marker");
+  });
+  m.def("beta_level", [](const Net& net, uintptr_t flat, uintptr_t wt, int R, std::vector<int> pa, uintptr_t lo,
+                         uintptr_t hi, uintptr_t va, uintptr_t vb, uintptr_t LBA, uintptr_t UBA, uintptr_t LBB,
+                         uintptr_t UBB, uintptr_t phA, uintptr_t phB, uintptr_t par, uintptr_t t, uintptr_t scratch,
+                         int iters, float lr_a, float lr_b, float lr_t, float decay, int lookahead, int beta_pos,
+                         uintptr_t bound, uintptr_t split, uintptr_t xstar, uintptr_t binit, uintptr_t stream) {
+    if (pa.size() > FA_MAX_PA) throw std::invalid_argument("beta_level: too many PA dims");
+    for (size_t q = 0; q < pa.size(); ++q)
+      if (pa[q] < 0 || pa[q] >= net.d.dims[0] || (q && pa[q] <= pa[q - 1]))
+        throw std::invalid_argument("beta_level: PA dims must be increasing input indices");
+    BetaArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.flat = P<const float>(flat);
+    a.wt = P<const float>(wt);
+    a.R = R;
+    a.npa = (int)pa.size();
+    for (size_t q = 0; q < pa.size(); ++q) a.pa_idx[q] = pa[q];
+    a.lo = P<const float>(lo);
+    a.hi = P<const float>(hi);
+    a.va = P<const float>(va);
+    a.vb = P<const float>(vb);
+    a.LBA = P<const float>(LBA);
+    a.UBA = P<const float>(UBA);
+    a.LBB = P<const float>(LBB);
+    a.UBB = P<const float>(UBB);
+    a.phA = P<const int8_t>(phA);
+    a.phB = P<const int8_t>(phB);
+    a.par = P<float>(par);
+    a.t = P<float>(t);
+    a.scratch = P<float>(scratch);
+    a.iters = iters;
+    a.lr_a = lr_a;
+    a.lr_b = lr_b;
+    a.lr_t = lr_t;
+    a.decay = decay;
+    a.lookahead = lookahead;
+    a.beta_pos = beta_pos;
+    a.bound = P<double>(bound);
+    a.split = P<int>(split);
+    a.xstar = P<float>(xstar);
+    a.binit = P<float>(binit);
+    return fa_beta_launch(net.d, a, reinterpret_cast<hipStream_t>(stream));
+  });
+  m.def("beta_fits", [](const Net& net) {
+    int w = 0, t = 0;
+    size_t b = 0;
+    return fa_beta_config(net.d, &w, &t, &b) == 0;
   });
   m.def("arch", []() { return std::string("gfx950"); });
   // raise the dynamic-LDS limit of every registered kernel once (common.h); Backend construction

@@ -220,7 +220,9 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
           // phase-fixed neurons too: a refined bound that contradicts the phase proves the node's
           // region empty (a.infeas)
           const bool fixed = a.phase_in && a.phase_in[(size_t)(rb + g) * NH + offk + j] != 0;
-          take = ((lb < 0.f && ub > 0.f) || fixed) && !(dm && dm[offk + j]);
+          // a dead-masked neuron outputs 0 whatever its bounds: REFINE skips it; FULL still bounds it
+          // (its slab entries start at -inf / +inf and are written back like every other neuron's)
+          take = ((lb < 0.f && ub > 0.f) || fixed) && !(dm && dm[offk + j] && !cfg.full);
         }
         if (take) list[atomicAdd(&rrun[G], 1)] = e;
       }

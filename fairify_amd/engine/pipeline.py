@@ -121,6 +121,13 @@ class VerifyConfig:
                                          # (profiles/r3/shard/diag_models_bench_config.jsonl: 38 % of a
                                          # bench step's nodes were AC-8 / AC-12 escalation spent on
                                          # partitions the relu stage then decided)
+    beta_budget: int = int(os.environ.get("FAIRIFY_BETA_BUDGET", "512"))
+                                         # beta-CROWN phase-split BaB (stage "beta", engine/beta_bab.py)
+                                         # on the residue: nodes per partition (0 = off); the anytime
+                                         # rounds grow it x anytime_growth per round
+    beta_min_width: int = 17             # ... on networks whose widest hidden layer is at least this
+                                         # (the narrower ones go to the relu stage, whose exact-zero
+                                         # concretisation their zero logits need)
     lp_budget: int = 4096                # verified-LP branch-and-bound (stage "lp", smt/lpbab.py) in
                                          # place of the untrusted MILP: LP nodes per partition (x growth
                                          # per anytime round); 0 = the round-2 MILP stage
@@ -255,6 +262,26 @@ def _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, limit, worke
         stage[hit] = "milp"
 
 
+def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes, status, stage, cex_x, cex_xp, nodes,
+                tm=None):
+    """beta-CROWN BaB (engine/beta_bab.py) on the partitions ``unk``: decided verdicts (sound SAT /
+    UNSAT) written into the stage arrays; returns how many it decided."""
+    from .beta_bab import BetaBaBSolver, BetaConfig
+
+    bs = BetaBaBSolver(be, q, BetaConfig(node_budget=budget, batch_nodes=min(batch_nodes, 32768),
+                                         time_budget=time_budget), **({"timer": tm} if tm is not None else {}))
+    br = bs.solve(lo_np[unk], hi_np[unk], mlp)
+    dec = np.isin(br.status, (SAT, UNSAT))
+    hit = unk[dec]
+    status[hit] = br.status[dec]
+    stage[hit] = "beta"
+    sb = br.status == SAT
+    cex_x[unk[sb]] = br.cex_x[sb]
+    cex_xp[unk[sb]] = br.cex_xp[sb]
+    nodes[unk] += br.nodes
+    return int(dec.sum())
+
+
 def _lp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, budget, limit, workers, status, stage, cex_x,
               cex_xp, deadline=None):
     """Verified-LP branch-and-bound (smt/lpbab.py) on the partitions ``unk``: HiGHS solves, a
@@ -277,7 +304,14 @@ def _lp_collect(mlp, pending, budget, status, stage, cex_x, cex_xp):
     """Wait for the LP searches of :func:`_lp_submit`; a partition another stage decided meanwhile
     keeps that verdict (both are sound)."""
     t_note = time.time()
+    # searches of partitions another stage decided meanwhile: not started ones are dropped, so the
+    # shared worker pool is not kept busy for nothing (running ones finish and are ignored)
+    for k, f in pending:
+        if status[k] != UNKNOWN:
+            f.cancel()
     for i, (k, f) in enumerate(pending):
+        if f.cancelled():
+            continue
         verdict, pair, _ = f.result()
         if _VERBOSE_ANYTIME and time.time() - t_note > 30.0:
             t_note = time.time()
@@ -564,6 +598,21 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             nodes[unk] += rres.nodes
             sync()
             t_bab += time.time() - t0
+    # ---------------- stage 3b': beta-CROWN phase-split BaB on the residue (the wide nets' UNSAT
+    # partitions need phase splits as constraints on the region: Lagrangian split multipliers)
+    from .beta_bab import supported as _beta_supported
+
+    beta_on = cfg.beta_budget > 0 and _beta_supported(q) and max(mlp.hidden or [0]) >= cfg.beta_min_width
+    if beta_on:
+        unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+        if unk.size:
+            t0 = time.time()
+            el = time.time() - t_start
+            with tm("beta"):
+                _beta_round(be, q, mlp, unk, lo_np, hi_np, cfg.beta_budget, max(0.0, budget - el), cfg.batch_nodes,
+                            status, stage, cex_x, cex_xp, nodes, tm)
+            sync()
+            t_bab += time.time() - t0
     if esc_after_relu:
         escalate()
 
@@ -632,12 +681,30 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         relu_any = _relu_supported(q)
         r_budget = max(cfg.relu_budget, 1) if relu_on else 64      # x growth before the first round
         bab_live, relu_live = True, True                          # stages still yielding
+        beta_any = cfg.beta_budget > 0 and _beta_supported(q)      # any width in the anytime rounds
+        beta_live = beta_any
+        b_budget = max(cfg.beta_budget, 1) // cfg.anytime_growth if not beta_on else cfg.beta_budget
         with tm("anytime"):
             while True:
                 unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
                 if not unk.size or time.time() >= deadline:
                     break
                 anytime_rounds += 1
+                # (b) beta-CROWN phase-split BaB with a growing budget first: it closes the wide nets'
+                # UNSAT residue on the GPU in a few dozen nodes per partition, before the host LP
+                # is handed what is left
+                if beta_any and beta_live:
+                    b_budget *= cfg.anytime_growth
+                    left = deadline - time.time()
+                    if left > 0:
+                        with tm("beta"):
+                            ndec = _beta_round(be, q, mlp, unk, lo_np, hi_np, b_budget, left, cfg.batch_nodes, status,
+                                               stage, cex_x, cex_xp, nodes, tm)
+                        if ndec < cfg.anytime_min_yield * unk.size:
+                            beta_live = False
+                    unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+                    if not unk.size:
+                        break
                 # (e, started first) verified-LP branch-and-bound on the host workers with a growing
                 # node budget, CONCURRENT with this round's GPU stages (collected at the round's end):
                 # on a residue the GPU stages do not converge on (trained AC-7) the round costs
@@ -670,7 +737,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                 e_budget *= cfg.anytime_growth
                 if e_budget > cfg.anytime_max_budget:
                     bab_live = False
-                if not (bab_live or (relu_any and cfg.relu_budget > 0 and relu_live) or use_milp):
+                if not (bab_live or (relu_any and cfg.relu_budget > 0 and relu_live) or use_milp or beta_live):
                     break                                       # nothing left that can still decide
                 unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
                 if _VERBOSE_ANYTIME:

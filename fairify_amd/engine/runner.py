@@ -291,6 +291,10 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         raise ValueError(f"balance must be 'queue' or 'strided', got {balance!r}")
     queue = balance == "queue" and info.world > 1
     claim = _claim_fn(info) if queue else None
+    # per-invocation nonce of the unit-queue keys: every rank counts its own run_preset calls in the
+    # store (SPMD: the same count on every rank), so a second call with the same preset / model /
+    # seed gets fresh counters instead of an exhausted one
+    run_id = claim(f"fairify/runs/{info.rank}") if queue else 0
     grid = preset.grid(seed=seed)
     q = preset.resolved()
     order = processing_order(grid, seed=seed)
@@ -336,13 +340,17 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         rank_work = [0.0, 0]  # this rank's BaB node expansions and partitions (balance report)
 
         def flush(item):
-            handle, rpos, retried = item
+            handle, rpos, retried, expect = item
             bufs = handle.wait()
             if not info.is_main:
                 return
             if rpos is None:        # unit queue: every rank's buffer carries its claimed positions
                 split = [_unpack_positions(b) for b in bufs]
                 rpos, bufs = [p for p, _ in split], [b for _, b in split]
+                got = np.sort(np.concatenate(rpos)) if rpos else np.zeros(0, np.int64)
+                if got.size != expect.size or not np.array_equal(got, np.sort(expect)):
+                    raise RuntimeError(f"unit queue: ranks verified {got.size} positions of a round block of "
+                                       f"{expect.size} (stale or shared queue key)")
             parts = [(p, wire.decode(b, order[p], acc, mlp.n_neurons, cfg.sim_size, q)) for p, b in zip(rpos, bufs)]
             gpos, grecs = wire.merge_rounds(parts)
             if grecs is None:
@@ -389,7 +397,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             if queue:
                 U = queue_unit_size(len(rblock), info.world, streams.workers, cfg.chunk)
                 n_units = -(-len(rblock) // U)
-                key = f"fairify/units/{preset.name}/{name}/{seed}/{r}"
+                key = f"fairify/units/{run_id}/{preset.name}/{name}/{seed}/{r}"
 
                 def worker(_):
                     done_units = []
@@ -428,7 +436,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             handle = D.gather_bytes(info, buf, async_op=True)
             if inflight is not None:
                 flush(inflight)
-            inflight = (handle, rpos, retried)
+            inflight = (handle, rpos, retried, rblock)
             if faults.crash_after() >= 0:          # fault injection: crash only after a checkpoint
                 flush(inflight)
                 inflight = None

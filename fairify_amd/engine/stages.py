@@ -10,6 +10,8 @@ Verdict / stage combinations:
   confirmed exactly on the ORIGINAL network (pair constraints + rigorous fp64 / rational logits).
 * ``bab`` UNSAT: every node of the partition closed by a rigorous input-split certificate.
 * ``relu`` UNSAT: closed by the ReLU phase-split search (engine/relu_bab.py), rigorous bounds.
+* ``beta`` UNSAT: closed by the beta-CROWN phase-split search (engine/beta_bab.py): every node's
+  Lagrangian bound re-evaluated in fp64 with rigorous rounding terms; SAT: a confirmed pair.
 * ``smt`` UNSAT: Z3 (exact rational arithmetic), when installed.
 * ``lp`` UNSAT: verified-LP branch-and-bound (smt/lpbab.py): HiGHS LP relaxations, every closed
   node certified by a rigorously evaluated weak-duality bound from the solver's multipliers;
@@ -24,11 +26,11 @@ Verdict / stage combinations:
 """
 from __future__ import annotations
 
-STAGES = ("", "sim", "bab", "heuristic", "smt", "falsify", "milp", "heuristic-confirmed", "relu", "lp")
+STAGES = ("", "sim", "bab", "heuristic", "smt", "falsify", "milp", "heuristic-confirmed", "relu", "lp", "beta")
 CODE = {s: k for k, s in enumerate(STAGES)}
 
-SOUND_SAT = frozenset({"sim", "bab", "falsify", "smt", "milp", "heuristic-confirmed", "relu", "lp", ""})
-SOUND_UNSAT = frozenset({"bab", "smt", "relu", "lp", ""})
+SOUND_SAT = frozenset({"sim", "bab", "falsify", "smt", "milp", "heuristic-confirmed", "relu", "lp", "beta", ""})
+SOUND_UNSAT = frozenset({"bab", "smt", "relu", "lp", "beta", ""})
 UNSOUND_UNSAT = frozenset({"heuristic", "milp"})
 
 

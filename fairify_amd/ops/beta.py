@@ -1,0 +1,344 @@
+"""Beta-CROWN bounds of ReLU-phase branch-and-bound nodes (stage ``beta``; csrc/beta.hip).
+
+The reference decides a partition with Z3, whose simplex case-splits every ReLU
+``If(z >= 0, z, 0)`` (utils/verif_utils.py:525-528, solved at src/AC/Verify-AC.py:146-158): inside
+a case split the phase is a LINEAR CONSTRAINT on the input region.  The round-4 GPU ReLU-phase
+stage (engine/relu_bab.py) only clamped intervals with the phases and closed none of trained
+AC-7's residue; the verified host LP (smt/lpbab.py) closed it, slowly, because its phase splits
+are constraints.  This module bounds a node the way that LP does, by Lagrangian duality, on the
+GPU:
+
+* node = (input box, ordered PA pair (va, vb), phase in {-1, 0, +1} of every hidden neuron of the
+  copies N(., va) and N(., vb)); both copies read the same x on the non-PA dims;
+* violation needs N(x, va) < 0 < N(x, vb), so for any t in [0, 1]
+  ``f_t(x) = t N(x, va) - (1 - t) N(x, vb) < 0``; a lower bound of f_t >= 0 over the node's
+  region closes the node;
+* the lower bound is a backward (CROWN) pass per copy with free lower slopes ``alpha`` in [0, 1]
+  for unstable neurons, the chord as upper relaxation, fixed phases exact (active: identity,
+  inactive: 0) and, for every fixed neuron, the Lagrangian term ``- beta_j s_j z_j`` (s_j z_j >= 0
+  on the region: beta >= 0 uses the phase constraint; beta < 0 the neuron's interval side,
+  ``- beta_j s_j z_j <= - beta_j s_j e_j`` with e = ub (active) / lb (inactive)) -- the split
+  constraint acts on the whole region, not only on the neuron's interval.  A child's new multiplier
+  starts where the parent's relaxation of that neuron is reproduced exactly (``binit``), so warm
+  starts never lose bound;
+* (alpha, beta, t) are optimised by projected Adam in fp32 (gradients in closed form: the bound is
+  the linearised network evaluated at the concretising vertex x*, so d/d alpha_j = lam_j z_j(x*),
+  d/d beta_j = -s_j (z_j(x*) - [beta_j < 0] e_j), d/dt = N_lin(x*, va) + N_lin(x*, vb)); children start from their
+  parent's values (warm start);
+* the bound that decides is re-evaluated in fp64 at the best parameters with rigorous rounding
+  terms (Higham gamma_k on every product and sum, chord slopes rounded up), so any parameter values
+  give a sound bound; intermediate (pre-activation) bounds are the rigorous fp32 bounds of the
+  node's partition (the same ones the verified LP uses), clamped by the phases;
+* branching: the unfixed unstable neuron (either copy) with the largest ``|lam_j| x`` relaxation
+  gap at x* (what fixing its phase recovers at the current optimum); with none, an input split on
+  the dim of largest |coefficient| x width; single lattice points are decided exactly.
+
+CPU prototype and measurements: tools/exp/beta_bab.py (trained AC-7 residue partitions that the LP
+closes in 40-5 000 nodes close here in ~9 per ordered pair).  This module is the reference
+semantics (CPU tests); ``level`` dispatches to the HIP kernel on the GPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import reference as ref
+
+U64 = ref.FP64_UNIT
+
+
+@dataclass
+class BetaLevel:
+    bound: torch.Tensor       # [R] float64 rigorous lower bound of f_t over the node region (+inf: empty)
+    split: torch.Tensor       # [R] int64: >= 0 neuron (copy A: j, copy B: NH + j); -1 - d: input dim d;
+    #                           -(n0 + 1): single lattice point (no split left)
+    xstar: torch.Tensor       # [R, n0] float32 concretising vertex (candidate pair's shared dims)
+    binit: torch.Tensor       # [R, 2] float32 beta of the split neuron in the (inactive, active) child
+    #                           that reproduces this node's relaxation of it (monotone warm start)
+
+
+def _layers(v: torch.Tensor, widths: Sequence[int]) -> List[torch.Tensor]:
+    out, o = [], 0
+    for w in widths:
+        out.append(v[:, o:o + w])
+        o += w
+    return out
+
+
+def _g(k: int) -> float:
+    return ref.gamma(k, U64)
+
+
+def _backward(ws, bs, LB, UB, ph, al, be, scale, hmax_in, rig: bool):
+    """One copy's backward pass for rows R, objective ``scale * logit``.  LB / UB / ph / al / be:
+    per hidden layer [R, w].  Returns (input coefficients [R, n0], constant [R], rounding error
+    [R] (rig only, else zeros), per-layer records (lam, kind, s) for the gradient / scores).
+    kind: 0 inactive, 1 active, 2 unstable with the alpha lower relaxation, 3 unstable chord."""
+    L = len(ws)
+    dt = scale.dtype
+    lam = scale[:, None] * ws[L - 1][:, 0][None]
+    c = scale * bs[L - 1][0]
+    err = torch.zeros_like(c)
+    if rig:
+        err = err + U64 * (lam.abs() * UB[L - 2].clamp(min=0)).sum(1) + U64 * c.abs()
+    rec = [None] * (L - 1)
+    for l in range(L - 2, -1, -1):
+        lb, ub, p = LB[l], UB[l], ph[l]
+        pf = p.to(dt)
+        dead = (ub <= 0) | (p < 0)
+        act = ((lb >= 0) | (p > 0)) & ~dead
+        un = ~(dead | act)
+        low = un & (lam >= 0)
+        upp = un & (lam < 0)
+        one = torch.ones_like(ub)
+        den = torch.where(un, ub - lb, one)
+        s = torch.where(un, ub / den, torch.zeros_like(ub))
+        if rig:
+            s = s * (1 + 4 * U64)              # rounded up: a steeper chord is still an upper bound
+        slope = torch.where(act, one, torch.where(low, al[l], torch.where(upp, s, torch.zeros_like(ub))))
+        base = lam * slope
+        kap = torch.where(upp, -base * lb, torch.zeros_like(ub))
+        bet = be[l]
+        mu = base - bet * pf
+        # a negative multiplier of a fixed neuron uses the interval side of its region instead:
+        # -beta s z <= -beta s e for s z in [0, s e] (e = ub active, lb inactive)
+        kb = torch.where((p != 0) & (bet < 0), bet * pf * torch.where(p > 0, ub, lb), torch.zeros_like(ub))
+        kap = kap + kb
+        zmax = torch.maximum(lb.abs(), ub.abs())
+        mb = mu * bs[l][None]
+        if rig:
+            e = torch.where(low, _g(1) * base.abs() * zmax, torch.zeros_like(ub))
+            e = e + torch.where(upp, 3 * U64 * (2 * base.abs() * zmax + kap.abs()), torch.zeros_like(ub))
+            e = e + torch.where(p != 0, _g(1) * (mu.abs() * zmax + kb.abs()), torch.zeros_like(ub))
+            w = lb.shape[1]
+            err = err + e.sum(1) + _g(2 * w + 1) * (c.abs() + mb.abs().sum(1) + kap.abs().sum(1))
+        c = c + mb.sum(1) + kap.sum(1)
+        kind = torch.where(dead, 0, torch.where(act, 1, torch.where(low, 2, 3)))
+        rec[l] = (lam, kind, s, slope)
+        W = ws[l]
+        lam = mu @ W.T
+        if rig:
+            hm = UB[l - 1].clamp(min=0) if l > 0 else hmax_in
+            err = err + (_g(W.shape[1]) * (mu.abs() @ W.abs().T) * hm).sum(1)
+    return lam, c, err, rec
+
+
+def _forward_lin(ws, bs, x, LB, rec, al):
+    """Pre-activations of the linearised network (each neuron's chosen relaxation) at x; logit."""
+    h = x
+    zs = []
+    for l in range(len(ws) - 1):
+        z = h @ ws[l] + bs[l][None]
+        zs.append(z)
+        lam, kind, s, _ = rec[l]
+        h = torch.where(kind == 1, z, torch.where(kind == 2, al[l] * z,
+                                                  torch.where(kind == 3, s * (z - LB[l]), torch.zeros_like(z))))
+    return zs, (h @ ws[-1] + bs[-1][None])[:, 0]
+
+
+def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t, rig: bool, need_lin: bool = True):
+    """The coupled bound of rows R at the given parameters (per-layer lists), in the dtype of
+    ``ws``.  ``rig``: fp64 with every rounding term subtracted (the sound bound).  Returns
+    (bound [R], grads dict, lin records, xstar, coef)."""
+    dt = ws[0].dtype
+    pa = list(pa)
+    free = torch.ones(lo.shape[1], dtype=torch.bool, device=lo.device)
+    free[pa] = False
+    hmA = torch.maximum(lo.abs(), hi.abs()).to(dt)
+    hmB = hmA.clone()
+    hmA[:, pa] = va.abs().to(dt)
+    hmB[:, pa] = vb.abs().to(dt)
+    cA, kA, eA, rA = _backward(ws, bs, bA[0], bA[1], phA, alA, beA, t, hmA, rig)
+    cB, kB, eB, rB = _backward(ws, bs, bB[0], bB[1], phB, alB, beB, -(1 - t), hmB, rig)
+    pA = cA[:, pa] * va.to(dt)
+    pB = cB[:, pa] * vb.to(dt)
+    coef = torch.where(free[None], cA + cB, torch.zeros_like(cA))
+    lo_, hi_ = lo.to(dt), hi.to(dt)
+    xs = torch.where(coef >= 0, lo_, hi_)
+    terms = coef * xs
+    B = terms.sum(1) + pA.sum(1) + pB.sum(1) + kA + kB
+    if rig:
+        n0 = lo.shape[1]
+        mag = terms.abs().sum(1) + pA.abs().sum(1) + pB.abs().sum(1) + kA.abs() + kB.abs()
+        econ = U64 * (coef.abs() * torch.maximum(lo_.abs(), hi_.abs())).sum(1) + _g(n0 + 4) * mag
+        B = B - (eA + eB + econ) * (1 + 1e-6)
+    if not need_lin:
+        return B, None, None, xs, coef
+    xa, xb = xs.clone(), xs.clone()
+    xa[:, pa] = va.to(dt)
+    xb[:, pa] = vb.to(dt)
+    zA, oA = _forward_lin(ws, bs, xa, bA[0], rA, alA)
+    zB, oB = _forward_lin(ws, bs, xb, bB[0], rB, alB)
+    g = {"t": oA + oB}
+    for nm, z, rec, ph, bet, bnd in (("A", zA, rA, phA, beA, bA), ("B", zB, rB, phB, beB, bB)):
+        g["al" + nm] = [torch.where(r[1] == 2, r[0] * zz, torch.zeros_like(zz)) for zz, r in zip(z, rec)]
+        g["be" + nm] = [torch.where(p == 0, torch.zeros_like(zz),
+                                    -p.to(dt) * (zz - torch.where(be_ < 0, torch.where(p > 0, ub, lb), torch.zeros_like(zz))))
+                        for zz, p, be_, lb, ub in zip(z, ph, bet, bnd[0], bnd[1])]
+    return B, g, ((zA, rA), (zB, rB)), xs, coef
+
+
+def _scores(bnd, lin, ph, al):
+    LB = bnd[0]
+    z, rec = lin
+    out = []
+    for l in range(len(z)):
+        lam, kind, s, _ = rec[l]
+        zz = z[l]
+        gap = torch.where(kind == 2, torch.relu(zz) - al[l] * zz,
+                          torch.where(kind == 3, s * (zz - LB[l]) - torch.relu(zz), torch.zeros_like(zz)))
+        out.append(torch.where((kind >= 2) & (ph[l] == 0), lam.abs() * gap.abs(), torch.zeros_like(zz)))
+    return torch.cat(out, 1)
+
+
+def _intercepts(bnd, lin, ph):
+    """BaBSR-style score: the constant the chord of an unfixed unstable neuron costs the bound."""
+    LB = bnd[0]
+    z, rec = lin
+    out = []
+    for l in range(len(z)):
+        lam, kind, s, _ = rec[l]
+        out.append(torch.where((kind == 3) & (ph[l] == 0), (lam * s * LB[l]).abs(), torch.zeros_like(lam)))
+    return torch.cat(out, 1)
+
+
+def _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, beA, beB, t, sc, lin,
+               K: int, j0):
+    """Filtered branching: the top-K neurons by relaxation-gap score and the top-K by chord intercept
+    are each tried -- both children bounded at the node's parameters with the new multiplier at 0
+    (one backward pass each) -- and the neuron whose worse child is best wins."""
+    R, NH = phA.shape
+    dev = lo.device
+    d = torch.float64
+    ic = torch.cat([_intercepts((_layers(lbA.to(d), widths), None), lin[0], _layers(phA, widths)),
+                    _intercepts((_layers(lbB.to(d), widths), None), lin[1], _layers(phB, widths))], 1)
+    k1 = min(K, sc.shape[1])
+    v1, c1 = sc.topk(k1, dim=1)
+    v2, c2 = ic.topk(k1, dim=1)
+    cand = torch.cat([c1, c2], 1)                                  # [R, 2K]
+    valid = torch.cat([v1 > 0, v2 > 0], 1)
+    C = cand.shape[1]
+    rows = torch.arange(R, device=dev).repeat_interleave(2 * C)
+    cc = cand.repeat_interleave(2, dim=1).reshape(-1)
+    sg = torch.tensor([-1, 1], dtype=torch.int8, device=dev).repeat(R * C)
+    pA2, pB2 = phA[rows].clone(), phB[rows].clone()
+    r_ = torch.arange(rows.numel(), device=dev)
+    ia = cc < NH
+    pA2[r_[ia], cc[ia]] = sg[ia]
+    pB2[r_[~ia], cc[~ia] - NH] = sg[~ia]
+    lA, uA, iA = clamp_bounds(lbA[rows], ubA[rows], pA2)
+    lB, uB, iB = clamp_bounds(lbB[rows], ubB[rows], pB2)
+    L = lambda v: _layers(v, widths)  # noqa: E731
+    Bc, _, _, _, _ = evaluate(ws32, bs32, lo[rows], hi[rows], pa, va[rows], vb[rows], (L(lA), L(uA)), (L(lB), L(uB)),
+                              L(pA2), L(pB2), L(alA[rows]), L(alB[rows]), L(beA[rows]), L(beB[rows]), t[rows],
+                              rig=False, need_lin=False)
+    Bc = torch.where(iA | iB, torch.full_like(Bc, float("inf")), Bc.float())
+    worst = Bc.reshape(R, C, 2).min(2).values
+    worst = torch.where(valid, worst, torch.full_like(worst, -float("inf")))
+    bw, bi = worst.max(1)
+    pick = cand.gather(1, bi[:, None])[:, 0]
+    return torch.where(torch.isfinite(bw) | (bw > 0), pick, j0)
+
+
+def clamp_bounds(LB: torch.Tensor, UB: torch.Tensor, ph: torch.Tensor):
+    """Phase-clamped pre-activation bounds [R, NH] and the rows whose region they prove empty."""
+    lb = torch.where(ph > 0, LB.clamp(min=0), LB)
+    ub = torch.where(ph < 0, UB.clamp(max=0), UB)
+    return lb, ub, (lb > ub).any(1)
+
+
+def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t,
+              iters: int, lr_a: float, lr_b: float, lr_t: float, decay: float = 1.0,
+              lookahead: int = 0, beta_pos: bool = True) -> BetaLevel:
+    """One BaB level of rows R (the HIP kernel's semantics, csrc/beta.hip): ``iters`` projected-Adam
+    steps in fp32 from the rows' current (alpha, beta, t) -- updated IN PLACE to the best iterate --
+    then the rigorous fp64 bound, the branching decision and x* at those parameters.
+
+    lo, hi [R, n0]; va, vb [R, npa]; LB*/UB* [R, NH] partition bounds (unclamped); ph* [R, NH] int8;
+    al*/be* [R, NH] float32; t [R] float32."""
+    R, n0 = lo.shape
+    dev = lo.device
+    lbA, ubA, infA = clamp_bounds(LBA, UBA, phA)
+    lbB, ubB, infB = clamp_bounds(LBB, UBB, phB)
+    infeas = infA | infB
+    L32 = lambda v: _layers(v, widths)  # noqa: E731
+    bA32, bB32 = (L32(lbA), L32(ubA)), (L32(lbB), L32(ubB))
+    pA, pB = L32(phA), L32(phB)
+    keys = ("alA", "alB", "beA", "beB")
+    par = {"alA": alA, "alB": alB, "beA": beA, "beB": beB}
+    best = torch.full((R,), -float("inf"), dtype=torch.float32, device=dev)
+    bestp = {k: v.clone() for k, v in par.items()}
+    best_t = t.clone()
+    cur = {k: v.clone() for k, v in par.items()}
+    ct = t.clone()
+    m = {k: torch.zeros_like(v) for k, v in par.items()}
+    vv = {k: torch.zeros_like(v) for k, v in par.items()}
+    mt = torch.zeros_like(t)
+    vt = torch.zeros_like(t)
+    b1, b2, eps = 0.9, 0.999, 1e-8
+    act = ~infeas
+    for it in range(iters):
+        B, g, _, _, _ = evaluate(ws32, bs32, lo, hi, pa, va, vb, bA32, bB32, pA, pB, L32(cur["alA"]), L32(cur["alB"]),
+                                 L32(cur["beA"]), L32(cur["beB"]), ct, rig=False)
+        imp = act & (B > best)
+        best = torch.where(imp, B, best)
+        for k in keys:
+            bestp[k] = torch.where(imp[:, None], cur[k], bestp[k])
+        best_t = torch.where(imp, ct, best_t)
+        act = act & ~(best > 0)
+        if not bool(act.any()):
+            break
+        c1 = 1 - b1 ** (it + 1)
+        c2 = 1 - b2 ** (it + 1)
+        dk = decay ** it
+        for k in keys:
+            gk = torch.cat(g[k], 1)
+            m[k] = b1 * m[k] + (1 - b1) * gk
+            vv[k] = b2 * vv[k] + (1 - b2) * gk * gk
+            lr = (lr_a if k.startswith("al") else lr_b) * dk
+            x = cur[k] + lr * (m[k] / c1) / ((vv[k] / c2).sqrt() + eps)
+            if k.startswith("al"):
+                x = x.clamp(0, 1)
+            elif beta_pos:
+                x = x.clamp(min=0)
+            cur[k] = torch.where(act[:, None], x, cur[k])
+        mt = b1 * mt + (1 - b1) * g["t"]
+        vt = b2 * vt + (1 - b2) * g["t"] * g["t"]
+        xt = (ct + lr_t * dk * (mt / c1) / ((vt / c2).sqrt() + eps)).clamp(0, 1)
+        ct = torch.where(act, xt, ct)
+    if iters == 0:
+        bestp = {k: v.clone() for k, v in par.items()}
+        best_t = t.clone()
+    for k in keys:
+        par[k].copy_(bestp[k])
+    t.copy_(best_t)
+    # rigorous fp64 evaluation at the kept parameters
+    d = torch.float64
+    ws64 = [w.to(d) for w in ws32]
+    bs64 = [b.to(d) for b in bs32]
+    L64 = lambda v: _layers(v.to(d), widths)  # noqa: E731
+    bA, bB = (L64(lbA), L64(ubA)), (L64(lbB), L64(ubB))
+    alA64, alB64 = L64(alA), L64(alB)
+    B, _, lin, xs, coef = evaluate(ws64, bs64, lo.to(d), hi.to(d), pa, va.to(d), vb.to(d), bA, bB, pA, pB, alA64,
+                                   alB64, L64(beA), L64(beB), t.to(d), rig=True)
+    B = torch.where(infeas, torch.full_like(B, float("inf")), B)
+    sc = torch.cat([_scores(bA, lin[0], pA, alA64), _scores(bB, lin[1], pB, alB64)], 1)
+    mx, j = sc.max(1)
+    if lookahead > 0:
+        j = _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, beA, beB, t,
+                       sc, lin, lookahead, j)
+    free = torch.ones(n0, dtype=torch.bool, device=dev)
+    free[list(pa)] = False
+    w = torch.where(free[None], (hi - lo).to(d), torch.zeros_like(coef))
+    isc = torch.where(w > 0, coef.abs() * w + 1e-9 * w, torch.full_like(w, -1.0))
+    im, dd = isc.max(1)
+    split = torch.where(mx > 0, j, torch.where(im > 0, -1 - dd, torch.full_like(dd, -(n0 + 1))))
+    # the split neuron's multipliers that make each child start from this node's relaxation of it
+    lam = torch.cat([torch.cat([r[0] for r in lin[0][1]], 1), torch.cat([r[0] for r in lin[1][1]], 1)], 1)
+    slope = torch.cat([torch.cat([r[3] for r in lin[0][1]], 1), torch.cat([r[3] for r in lin[1][1]], 1)], 1)
+    jj = j.clamp(min=0)[:, None]
+    lj, sj = lam.gather(1, jj)[:, 0], slope.gather(1, jj)[:, 0]
+    binit = torch.stack([lj * sj, lj * (1 - sj)], 1).to(torch.float32)
+    return BetaLevel(bound=B, split=split, xstar=xs.to(torch.float32), binit=binit)

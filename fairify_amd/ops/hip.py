@@ -318,7 +318,9 @@ def backward_bounds(be, lo: torch.Tensor, hi: torch.Tensor, dead: Optional[torch
         res.lay_lb_full, res.lay_ub_full = lay_lb, lay_ub
         Nh = be.n_hidden
         res.dead = lay_ub[:, :Nh] <= 0
-        res.active = lay_lb[:, :Nh] >= 0
+        if d is not None:
+            res.dead = res.dead | d.bool()
+        res.active = (lay_lb[:, :Nh] >= 0) & ~res.dead
     return res
 
 
@@ -593,3 +595,68 @@ def agree(be, rows: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor, pids: torc
                      pids_c.data_ptr(), dead_c.data_ptr(), int(n_samples), int(seed) & 0xFFFFFFFF, out.data_ptr(),
                      _stream(dev))
     return out if ok else None
+
+
+# ------------------------------------------------------------------------------------------------
+def _beta_wt(be) -> torch.Tensor:
+    """Per layer W_l transposed ([out][in] row-major) at the flat offsets of W_l (csrc/beta.hip's
+    backward-operand copy), cached on the backend."""
+    wt = getattr(be, "_beta_wt", None)
+    if wt is None:
+        import numpy as np
+
+        parts = []
+        for w, b in zip(be.mlp.weights, be.mlp.biases):
+            parts += [np.ascontiguousarray(np.asarray(w, np.float32).T).reshape(-1), np.zeros(np.size(b), np.float32)]
+        wt = torch.from_numpy(np.concatenate(parts)).to(be.device)
+        be._beta_wt = wt
+    return wt
+
+
+def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t, iters, lr_a, lr_b, lr_t,
+               decay=1.0, lookahead=0, beta_pos=True):
+    """One beta-CROWN BaB level on the device (``fa_beta_kernel``, csrc/beta.hip): the rows'
+    (alpha, beta, t) are optimised IN PLACE (kept at the best iterate) and their rigorous fp64
+    bounds, branching decisions, concretising vertices and child multipliers returned
+    (:class:`ops.beta.BetaLevel`)."""
+    from . import beta as B
+
+    R, n0 = lo.shape
+    NH = be.n_hidden
+    dev = lo.device
+    npa = len(pa)
+    if list(pa) != sorted(pa):
+        raise ValueError("beta_level: PA dims must be increasing")
+    f32 = dict(dtype=torch.float32, device=dev)
+    lo_c = _c(lo, torch.float32, (R, n0), "lo")
+    hi_c = _c(hi, torch.float32, (R, n0), "hi")
+    va_c = _c(va, torch.float32, (R, npa), "va")
+    vb_c = _c(vb, torch.float32, (R, npa), "vb")
+    bnd = [_c(x, torch.float32, (R, NH), nm) for x, nm in ((LBA, "LBA"), (UBA, "UBA"), (LBB, "LBB"), (UBB, "UBB"))]
+    pA = _c(phA, torch.int8, (R, NH), "phA")
+    pB = _c(phB, torch.int8, (R, NH), "phB")
+    for x, nm in ((alA, "alA"), (alB, "alB"), (beA, "beA"), (beB, "beB")):
+        if tuple(x.shape) != (R, NH) or x.dtype != torch.float32:
+            raise ValueError(f"{nm}: expected float32 [{R}, {NH}]")
+    if tuple(t.shape) != (R,) or t.dtype != torch.float32 or not t.is_contiguous():
+        raise ValueError("t: expected contiguous float32 [R]")
+    par = torch.stack([alA, alB, beA, beB], 1).contiguous()          # [R, 4, NH]
+    scratch = torch.empty(R, 12, NH, **f32)
+    bound = torch.empty(R, dtype=torch.float64, device=dev)
+    split = torch.empty(R, dtype=torch.int32, device=dev)
+    xstar = torch.empty(R, n0, **f32)
+    binit = torch.empty(R, 2, **f32)
+    if R:
+        rc = ext().beta_level(_net(be), be.flat.data_ptr(), _beta_wt(be).data_ptr(), R, [int(d) for d in pa],
+                              lo_c.data_ptr(), hi_c.data_ptr(), va_c.data_ptr(), vb_c.data_ptr(),
+                              *[x.data_ptr() for x in bnd], pA.data_ptr(), pB.data_ptr(), par.data_ptr(),
+                              t.data_ptr(), scratch.data_ptr(), int(iters), float(lr_a), float(lr_b), float(lr_t),
+                              float(decay), int(lookahead), int(bool(beta_pos)), bound.data_ptr(), split.data_ptr(),
+                              xstar.data_ptr(), binit.data_ptr(), _stream(dev))
+        if rc != 0:
+            raise RuntimeError(f"fa_beta_kernel launch failed ({rc}): network not supported by the beta kernel")
+        alA.copy_(par[:, 0])
+        alB.copy_(par[:, 1])
+        beA.copy_(par[:, 2])
+        beB.copy_(par[:, 3])
+    return B.BetaLevel(bound=bound, split=split.long(), xstar=xstar, binit=binit)

@@ -515,7 +515,9 @@ def backward_bounds(ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor], lo: 
     r.layer_ub = ubs + [r.out_ub[:, None]]
     if lbs:
         r.dead = torch.cat([u <= 0 for u in ubs], dim=1)
-        r.active = torch.cat([l >= 0 for l in lbs], dim=1)
+        if dead is not None:
+            r.dead = r.dead | dead.bool()       # forced-zero neurons are dead whatever their bounds
+        r.active = torch.cat([l >= 0 for l in lbs], dim=1) & ~r.dead
     return r
 
 

@@ -95,9 +95,10 @@ def _visible(n: int) -> List[int]:
     return idx
 
 
-def gpu_pci_addresses(sysfs: str = "/sys") -> List[str]:
+def gpu_pci_addresses(sysfs: str = "/sys", visible_only: bool = True) -> List[str]:
     """PCI addresses ("dddd:bb:dd.f") of the GPUs in KFD topology order (the order ROCr
-    enumerates them), restricted to the visible devices.  [] when the topology is unreadable."""
+    enumerates them), restricted to the visible devices (``visible_only``; else every GPU of
+    the node, indexed by physical id).  [] when the topology is unreadable."""
     base = os.path.join(sysfs, "class", "kfd", "kfd", "topology", "nodes")
     try:
         nodes = sorted((int(d) for d in os.listdir(base) if d.isdigit()))
@@ -114,12 +115,12 @@ def gpu_pci_addresses(sysfs: str = "/sys") -> List[str]:
             continue
         loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
         addrs.append(f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 0x7}")
-    return [addrs[k] for k in _visible(len(addrs))]
+    return [addrs[k] for k in _visible(len(addrs))] if visible_only else addrs
 
 
-def gpu_local_cpus(device_index: int, sysfs: str = "/sys") -> List[int]:
+def gpu_local_cpus(device_index: int, sysfs: str = "/sys", visible_only: bool = True) -> List[int]:
     """CPUs local to GPU ``device_index`` (its PCI device's ``local_cpulist``); [] if unknown."""
-    addrs = gpu_pci_addresses(sysfs)
+    addrs = gpu_pci_addresses(sysfs, visible_only)
     if not addrs:
         return []
     addr = addrs[device_index % len(addrs)]
@@ -151,7 +152,15 @@ def rank_cpuset(local_rank: int, local_world: int, cpus: Sequence[int] = None, s
         return list(cpus)
     if numa:
         allowed = set(cpus)
-        sets = [tuple(c for c in gpu_local_cpus(r, sysfs) if c in allowed) for r in range(local_world)]
+        # a launcher that gives each rank only its own GPU (HIP / ROCR_VISIBLE_DEVICES = one id)
+        # leaves fewer visible GPUs than local ranks: then local rank r is physical GPU r of the
+        # node's KFD topology (an index into the visible list would make every rank a peer of all
+        # the others); with fewer GPUs than ranks even there, the peers are unknown -> slices
+        vis = len(gpu_pci_addresses(sysfs)) >= local_world
+        if not vis and len(gpu_pci_addresses(sysfs, visible_only=False)) < local_world:
+            return _slice(cpus, local_rank, local_world)
+        sets = [tuple(c for c in gpu_local_cpus(r, sysfs, visible_only=vis) if c in allowed)
+                for r in range(local_world)]
         if all(sets):
             peers = [r for r in range(local_world) if sets[r] == sets[local_rank]]
             return _slice(sets[local_rank], peers.index(local_rank), len(peers))

@@ -525,24 +525,22 @@ def solve_partition(weights, biases, lo, hi, pa_idx, values, pairs, row_bounds, 
 _PPOOL = None
 _PPOOL_N = 0
 _PPOOL_LOCK = threading.Lock()
-_PPOOL_RETIRED: list = []
 
 
 def process_pool(workers: int):
     """Worker processes of the LP stage (spawned children: numpy / SciPy only, no GPU context).
     HiGHS through SciPy keeps the GIL, so threads do not scale (measured 1.2x on 4 threads).
 
-    Chunk threads (4-8 per rank) call this concurrently: creation happens under a lock, and a pool
-    replaced by a larger one is retired, never shut down while another thread may still submit to
-    it (its workers exit with the process)."""
+    Sized ONCE per process, by the first caller (the rank's configured worker count; chunk threads
+    call this concurrently, creation happens under a lock): a later request for more workers gets
+    the same pool, so no second pool ever oversubscribes the rank's pinned CPU slice and no pool
+    is replaced while another thread may still be submitting to it."""
     global _PPOOL, _PPOOL_N
     with _PPOOL_LOCK:
-        if _PPOOL is None or _PPOOL_N < workers:
+        if _PPOOL is None:
             import multiprocessing as mp
             from concurrent.futures import ProcessPoolExecutor
 
-            if _PPOOL is not None:
-                _PPOOL_RETIRED.append(_PPOOL)
             _PPOOL = ProcessPoolExecutor(max_workers=max(1, workers), mp_context=mp.get_context("spawn"))
             _PPOOL_N = workers
         return _PPOOL

@@ -50,6 +50,25 @@ def test_numa_local_slices(tmp_path, monkeypatch):
     assert BL.rank_cpuset(4, 8, list(range(8)) + list(range(16, 24)), sysfs=str(tmp_path)) == [16, 17]
 
 
+def test_numa_one_visible_gpu_per_rank(tmp_path, monkeypatch):
+    """Each rank sees only its own GPU (HIP_VISIBLE_DEVICES=<one id>): local rank r is physical GPU r,
+    so the 4 ranks of a socket split its CPUs 4 ways (not 8 ways as if every rank were a peer)."""
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    gpus = [(0, 0x10 + k, "0-15" if k < 4 else "16-31") for k in range(8)]
+    _fake_sysfs(str(tmp_path), gpus)
+    cpus = list(range(32))
+    sets = []
+    for r in range(8):
+        monkeypatch.setenv("HIP_VISIBLE_DEVICES", str(r))
+        sets.append(BL.rank_cpuset(r, 8, cpus, sysfs=str(tmp_path)))
+    assert sets[0] == [0, 1, 2, 3] and sets[5] == [20, 21, 22, 23]
+    assert sorted(c for s in sets for c in s) == cpus
+    # more local ranks than GPUs in the node: peers unknown -> contiguous slices
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert BL.rank_cpuset(9, 16, cpus, sysfs=str(tmp_path)) == [18, 19]
+
+
 def test_fallback_contiguous(tmp_path):
     # no KFD topology: the contiguous slices of the allowed CPUs
     cpus = list(range(16))

@@ -42,6 +42,16 @@ def test_self_launch_totals_match_one_rank():
         # per rank, so only the guarantee is asserted there
         assert dd["balance"] == "lpt" and dd["predicted_cost_ratio"] <= (
             min(dd["predicted_cost_bound"], 1.1) if n == 2 else dd["predicted_cost_bound"]), dd
+    # every key the bench docstring names is emitted
+    import re
+
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    doc = src.split('"""')[1]
+    para = doc.split("JSON keys")[1].split(":", 1)[1].split("\n\n")[0]
+    names = re.findall(r"[a-z_]+", para)
+    assert len(names) >= 20, names
+    missing = [k for k in names if k not in one]
+    assert not missing, missing
     # honest accounting fields add up
     assert one["unsat_sound"] + one["unsat_heuristic"] == one["unsat"]
     assert sum(one["sat_by_stage"].values()) == one["sat"]

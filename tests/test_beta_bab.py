@@ -1,0 +1,190 @@
+"""beta-CROWN ReLU-phase branch-and-bound (ops/beta.py, engine/beta_bab.py, stage "beta") on CPU:
+the rigorous bound against brute-force lattice enumeration on the phase regions, the monotone warm
+start of the children, verdicts against enumeration, and the trained AC-7 residue the round-4
+stages could not close (profiles/r4/lp_tree_sizes_ac7_trained.jsonl)."""
+import itertools
+
+import numpy as np
+import pytest
+import torch
+
+from fairify_amd import presets
+from fairify_amd.engine import exact
+from fairify_amd.engine.bab import SAT, UNKNOWN, UNSAT
+from fairify_amd.engine.beta_bab import BetaBaBSolver, BetaConfig
+from fairify_amd.models.mlp import random_mlp
+from fairify_amd.models.zoo import get_model
+from fairify_amd.ops import beta as B
+from fairify_amd.ops import reference as ref
+from fairify_amd.ops.backend import Backend
+from fairify_amd.partition import processing_order
+
+
+def _lattice(lo, hi):
+    return np.array(list(itertools.product(*[range(int(a), int(b) + 1) for a, b in zip(lo, hi)])), dtype=np.float64)
+
+
+def _setup(seed, widths=(6, 5, 4), n0=4, R=6, fix=0.3):
+    g = np.random.default_rng(seed)
+    m = random_mlp(n0, list(widths), seed=seed, bias_scale=0.5)
+    ws = [torch.tensor(np.asarray(w), dtype=torch.float32) for w in m.weights]
+    bs = [torch.tensor(np.asarray(b), dtype=torch.float32).reshape(-1) for b in m.biases]
+    pa = [1]
+    lo = np.tile(np.array([0, 0, 1, -2], np.float32)[:n0], (R, 1))
+    hi = lo + g.integers(1, 3, size=(R, n0)).astype(np.float32)
+    lo[:, pa] = 0
+    hi[:, pa] = 1
+    va = np.zeros((R, 1), np.float32)
+    vb = np.ones((R, 1), np.float32)
+    # partition bounds of each copy: the reference's rigorous symbolic bounds
+    be = Backend(m)
+    NH = be.n_hidden
+    out = []
+    for v in (va, vb):
+        rl, rh = lo.copy(), hi.copy()
+        rl[:, pa] = v
+        rh[:, pa] = v
+        res = be.bounds(torch.from_numpy(rl), torch.from_numpy(rh), keep_layers=True)
+        out.append((torch.cat(res.layer_lb, 1)[:, :NH].float(), torch.cat(res.layer_ub, 1)[:, :NH].float()))
+    ph = []
+    for c in range(2):
+        p = g.integers(-1, 2, size=(R, NH)) * (g.random((R, NH)) < fix)
+        ph.append(torch.from_numpy(p.astype(np.int8)))
+    return m, ws, bs, pa, torch.from_numpy(lo), torch.from_numpy(hi), torch.from_numpy(va), torch.from_numpy(vb), out, ph
+
+
+def _true_min(m, lo, hi, pa, va, vb, phA, phB, t, widths):
+    """min over lattice points of the box satisfying both copies' phases of t N(x,va) - (1-t) N(x,vb)
+    (exact enough in fp64 for these small integer boxes), or +inf when none does."""
+    X = _lattice(lo, hi)
+    ok = np.ones(len(X), bool)
+    outs = []
+    for v, ph in ((va, phA), (vb, phB)):
+        h = X.copy()
+        h[:, pa] = v
+        o = 0
+        for l, (W, b) in enumerate(zip(m.weights, m.biases)):
+            z = h @ np.asarray(W, np.float64) + np.asarray(b, np.float64)
+            if l < len(m.weights) - 1:
+                p = ph[o:o + z.shape[1]]
+                ok &= ((p[None] * z) >= 0).all(1)
+                o += z.shape[1]
+                h = np.maximum(z, 0)
+            else:
+                h = z
+        outs.append(h[:, 0])
+    f = t * outs[0] - (1 - t) * outs[1]
+    return f[ok].min() if ok.any() else np.inf
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+@pytest.mark.parametrize("neg_beta", [False, True])
+def test_rigorous_bound_below_every_phase_feasible_point(seed, neg_beta):
+    m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(seed)
+    R = lo.shape[0]
+    widths = [w.shape[1] for w in ws[:-1]]
+    NH = sum(widths)
+    g = torch.Generator().manual_seed(seed)
+    al = [torch.rand(R, NH, generator=g) for _ in range(2)]
+    be_ = [torch.rand(R, NH, generator=g) * (2 if neg_beta else 1) - (1 if neg_beta else 0) for _ in range(2)]
+    t = torch.rand(R, generator=g)
+    lev = B.level_ref(ws, bs, widths, lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1],
+                      al[0], al[1], be_[0], be_[1], t, iters=0, lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    for r in range(R):
+        tm = _true_min(m, lo[r].numpy(), hi[r].numpy(), pa, va[r].numpy(), vb[r].numpy(), ph[0][r].numpy(),
+                       ph[1][r].numpy(), float(t[r]), widths)
+        assert float(lev.bound[r]) <= tm, (r, float(lev.bound[r]), tm)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_optimised_bound_sound_and_not_worse(seed):
+    m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(seed, fix=0.15)
+    R = lo.shape[0]
+    widths = [w.shape[1] for w in ws[:-1]]
+    NH = sum(widths)
+    mk = lambda: ([torch.full((R, NH), 0.5) for _ in range(2)], [torch.zeros(R, NH) for _ in range(2)],  # noqa: E731
+                  torch.full((R,), 0.5))
+    al0, be0, t0 = mk()
+    l0 = B.level_ref(ws, bs, widths, lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1],
+                     al0[0], al0[1], be0[0], be0[1], t0, iters=0, lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    al1, be1, t1 = mk()
+    l1 = B.level_ref(ws, bs, widths, lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1],
+                     al1[0], al1[1], be1[0], be1[1], t1, iters=60, lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    fin = torch.isfinite(l0.bound)
+    assert bool((l1.bound[fin] >= l0.bound[fin] - 1e-5 * (1 + l0.bound[fin].abs())).all())
+    assert bool((l1.bound[fin] > l0.bound[fin] + 1e-3).any())          # the optimiser does something
+    for r in range(R):
+        tm = _true_min(m, lo[r].numpy(), hi[r].numpy(), pa, va[r].numpy(), vb[r].numpy(), ph[0][r].numpy(),
+                       ph[1][r].numpy(), float(t1[r]), widths)
+        assert float(l1.bound[r]) <= tm
+
+
+def test_children_start_at_parent_bound():
+    """binit reproduces the parent's relaxation of the split neuron: each child's bound at the
+    parent's parameters equals the parent's bound (warm starts never lose bound)."""
+    m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(5, fix=0.0)
+    R = lo.shape[0]
+    widths = [w.shape[1] for w in ws[:-1]]
+    NH = sum(widths)
+    al = [torch.full((R, NH), 0.5) for _ in range(2)]
+    be_ = [torch.zeros(R, NH) for _ in range(2)]
+    t = torch.full((R,), 0.5)
+    lev = B.level_ref(ws, bs, widths, lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1],
+                      al[0], al[1], be_[0], be_[1], t, iters=30, lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    nd = {"phA": ph[0], "phB": ph[1], "alA": al[0], "alB": al[1], "beA": be_[0], "beB": be_[1], "t": t,
+          "lo": lo, "hi": hi, "va": va, "vb": vb, "LBA": bnd[0][0], "UBA": bnd[0][1], "LBB": bnd[1][0],
+          "UBB": bnd[1][1], "part": torch.arange(R), "root": torch.ones(R, dtype=torch.bool)}
+    sel = torch.nonzero(lev.split >= 0).flatten()
+    assert sel.numel() > 0
+    kid = BetaBaBSolver._children({k: v[sel] for k, v in nd.items()}, lev.split[sel], lev.binit[sel], NH, lo.shape[1])
+    lk = B.level_ref(ws, bs, widths, kid["lo"], kid["hi"], pa, kid["va"], kid["vb"], kid["LBA"], kid["UBA"],
+                     kid["LBB"], kid["UBB"], kid["phA"], kid["phB"], kid["alA"], kid["alB"], kid["beA"], kid["beB"],
+                     kid["t"], iters=0, lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    par = lev.bound[sel].repeat_interleave(2)
+    fin = torch.isfinite(lk.bound)
+    # equal up to the fp32 rounding of the stored multiplier
+    assert bool((lk.bound[fin] >= par[fin] - 1e-6 * (1 + par[fin].abs())).all())
+
+
+def _brute_pair(m, lo, hi, pa):
+    X = _lattice(lo, hi)
+    a = X.copy()
+    b = X.copy()
+    a[:, pa] = 0
+    b[:, pa] = 1
+    z0, z1 = m.logits(a), m.logits(b)
+    return bool((((z0 > 0) & (z1 < 0)) | ((z0 < 0) & (z1 > 0))).any())
+
+
+@pytest.mark.parametrize("seed", [3, 6])
+def test_beta_bab_matches_bruteforce(seed):
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, 0)[:24]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 1)
+    m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
+    res = BetaBaBSolver(Backend(m), q, BetaConfig(node_budget=256, iters=20, root_iters=40)).solve(lo, hi, m)
+    pa = q.pa_idx[0]
+    assert (res.status != UNKNOWN).mean() > 0.5
+    for k in range(len(ids)):
+        if res.status[k] == UNKNOWN:
+            continue
+        assert (res.status[k] == SAT) == _brute_pair(m, lo[k], hi[k], pa), k
+    sat = np.nonzero(res.status == SAT)[0]
+    if sat.size:
+        assert exact.is_violation(m, res.cex_x[sat], res.cex_xp[sat]).all()
+
+
+@pytest.mark.slow
+def test_beta_closes_trained_ac7_residue():
+    """Trained AC-7 partitions the input-split and interval ReLU-phase stages leave open and the
+    verified LP needs 21-5 000 nodes for (profiles/r4/lp_tree_sizes_ac7_trained.jsonl): the beta
+    stage proves them within a few dozen nodes."""
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    m = get_model("AC-7", weights="zoo", seed=0)
+    ids = np.array([12596, 4387, 6769, 6543, 4330, 13901])
+    lo, hi = grid.decode(ids)
+    res = BetaBaBSolver(Backend(m), q, BetaConfig(node_budget=200)).solve(lo, hi, m)
+    assert (res.status == UNSAT).sum() >= 5, res.status

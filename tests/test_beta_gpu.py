@@ -1,0 +1,131 @@
+"""fa_beta_kernel (csrc/beta.hip) against the PyTorch reference of the same op (ops/beta.py:level_ref)
+and against brute-force lattice enumeration; the beta BaB stage on the device."""
+import numpy as np
+import pytest
+import torch
+
+from fairify_amd import presets
+from fairify_amd.engine import exact
+from fairify_amd.engine.bab import SAT, UNKNOWN, UNSAT
+from fairify_amd.engine.beta_bab import BetaBaBSolver, BetaConfig
+from fairify_amd.models.mlp import random_mlp
+from fairify_amd.models.zoo import get_model
+from fairify_amd.ops import beta as B
+from fairify_amd.ops import hip
+from fairify_amd.ops.backend import Backend
+from fairify_amd.partition import processing_order
+
+from test_beta_bab import _brute_pair, _setup, _true_min
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(R, NH, seed, neg):
+    g = torch.Generator().manual_seed(seed)
+    al = [torch.rand(R, NH, generator=g) for _ in range(2)]
+    be_ = [torch.rand(R, NH, generator=g) * (2 if neg else 1) - (1 if neg else 0) for _ in range(2)]
+    t = torch.rand(R, generator=g)
+    return al, be_, t
+
+
+def _both(cuda, seed, iters, neg=False, lookahead=0, fix=0.3, widths=(6, 5, 4)):
+    m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(seed, widths=widths, fix=fix)
+    R = lo.shape[0]
+    w = [x.shape[1] for x in ws[:-1]]
+    NH = sum(w)
+    al, be_, t = _params(R, NH, seed, neg)
+    lr = dict(lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    cpu = [x.clone() for x in (al[0], al[1], be_[0], be_[1], t)]
+    lr_ = B.level_ref(ws, bs, w, lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1], *cpu,
+                      iters=iters, lookahead=lookahead, beta_pos=not neg, **lr)
+    gb = Backend(m, cuda)
+    d = lambda x: x.to(cuda).contiguous()  # noqa: E731
+    gpu = [d(x.clone()) for x in (al[0], al[1], be_[0], be_[1], t)]
+    lg = hip.beta_level(gb, d(lo), d(hi), pa, d(va), d(vb), d(bnd[0][0]), d(bnd[0][1]), d(bnd[1][0]), d(bnd[1][1]),
+                        d(ph[0]), d(ph[1]), *gpu, iters=iters, lookahead=lookahead, beta_pos=not neg, **lr)
+    torch.cuda.synchronize()
+    return m, w, (lo, hi, va, vb, ph, pa), lr_, lg, cpu, [x.cpu() for x in gpu]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+@pytest.mark.parametrize("neg", [False, True])
+def test_beta_kernel_rigorous_bound_matches_reference(cuda, seed, neg):
+    """iters = 0: both evaluate the same parameters -- the fp64 bounds agree to rounding-term
+    size, and the kernel's bound is below every phase-feasible lattice point."""
+    m, w, (lo, hi, va, vb, ph, pa), lr_, lg, _, gp = _both(cuda, seed, 0, neg)
+    bg = lg.bound.cpu()
+    fin = torch.isfinite(lr_.bound)
+    assert bool((torch.isfinite(bg) == fin).all())
+    assert torch.allclose(bg[fin], lr_.bound[fin], rtol=1e-9, atol=1e-9)
+    assert torch.equal(lg.xstar.cpu()[fin], lr_.xstar[fin])
+    t = gp[4]
+    for r in range(lo.shape[0]):
+        tm = _true_min(m, lo[r].numpy(), hi[r].numpy(), pa, va[r].numpy(), vb[r].numpy(), ph[0][r].numpy(),
+                       ph[1][r].numpy(), float(t[r]), w)
+        assert float(bg[r]) <= tm
+
+
+@pytest.mark.parametrize("seed", [3, 4, 5])
+def test_beta_kernel_split_and_binit_match_reference(cuda, seed):
+    m, w, _, lr_, lg, _, _ = _both(cuda, seed, 0, fix=0.1)
+    sg, sr = lg.split.cpu(), lr_.split
+    ok = sg == sr
+    assert ok.float().mean() >= 0.8                 # near-ties may break differently (fp32 vs fp64 scores)
+    nb = ok & (sr >= 0)
+    assert torch.allclose(lg.binit.cpu()[nb], lr_.binit[nb], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+@pytest.mark.parametrize("look", [0, 4])
+def test_beta_kernel_optimises_soundly(cuda, seed, look):
+    m, w, (lo, hi, va, vb, ph, pa), lr_, lg, _, gp = _both(cuda, seed, 60, lookahead=look, fix=0.15)
+    m0, _, _, lr0, lg0, _, _ = _both(cuda, seed, 0, lookahead=look, fix=0.15)
+    bg, b0 = lg.bound.cpu(), lg0.bound.cpu()
+    fin = torch.isfinite(b0)
+    # the start parameters here are random: 60 steps never end below them and usually well above
+    assert bool((bg[fin] >= b0[fin] - 1e-5 * (1 + b0[fin].abs())).all())
+    assert bool((bg[fin] > b0[fin] + 1e-3).any())
+    # fp32 trajectories differ from the reference's only by summation order: same ball-park
+    assert float((bg[fin] - lr_.bound[fin]).abs().max()) < 0.05 * (1 + float(lr_.bound[fin].abs().max()))
+    t = gp[4]
+    for r in range(lo.shape[0]):
+        tm = _true_min(m, lo[r].numpy(), hi[r].numpy(), pa, va[r].numpy(), vb[r].numpy(), ph[0][r].numpy(),
+                       ph[1][r].numpy(), float(t[r]), w)
+        assert float(bg[r]) <= tm
+
+
+def test_beta_kernel_wide_layers(cuda):
+    """Layers wider than a wave (lanes loop over neurons) and deeper nets."""
+    m, w, (lo, hi, va, vb, ph, pa), lr_, lg, _, gp = _both(cuda, 7, 0, widths=(100, 70, 3))
+    fin = torch.isfinite(lr_.bound)
+    assert torch.allclose(lg.bound.cpu()[fin], lr_.bound[fin], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("seed", [3, 6])
+def test_beta_bab_gpu_matches_bruteforce(cuda, seed):
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, 0)[:24]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 1)
+    m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
+    res = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=256, iters=20, root_iters=40)).solve(lo, hi, m)
+    pa = q.pa_idx[0]
+    assert (res.status != UNKNOWN).mean() > 0.5
+    for k in range(len(ids)):
+        if res.status[k] != UNKNOWN:
+            assert (res.status[k] == SAT) == _brute_pair(m, lo[k], hi[k], pa), k
+    sat = np.nonzero(res.status == SAT)[0]
+    if sat.size:
+        assert exact.is_violation(m, res.cex_x[sat], res.cex_xp[sat]).all()
+
+
+def test_beta_gpu_closes_trained_ac7_residue(cuda):
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    m = get_model("AC-7", weights="zoo", seed=0)
+    ids = np.array([12596, 4387, 6769, 6543, 4330, 13901, 956, 7121, 4516, 5716, 5527, 14939])
+    lo, hi = grid.decode(ids)
+    res = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=400)).solve(lo, hi, m)
+    assert (res.status == UNSAT).sum() >= 10, res.status
+    assert (res.status == SAT).sum() == 0              # the verified LP proves all 12 UNSAT

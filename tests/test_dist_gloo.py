@@ -52,23 +52,28 @@ _TIMES = {"SV-time", "S-time", "HV-Time", "H-Time", "Total-Time"}
 
 
 def test_ranks_match_one_rank(tmp_path):
-    """1, 2 and 4 ranks write identical CSVs (every column but the measured times) through the
-    compact rank-0 gather."""
-    dirs = {w: str(tmp_path / f"w{w}") for w in (1, 2, 4)}
+    """1, 2, 4 and 8 ranks (the CLI's dynamic unit queue for world > 1) write identical CSVs (every
+    column but the measured times) through the compact rank-0 gather, and the per-rank partition
+    counts of summary.json cover each model's partitions exactly once."""
+    dirs = {w: str(tmp_path / f"w{w}") for w in (1, 2, 4, 8)}
     for w, d in dirs.items():
         _run(w, d)
     for m in ["GC-1", "GC-4"]:
         a = read_csv(os.path.join(dirs[1], f"{m}.csv"))
         assert len(a) == 70
-        for w in (2, 4):
+        for w in (2, 4, 8):
             b = read_csv(os.path.join(dirs[w], f"{m}.csv"))
             assert len(b) == 70
             for ra, rb in zip(a, b):
                 for col in ra:
                     if col not in _TIMES:
                         assert ra[col] == rb[col], (m, w, col)
-    s = json.load(open(os.path.join(dirs[4], "summary.json")))
-    assert s["n_ranks"] == 4
+    for w in (1, 2, 4, 8):
+        s = json.load(open(os.path.join(dirs[w], "summary.json")))
+        assert s["n_ranks"] == w
+        rows = s["rows"] if "rows" in s else s["models"]
+        for row in rows:
+            assert len(row["rank_partitions"]) == w and sum(row["rank_partitions"]) == 70, (w, row["rank_partitions"])
 
 
 def test_resume_skips_finished(tmp_path):
@@ -235,14 +240,49 @@ def _claim_worker(rank, world, port, q):
     D.destroy(info)
 
 
-def test_unit_queue_claims_every_unit_once():
-    """The runner's dynamic unit queue (rendezvous-store atomic counter): 4 ranks x 3 threads claim
-    200 units, each exactly once."""
+@pytest.mark.parametrize("world", [4, 8])
+def test_unit_queue_claims_every_unit_once(world):
+    """The runner's dynamic unit queue (rendezvous-store atomic counter): 4 / 8 ranks x 3 threads
+    claim 200 units, each exactly once."""
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    mp.spawn(_claim_worker, args=(4, port, q), nprocs=4, join=True)
+    mp.spawn(_claim_worker, args=(world, port, q), nprocs=world, join=True)
     assert q.get() == list(range(200))
+
+
+def _worker_twice(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch
+
+    torch.set_num_threads(1)
+    from fairify_amd import presets
+    from fairify_amd.engine.pipeline import VerifyConfig
+    from fairify_amd.engine.runner import run_preset
+    from fairify_amd.parallel import dist as D
+
+    info = D.init("cpu")
+    cfg = VerifyConfig(sim_size=100, chunk=8, node_budget=256, smt_backend="none")
+    for k in range(2):
+        run_preset(presets.get("src/GC-age"), models=["GC-4"], out_dir=os.path.join(out, str(k)), cfg=cfg, info=info,
+                   max_partitions=40, accuracy=False, verbose=False, balance="queue")
+    D.destroy(info)
+
+
+def test_unit_queue_second_run_same_process_group(tmp_path):
+    """A second run_preset of the same preset / model / seed in one process group gets fresh unit
+    counters (per-invocation nonce) and verifies every partition again (the stale key used to drop
+    the whole run silently)."""
+    port = _free_port()
+    mp.spawn(_worker_twice, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    a = read_csv(os.path.join(str(tmp_path), "0", "GC-4.csv"))
+    b = read_csv(os.path.join(str(tmp_path), "1", "GC-4.csv"))
+    assert len(a) == len(b) == 40
+    for ra, rb in zip(a, b):
+        for col in ra:
+            if col not in _TIMES:
+                assert ra[col] == rb[col], col
 
 
 def test_strided_and_queue_balance_agree(tmp_path):

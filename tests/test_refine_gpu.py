@@ -281,7 +281,33 @@ def test_phase_refine_sound_and_infeasibility_exact(cuda, seed):
             continue
         n_feas_rows += 1
         Zf = Z[ok]
-        tol = 1e-5 * (1 + Zf.abs())
-        assert torch.all(Zf >= llb[r, :Nh] - tol), r
-        assert torch.all(Zf <= lub[r, :Nh] + tol), r
+        # rigorous bounds: no slack beyond the fp64 evaluation of the lattice points themselves
+        # (the kernel's fp32 rounding terms are ~1e-6 relative; fp64 noise here is ~1e-15)
+        assert torch.all(Zf >= llb[r, :Nh] - 1e-9), r
+        assert torch.all(Zf <= lub[r, :Nh] + 1e-9), r
     assert n_feas_rows > 0
+
+
+def test_backward_kernel_with_dead_mask(cuda):
+    """Mode FULL with a forced-dead mask (heuristically pruned nets): every neuron gets finite bounds
+    that match ref.backward_bounds on the same mask, and the masked neurons are reported dead (the
+    kernel used to leave them at -inf / +inf and alive)."""
+    n0, hidden = 6, [16, 12, 8]
+    m = random_mlp(n0, hidden, seed=77, bias_scale=0.3)
+    lo, hi = _boxes(n0, 64, 3)
+    R, NH = lo.shape[0], sum(hidden)
+    g = torch.Generator().manual_seed(3)
+    dead = (torch.rand(R, NH, generator=g) < 0.2).to(torch.uint8)
+    gpu = Backend(m, cuda)
+    rg = gpu.bounds(lo.to(cuda), hi.to(cuda), mode="backward", dead=dead.to(cuda))
+    ws = [w.double() for w in Backend(m, "cpu").ws]
+    bs = [b.double() for b in Backend(m, "cpu").bs]
+    rr = ref.backward_bounds(ws, bs, lo.double(), hi.double(), dead=dead.bool(), unit=ref.FP32_UNIT)
+    for k in range(len(hidden)):
+        a, b = rg.layer_lb[k].cpu().double(), rr.layer_lb[k]
+        assert torch.isfinite(a).all() and torch.isfinite(rg.layer_ub[k].cpu()).all(), k
+        scale = float((rr.layer_ub[k] - b).abs().max() + rr.layer_ub[k].abs().max() + 1e-3)
+        assert float((a - b).abs().max()) <= 0.05 * scale, k
+    assert bool((rg.dead.cpu() | ~dead.bool()).all())           # masked -> dead
+    assert bool((rr.dead | ~dead.bool()).all())
+    assert float((rg.dead.cpu() == rr.dead).double().mean()) >= 0.99
