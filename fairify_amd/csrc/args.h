@@ -410,4 +410,9 @@ struct BetaArgs {
   int* split;               // [R] >= 0 neuron (A: j, B: NH + j), -1-d input dim d, -(n0+1) leaf
   float* xstar;             // [R, n0] concretising vertex
   float* binit;             // [R, 2] split multiplier of the (inactive, active) child
+  // relaxed queries: copy B reads x' whose RA dims (bit d of ramask) range over [plo, phi] ([R, n0])
+  unsigned long long ramask;
+  const float* plo;
+  const float* phi;
+  float* xpstar;            // [R, n0] copy B's vertex (RA dims from x''s box), or nullptr
 };

@@ -83,11 +83,15 @@ struct Slab {            // per-wave LDS workspace
   double* hm[2];         // |input| maxima per copy [n0]
   float* cft;            // input coefficients of a look-ahead pass [n0]
   float* xs;             // concretising vertex [n0]
+  float* xps;            // copy B's vertex [n0] (relaxed: RA dims from x''s box; else = xs)
 };
 
 struct Node {            // per-node constants (wave-uniform)
   const float* lo;
   const float* hi;
+  const float* plo;      // relaxed: x''s box on the RA dims (ramask), else nullptr
+  const float* phi;
+  unsigned long long ramask;
   float va[FA_MAX_PA];
   float vb[FA_MAX_PA];
   unsigned long long pamask;
@@ -210,9 +214,10 @@ __device__ T bwd(const NetDesc& nd, const float* Wf, const float* Wt, const Slab
   return wsum(cpart);
 }
 
-// Concretisation of the coupled input form over the node box (PA dims: va / vb); writes x* to
-// S.xs.  RIG: returns the bound less every rounding term (errA + errB passed in).
-template <typename T, bool RIG>
+// Concretisation of the coupled input form over the node box (PA dims: va / vb; relaxed RA dims:
+// each copy over its own box, the tie |x_r - x'_r| <= tau dropped); WX: writes x* / x'* to S.xs /
+// S.xps.  RIG: returns the bound less every rounding term (errA + errB passed in).
+template <typename T, bool RIG, bool WX>
 __device__ T conc(const NetDesc& nd, const Slab& S, const Node& N, const T* cA, const T* cB, T kA, T kB, T eAB) {
   const int lane = threadIdx.x & 63;
   const int n0 = nd.dims[0];
@@ -221,12 +226,27 @@ __device__ T conc(const NetDesc& nd, const Slab& S, const Node& N, const T* cA, 
     const float lo = N.lo[i], hi = N.hi[i];
     if ((N.pamask >> i) & 1ull) {
       // this PA dim's position in the value list
-      int q = __popcll(N.pamask & ((1ull << i) - 1ull));
+      const int q = __popcll(N.pamask & ((1ull << i) - 1ull));
       const T ta = cA[i] * (T)N.va[q];
       const T tb = cB[i] * (T)N.vb[q];
       part += ta + tb;
       if (RIG) mag += tabs(ta) + tabs(tb);
-      S.xs[i] = lo;
+      if (WX) {
+        S.xs[i] = lo;
+        S.xps[i] = lo;
+      }
+    } else if ((N.ramask >> i) & 1ull) {
+      const float plo = N.plo[i], phi = N.phi[i];
+      const float xa = cA[i] >= 0 ? lo : hi;
+      const float xb = cB[i] >= 0 ? plo : phi;
+      const T ta = cA[i] * (T)xa;
+      const T tb = cB[i] * (T)xb;
+      part += ta + tb;
+      if (RIG) mag += tabs(ta) + tabs(tb);
+      if (WX) {
+        S.xs[i] = xa;
+        S.xps[i] = xb;
+      }
     } else {
       const T cf = cA[i] + cB[i];
       const float x = cf >= 0 ? lo : hi;
@@ -236,13 +256,16 @@ __device__ T conc(const NetDesc& nd, const Slab& S, const Node& N, const T* cA, 
         mag += tabs(tm);
         emag += tabs(cf) * (T)fmaxf(fabsf(lo), fabsf(hi));
       }
-      S.xs[i] = x;
+      if (WX) {
+        S.xs[i] = x;
+        S.xps[i] = x;
+      }
     }
   }
   T B = wsum(part) + kA + kB;
   if (RIG) {
     const T m = wsum(mag) + tabs(kA) + tabs(kB);
-    const T econ = (T)U64 * wsum(emag) + (T)g64(n0 + 8) * m;
+    const T econ = (T)U64 * wsum(emag) + (T)g64(2 * n0 + 4) * m;
     B -= (eAB + econ) * (T)(1.0 + 1e-6);
   }
   wsync();
@@ -258,8 +281,9 @@ __device__ T fwd(const NetDesc& nd, const float* Wf, const Slab& S, const Node& 
   const int n0 = nd.dims[0];
   T* h0 = reinterpret_cast<T*>(S.b0);
   T* h1 = reinterpret_cast<T*>(S.b1);
+  const float* xin = c == 0 ? S.xs : S.xps;
   for (int i = lane; i < n0; i += 64) {
-    T x = (T)S.xs[i];
+    T x = (T)xin[i];
     if ((N.pamask >> i) & 1ull) x = (T)v[__popcll(N.pamask & ((1ull << i) - 1ull))];
     h0[i] = x;
   }
@@ -325,7 +349,7 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   const int NHp = (NH + 3) & ~3;
   const int n0p = (n0 + 3) & ~3;
   const int mwp = (mw + 3) & ~3;
-  const int slab = 11 * NHp + 4 * mwp + 10 * n0p + 32;
+  const int slab = 11 * NHp + 4 * mwp + 11 * n0p + 32;
   float* base = smem + tot4 * (WTL ? 2 : 1) + wave * slab;
   Slab S;
   S.lb[0] = base; S.ub[0] = base + NHp; S.lb[1] = base + 2 * NHp; S.ub[1] = base + 3 * NHp;
@@ -339,11 +363,15 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   S.cf[0] = dbase + 2 * mwp; S.cf[1] = S.cf[0] + n0p; S.hm[0] = S.cf[1] + n0p; S.hm[1] = S.hm[0] + n0p;
   S.cft = reinterpret_cast<float*>(S.hm[1] + n0p);
   S.xs = S.cft + n0p;
-  int* cand = reinterpret_cast<int*>(S.xs + n0p);      // look-ahead candidates [32]
+  S.xps = S.xs + n0p;
+  int* cand = reinterpret_cast<int*>(S.xps + n0p);     // look-ahead candidates [32]
 
   Node N;
   N.lo = a.lo + (size_t)r * n0;
   N.hi = a.hi + (size_t)r * n0;
+  N.ramask = a.plo ? a.ramask : 0ull;
+  N.plo = a.plo ? a.plo + (size_t)r * n0 : nullptr;
+  N.phi = a.phi ? a.phi + (size_t)r * n0 : nullptr;
   N.pamask = 0;
   for (int q = 0; q < a.npa; ++q) {
     N.va[q] = a.va[(size_t)r * a.npa + q];
@@ -375,6 +403,9 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         const int q = __popcll(N.pamask & ((1ull << i) - 1ull));
         S.hm[0][i] = fabs((double)N.va[q]);
         S.hm[1][i] = fabs((double)N.vb[q]);
+      } else if ((N.ramask >> i) & 1ull) {
+        S.hm[0][i] = m;
+        S.hm[1][i] = fmax(fabs((double)N.plo[i]), fabs((double)N.phi[i]));
       } else {
         S.hm[0][i] = m;
         S.hm[1][i] = m;
@@ -389,11 +420,14 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   if (__any(bad)) {
     if (lane == 0) {
       a.bound[r] = __builtin_inf();
-      a.split[r] = -(n0 + 1);
+      a.split[r] = -(2 * n0 + 1);
       a.binit[2 * r] = 0.f;
       a.binit[2 * r + 1] = 0.f;
     }
-    for (int i = lane; i < n0; i += 64) a.xstar[(size_t)r * n0 + i] = N.lo[i];
+    for (int i = lane; i < n0; i += 64) {
+      a.xstar[(size_t)r * n0 + i] = N.lo[i];
+      if (a.xpstar) a.xpstar[(size_t)r * n0 + i] = N.ramask >> i & 1ull ? N.plo[i] : N.lo[i];
+    }
     return;
   }
   // every neuron's state is touched by the SAME lane everywhere (lane j of its layer), so no
@@ -417,7 +451,7 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
                                                   nullptr);
     const float kB = bwd<float, false, true, WTL>(nd, Wf, Wt, S, 1, -(1.f - tc), cur + NH, cur + 3 * NH, -1, 0, cB,
                                                   nullptr, nullptr);
-    const float Bv = conc<float, false>(nd, S, N, cA, cB, kA, kB, 0.f);
+    const float Bv = conc<float, false, true>(nd, S, N, cA, cB, kA, kB, 0.f);
     if (Bv > best) {
       best = Bv;
       tbest = tc;
@@ -488,9 +522,13 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
                                                  &eA, nullptr);
   const double kB = bwd<double, true, true, WTL>(nd, Wf, Wt, S, 1, -(1.0 - (double)tf), par + NH, par + 3 * NH, -1,
                                                  0, S.cf[1], &eB, nullptr);
-  const double Bd = conc<double, true>(nd, S, N, S.cf[0], S.cf[1], kA, kB, eA + eB);
+  const double Bd = conc<double, true, true>(nd, S, N, S.cf[0], S.cf[1], kA, kB, eA + eB);
   (void)fwd<double>(nd, Wf, S, N, 0, N.va, par);
   (void)fwd<double>(nd, Wf, S, N, 1, N.vb, par + NH);
+  for (int i = lane; i < n0; i += 64) {
+    a.xstar[(size_t)r * n0 + i] = S.xs[i];
+    if (a.xpstar) a.xpstar[(size_t)r * n0 + i] = S.xps[i];
+  }
 
   // ---- branching scores: |lam| x relaxation gap at x* of unfixed unstable neurons
   for (int c = 0; c < 2; ++c)
@@ -573,18 +611,11 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         int inf = 0;
         const float kc = bwd<float, false, false, WTL>(nd, Wf, Wt, S, c, c == 0 ? tf : -(1.f - tf), par + c * NH,
                                                        par + (2 + c) * NH, k, sg, cA32, nullptr, &inf);
-        float part = 0.f;
-        for (int i = lane; i < n0; i += 64) {
-          const float other = (float)S.cf[1 - c][i];
-          if ((N.pamask >> i) & 1ull) {
-            const int qq = __popcll(N.pamask & ((1ull << i) - 1ull));
-            part += cA32[i] * (c == 0 ? N.va[qq] : N.vb[qq]) + other * (c == 0 ? N.vb[qq] : N.va[qq]);
-          } else {
-            const float cf = cA32[i] + other;
-            part += cf * (cf >= 0.f ? N.lo[i] : N.hi[i]);
-          }
-        }
-        float Bc = wsum(part) + kc + (float)(c == 0 ? kB : kA);
+        float* oth = reinterpret_cast<float*>(S.b1);       // the other copy's coefficients (fp32)
+        for (int i = lane; i < n0; i += 64) oth[i] = (float)S.cf[1 - c][i];
+        wsync();
+        float Bc = c == 0 ? conc<float, false, false>(nd, S, N, cA32, oth, kc, (float)kB, 0.f)
+                          : conc<float, false, false>(nd, S, N, oth, cA32, (float)kA, kc, 0.f);
         if (inf) Bc = FLT_MAX;
         worst = fminf(worst, Bc);
         wsync();
@@ -613,26 +644,38 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
       b_in = lam * slope;
       b_ac = lam * (1.f - slope);
     } else {
-      // input split: |coefficient| x width over the non-PA dims; none left: a lattice leaf
+      // input split: |coefficient| x width over x's non-PA dims (an RA dim: copy A's coefficient)
+      // and, relaxed, x''s RA dims (copy B's, code n0 + d); none left: a lattice leaf
       float bv = -1.f;
       int bd = -1;
       for (int i = 0; i < n0; ++i) {
         if ((N.pamask >> i) & 1ull) continue;
+        const bool ra = (N.ramask >> i) & 1ull;
         const float wd = N.hi[i] - N.lo[i];
-        if (!(wd > 0.f)) continue;
-        const float s = (float)fabs(S.cf[0][i] + S.cf[1][i]) * wd + 1e-9f * wd;
-        if (s > bv) {
-          bv = s;
-          bd = i;
+        if (wd > 0.f) {
+          const float s = (float)fabs(ra ? S.cf[0][i] : S.cf[0][i] + S.cf[1][i]) * wd + 1e-9f * wd;
+          if (s > bv) {
+            bv = s;
+            bd = i;
+          }
+        }
+        if (ra) {
+          const float wp = N.phi[i] - N.plo[i];
+          if (wp > 0.f) {
+            const float s = (float)fabs(S.cf[1][i]) * wp + 1e-9f * wp;
+            if (s > bv) {
+              bv = s;
+              bd = n0 + i;
+            }
+          }
         }
       }
-      sp = bd >= 0 ? -1 - bd : -(n0 + 1);
+      sp = bd >= 0 ? -1 - bd : -(2 * n0 + 1);
     }
     a.split[r] = sp;
     a.binit[2 * r] = b_in;
     a.binit[2 * r + 1] = b_ac;
   }
-  for (int i = lane; i < n0; i += 64) a.xstar[(size_t)r * n0 + i] = S.xs[i];
 }
 
 FA_LDS_REGISTER(FA_LDS_K(fa_beta_kernel<true>), FA_LDS_K(fa_beta_kernel<false>));
@@ -643,7 +686,7 @@ extern "C" size_t fa_beta_slab_floats(const NetDesc& nd) {
   const int NHp = (nd.n_hidden + 3) & ~3;
   const int n0p = (nd.dims[0] + 3) & ~3;
   const int mwp = (nd.max_width + 3) & ~3;
-  return (size_t)(11 * NHp + 4 * mwp + 10 * n0p + 32);
+  return (size_t)(11 * NHp + 4 * mwp + 11 * n0p + 32);
 }
 
 // Launch configuration: waves per workgroup and whether the transposed weights fit in LDS next to

@@ -507,7 +507,8 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t hi, uintptr_t va, uintptr_t vb, uintptr_t LBA, uintptr_t UBA, uintptr_t LBB,
                          uintptr_t UBB, uintptr_t phA, uintptr_t phB, uintptr_t par, uintptr_t t, uintptr_t scratch,
                          int iters, float lr_a, float lr_b, float lr_t, float decay, int lookahead, int beta_pos,
-                         uintptr_t bound, uintptr_t split, uintptr_t xstar, uintptr_t binit, uintptr_t stream) {
+                         uintptr_t bound, uintptr_t split, uintptr_t xstar, uintptr_t binit,
+                         unsigned long long ramask, uintptr_t plo, uintptr_t phi, uintptr_t xpstar, uintptr_t stream) {
     if (pa.size() > FA_MAX_PA) throw std::invalid_argument("beta_level: too many PA dims");
     for (size_t q = 0; q < pa.size(); ++q)
       if (pa[q] < 0 || pa[q] >= net.d.dims[0] || (q && pa[q] <= pa[q - 1]))
@@ -543,6 +544,12 @@ PYBIND11_MODULE(_C, m) {
     a.split = P<int>(split);
     a.xstar = P<float>(xstar);
     a.binit = P<float>(binit);
+    a.ramask = ramask;
+    a.plo = P<const float>(plo);
+    a.phi = P<const float>(phi);
+    a.xpstar = P<float>(xpstar);
+    if ((net.d.dims[0] < 64 && (ramask >> net.d.dims[0])) || (ramask && (!plo || !phi)))
+      throw std::invalid_argument("beta_level: RA mask beyond the inputs or no x' box");
     return fa_beta_launch(net.d, a, reinterpret_cast<hipStream_t>(stream));
   });
   m.def("beta_fits", [](const Net& net) {

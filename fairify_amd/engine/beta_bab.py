@@ -16,13 +16,14 @@ such pair), its concretising vertex pair is screened with rigorous point bounds 
 on the host (SAT), a single lattice point is decided exactly, and a partition whose nodes all
 closed is UNSAT.  A partition past its node budget ends UNKNOWN.
 
-PA-only queries (relaxed queries keep the relu / LP stages).  CPU tests pin verdicts to brute-force
+Relaxed queries (|x_r - x'_r| <= tau, x' unclipped): every node also carries x''s box on the RA
+dims, split like the input dims, and the second orientation runs on the negated network.  CPU tests pin verdicts to brute-force
 enumeration (tests/test_beta_bab.py); the GPU kernel to this module's reference (tests/test_beta_gpu.py).
 """
 from __future__ import annotations
 
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 from typing import Optional
 
 import numpy as np
@@ -48,8 +49,10 @@ class BetaConfig:
     child_lr: float = 0.3            # children (warm-started at their parent's optimum): lr x this
     decay: float = 0.98              # lr decay per step
     warm_beta: bool = True           # split multiplier starts at the parent's relaxation (else 0)
-    cold: bool = False               # children: also optimise from the cold start, keep the better
     lookahead: int = 8               # filtered branching: candidates per score (0 = best gap score)
+    tighten: bool = True             # children: re-bound every hidden neuron over the node's box and
+    #                                  phase region (csrc/refine.hip with phases), intersected with
+    #                                  the inherited bounds; an empty region closes the node
     beta_pos: bool = True            # split multipliers projected >= 0 (free-signed ones, which may
     #                                  use the interval side, make Adam oscillate around 0: measured
     #                                  8 / 10 -> 0 / 10 trained AC-7 partitions closed, tools/exp)
@@ -59,7 +62,8 @@ class BetaConfig:
 
 
 def supported(q: ResolvedQuery) -> bool:
-    return not q.relaxed
+    """PA-only and relaxed queries (x' RA box per node, second orientation on the negated net)."""
+    return True
 
 
 def fits(be: Backend) -> bool:
@@ -83,6 +87,10 @@ class BetaBaBSolver:
 
     def solve(self, lo_np: np.ndarray, hi_np: np.ndarray, mlp_exact: MLP,
               init_status: Optional[np.ndarray] = None) -> BaBResult:
+        """Relaxed queries: N(x, v) < 0 < N(x', v') on this backend's network, then, on the partitions
+        that closed, N(x, v) > 0 > N(x', v') as the same search on the network with its logit
+        negated (x' may leave the box, so swapping the pair does not cover it); UNSAT when both
+        close, SAT when either finds a pair (confirmed on ``mlp_exact``, orientation-free)."""
         t0 = time.time()
         P, n = lo_np.shape
         status = np.full(P, RUNNING, dtype=np.int8) if init_status is None else init_status.astype(np.int8).copy()
@@ -93,6 +101,34 @@ class BetaBaBSolver:
             status[status == RUNNING] = UNKNOWN
             return BaBResult(status, cex_x, cex_xp, nodes)
         self.stats = {"levels": 0, "nodes": 0}
+        r1 = self._solve_all(lo_np, hi_np, mlp_exact, status, t0)
+        if not self.q.relaxed or getattr(self, "_second", False):
+            return r1
+        closed = (r1.status == UNSAT) & (status == RUNNING)
+        if not closed.any():
+            return r1
+        from .relu_bab import negated
+
+        neg = BetaBaBSolver(Backend(negated(self.be.mlp), device=self.dev), self.q,
+                            replace(self.cfg, time_budget=max(0.0, self.cfg.time_budget - (time.time() - t0))),
+                            timer=self.tm)
+        neg._second = True
+        r2 = neg.solve(lo_np, hi_np, mlp_exact, init_status=np.where(closed, RUNNING, UNKNOWN).astype(np.int8))
+        out = r1.status.copy()
+        out[closed] = r2.status[closed]
+        cx, cxp = r1.cex_x.copy(), r1.cex_xp.copy()
+        s2 = closed & (r2.status == SAT)
+        cx[s2], cxp[s2] = r2.cex_x[s2], r2.cex_xp[s2]
+        self.stats["nodes"] += neg.stats.get("nodes", 0)
+        self.stats["levels"] += neg.stats.get("levels", 0)
+        return BaBResult(out, cx, cxp, r1.nodes + r2.nodes, 0, time.time() - t0)
+
+    def _solve_all(self, lo_np, hi_np, mlp_exact, status, t0) -> BaBResult:
+        P, n = lo_np.shape
+        status = status.copy()
+        cex_x = np.zeros((P, n), dtype=np.int64)
+        cex_xp = np.zeros((P, n), dtype=np.int64)
+        nodes = np.zeros(P, dtype=np.int64)
         for g in pa_groups(self.q, lo_np, hi_np):
             left = max(0.0, self.cfg.time_budget - (time.time() - t0))
             st, cx, cxp, nd = self._solve_group(lo_np[g], hi_np[g], mlp_exact, status[g], left)
@@ -100,9 +136,10 @@ class BetaBaBSolver:
         return BaBResult(status, cex_x, cex_xp, nodes, 0, time.time() - t0)
 
     # ------------------------------------------------------------------------------------------
-    def _root_bounds(self, lo: torch.Tensor, hi: torch.Tensor, values: torch.Tensor):
+    def _root_bounds(self, lo: torch.Tensor, hi: torch.Tensor, values: torch.Tensor, widen: bool = False):
         """Rigorous per-layer pre-activation bounds [P * V, NH] of every (partition, PA value) row
-        (the verified LP's bounds, smt/milp.py:layer_bounds_rows, kept on the device)."""
+        (the verified LP's bounds, smt/milp.py:layer_bounds_rows, kept on the device); ``widen``:
+        the x' rows of a relaxed query (RA dims widened by tau, unclipped)."""
         be, q = self.be, self.q
         P, n0 = lo.shape
         V = values.shape[0]
@@ -112,6 +149,10 @@ class BetaBaBSolver:
         vv = values.repeat(P, 1)
         rlo[:, pa] = vv
         rhi[:, pa] = vv
+        if widen and q.relaxed:
+            ra = list(q.ra_idx)
+            rlo[:, ra] -= q.tau
+            rhi[:, ra] += q.tau
         rf = len(be.widths) - 1 >= 2        # refined hidden bounds: every relaxation above layer 0 tightens
         res = be.bounds(rlo, rhi, mode="symbolic", keep_layers=True, crown=rf, refine=rf)
         NH = be.n_hidden
@@ -138,6 +179,11 @@ class BetaBaBSolver:
         if run.size == 0:
             return status, cex_x, cex_xp, nodes_np
         pa = list(q.pa_idx)
+        relaxed = q.relaxed
+        ra = list(q.ra_idx) if relaxed else []
+        tau = float(q.tau)
+        ram = torch.zeros(n0, dtype=torch.bool, device=dev)
+        ram[ra] = True
         f32 = dict(dtype=torch.float32, device=dev)
         values = torch.from_numpy(values_np.astype(np.float32)).to(dev)
         V = values.shape[0]
@@ -145,32 +191,41 @@ class BetaBaBSolver:
         hi_r = torch.from_numpy(hi_np[run].astype(np.float32)).to(dev)
         with self.tm("beta.roots"):
             rlb, rub = self._root_bounds(lo_r, hi_r, values)
+            rlbp, rubp = self._root_bounds(lo_r, hi_r, values, widen=True) if relaxed else (rlb, rub)
         # one root per (running partition, ordered pair)
         k = torch.arange(run.size, device=dev).repeat_interleave(Pp)
         pr = torch.from_numpy(pairs_np.astype(np.int64)).to(dev).repeat(run.size, 1)
-        ra, rb = k * V + pr[:, 0], k * V + pr[:, 1]
+        ia, ib = k * V + pr[:, 0], k * V + pr[:, 1]
+        R0 = k.numel()
+        plo = lo_r[k].clone()
+        phi = hi_r[k].clone()
+        if relaxed:                 # x' on the RA dims: [lo - tau, hi + tau], unclipped
+            plo[:, ra] -= tau
+            phi[:, ra] += tau
         pool = {
             "part": torch.from_numpy(run).to(dev)[k],
-            "lo": lo_r[k].clone(), "hi": hi_r[k].clone(),
+            "lo": lo_r[k].clone(), "hi": hi_r[k].clone(), "plo": plo, "phi": phi,
             "va": values[pr[:, 0]].clone(), "vb": values[pr[:, 1]].clone(),
-            "LBA": rlb[ra], "UBA": rub[ra], "LBB": rlb[rb], "UBB": rub[rb],
-            "phA": torch.zeros(k.numel(), NH, dtype=torch.int8, device=dev),
-            "phB": torch.zeros(k.numel(), NH, dtype=torch.int8, device=dev),
-            "alA": torch.full((k.numel(), NH), 0.5, **f32), "alB": torch.full((k.numel(), NH), 0.5, **f32),
-            "beA": torch.zeros(k.numel(), NH, **f32), "beB": torch.zeros(k.numel(), NH, **f32),
-            "t": torch.full((k.numel(),), 0.5, **f32),
-            "root": torch.ones(k.numel(), dtype=torch.bool, device=dev),
+            "LBA": rlb[ia], "UBA": rub[ia], "LBB": rlbp[ib], "UBB": rubp[ib],
+            "phA": torch.zeros(R0, NH, dtype=torch.int8, device=dev),
+            "phB": torch.zeros(R0, NH, dtype=torch.int8, device=dev),
+            "alA": torch.full((R0, NH), 0.5, **f32), "alB": torch.full((R0, NH), 0.5, **f32),
+            "beA": torch.zeros(R0, NH, **f32), "beB": torch.zeros(R0, NH, **f32),
+            "t": torch.full((R0,), 0.5, **f32),
+            "root": torch.ones(R0, dtype=torch.bool, device=dev),
         }
-        free = torch.ones(n0, dtype=torch.bool, device=dev)
-        free[pa] = False
         levels = 0
         timed_out = False
         while pool["part"].numel():
             if time.time() - t0 > time_budget:
                 timed_out = True
                 break
-            # drop nodes of decided / over-budget partitions
+            # drop nodes of decided / over-budget partitions, and (relaxed) nodes whose x and x'
+            # RA boxes are more than tau apart (no admissible pair left)
             alive = torch.from_numpy(status == RUNNING).to(dev)[pool["part"]]
+            if relaxed:
+                alive &= ~((pool["plo"][:, ra] > pool["hi"][:, ra] + tau) |
+                           (pool["phi"][:, ra] < pool["lo"][:, ra] - tau)).any(1)
             if not bool(alive.all()):
                 pool = {kk: v[alive] for kk, v in pool.items()}
                 if not pool["part"].numel():
@@ -183,36 +238,31 @@ class BetaBaBSolver:
             cur = {kk: v[:nb] for kk, v in pool.items()}
             rest = {kk: v[nb:] for kk, v in pool.items()}
             levels += 1
-            part_np = cur["part"].cpu().numpy()
-            np.add.at(nodes_np, part_np, 1)
+            np.add.at(nodes_np, cur["part"].cpu().numpy(), 1)
             sc = 1.0 if is_root else cfg.child_lr
+            empty = None
+            if cfg.tighten and not is_root:
+                with self.tm("beta.tighten"):
+                    empty = self._tighten(cur, pa, ram if relaxed else None)
+            rx = (ram, cur["plo"], cur["phi"]) if relaxed else None
             with self.tm("beta.level"):
                 lev = be.beta_level(cur["lo"], cur["hi"], pa, cur["va"], cur["vb"], cur["LBA"], cur["UBA"],
                                     cur["LBB"], cur["UBB"], cur["phA"], cur["phB"], cur["alA"], cur["alB"],
                                     cur["beA"], cur["beB"], cur["t"], cfg.root_iters if is_root else cfg.iters,
-                                    cfg.lr_a * sc, cfg.lr_b * sc, cfg.lr_t * sc, cfg.decay, cfg.lookahead, cfg.beta_pos)
-            if cfg.cold and not is_root:
-                c2 = {kk: cur[kk].clone() for kk in ("alA", "alB", "beA", "beB", "t")}
-                c2["alA"].fill_(0.5); c2["alB"].fill_(0.5); c2["beA"].zero_(); c2["beB"].zero_(); c2["t"].fill_(0.5)
-                lev2 = be.beta_level(cur["lo"], cur["hi"], pa, cur["va"], cur["vb"], cur["LBA"], cur["UBA"],
-                                     cur["LBB"], cur["UBB"], cur["phA"], cur["phB"], c2["alA"], c2["alB"],
-                                     c2["beA"], c2["beB"], c2["t"], cfg.root_iters, cfg.lr_a, cfg.lr_b, cfg.lr_t,
-                                     cfg.decay, cfg.lookahead, cfg.beta_pos)
-                use = lev2.bound > lev.bound
-                for kk in c2:
-                    cur[kk][use] = c2[kk][use]
-                lev = B.BetaLevel(bound=torch.where(use, lev2.bound, lev.bound),
-                                  split=torch.where(use, lev2.split, lev.split),
-                                  xstar=torch.where(use[:, None], lev2.xstar, lev.xstar),
-                                  binit=torch.where(use[:, None], lev2.binit, lev.binit))
+                                    cfg.lr_a * sc, cfg.lr_b * sc, cfg.lr_t * sc, cfg.decay, cfg.lookahead,
+                                    cfg.beta_pos, rx)
+            if empty is not None:
+                lev.bound = torch.where(empty, torch.full_like(lev.bound, float("inf")), lev.bound)
             closed = lev.bound >= 0
-            leaf = lev.split == -(n0 + 1)
+            leaf = lev.split == B.LEAF(n0)
             # candidate vertex pairs of the nodes that stay open (and the lattice leaves): rigorous
             # point bounds screen, then the exact check on the host
             cand = torch.nonzero(~closed).flatten()
             if cand.numel():
                 xa = lev.xstar[cand].clone()
-                xb = xa.clone()
+                xb = (lev.xpstar[cand] if lev.xpstar is not None else lev.xstar[cand]).clone()
+                if relaxed:         # x'_r: its vertex, pulled into [x_r - tau, x_r + tau]
+                    xb[:, ra] = torch.minimum(torch.maximum(xb[:, ra], xa[:, ra] - tau), xa[:, ra] + tau)
                 xa[:, pa] = cur["va"][cand]
                 xb[:, pa] = cur["vb"][cand]
                 with self.tm("beta.cand"):
@@ -245,12 +295,38 @@ class BetaBaBSolver:
         self.stats["nodes"] = self.stats.get("nodes", 0) + int(nodes_np.sum())
         return status, cex_x, cex_xp, nodes_np
 
+    def _tighten(self, cur, pa, ram=None):
+        """Phase-aware bounds of the batch's nodes (both copies in one launch pair; copy B over x',
+        i.e. its RA dims over [plo, phi] when ``ram``), intersected in place with the bounds they
+        inherited; returns the nodes whose region is empty."""
+        R = cur["lo"].shape[0]
+        loB, hiB = cur["lo"], cur["hi"]
+        if ram is not None:
+            loB = torch.where(ram[None], cur["plo"], cur["lo"])
+            hiB = torch.where(ram[None], cur["phi"], cur["hi"])
+        lo = torch.cat([cur["lo"], loB])
+        hi = torch.cat([cur["hi"], hiB])
+        v = torch.cat([cur["va"], cur["vb"]])
+        lo[:, pa] = v
+        hi[:, pa] = v
+        ph = torch.cat([cur["phA"], cur["phB"]])
+        lb, ub, inf = self.be.phase_layer_bounds(lo, hi, ph)
+        lb, ub = lb.float(), ub.float()
+        for k, (a, b) in (("LBA", (0, R)), ("LBB", (R, 2 * R))):
+            cur[k].copy_(torch.maximum(cur[k], lb[a:b]))
+        for k, (a, b) in (("UBA", (0, R)), ("UBB", (R, 2 * R))):
+            cur[k].copy_(torch.minimum(cur[k], ub[a:b]))
+        empty = torch.zeros(R, dtype=torch.bool, device=lo.device)
+        if inf is not None:
+            empty = inf[:R] | inf[R:]
+        return empty
+
     @staticmethod
     def _children(nd, split, binit, NH: int, n0: int):
         """Two children per node: a phase split (split >= 0: copy A neuron split, copy B NH + j)
         inheriting the parent's parameters (the new multiplier from ``binit``: the child starts at
-        the parent's bound), or an input split
-        (split = -1 - d) halving dim d."""
+        the parent's bound), or an input split (split = -1 - d) halving x's dim d (d < n0) or x''s
+        RA dim d - n0."""
         R = split.numel()
         dev = split.device
         rep = torch.arange(R, device=dev).repeat_interleave(2)
@@ -273,15 +349,18 @@ class BetaBaBSolver:
             kid["phB"][r_[inB], sp[inB] - NH] = sgn[inB]
             kid["beB"][r_[inB], sp[inB] - NH] = bi[inB]
         inp = ~neu
-        if bool(inp.any()):
-            d = (-1 - sp[inp]).clamp(0, n0 - 1)
-            ri = r_[inp]
-            lo_d = kid["lo"][ri, d]
-            hi_d = kid["hi"][ri, d]
+        for lk, hk, sel in (("lo", "hi", inp & (-1 - sp < n0)), ("plo", "phi", inp & (-1 - sp >= n0))):
+            if not bool(sel.any()):
+                continue
+            d = (-1 - sp[sel]) % n0
+            ri = r_[sel]
+            lo_d = kid[lk][ri, d]
+            hi_d = kid[hk][ri, d]
             mid = torch.floor((lo_d + hi_d) / 2)
-            low_child = side[inp] == 0
-            kid["hi"][ri[low_child], d[low_child]] = mid[low_child]
-            kid["lo"][ri[~low_child], d[~low_child]] = mid[~low_child] + 1
+            low_child = side[sel] == 0
+            kid[hk][ri[low_child], d[low_child]] = mid[low_child]
+            kid[lk][ri[~low_child], d[~low_child]] = mid[~low_child] + 1
+        # (plo / phi are read on the RA dims only; x' shares x's box everywhere else)
         return kid
 
     def _confirm(self, parts, xa, xb, status, cex_x, cex_xp, mlp_exact, lo_np, hi_np):

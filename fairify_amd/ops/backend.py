@@ -198,21 +198,42 @@ class Backend:
             return hip.point_bounds(self, x, dead)
         return ref.point_bounds(self.ws, self.bs, x, dead, unit=self.unit)
 
+    def phase_layer_bounds(self, lo: torch.Tensor, hi: torch.Tensor, phase: torch.Tensor):
+        """Rigorous pre-activation bounds [R, NH] of every hidden neuron over each row's box AND its
+        phase region (forward symbolic with the phases fixed, then back-substituted refinement:
+        csrc/refine.hip with ``phase_in``), and the rows whose region those bounds prove empty.
+        CPU: the reference refines without the phases (valid, looser)."""
+        NH = self.n_hidden
+        lo = lo.to(self.dtype)
+        hi = hi.to(self.dtype)
+        if self.hip:
+            from . import hip
+
+            r = hip.bounds(self, lo, hi, mode="symbolic", keep_layers=True, phase=phase)
+            r = hip.refine(self, lo, hi, r, phase=phase)
+            return r.lay_lb_full[:, :NH], r.lay_ub_full[:, :NH], r.infeasible
+        r = ref.bounds(self.ws, self.bs, lo, hi, mode="symbolic", unit=self.unit, keep_layers=True, phase=phase)
+        inf = r.infeasible
+        r = ref.crown_refine(self.ws, self.bs, lo, hi, r, unit=self.unit)
+        lb = torch.cat([t for t in r.layer_lb], 1)[:, :NH]
+        ub = torch.cat([t for t in r.layer_ub], 1)[:, :NH]
+        return lb, ub, inf
+
     def beta_level(self, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t, iters: int,
                    lr_a: float, lr_b: float, lr_t: float, decay: float = 1.0, lookahead: int = 0,
-                   beta_pos: bool = True):
+                   beta_pos: bool = True, rx=None):
         """One beta-CROWN BaB level (ops/beta.py): optimises the rows' (alpha, beta, t) IN PLACE and
         returns their rigorous fp64 bounds, branching decisions and concretising vertices."""
         if self.hip:
             from . import hip
 
             return hip.beta_level(self, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t,
-                                  iters, lr_a, lr_b, lr_t, decay, lookahead, beta_pos)
+                                  iters, lr_a, lr_b, lr_t, decay, lookahead, beta_pos, rx)
         from . import beta
 
         return beta.level_ref([w.float() for w in self.ws], [b.float() for b in self.bs], self.widths[:-1], lo, hi,
                               pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t, iters, lr_a, lr_b,
-                              lr_t, decay, lookahead, beta_pos)
+                              lr_t, decay, lookahead, beta_pos, rx)
 
     # ----------------------------------------------------------------------------- BaB node test
     def pair_certify(self, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, shared, relaxed):

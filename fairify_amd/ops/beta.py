@@ -52,11 +52,17 @@ U64 = ref.FP64_UNIT
 @dataclass
 class BetaLevel:
     bound: torch.Tensor       # [R] float64 rigorous lower bound of f_t over the node region (+inf: empty)
-    split: torch.Tensor       # [R] int64: >= 0 neuron (copy A: j, copy B: NH + j); -1 - d: input dim d;
-    #                           -(n0 + 1): single lattice point (no split left)
+    split: torch.Tensor       # [R] int64: >= 0 neuron (copy A: j, copy B: NH + j); -1 - d: input dim d
+    #                           (d >= n0: x''s RA dim d - n0); LEAF(n0): single lattice point
     xstar: torch.Tensor       # [R, n0] float32 concretising vertex (candidate pair's shared dims)
     binit: torch.Tensor       # [R, 2] float32 beta of the split neuron in the (inactive, active) child
     #                           that reproduces this node's relaxation of it (monotone warm start)
+    xpstar: Optional[torch.Tensor] = None   # [R, n0] copy B's vertex (relaxed: its RA dims from x''s box)
+
+
+def LEAF(n0: int) -> int:
+    """Split code of a node with no input width left (x and, relaxed, x' RA dims): decided exactly."""
+    return -(2 * n0 + 1)
 
 
 def _layers(v: torch.Tensor, widths: Sequence[int]) -> List[torch.Tensor]:
@@ -138,35 +144,56 @@ def _forward_lin(ws, bs, x, LB, rec, al):
     return zs, (h @ ws[-1] + bs[-1][None])[:, 0]
 
 
-def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t, rig: bool, need_lin: bool = True):
+def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t, rig: bool, need_lin: bool = True,
+             rx=None):
     """The coupled bound of rows R at the given parameters (per-layer lists), in the dtype of
-    ``ws``.  ``rig``: fp64 with every rounding term subtracted (the sound bound).  Returns
-    (bound [R], grads dict, lin records, xstar, coef)."""
+    ``ws``.  ``rig``: fp64 with every rounding term subtracted (the sound bound).
+
+    ``rx`` = (ra [n0] bool, plo, phi [R, n0]) for relaxed queries: copy B reads x' whose RA dims
+    range over their own box [plo, phi] (unclipped, reference semantics); on those dims the two
+    copies are concretised separately (the tie |x_r - x'_r| <= tau is dropped: only looser).
+    Returns a dict: B [R], g (gradients), lin (per-copy records), xs (x*), xps (x'*), cA, cB."""
     dt = ws[0].dtype
     pa = list(pa)
-    free = torch.ones(lo.shape[1], dtype=torch.bool, device=lo.device)
+    n0 = lo.shape[1]
+    free = torch.ones(n0, dtype=torch.bool, device=lo.device)
     free[pa] = False
-    hmA = torch.maximum(lo.abs(), hi.abs()).to(dt)
-    hmB = hmA.clone()
+    lo_, hi_ = lo.to(dt), hi.to(dt)
+    if rx is not None:
+        ram = rx[0].to(lo.device)
+        loB = torch.where(ram[None], rx[1].to(dt), lo_)
+        hiB = torch.where(ram[None], rx[2].to(dt), hi_)
+    else:
+        ram = torch.zeros(n0, dtype=torch.bool, device=lo.device)
+        loB, hiB = lo_, hi_
+    hmA = torch.maximum(lo_.abs(), hi_.abs())
+    hmB = torch.maximum(loB.abs(), hiB.abs())
     hmA[:, pa] = va.abs().to(dt)
     hmB[:, pa] = vb.abs().to(dt)
     cA, kA, eA, rA = _backward(ws, bs, bA[0], bA[1], phA, alA, beA, t, hmA, rig)
     cB, kB, eB, rB = _backward(ws, bs, bB[0], bB[1], phB, alB, beB, -(1 - t), hmB, rig)
     pA = cA[:, pa] * va.to(dt)
     pB = cB[:, pa] * vb.to(dt)
-    coef = torch.where(free[None], cA + cB, torch.zeros_like(cA))
-    lo_, hi_ = lo.to(dt), hi.to(dt)
+    shared = free & ~ram
+    coef = torch.where(shared[None], cA + cB, torch.zeros_like(cA))
     xs = torch.where(coef >= 0, lo_, hi_)
     terms = coef * xs
-    B = terms.sum(1) + pA.sum(1) + pB.sum(1) + kA + kB
+    xA = torch.where(cA >= 0, lo_, hi_)
+    xB = torch.where(cB >= 0, loB, hiB)
+    tA = torch.where(ram[None], cA * xA, torch.zeros_like(cA))
+    tB = torch.where(ram[None], cB * xB, torch.zeros_like(cB))
+    xs = torch.where(ram[None], xA, xs)
+    xps = torch.where(ram[None], xB, xs)
+    B = terms.sum(1) + tA.sum(1) + tB.sum(1) + pA.sum(1) + pB.sum(1) + kA + kB
     if rig:
-        n0 = lo.shape[1]
-        mag = terms.abs().sum(1) + pA.abs().sum(1) + pB.abs().sum(1) + kA.abs() + kB.abs()
-        econ = U64 * (coef.abs() * torch.maximum(lo_.abs(), hi_.abs())).sum(1) + _g(n0 + 4) * mag
+        mag = terms.abs().sum(1) + tA.abs().sum(1) + tB.abs().sum(1) + pA.abs().sum(1) + pB.abs().sum(1) + \
+            kA.abs() + kB.abs()
+        econ = U64 * (coef.abs() * torch.maximum(lo_.abs(), hi_.abs())).sum(1) + _g(2 * n0 + 4) * mag
         B = B - (eA + eB + econ) * (1 + 1e-6)
+    out = {"B": B, "xs": xs, "xps": xps, "cA": cA, "cB": cB, "coef": coef, "g": None, "lin": None}
     if not need_lin:
-        return B, None, None, xs, coef
-    xa, xb = xs.clone(), xs.clone()
+        return out
+    xa, xb = xs.clone(), xps.clone()
     xa[:, pa] = va.to(dt)
     xb[:, pa] = vb.to(dt)
     zA, oA = _forward_lin(ws, bs, xa, bA[0], rA, alA)
@@ -177,7 +204,9 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
         g["be" + nm] = [torch.where(p == 0, torch.zeros_like(zz),
                                     -p.to(dt) * (zz - torch.where(be_ < 0, torch.where(p > 0, ub, lb), torch.zeros_like(zz))))
                         for zz, p, be_, lb, ub in zip(z, ph, bet, bnd[0], bnd[1])]
-    return B, g, ((zA, rA), (zB, rB)), xs, coef
+    out["g"] = g
+    out["lin"] = ((zA, rA), (zB, rB))
+    return out
 
 
 def _scores(bnd, lin, ph, al):
@@ -205,7 +234,7 @@ def _intercepts(bnd, lin, ph):
 
 
 def _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, beA, beB, t, sc, lin,
-               K: int, j0):
+               K: int, j0, rx=None):
     """Filtered branching: the top-K neurons by relaxation-gap score and the top-K by chord intercept
     are each tried -- both children bounded at the node's parameters with the new multiplier at 0
     (one backward pass each) -- and the neuron whose worse child is best wins."""
@@ -231,9 +260,10 @@ def _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, 
     lA, uA, iA = clamp_bounds(lbA[rows], ubA[rows], pA2)
     lB, uB, iB = clamp_bounds(lbB[rows], ubB[rows], pB2)
     L = lambda v: _layers(v, widths)  # noqa: E731
-    Bc, _, _, _, _ = evaluate(ws32, bs32, lo[rows], hi[rows], pa, va[rows], vb[rows], (L(lA), L(uA)), (L(lB), L(uB)),
-                              L(pA2), L(pB2), L(alA[rows]), L(alB[rows]), L(beA[rows]), L(beB[rows]), t[rows],
-                              rig=False, need_lin=False)
+    rxr = None if rx is None else (rx[0], rx[1][rows], rx[2][rows])
+    Bc = evaluate(ws32, bs32, lo[rows], hi[rows], pa, va[rows], vb[rows], (L(lA), L(uA)), (L(lB), L(uB)),
+                  L(pA2), L(pB2), L(alA[rows]), L(alB[rows]), L(beA[rows]), L(beB[rows]), t[rows],
+                  rig=False, need_lin=False, rx=rxr)["B"]
     Bc = torch.where(iA | iB, torch.full_like(Bc, float("inf")), Bc.float())
     worst = Bc.reshape(R, C, 2).min(2).values
     worst = torch.where(valid, worst, torch.full_like(worst, -float("inf")))
@@ -251,13 +281,15 @@ def clamp_bounds(LB: torch.Tensor, UB: torch.Tensor, ph: torch.Tensor):
 
 def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t,
               iters: int, lr_a: float, lr_b: float, lr_t: float, decay: float = 1.0,
-              lookahead: int = 0, beta_pos: bool = True) -> BetaLevel:
+              lookahead: int = 0, beta_pos: bool = True, rx=None) -> BetaLevel:
     """One BaB level of rows R (the HIP kernel's semantics, csrc/beta.hip): ``iters`` projected-Adam
     steps in fp32 from the rows' current (alpha, beta, t) -- updated IN PLACE to the best iterate --
     then the rigorous fp64 bound, the branching decision and x* at those parameters.
 
     lo, hi [R, n0]; va, vb [R, npa]; LB*/UB* [R, NH] partition bounds (unclamped); ph* [R, NH] int8;
-    al*/be* [R, NH] float32; t [R] float32."""
+    al*/be* [R, NH] float32; t [R] float32.  ``rx`` = (ra [n0] bool, plo, phi [R, n0]): relaxed
+    queries, copy B's RA dims over their own box (:func:`evaluate`); x' RA dims are split too
+    (``split`` = -1 - (n0 + d))."""
     R, n0 = lo.shape
     dev = lo.device
     lbA, ubA, infA = clamp_bounds(LBA, UBA, phA)
@@ -280,8 +312,9 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     b1, b2, eps = 0.9, 0.999, 1e-8
     act = ~infeas
     for it in range(iters):
-        B, g, _, _, _ = evaluate(ws32, bs32, lo, hi, pa, va, vb, bA32, bB32, pA, pB, L32(cur["alA"]), L32(cur["alB"]),
-                                 L32(cur["beA"]), L32(cur["beB"]), ct, rig=False)
+        ev = evaluate(ws32, bs32, lo, hi, pa, va, vb, bA32, bB32, pA, pB, L32(cur["alA"]), L32(cur["alB"]),
+                      L32(cur["beA"]), L32(cur["beB"]), ct, rig=False, rx=rx)
+        B, g = ev["B"], ev["g"]
         imp = act & (B > best)
         best = torch.where(imp, B, best)
         for k in keys:
@@ -321,24 +354,32 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     L64 = lambda v: _layers(v.to(d), widths)  # noqa: E731
     bA, bB = (L64(lbA), L64(ubA)), (L64(lbB), L64(ubB))
     alA64, alB64 = L64(alA), L64(alB)
-    B, _, lin, xs, coef = evaluate(ws64, bs64, lo.to(d), hi.to(d), pa, va.to(d), vb.to(d), bA, bB, pA, pB, alA64,
-                                   alB64, L64(beA), L64(beB), t.to(d), rig=True)
+    ev = evaluate(ws64, bs64, lo.to(d), hi.to(d), pa, va.to(d), vb.to(d), bA, bB, pA, pB, alA64, alB64, L64(beA),
+                  L64(beB), t.to(d), rig=True, rx=rx)
+    B, lin, xs, coef = ev["B"], ev["lin"], ev["xs"], ev["coef"]
     B = torch.where(infeas, torch.full_like(B, float("inf")), B)
     sc = torch.cat([_scores(bA, lin[0], pA, alA64), _scores(bB, lin[1], pB, alB64)], 1)
     mx, j = sc.max(1)
     if lookahead > 0:
         j = _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, beA, beB, t,
-                       sc, lin, lookahead, j)
+                       sc, lin, lookahead, j, rx)
     free = torch.ones(n0, dtype=torch.bool, device=dev)
     free[list(pa)] = False
+    # input split: |coefficient| x width over x's non-PA dims (RA dims: copy A's coefficient) and,
+    # relaxed, x''s RA dims (copy B's); none left: a lattice leaf
+    cx = torch.where(coef != 0, coef, ev["cA"])
     w = torch.where(free[None], (hi - lo).to(d), torch.zeros_like(coef))
-    isc = torch.where(w > 0, coef.abs() * w + 1e-9 * w, torch.full_like(w, -1.0))
+    isc = torch.where(w > 0, cx.abs() * w + 1e-9 * w, torch.full_like(w, -1.0))
+    if rx is not None:
+        wp = torch.where(rx[0][None], (rx[2] - rx[1]).to(d), torch.zeros_like(coef))
+        isc = torch.cat([isc, torch.where(wp > 0, ev["cB"].abs() * wp + 1e-9 * wp, torch.full_like(wp, -1.0))], 1)
     im, dd = isc.max(1)
-    split = torch.where(mx > 0, j, torch.where(im > 0, -1 - dd, torch.full_like(dd, -(n0 + 1))))
+    split = torch.where(mx > 0, j, torch.where(im > 0, -1 - dd, torch.full_like(dd, LEAF(n0))))
     # the split neuron's multipliers that make each child start from this node's relaxation of it
     lam = torch.cat([torch.cat([r[0] for r in lin[0][1]], 1), torch.cat([r[0] for r in lin[1][1]], 1)], 1)
     slope = torch.cat([torch.cat([r[3] for r in lin[0][1]], 1), torch.cat([r[3] for r in lin[1][1]], 1)], 1)
     jj = j.clamp(min=0)[:, None]
     lj, sj = lam.gather(1, jj)[:, 0], slope.gather(1, jj)[:, 0]
     binit = torch.stack([lj * sj, lj * (1 - sj)], 1).to(torch.float32)
-    return BetaLevel(bound=B, split=split, xstar=xs.to(torch.float32), binit=binit)
+    return BetaLevel(bound=B, split=split, xstar=xs.to(torch.float32), binit=binit,
+                     xpstar=ev["xps"].to(torch.float32))

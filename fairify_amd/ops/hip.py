@@ -614,7 +614,7 @@ def _beta_wt(be) -> torch.Tensor:
 
 
 def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t, iters, lr_a, lr_b, lr_t,
-               decay=1.0, lookahead=0, beta_pos=True):
+               decay=1.0, lookahead=0, beta_pos=True, rx=None):
     """One beta-CROWN BaB level on the device (``fa_beta_kernel``, csrc/beta.hip): the rows'
     (alpha, beta, t) are optimised IN PLACE (kept at the best iterate) and their rigorous fp64
     bounds, branching decisions, concretising vertices and child multipliers returned
@@ -646,17 +646,25 @@ def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, b
     split = torch.empty(R, dtype=torch.int32, device=dev)
     xstar = torch.empty(R, n0, **f32)
     binit = torch.empty(R, 2, **f32)
+    xpstar = torch.empty(R, n0, **f32)
+    ramask, plo_c, phi_c = 0, None, None
+    if rx is not None:          # relaxed: copy B's RA dims over [plo, phi]
+        for d in torch.nonzero(rx[0].cpu()).flatten().tolist():
+            ramask |= 1 << int(d)
+        plo_c = _c(rx[1], torch.float32, (R, n0), "plo")
+        phi_c = _c(rx[2], torch.float32, (R, n0), "phi")
     if R:
         rc = ext().beta_level(_net(be), be.flat.data_ptr(), _beta_wt(be).data_ptr(), R, [int(d) for d in pa],
                               lo_c.data_ptr(), hi_c.data_ptr(), va_c.data_ptr(), vb_c.data_ptr(),
                               *[x.data_ptr() for x in bnd], pA.data_ptr(), pB.data_ptr(), par.data_ptr(),
                               t.data_ptr(), scratch.data_ptr(), int(iters), float(lr_a), float(lr_b), float(lr_t),
                               float(decay), int(lookahead), int(bool(beta_pos)), bound.data_ptr(), split.data_ptr(),
-                              xstar.data_ptr(), binit.data_ptr(), _stream(dev))
+                              xstar.data_ptr(), binit.data_ptr(), int(ramask), _ptr(plo_c), _ptr(phi_c),
+                              xpstar.data_ptr(), _stream(dev))
         if rc != 0:
             raise RuntimeError(f"fa_beta_kernel launch failed ({rc}): network not supported by the beta kernel")
         alA.copy_(par[:, 0])
         alB.copy_(par[:, 1])
         beA.copy_(par[:, 2])
         beB.copy_(par[:, 3])
-    return B.BetaLevel(bound=bound, split=split.long(), xstar=xstar, binit=binit)
+    return B.BetaLevel(bound=bound, split=split.long(), xstar=xstar, binit=binit, xpstar=xpstar)

@@ -188,3 +188,44 @@ def test_beta_closes_trained_ac7_residue():
     lo, hi = grid.decode(ids)
     res = BetaBaBSolver(Backend(m), q, BetaConfig(node_budget=200)).solve(lo, hi, m)
     assert (res.status == UNSAT).sum() >= 5, res.status
+
+
+@pytest.mark.parametrize("seed,tau", [(21, 2), (24, 3)])
+def test_beta_bab_relaxed_matches_bruteforce(seed, tau):
+    """Relaxed queries (|x_r - x'_r| <= tau on RA = age, x' unclipped): nodes carry x''s box on the
+    RA dims (split like input dims), the second orientation runs on the negated network; every
+    decided verdict equals enumeration of all (x, x') pairs, every SAT pair is exactly confirmed."""
+    from fairify_amd.spec import ADULT, Query
+
+    q = Query(pa=("sex",), ra=("age",), tau=tau).resolve(ADULT)
+    grid = presets.get("src/AC-sex").grid()
+    ids = processing_order(grid, 0)[:16]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 1)
+    pa, ra = q.pa_idx[0], q.ra_idx[0]
+    m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
+    res = BetaBaBSolver(Backend(m), q, BetaConfig(node_budget=512, iters=20, root_iters=40)).solve(lo, hi, m)
+    decided = 0
+    for k in range(len(ids)):
+        pts = _lattice(lo[k], hi[k])
+        truth = False
+        for s1 in (0, 1):
+            x = pts.copy()
+            x[:, pa] = s1
+            z = m.logits(x)
+            for d in range(-tau, tau + 1):
+                xp = x.copy()
+                xp[:, pa] = 1 - s1
+                xp[:, ra] += d
+                zp = m.logits(xp)
+                if (((z < 0) & (zp > 0)) | ((z > 0) & (zp < 0))).any():
+                    truth = True
+        if res.status[k] == SAT:
+            assert truth, k
+            ok = exact.check_pair_constraints(res.cex_x[k:k + 1], res.cex_xp[k:k + 1], lo[k:k + 1], hi[k:k + 1],
+                                              q.pa_idx, q.ra_idx, q.tau)
+            assert ok[0] and exact.is_violation(m, res.cex_x[k:k + 1], res.cex_xp[k:k + 1])[0]
+        elif res.status[k] == UNSAT:
+            assert not truth, k
+        decided += res.status[k] != UNKNOWN
+    assert decided >= 0.5 * len(ids)

@@ -129,3 +129,79 @@ def test_beta_gpu_closes_trained_ac7_residue(cuda):
     res = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=400)).solve(lo, hi, m)
     assert (res.status == UNSAT).sum() >= 10, res.status
     assert (res.status == SAT).sum() == 0              # the verified LP proves all 12 UNSAT
+
+
+def _true_min_rx(m, lo, hi, plo, phi, pa, ra, va, vb, phA, phB, t):
+    """min of t N(x, va) - (1 - t) N(x', vb) over lattice x in the box and x' = x except its RA dims,
+    which range over [plo, phi] independently (the bound drops the tau tie, so it must hold on this
+    superset), restricted to points satisfying both copies' phases."""
+    import itertools
+
+    X = np.array(list(itertools.product(*[range(int(a), int(b) + 1) for a, b in zip(lo, hi)])), dtype=np.float64)
+    D = np.array(list(itertools.product(*[range(int(plo[r]), int(phi[r]) + 1) for r in ra])), dtype=np.float64)
+
+    def run(h, ph):
+        ok = np.ones(len(h), bool)
+        o = 0
+        for l, (W, b) in enumerate(zip(m.weights, m.biases)):
+            z = h @ np.asarray(W, np.float64) + np.asarray(b, np.float64)
+            if l < len(m.weights) - 1:
+                p = ph[o:o + z.shape[1]]
+                ok &= ((p[None] * z) >= 0).all(1)
+                o += z.shape[1]
+                h = np.maximum(z, 0)
+            else:
+                h = z
+        return h[:, 0], ok
+
+    xa = X.copy()
+    xa[:, pa] = va
+    fa, oka = run(xa, phA)
+    best = np.inf
+    for dv in D:
+        xb = X.copy()
+        xb[:, pa] = vb
+        xb[:, ra] = dv
+        fb, okb = run(xb, phB)
+        ok = oka & okb
+        if ok.any():
+            best = min(best, float((t * fa - (1 - t) * fb)[ok].min()))
+    return best
+
+
+@pytest.mark.parametrize("seed", [0, 2])
+def test_beta_kernel_relaxed_matches_reference_and_is_sound(cuda, seed):
+    m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(seed)
+    R, n0 = lo.shape
+    w = [x.shape[1] for x in ws[:-1]]
+    NH = sum(w)
+    ra = [2]
+    ram = torch.zeros(n0, dtype=torch.bool)
+    ram[ra] = True
+    plo, phi = lo.clone(), hi.clone()
+    plo[:, ra] -= 2
+    phi[:, ra] += 1
+    # copy B's partition bounds over x''s box (RA dims widened), as the solver supplies them
+    rl, rh = plo.clone(), phi.clone()
+    rl[:, pa] = vb
+    rh[:, pa] = vb
+    rb = Backend(m).bounds(rl, rh, keep_layers=True)
+    bnd = [bnd[0], (torch.cat(rb.layer_lb, 1)[:, :NH].float(), torch.cat(rb.layer_ub, 1)[:, :NH].float())]
+    al, be_, t = _params(R, NH, seed, False)
+    lr = dict(lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    cpu = [x.clone() for x in (al[0], al[1], be_[0], be_[1], t)]
+    lr_ = B.level_ref(ws, bs, w, lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1], *cpu,
+                      iters=0, rx=(ram, plo, phi), **lr)
+    d = lambda x: x.to(cuda).contiguous()  # noqa: E731
+    gpu = [d(x.clone()) for x in (al[0], al[1], be_[0], be_[1], t)]
+    lg = hip.beta_level(Backend(m, cuda), d(lo), d(hi), pa, d(va), d(vb), d(bnd[0][0]), d(bnd[0][1]), d(bnd[1][0]),
+                        d(bnd[1][1]), d(ph[0]), d(ph[1]), *gpu, iters=0, rx=(ram, d(plo), d(phi)), **lr)
+    torch.cuda.synchronize()
+    bg = lg.bound.cpu()
+    fin = torch.isfinite(lr_.bound)
+    assert torch.allclose(bg[fin], lr_.bound[fin], rtol=1e-9, atol=1e-9)
+    assert torch.equal(lg.xpstar.cpu()[fin][:, ra], lr_.xpstar[fin][:, ra])
+    for r in range(R):
+        tm = _true_min_rx(m, lo[r].numpy(), hi[r].numpy(), plo[r].numpy(), phi[r].numpy(), pa, ra, va[r].numpy(),
+                          vb[r].numpy(), ph[0][r].numpy(), ph[1][r].numpy(), float(t[r]))
+        assert float(bg[r]) <= tm, (r, float(bg[r]), tm)
