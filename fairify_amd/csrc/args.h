@@ -404,6 +404,7 @@ struct BetaArgs {
   float lr_a, lr_b, lr_t, decay;
   int lookahead;            // candidates per score of the filtered branching (0: best gap score)
   int beta_pos;             // project beta >= 0 (1) or keep it free-signed (0)
+  int stall;                // 1: when no look-ahead candidate's children beat the node, split the input
   int wpb;                  // waves per workgroup
   int wt_lds;               // 1: transposed weights staged in LDS too
   double* bound;            // [R] rigorous lower bound of t N(x,va) - (1-t) N(x,vb) (+inf: empty region)

@@ -626,6 +626,9 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
       }
     }
     if (bj >= 0) jsel = bj;
+    // no candidate's children beat this node: the relaxations are not what keeps it open -- split
+    // the input box instead (as the verified LP does)
+    if (a.stall && (double)bw <= Bd) mx = 0.f;
   }
   // ---- outputs
   if (lane == 0) {

@@ -507,6 +507,7 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t hi, uintptr_t va, uintptr_t vb, uintptr_t LBA, uintptr_t UBA, uintptr_t LBB,
                          uintptr_t UBB, uintptr_t phA, uintptr_t phB, uintptr_t par, uintptr_t t, uintptr_t scratch,
                          int iters, float lr_a, float lr_b, float lr_t, float decay, int lookahead, int beta_pos,
+                         int stall,
                          uintptr_t bound, uintptr_t split, uintptr_t xstar, uintptr_t binit,
                          unsigned long long ramask, uintptr_t plo, uintptr_t phi, uintptr_t xpstar, uintptr_t stream) {
     if (pa.size() > FA_MAX_PA) throw std::invalid_argument("beta_level: too many PA dims");
@@ -540,6 +541,7 @@ PYBIND11_MODULE(_C, m) {
     a.decay = decay;
     a.lookahead = lookahead;
     a.beta_pos = beta_pos;
+    a.stall = stall;
     a.bound = P<double>(bound);
     a.split = P<int>(split);
     a.xstar = P<float>(xstar);

@@ -121,10 +121,13 @@ class VerifyConfig:
                                          # (profiles/r3/shard/diag_models_bench_config.jsonl: 38 % of a
                                          # bench step's nodes were AC-8 / AC-12 escalation spent on
                                          # partitions the relu stage then decided)
-    beta_budget: int = int(os.environ.get("FAIRIFY_BETA_BUDGET", "512"))
+    beta_budget: int = int(os.environ.get("FAIRIFY_BETA_BUDGET", "64"))
                                          # beta-CROWN phase-split BaB (stage "beta", engine/beta_bab.py)
-                                         # on the residue: nodes per partition (0 = off); the anytime
-                                         # rounds grow it x anytime_growth per round
+                                         # on the residue: nodes per partition (0 = off); the trained
+                                         # AC-7 residue closes in 10-60 nodes, the random-init bench
+                                         # residue mostly does not (512 nodes: +3.4 s per step for 147
+                                         # verdicts, gpurun_out/s5_c); the anytime rounds grow it x
+                                         # anytime_growth per round
     beta_min_width: int = 17             # ... on networks whose widest hidden layer is at least this
                                          # (the narrower ones go to the relu stage, whose exact-zero
                                          # concretisation their zero logits need)

@@ -58,6 +58,7 @@ class BetaLevel:
     binit: torch.Tensor       # [R, 2] float32 beta of the split neuron in the (inactive, active) child
     #                           that reproduces this node's relaxation of it (monotone warm start)
     xpstar: Optional[torch.Tensor] = None   # [R, n0] copy B's vertex (relaxed: its RA dims from x''s box)
+    scores: Optional[torch.Tensor] = None   # [R, 2 NH] branching scores (reference only: tests)
 
 
 def LEAF(n0: int) -> int:
@@ -269,7 +270,7 @@ def _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, 
     worst = torch.where(valid, worst, torch.full_like(worst, -float("inf")))
     bw, bi = worst.max(1)
     pick = cand.gather(1, bi[:, None])[:, 0]
-    return torch.where(torch.isfinite(bw) | (bw > 0), pick, j0)
+    return torch.where(torch.isfinite(bw) | (bw > 0), pick, j0), bw
 
 
 def clamp_bounds(LB: torch.Tensor, UB: torch.Tensor, ph: torch.Tensor):
@@ -281,7 +282,7 @@ def clamp_bounds(LB: torch.Tensor, UB: torch.Tensor, ph: torch.Tensor):
 
 def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t,
               iters: int, lr_a: float, lr_b: float, lr_t: float, decay: float = 1.0,
-              lookahead: int = 0, beta_pos: bool = True, rx=None) -> BetaLevel:
+              lookahead: int = 0, beta_pos: bool = True, rx=None, stall: bool = True) -> BetaLevel:
     """One BaB level of rows R (the HIP kernel's semantics, csrc/beta.hip): ``iters`` projected-Adam
     steps in fp32 from the rows' current (alpha, beta, t) -- updated IN PLACE to the best iterate --
     then the rigorous fp64 bound, the branching decision and x* at those parameters.
@@ -361,8 +362,12 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     sc = torch.cat([_scores(bA, lin[0], pA, alA64), _scores(bB, lin[1], pB, alB64)], 1)
     mx, j = sc.max(1)
     if lookahead > 0:
-        j = _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, beA, beB, t,
-                       sc, lin, lookahead, j, rx)
+        j, bw = _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, beA, beB,
+                           t, sc, lin, lookahead, j, rx)
+        if stall:
+            # no candidate's children beat this node: the relaxations are not what keeps it open
+            # -- split the input box instead (as the verified LP does)
+            mx = torch.where(bw.double() <= B, torch.zeros_like(mx), mx)
     free = torch.ones(n0, dtype=torch.bool, device=dev)
     free[list(pa)] = False
     # input split: |coefficient| x width over x's non-PA dims (RA dims: copy A's coefficient) and,
@@ -382,4 +387,4 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     lj, sj = lam.gather(1, jj)[:, 0], slope.gather(1, jj)[:, 0]
     binit = torch.stack([lj * sj, lj * (1 - sj)], 1).to(torch.float32)
     return BetaLevel(bound=B, split=split, xstar=xs.to(torch.float32), binit=binit,
-                     xpstar=ev["xps"].to(torch.float32))
+                     xpstar=ev["xps"].to(torch.float32), scores=sc)
