@@ -53,6 +53,9 @@ class BetaConfig:
     tighten: bool = True             # children: re-bound every hidden neuron over the node's box and
     #                                  phase region (csrc/refine.hip with phases), intersected with
     #                                  the inherited bounds; an empty region closes the node
+    probe_levels: int = 0            # > 0: after this many levels, stop the call unless it has decided
+    probe_yield: float = 0.02        # at least this fraction of its partitions (a residue it does not
+    #                                  converge on -- random-init bench nets -- costs a few levels only)
     beta_pos: bool = True            # split multipliers projected >= 0 (free-signed ones, which may
     #                                  use the interval side, make Adam oscillate around 0: measured
     #                                  8 / 10 -> 0 / 10 trained AC-7 partitions closed, tools/exp)
@@ -238,6 +241,12 @@ class BetaBaBSolver:
             cur = {kk: v[:nb] for kk, v in pool.items()}
             rest = {kk: v[nb:] for kk, v in pool.items()}
             levels += 1
+            if cfg.probe_levels and levels == cfg.probe_levels + 1 and not is_root:
+                dec = int(np.isin(status[run], (SAT, UNSAT)).sum()) + int(self._closed_parts(pool, run, dev))
+                if dec < cfg.probe_yield * run.size:
+                    self.stats["probe_stop"] = self.stats.get("probe_stop", 0) + 1
+                    status[run[status[run] == RUNNING]] = UNKNOWN
+                    break
             np.add.at(nodes_np, cur["part"].cpu().numpy(), 1)
             sc = 1.0 if is_root else cfg.child_lr
             empty = None
@@ -294,6 +303,14 @@ class BetaBaBSolver:
         self.stats["levels"] = self.stats.get("levels", 0) + levels
         self.stats["nodes"] = self.stats.get("nodes", 0) + int(nodes_np.sum())
         return status, cex_x, cex_xp, nodes_np
+
+    @staticmethod
+    def _closed_parts(pool, run, dev) -> int:
+        """RUNNING partitions of ``run`` with no node left in the pool (all their nodes closed)."""
+        left = torch.zeros(int(run.max()) + 1 if run.size else 1, dtype=torch.bool, device=dev)
+        if pool["part"].numel():
+            left[pool["part"]] = True
+        return int((~left[torch.from_numpy(run).to(dev)]).sum())
 
     def _tighten(self, cur, pa, ram=None):
         """Phase-aware bounds of the batch's nodes (both copies in one launch pair; copy B over x',

@@ -128,6 +128,8 @@ class VerifyConfig:
                                          # residue mostly does not (512 nodes: +3.4 s per step for 147
                                          # verdicts, gpurun_out/s5_c); the anytime rounds grow it x
                                          # anytime_growth per round
+    beta_probe_levels: int = 4           # fixed pass: the stage gives up after this many levels unless
+                                         # 2 % of its partitions are decided (0 = never)
     beta_min_width: int = 17             # ... on networks whose widest hidden layer is at least this
                                          # (the narrower ones go to the relu stage, whose exact-zero
                                          # concretisation their zero logits need)
@@ -266,13 +268,15 @@ def _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, limit, worke
 
 
 def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes, status, stage, cex_x, cex_xp, nodes,
-                tm=None):
+                tm=None, probe_levels: int = 0):
     """beta-CROWN BaB (engine/beta_bab.py) on the partitions ``unk``: decided verdicts (sound SAT /
-    UNSAT) written into the stage arrays; returns how many it decided."""
+    UNSAT) written into the stage arrays; returns how many it decided.  ``probe_levels``: give up
+    after that many levels unless 2 % of the partitions are decided by then (BetaConfig)."""
     from .beta_bab import BetaBaBSolver, BetaConfig
 
     bs = BetaBaBSolver(be, q, BetaConfig(node_budget=budget, batch_nodes=min(batch_nodes, 32768),
-                                         time_budget=time_budget), **({"timer": tm} if tm is not None else {}))
+                                         time_budget=time_budget, probe_levels=probe_levels),
+                       **({"timer": tm} if tm is not None else {}))
     br = bs.solve(lo_np[unk], hi_np[unk], mlp)
     dec = np.isin(br.status, (SAT, UNSAT))
     hit = unk[dec]
@@ -613,7 +617,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             el = time.time() - t_start
             with tm("beta"):
                 _beta_round(be, q, mlp, unk, lo_np, hi_np, cfg.beta_budget, max(0.0, budget - el), cfg.batch_nodes,
-                            status, stage, cex_x, cex_xp, nodes, tm)
+                            status, stage, cex_x, cex_xp, nodes, tm, probe_levels=cfg.beta_probe_levels)
             sync()
             t_bab += time.time() - t0
     if esc_after_relu:
@@ -700,9 +704,11 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                     b_budget *= cfg.anytime_growth
                     left = deadline - time.time()
                     if left > 0:
+                        # at most half of what is left: where it does not converge (random-init
+                        # residue) the other stages keep their time
                         with tm("beta"):
-                            ndec = _beta_round(be, q, mlp, unk, lo_np, hi_np, b_budget, left, cfg.batch_nodes, status,
-                                               stage, cex_x, cex_xp, nodes, tm)
+                            ndec = _beta_round(be, q, mlp, unk, lo_np, hi_np, b_budget, 0.5 * left, cfg.batch_nodes,
+                                               status, stage, cex_x, cex_xp, nodes, tm)
                         if ndec < cfg.anytime_min_yield * unk.size:
                             beta_live = False
                     unk = np.nonzero((status == UNKNOWN) & ~forced)[0]

@@ -140,7 +140,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--group", default=None)
     ap.add_argument("--models", default=None)
-    ap.add_argument("--out", default="gpurun_out/r4/base")
+    ap.add_argument("--out", default=os.environ.get("FAIRIFY_BASE_OUT", "gpurun_out/base"))
     ap.add_argument("--head", default=os.environ.get("FAIRIFY_HEAD", ""))
     ap.add_argument("--anytime-budget", type=float, default=120.0, help="tablev: seconds per model")
     ap.add_argument("--all-anytime", action="store_true", help="anytime mode for the other groups too")

@@ -7,6 +7,8 @@
 #   tests[:PYTEST_K]          GPU test tier (optionally -k filter)
 #   bench[:ARGS]              bench.py with ARGS ("_" separates arguments), JSON to OUT/bench*.json
 #   envbench:VAR=VAL[:ARGS]   the same with one environment variable set (A/B of FAIRIFY_* switches)
+#   profpy:SCRIPT[:ARGS]      rocprofv3 --kernel-trace --stats of python SCRIPT ARGS (trace reduced to
+#                             OUT/profN.busy.txt, then deleted)
 #   prof[:ARGS]               rocprofv3 --kernel-trace --stats of bench.py ARGS (the trace csv is
 #                             reduced to OUT/profN.busy.txt (whole run) and OUT/profN.window.txt (timed
 #                             steps only, between bench.py's marker kernels) by tools/trace_busy.py, then deleted;
@@ -50,6 +52,17 @@ for step in "$@"; do
       done
       find $OUT/prof$n -name '*kernel_trace.csv' -delete
       cat $OUT/prof$n.out; [ $rc -ne 0 ] && tail -30 $OUT/prof$n.err ;;
+    profpy)
+      # rocprofv3 kernel trace of any python script: profpy:SCRIPT:ARGS
+      scr=${rest%%:*}; a2=${rest#*:}; [ "$a2" = "$rest" ] && a2=""
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d $ROOT/$OUT/prof$n -o run -- python3 -u $ROOT/$scr ${a2//_/ } > $ROOT/$OUT/prof$n.out 2> $ROOT/$OUT/prof$n.err)
+      rc=$?
+      for t in $(find $OUT/prof$n -name '*kernel_trace.csv'); do
+        python tools/trace_busy.py $t > $OUT/prof$n.busy.txt
+      done
+      find $OUT/prof$n -name '*kernel_trace.csv' -delete
+      tail -5 $OUT/prof$n.out; [ $rc -ne 0 ] && tail -30 $OUT/prof$n.err ;;
     pmc)
       ctr=${rest%%:*}; a2=${rest#*:}; [ "$a2" = "$rest" ] && a2=""
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } --output-format csv \
