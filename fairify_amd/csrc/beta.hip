@@ -530,6 +530,16 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
     if (a.xpstar) a.xpstar[(size_t)r * n0 + i] = S.xps[i];
   }
 
+  // a closed node is not branched: no scores, no look-ahead
+  if (Bd >= 0.0) {
+    if (lane == 0) {
+      a.bound[r] = Bd;
+      a.split[r] = -(2 * n0 + 1);
+      a.binit[2 * r] = 0.f;
+      a.binit[2 * r + 1] = 0.f;
+    }
+    return;
+  }
   // ---- branching scores: |lam| x relaxation gap at x* of unfixed unstable neurons
   for (int c = 0; c < 2; ++c)
     for (int k = lane; k < NH; k += 64) {

@@ -73,9 +73,10 @@ def test_beta_kernel_split_and_binit_match_reference(cuda, seed):
     sg, sr = lg.split.cpu(), lr_.split
     sc = lr_.scores
     for r in range(sg.numel()):
-        if not torch.isfinite(lr_.bound[r]):
-            # an empty region: closed whatever the split (the kernel returns at once with LEAF)
-            assert not torch.isfinite(lg.bound[r].cpu())
+        if not torch.isfinite(lr_.bound[r]) or lr_.bound[r] >= 0:
+            # closed (an empty region, or the bound proves it): never branched, the kernel skips
+            # scores and look-ahead and returns LEAF
+            assert float(lg.bound[r].cpu()) >= 0
             continue
         if sr[r] >= 0:
             assert sg[r] >= 0, (r, int(sg[r]), int(sr[r]))
@@ -84,7 +85,7 @@ def test_beta_kernel_split_and_binit_match_reference(cuda, seed):
                                                                      float(sc[r, sg[r]]), best)
         else:
             assert int(sg[r]) == int(sr[r]), (r, int(sg[r]), int(sr[r]))
-    nb = (sg == sr) & (sr >= 0) & torch.isfinite(lr_.bound)
+    nb = (sg == sr) & (sr >= 0) & (lr_.bound < 0)
     assert torch.allclose(lg.binit.cpu()[nb], lr_.binit[nb], rtol=1e-4, atol=1e-6)
 
 
