@@ -94,6 +94,11 @@ def parse_args(argv=None):
                     help="run the relu stage only on networks whose hidden layers are at most this wide")
     ap.add_argument("--relu-escalate-cap", type=int, default=2048,
                     help="models the relu stage runs on: cap the input-split escalation budget (0 = no cap)")
+    ap.add_argument("--beta-budget", type=int, default=0,
+                    help="beta-CROWN phase-split BaB (stage 'beta') in the fixed passes: nodes per partition "
+                         "(0 = only in the budget pass's anytime rounds).  On this random-init suite its "
+                         "fixed-pass yield is ~60 verdicts per step for +350-420 ms (profiles/r5/bench_ab); on "
+                         "trained nets it decides the residue (profiles/r5/ac7_trained)")
     ap.add_argument("--batch-nodes", type=int, default=65536,
                     help="BaB nodes bounded per sub-batch launch (memory per runtime scales with it)")
     ap.add_argument("--smt", default="none",
@@ -247,6 +252,7 @@ def main() -> None:
                        escalate_max_open=args.escalate_max_open, batch_nodes=args.batch_nodes,
                        smt_backend=args.smt, trust_milp=args.trust_milp, lp_budget=args.lp_budget, relu_budget=args.relu_budget,
                        relu_max_width=args.relu_max_width, relu_escalate_cap=args.relu_escalate_cap,
+                       beta_budget=args.beta_budget,
                        escalate_probation=tuple(tuple(int(v) for v in st.split(":"))
                                                 for st in args.escalate_probation.split(",") if st),
                        escalate_stages=tuple(tuple(int(v) for v in st.split(":")) for st in args.stages.split(",") if st))
@@ -483,6 +489,7 @@ def main() -> None:
                    "escalate_budget": cfg.escalate_budget, "escalate_max_open": cfg.escalate_max_open,
                    "heuristic_node_budget": cfg.heuristic_node_budget, "relu_budget": cfg.relu_budget,
                    "relu_max_width": cfg.relu_max_width, "relu_escalate_cap": cfg.relu_escalate_cap,
+                   "beta_budget": cfg.beta_budget, "anytime_beta": cfg.anytime_beta,
                    "escalate_probation": [list(st) for st in cfg.escalate_probation],
                    "stages": [list(st) for st in cfg.escalate_stages], "heuristic": cfg.heuristic,
                    "batch_nodes": cfg.batch_nodes,

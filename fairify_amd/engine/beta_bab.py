@@ -40,7 +40,7 @@ from .bab import RUNNING, SAT, UNKNOWN, UNSAT, BaBResult, _pa_table, pa_groups
 
 @dataclass
 class BetaConfig:
-    node_budget: int = 512           # nodes per partition (all its pair trees together)
+    node_budget: int = 512           # nodes per partition (all its pair trees together; x Pp / 2)
     iters: int = 64                  # optimisation steps per node (warm-started from the parent)
     root_iters: int = 200            # ... per root node
     lr_a: float = 0.1                # Adam step of the slopes alpha
@@ -217,6 +217,9 @@ class BetaBaBSolver:
             "t": torch.full((R0,), 0.5, **f32),
             "root": torch.ones(R0, dtype=torch.bool, device=dev),
         }
+        # node budget per partition, scaled with its ordered pairs (a multi-valued PA -- race: 20
+        # pairs -- gets the budget a binary one gets per pair)
+        budget = int(cfg.node_budget * max(1.0, Pp / 2.0))
         levels = 0
         timed_out = False
         while pool["part"].numel():
@@ -285,7 +288,7 @@ class BetaBaBSolver:
             grow = ~closed & ~leaf
             run_t = torch.from_numpy(status == RUNNING).to(dev)[cur["part"]]
             grow &= run_t
-            over = torch.from_numpy(nodes_np >= cfg.node_budget).to(dev)[cur["part"]] & grow
+            over = torch.from_numpy(nodes_np >= budget).to(dev)[cur["part"]] & grow
             if bool(over.any()):
                 status[np.unique(cur["part"][over].cpu().numpy())] = UNKNOWN
                 grow &= ~over

@@ -128,6 +128,9 @@ class VerifyConfig:
                                          # residue mostly does not (512 nodes: +3.4 s per step for 147
                                          # verdicts, gpurun_out/s5_c); the anytime rounds grow it x
                                          # anytime_growth per round
+    anytime_beta: int = 64               # anytime rounds: beta BaB nodes per partition of the first round
+                                         # (x anytime_growth per round; 0 = off), independent of the
+                                         # fixed-pass beta_budget
     beta_probe_levels: int = 4           # fixed pass: the stage gives up after this many levels unless
                                          # 2 % of its partitions are decided (0 = never)
     beta_min_width: int = 17             # ... on networks whose widest hidden layer is at least this
@@ -688,9 +691,10 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         relu_any = _relu_supported(q)
         r_budget = max(cfg.relu_budget, 1) if relu_on else 64      # x growth before the first round
         bab_live, relu_live = True, True                          # stages still yielding
-        beta_any = cfg.beta_budget > 0 and _beta_supported(q)      # any width in the anytime rounds
+        beta_any = cfg.anytime_beta > 0 and _beta_supported(q)     # any width in the anytime rounds
         beta_live = beta_any
-        b_budget = max(cfg.beta_budget, 1) // cfg.anytime_growth if not beta_on else cfg.beta_budget
+        b_budget = max(cfg.anytime_beta // cfg.anytime_growth, 1) if not beta_on else max(cfg.beta_budget,
+                                                                                         cfg.anytime_beta)
         with tm("anytime"):
             while True:
                 unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
