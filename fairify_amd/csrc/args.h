@@ -416,4 +416,7 @@ struct BetaArgs {
   const float* plo;
   const float* phi;
   float* xpstar;            // [R, n0] copy B's vertex (RA dims from x''s box), or nullptr
+  float* gtie;              // [R, 2, n0] multipliers of the tie |x_r - x'_r| <= tau (in = start, out =
+                            // best), or nullptr (tie dropped)
+  float tau;
 };

@@ -84,6 +84,7 @@ struct Slab {            // per-wave LDS workspace
   float* cft;            // input coefficients of a look-ahead pass [n0]
   float* xs;             // concretising vertex [n0]
   float* xps;            // copy B's vertex [n0] (relaxed: RA dims from x''s box; else = xs)
+  float* gt[2];          // relaxed: current multipliers gP, gM of the tie |x_r - x'_r| <= tau [n0]
 };
 
 struct Node {            // per-node constants (wave-uniform)
@@ -92,6 +93,8 @@ struct Node {            // per-node constants (wave-uniform)
   const float* plo;      // relaxed: x''s box on the RA dims (ramask), else nullptr
   const float* phi;
   unsigned long long ramask;
+  float tau;             // relaxed: the tie's tolerance (its multipliers in Slab::gt; 0 / none: dropped)
+  bool tie;
   float va[FA_MAX_PA];
   float vb[FA_MAX_PA];
   unsigned long long pamask;
@@ -236,13 +239,23 @@ __device__ T conc(const NetDesc& nd, const Slab& S, const Node& N, const T* cA, 
         S.xps[i] = lo;
       }
     } else if ((N.ramask >> i) & 1ull) {
+      // the tie's multipliers move coefficient between the copies: f >= f + gP (x_r - x'_r - tau)
+      // + gM (x'_r - x_r - tau) on every admissible pair
       const float plo = N.plo[i], phi = N.phi[i];
-      const float xa = cA[i] >= 0 ? lo : hi;
-      const float xb = cB[i] >= 0 ? plo : phi;
-      const T ta = cA[i] * (T)xa;
-      const T tb = cB[i] * (T)xb;
-      part += ta + tb;
-      if (RIG) mag += tabs(ta) + tabs(tb);
+      const T gp = N.tie ? (T)S.gt[0][i] : (T)0, gm = N.tie ? (T)S.gt[1][i] : (T)0;
+      const T ca = cA[i] + (gp - gm);
+      const T cb = cB[i] + (gm - gp);
+      const float xa = ca >= 0 ? lo : hi;
+      const float xb = cb >= 0 ? plo : phi;
+      const T ta = ca * (T)xa;
+      const T tb = cb * (T)xb;
+      const T tt = -(T)N.tau * (gp + gm);
+      part += ta + tb + tt;
+      if (RIG) {
+        mag += tabs(ta) + tabs(tb) + tabs(tt);
+        emag += (T)2 * (tabs(ca) * (T)fmaxf(fabsf(lo), fabsf(hi)) + tabs(cb) * (T)fmaxf(fabsf(plo), fabsf(phi)) +
+                        tabs(tt));
+      }
       if (WX) {
         S.xs[i] = xa;
         S.xps[i] = xb;
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   const int NHp = (NH + 3) & ~3;
   const int n0p = (n0 + 3) & ~3;
   const int mwp = (mw + 3) & ~3;
-  const int slab = 11 * NHp + 4 * mwp + 11 * n0p + 32;
+  const int slab = 11 * NHp + 4 * mwp + 13 * n0p + 32;
   float* base = smem + tot4 * (WTL ? 2 : 1) + wave * slab;
   Slab S;
   S.lb[0] = base; S.ub[0] = base + NHp; S.lb[1] = base + 2 * NHp; S.ub[1] = base + 3 * NHp;
@@ -364,12 +377,16 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   S.cft = reinterpret_cast<float*>(S.hm[1] + n0p);
   S.xs = S.cft + n0p;
   S.xps = S.xs + n0p;
-  int* cand = reinterpret_cast<int*>(S.xps + n0p);     // look-ahead candidates [32]
+  S.gt[0] = S.xps + n0p;
+  S.gt[1] = S.gt[0] + n0p;
+  int* cand = reinterpret_cast<int*>(S.gt[1] + n0p);   // look-ahead candidates [32]
 
   Node N;
   N.lo = a.lo + (size_t)r * n0;
   N.hi = a.hi + (size_t)r * n0;
   N.ramask = a.plo ? a.ramask : 0ull;
+  N.tie = N.ramask && a.gtie;
+  N.tau = a.tau;
   N.plo = a.plo ? a.plo + (size_t)r * n0 : nullptr;
   N.phi = a.phi ? a.phi + (size_t)r * n0 : nullptr;
   N.pamask = 0;
@@ -442,6 +459,17 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
       }
   float tc = a.t[r], tbest = tc, mt = 0.f, vt = 0.f;
   float best = -FLT_MAX;
+  // relaxed: the tie's multipliers of this lane's RA dim (lane = input dim; n0 <= 64)
+  const bool my_ra = N.tie && lane < n0 && ((N.ramask >> lane) & 1ull);
+  float* gio = N.tie ? a.gtie + (size_t)r * 2 * n0 : nullptr;
+  float gbp = 0.f, gbm = 0.f, mgp = 0.f, vgp = 0.f, mgm = 0.f, vgm = 0.f;
+  if (lane < n0) {
+    S.gt[0][lane] = my_ra ? gio[lane] : 0.f;
+    S.gt[1][lane] = my_ra ? gio[n0 + lane] : 0.f;
+    gbp = S.gt[0][lane];
+    gbm = S.gt[1][lane];
+  }
+  wsync();
   float* cA = reinterpret_cast<float*>(S.cf[0]);   // fp32 passes borrow the rigorous arrays
   float* cB = reinterpret_cast<float*>(S.cf[1]);
   const float b1c = 0.9f, b2c = 0.999f;
@@ -455,6 +483,10 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
     if (Bv > best) {
       best = Bv;
       tbest = tc;
+      if (lane < n0) {
+        gbp = S.gt[0][lane];
+        gbm = S.gt[1][lane];
+      }
       for (int l = 0; l < L - 1; ++l)
         for (int j = lane; j < nd.dims[l + 1]; j += 64)
           for (int q = 0; q < 4; ++q) par[q * NH + nd.neuron_off[l] + j] = cur[q * NH + nd.neuron_off[l] + j];
@@ -510,11 +542,30 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
       vt = b2c * vt + (1.f - b2c) * g * g;
       tc = fminf(fmaxf(tc + a.lr_t * dk * (mt / c1) / (sqrtf(vt / c2) + 1e-8f), 0.f), 1.f);
     }
+    if (my_ra) {      // tie multipliers: d/d gP = x_r* - x'_r* - tau, d/d gM = x'_r* - x_r* - tau
+      const float d = S.xs[lane] - S.xps[lane];
+      const float gp = d - N.tau, gm = -d - N.tau;
+      mgp = b1c * mgp + (1.f - b1c) * gp;
+      vgp = b2c * vgp + (1.f - b2c) * gp * gp;
+      mgm = b1c * mgm + (1.f - b1c) * gm;
+      vgm = b2c * vgm + (1.f - b2c) * gm * gm;
+      S.gt[0][lane] = fmaxf(S.gt[0][lane] + a.lr_t * dk * (mgp / c1) / (sqrtf(vgp / c2) + 1e-8f), 0.f);
+      S.gt[1][lane] = fmaxf(S.gt[1][lane] + a.lr_t * dk * (mgm / c1) / (sqrtf(vgm / c2) + 1e-8f), 0.f);
+    }
     dk *= a.decay;
     wsync();
   }
   if (lane == 0) a.t[r] = a.iters > 0 ? tbest : tc;
   const float tf = a.iters > 0 ? tbest : tc;
+  if (a.iters > 0 && lane < n0) {      // the kept (best) tie multipliers
+    S.gt[0][lane] = gbp;
+    S.gt[1][lane] = gbm;
+    if (my_ra) {
+      gio[lane] = gbp;
+      gio[n0 + lane] = gbm;
+    }
+  }
+  wsync();
 
   // ---- rigorous fp64 bound at the kept parameters
   double eA = 0, eB = 0;
@@ -665,8 +716,9 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         if ((N.pamask >> i) & 1ull) continue;
         const bool ra = (N.ramask >> i) & 1ull;
         const float wd = N.hi[i] - N.lo[i];
+        const double dg = ra && N.tie ? (double)S.gt[0][i] - (double)S.gt[1][i] : 0.0;
         if (wd > 0.f) {
-          const float s = (float)fabs(ra ? S.cf[0][i] : S.cf[0][i] + S.cf[1][i]) * wd + 1e-9f * wd;
+          const float s = (float)fabs(ra ? S.cf[0][i] + dg : S.cf[0][i] + S.cf[1][i]) * wd + 1e-9f * wd;
           if (s > bv) {
             bv = s;
             bd = i;
@@ -675,7 +727,7 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         if (ra) {
           const float wp = N.phi[i] - N.plo[i];
           if (wp > 0.f) {
-            const float s = (float)fabs(S.cf[1][i]) * wp + 1e-9f * wp;
+            const float s = (float)fabs(S.cf[1][i] - dg) * wp + 1e-9f * wp;
             if (s > bv) {
               bv = s;
               bd = n0 + i;
@@ -699,7 +751,7 @@ extern "C" size_t fa_beta_slab_floats(const NetDesc& nd) {
   const int NHp = (nd.n_hidden + 3) & ~3;
   const int n0p = (nd.dims[0] + 3) & ~3;
   const int mwp = (nd.max_width + 3) & ~3;
-  return (size_t)(11 * NHp + 4 * mwp + 11 * n0p + 32);
+  return (size_t)(11 * NHp + 4 * mwp + 13 * n0p + 32);
 }
 
 // Launch configuration: waves per workgroup and whether the transposed weights fit in LDS next to

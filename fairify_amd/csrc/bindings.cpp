@@ -509,7 +509,8 @@ PYBIND11_MODULE(_C, m) {
                          int iters, float lr_a, float lr_b, float lr_t, float decay, int lookahead, int beta_pos,
                          int stall,
                          uintptr_t bound, uintptr_t split, uintptr_t xstar, uintptr_t binit,
-                         unsigned long long ramask, uintptr_t plo, uintptr_t phi, uintptr_t xpstar, uintptr_t stream) {
+                         unsigned long long ramask, uintptr_t plo, uintptr_t phi, uintptr_t xpstar, uintptr_t gtie,
+                         float tau, uintptr_t stream) {
     if (pa.size() > FA_MAX_PA) throw std::invalid_argument("beta_level: too many PA dims");
     for (size_t q = 0; q < pa.size(); ++q)
       if (pa[q] < 0 || pa[q] >= net.d.dims[0] || (q && pa[q] <= pa[q - 1]))
@@ -550,6 +551,8 @@ PYBIND11_MODULE(_C, m) {
     a.plo = P<const float>(plo);
     a.phi = P<const float>(phi);
     a.xpstar = P<float>(xpstar);
+    a.gtie = P<float>(gtie);
+    a.tau = tau;
     if ((net.d.dims[0] < 64 && (ramask >> net.d.dims[0])) || (ramask && (!plo || !phi)))
       throw std::invalid_argument("beta_level: RA mask beyond the inputs or no x' box");
     return fa_beta_launch(net.d, a, reinterpret_cast<hipStream_t>(stream));

@@ -216,6 +216,8 @@ class BetaBaBSolver:
             "beA": torch.zeros(R0, NH, **f32), "beB": torch.zeros(R0, NH, **f32),
             "t": torch.full((R0,), 0.5, **f32),
             "root": torch.ones(R0, dtype=torch.bool, device=dev),
+            # relaxed: Lagrange multipliers of the tie |x_r - x'_r| <= tau (RA dims)
+            "gP": torch.zeros(R0, n0, **f32), "gM": torch.zeros(R0, n0, **f32),
         }
         # node budget per partition, scaled with its ordered pairs (a multi-valued PA -- race: 20
         # pairs -- gets the budget a binary one gets per pair)
@@ -256,7 +258,7 @@ class BetaBaBSolver:
             if cfg.tighten and not is_root:
                 with self.tm("beta.tighten"):
                     empty = self._tighten(cur, pa, ram if relaxed else None)
-            rx = (ram, cur["plo"], cur["phi"]) if relaxed else None
+            rx = (ram, cur["plo"], cur["phi"], tau, cur["gP"], cur["gM"]) if relaxed else None
             with self.tm("beta.level"):
                 lev = be.beta_level(cur["lo"], cur["hi"], pa, cur["va"], cur["vb"], cur["LBA"], cur["UBA"],
                                     cur["LBB"], cur["UBB"], cur["phA"], cur["phB"], cur["alA"], cur["alB"],

@@ -150,9 +150,11 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
     """The coupled bound of rows R at the given parameters (per-layer lists), in the dtype of
     ``ws``.  ``rig``: fp64 with every rounding term subtracted (the sound bound).
 
-    ``rx`` = (ra [n0] bool, plo, phi [R, n0]) for relaxed queries: copy B reads x' whose RA dims
-    range over their own box [plo, phi] (unclipped, reference semantics); on those dims the two
-    copies are concretised separately (the tie |x_r - x'_r| <= tau is dropped: only looser).
+    ``rx`` = (ra [n0] bool, plo, phi [R, n0][, tau, gP, gM]) for relaxed queries: copy B reads x'
+    whose RA dims range over their own box [plo, phi] (unclipped, reference semantics); on those dims
+    the two copies are concretised separately, and the tie |x_r - x'_r| <= tau enters through its
+    own Lagrange multipliers gP, gM >= 0 [R, n0] (``f >= f + gP (x_r - x'_r - tau) + gM (x'_r - x_r -
+    tau)`` on every admissible pair; all zero: the tie dropped, as the relu stage does).
     Returns a dict: B [R], g (gradients), lin (per-copy records), xs (x*), xps (x'*), cA, cB."""
     dt = ws[0].dtype
     pa = list(pa)
@@ -179,19 +181,34 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
     coef = torch.where(shared[None], cA + cB, torch.zeros_like(cA))
     xs = torch.where(coef >= 0, lo_, hi_)
     terms = coef * xs
-    xA = torch.where(cA >= 0, lo_, hi_)
-    xB = torch.where(cB >= 0, loB, hiB)
-    tA = torch.where(ram[None], cA * xA, torch.zeros_like(cA))
-    tB = torch.where(ram[None], cB * xB, torch.zeros_like(cB))
+    # the tau tie's multipliers move coefficient between the copies on the RA dims
+    tie = rx is not None and len(rx) > 3 and rx[4] is not None
+    if tie:
+        tau = float(rx[3])
+        gP = torch.where(ram[None], rx[4].to(dt), torch.zeros_like(cA))
+        gM = torch.where(ram[None], rx[5].to(dt), torch.zeros_like(cA))
+        cAe = cA + (gP - gM)
+        cBe = cB + (gM - gP)
+        ktie = -tau * (gP + gM).sum(1)
+    else:
+        cAe, cBe = cA, cB
+        ktie = torch.zeros_like(kA)
+    xA = torch.where(cAe >= 0, lo_, hi_)
+    xB = torch.where(cBe >= 0, loB, hiB)
+    tA = torch.where(ram[None], cAe * xA, torch.zeros_like(cA))
+    tB = torch.where(ram[None], cBe * xB, torch.zeros_like(cB))
     xs = torch.where(ram[None], xA, xs)
     xps = torch.where(ram[None], xB, xs)
-    B = terms.sum(1) + tA.sum(1) + tB.sum(1) + pA.sum(1) + pB.sum(1) + kA + kB
+    B = terms.sum(1) + tA.sum(1) + tB.sum(1) + pA.sum(1) + pB.sum(1) + kA + kB + ktie
     if rig:
         mag = terms.abs().sum(1) + tA.abs().sum(1) + tB.abs().sum(1) + pA.abs().sum(1) + pB.abs().sum(1) + \
-            kA.abs() + kB.abs()
+            kA.abs() + kB.abs() + ktie.abs()
         econ = U64 * (coef.abs() * torch.maximum(lo_.abs(), hi_.abs())).sum(1) + _g(2 * n0 + 4) * mag
+        if tie:     # the RA coefficient sums cA + (gP - gM) etc. and tau (gP + gM)
+            econ = econ + 2 * U64 * torch.where(ram[None], cAe.abs() * hmA + cBe.abs() * hmB, torch.zeros_like(cA)).sum(1) \
+                + 2 * U64 * ktie.abs()
         B = B - (eA + eB + econ) * (1 + 1e-6)
-    out = {"B": B, "xs": xs, "xps": xps, "cA": cA, "cB": cB, "coef": coef, "g": None, "lin": None}
+    out = {"B": B, "xs": xs, "xps": xps, "cA": cAe, "cB": cBe, "coef": coef, "g": None, "lin": None}
     if not need_lin:
         return out
     xa, xb = xs.clone(), xps.clone()
@@ -200,6 +217,9 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
     zA, oA = _forward_lin(ws, bs, xa, bA[0], rA, alA)
     zB, oB = _forward_lin(ws, bs, xb, bB[0], rB, alB)
     g = {"t": oA + oB}
+    if tie:
+        g["gP"] = torch.where(ram[None], xs - xps - tau, torch.zeros_like(xs))
+        g["gM"] = torch.where(ram[None], xps - xs - tau, torch.zeros_like(xs))
     for nm, z, rec, ph, bet, bnd in (("A", zA, rA, phA, beA, bA), ("B", zB, rB, phB, beB, bB)):
         g["al" + nm] = [torch.where(r[1] == 2, r[0] * zz, torch.zeros_like(zz)) for zz, r in zip(z, rec)]
         g["be" + nm] = [torch.where(p == 0, torch.zeros_like(zz),
@@ -261,7 +281,8 @@ def _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, 
     lA, uA, iA = clamp_bounds(lbA[rows], ubA[rows], pA2)
     lB, uB, iB = clamp_bounds(lbB[rows], ubB[rows], pB2)
     L = lambda v: _layers(v, widths)  # noqa: E731
-    rxr = None if rx is None else (rx[0], rx[1][rows], rx[2][rows])
+    rxr = None if rx is None else ((rx[0], rx[1][rows], rx[2][rows]) if len(rx) <= 3 or rx[4] is None else
+                                   (rx[0], rx[1][rows], rx[2][rows], rx[3], rx[4][rows], rx[5][rows]))
     Bc = evaluate(ws32, bs32, lo[rows], hi[rows], pa, va[rows], vb[rows], (L(lA), L(uA)), (L(lB), L(uB)),
                   L(pA2), L(pB2), L(alA[rows]), L(alB[rows]), L(beA[rows]), L(beB[rows]), t[rows],
                   rig=False, need_lin=False, rx=rxr)["B"]
@@ -301,6 +322,11 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     pA, pB = L32(phA), L32(phB)
     keys = ("alA", "alB", "beA", "beB")
     par = {"alA": alA, "alB": alB, "beA": beA, "beB": beB}
+    tie = rx is not None and len(rx) > 3 and rx[4] is not None
+    if tie:                     # the tau tie's multipliers (relaxed): optimised like beta, >= 0
+        keys = keys + ("gP", "gM")
+        par["gP"], par["gM"] = rx[4], rx[5]
+    rxc = lambda c: rx if not tie else (rx[0], rx[1], rx[2], rx[3], c["gP"], c["gM"])  # noqa: E731
     best = torch.full((R,), -float("inf"), dtype=torch.float32, device=dev)
     bestp = {k: v.clone() for k, v in par.items()}
     best_t = t.clone()
@@ -314,7 +340,7 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     act = ~infeas
     for it in range(iters):
         ev = evaluate(ws32, bs32, lo, hi, pa, va, vb, bA32, bB32, pA, pB, L32(cur["alA"]), L32(cur["alB"]),
-                      L32(cur["beA"]), L32(cur["beB"]), ct, rig=False, rx=rx)
+                      L32(cur["beA"]), L32(cur["beB"]), ct, rig=False, rx=rxc(cur))
         B, g = ev["B"], ev["g"]
         imp = act & (B > best)
         best = torch.where(imp, B, best)
@@ -328,14 +354,14 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
         c2 = 1 - b2 ** (it + 1)
         dk = decay ** it
         for k in keys:
-            gk = torch.cat(g[k], 1)
+            gk = torch.cat(g[k], 1) if isinstance(g[k], list) else g[k]
             m[k] = b1 * m[k] + (1 - b1) * gk
             vv[k] = b2 * vv[k] + (1 - b2) * gk * gk
-            lr = (lr_a if k.startswith("al") else lr_b) * dk
+            lr = (lr_a if k.startswith("al") else (lr_t if k.startswith("g") else lr_b)) * dk
             x = cur[k] + lr * (m[k] / c1) / ((vv[k] / c2).sqrt() + eps)
             if k.startswith("al"):
                 x = x.clamp(0, 1)
-            elif beta_pos:
+            elif beta_pos or k.startswith("g"):
                 x = x.clamp(min=0)
             cur[k] = torch.where(act[:, None], x, cur[k])
         mt = b1 * mt + (1 - b1) * g["t"]
@@ -356,7 +382,7 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     bA, bB = (L64(lbA), L64(ubA)), (L64(lbB), L64(ubB))
     alA64, alB64 = L64(alA), L64(alB)
     ev = evaluate(ws64, bs64, lo.to(d), hi.to(d), pa, va.to(d), vb.to(d), bA, bB, pA, pB, alA64, alB64, L64(beA),
-                  L64(beB), t.to(d), rig=True, rx=rx)
+                  L64(beB), t.to(d), rig=True, rx=rxc(par))
     B, lin, xs, coef = ev["B"], ev["lin"], ev["xs"], ev["coef"]
     B = torch.where(infeas, torch.full_like(B, float("inf")), B)
     sc = torch.cat([_scores(bA, lin[0], pA, alA64), _scores(bB, lin[1], pB, alB64)], 1)

@@ -647,12 +647,18 @@ def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, b
     xstar = torch.empty(R, n0, **f32)
     binit = torch.empty(R, 2, **f32)
     xpstar = torch.empty(R, n0, **f32)
-    ramask, plo_c, phi_c = 0, None, None
+    ramask, plo_c, phi_c, gt, tau = 0, None, None, None, 0.0
     if rx is not None:          # relaxed: copy B's RA dims over [plo, phi]
         for d in torch.nonzero(rx[0].cpu()).flatten().tolist():
             ramask |= 1 << int(d)
         plo_c = _c(rx[1], torch.float32, (R, n0), "plo")
         phi_c = _c(rx[2], torch.float32, (R, n0), "phi")
+        if len(rx) > 3 and rx[4] is not None:       # the tau tie's multipliers (in / out)
+            tau = float(rx[3])
+            for x, nm in ((rx[4], "gP"), (rx[5], "gM")):
+                if tuple(x.shape) != (R, n0) or x.dtype != torch.float32:
+                    raise ValueError(f"{nm}: expected float32 [{R}, {n0}]")
+            gt = torch.stack([rx[4], rx[5]], 1).contiguous()       # [R, 2, n0]
     if R:
         rc = ext().beta_level(_net(be), be.flat.data_ptr(), _beta_wt(be).data_ptr(), R, [int(d) for d in pa],
                               lo_c.data_ptr(), hi_c.data_ptr(), va_c.data_ptr(), vb_c.data_ptr(),
@@ -661,9 +667,12 @@ def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, b
                               float(decay), int(lookahead), int(bool(beta_pos)), int(bool(stall)), bound.data_ptr(),
                               split.data_ptr(),
                               xstar.data_ptr(), binit.data_ptr(), int(ramask), _ptr(plo_c), _ptr(phi_c),
-                              xpstar.data_ptr(), _stream(dev))
+                              xpstar.data_ptr(), _ptr(gt), float(tau), _stream(dev))
         if rc != 0:
             raise RuntimeError(f"fa_beta_kernel launch failed ({rc}): network not supported by the beta kernel")
+        if gt is not None:
+            rx[4].copy_(gt[:, 0])
+            rx[5].copy_(gt[:, 1])
         alA.copy_(par[:, 0])
         alB.copy_(par[:, 1])
         beA.copy_(par[:, 2])

@@ -145,7 +145,7 @@ def test_beta_gpu_closes_trained_ac7_residue(cuda):
     assert (res.status == SAT).sum() == 0              # the verified LP proves all 12 UNSAT
 
 
-def _true_min_rx(m, lo, hi, plo, phi, pa, ra, va, vb, phA, phB, t):
+def _true_min_rx(m, lo, hi, plo, phi, pa, ra, va, vb, phA, phB, t, tau=None):
     """min of t N(x, va) - (1 - t) N(x', vb) over lattice x in the box and x' = x except its RA dims,
     which range over [plo, phi] independently (the bound drops the tau tie, so it must hold on this
     superset), restricted to points satisfying both copies' phases."""
@@ -178,13 +178,15 @@ def _true_min_rx(m, lo, hi, plo, phi, pa, ra, va, vb, phA, phB, t):
         xb[:, ra] = dv
         fb, okb = run(xb, phB)
         ok = oka & okb
+        if tau is not None:         # the tie |x_r - x'_r| <= tau (a bound using its multipliers)
+            ok &= (np.abs(X[:, ra] - dv[None]) <= tau).all(1)
         if ok.any():
             best = min(best, float((t * fa - (1 - t) * fb)[ok].min()))
     return best
 
 
-@pytest.mark.parametrize("seed", [0, 2])
-def test_beta_kernel_relaxed_matches_reference_and_is_sound(cuda, seed):
+@pytest.mark.parametrize("seed,tie", [(0, False), (2, False), (0, True), (3, True)])
+def test_beta_kernel_relaxed_matches_reference_and_is_sound(cuda, seed, tie):
     m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(seed)
     R, n0 = lo.shape
     w = [x.shape[1] for x in ws[:-1]]
@@ -193,7 +195,7 @@ def test_beta_kernel_relaxed_matches_reference_and_is_sound(cuda, seed):
     ram = torch.zeros(n0, dtype=torch.bool)
     ram[ra] = True
     plo, phi = lo.clone(), hi.clone()
-    plo[:, ra] -= 2
+    plo[:, ra] -= 1
     phi[:, ra] += 1
     # copy B's partition bounds over x''s box (RA dims widened), as the solver supplies them
     rl, rh = plo.clone(), phi.clone()
@@ -204,12 +206,18 @@ def test_beta_kernel_relaxed_matches_reference_and_is_sound(cuda, seed):
     al, be_, t = _params(R, NH, seed, False)
     lr = dict(lr_a=0.1, lr_b=0.5, lr_t=0.1)
     cpu = [x.clone() for x in (al[0], al[1], be_[0], be_[1], t)]
+    tau = 1.0
+    g = torch.Generator().manual_seed(seed + 100)
+    gP = torch.rand(R, n0, generator=g) * ram.float()
+    gM = torch.rand(R, n0, generator=g) * ram.float()
+    rxc = (ram, plo, phi, tau, gP.clone(), gM.clone()) if tie else (ram, plo, phi)
     lr_ = B.level_ref(ws, bs, w, lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1], *cpu,
-                      iters=0, rx=(ram, plo, phi), **lr)
+                      iters=0, rx=rxc, **lr)
     d = lambda x: x.to(cuda).contiguous()  # noqa: E731
     gpu = [d(x.clone()) for x in (al[0], al[1], be_[0], be_[1], t)]
+    rxg = (ram, d(plo), d(phi), tau, d(gP), d(gM)) if tie else (ram, d(plo), d(phi))
     lg = hip.beta_level(Backend(m, cuda), d(lo), d(hi), pa, d(va), d(vb), d(bnd[0][0]), d(bnd[0][1]), d(bnd[1][0]),
-                        d(bnd[1][1]), d(ph[0]), d(ph[1]), *gpu, iters=0, rx=(ram, d(plo), d(phi)), **lr)
+                        d(bnd[1][1]), d(ph[0]), d(ph[1]), *gpu, iters=0, rx=rxg, **lr)
     torch.cuda.synchronize()
     bg = lg.bound.cpu()
     fin = torch.isfinite(lr_.bound)
@@ -217,5 +225,5 @@ def test_beta_kernel_relaxed_matches_reference_and_is_sound(cuda, seed):
     assert torch.equal(lg.xpstar.cpu()[fin][:, ra], lr_.xpstar[fin][:, ra])
     for r in range(R):
         tm = _true_min_rx(m, lo[r].numpy(), hi[r].numpy(), plo[r].numpy(), phi[r].numpy(), pa, ra, va[r].numpy(),
-                          vb[r].numpy(), ph[0][r].numpy(), ph[1][r].numpy(), float(t[r]))
+                          vb[r].numpy(), ph[0][r].numpy(), ph[1][r].numpy(), float(t[r]), tau if tie else None)
         assert float(bg[r]) <= tm, (r, float(bg[r]), tm)
