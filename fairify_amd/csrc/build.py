@@ -34,7 +34,11 @@ def _flags(debug: bool):
     opt = ["-O0", "-g"] if debug else ["-O3"]
     # FAIRIFY_HIPCC_DEFINES="A=1 B=2": extra -D flags (occupancy A/B builds, tools/variants)
     defs = ["-D" + d for d in os.environ.get("FAIRIFY_HIPCC_DEFINES", "").split() if d]
-    return inc + opt + defs + ["-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+    # loops bounded by a template tile count but exited early at the layer's width ("if (t >= tin)
+    # break") unroll only up to LLVM's upper-bound limit of 8 trips: the 10-tile kernels (BM-4's
+    # 150-wide layer) kept their operand arrays in scratch (points 656 B/lane, refine 336 B/lane)
+    unroll = ["-mllvm", "-unroll-max-upperbound=16"]
+    return inc + opt + defs + unroll + ["-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 
 def _newer(src: str, obj: str, headers) -> bool:

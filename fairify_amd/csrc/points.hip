@@ -141,7 +141,11 @@ PointKernel select_point(int TM) {
   if (TM <= 2) return fa_point_kernel<2>;
   if (TM <= 4) return fa_point_kernel<4>;
   if (TM <= 7) return fa_point_kernel<7>;
-  return nullptr;   // wider layers (BM-4's 150) would spill: the caller falls back to IBP
+  // BM-4's 150-wide layer: the unroller gives up on the 10x10-tile body and the operand arrays
+  // live in scratch (656 B/lane), still far cheaper than the IBP fallback, which stages each
+  // layer's W per box row (one 90 KB row per workgroup: G = 1)
+  if (TM <= 10) return fa_point_kernel<10>;
+  return nullptr;   // wider layers: the caller falls back to IBP
 }
 
 int point_cus() {
@@ -205,4 +209,4 @@ extern "C" int fa_point_try_launch(const NetDesc& net, BoundArgs a, hipStream_t 
 }
 
 FA_LDS_REGISTER(FA_LDS_K(fa_point_kernel<1>), FA_LDS_K(fa_point_kernel<2>), FA_LDS_K(fa_point_kernel<4>),
-                FA_LDS_K(fa_point_kernel<7>));
+                FA_LDS_K(fa_point_kernel<7>), FA_LDS_K(fa_point_kernel<10>));

@@ -218,7 +218,9 @@ class BetaBaBSolver:
             "root": torch.ones(R0, dtype=torch.bool, device=dev),
             # relaxed: Lagrange multipliers of the tie |x_r - x'_r| <= tau (RA dims)
             "gP": torch.zeros(R0, n0, **f32), "gM": torch.zeros(R0, n0, **f32),
+            "tree": torch.arange(R0, device=dev),        # the (partition, ordered pair) root
         }
+        tree_run = run[k.cpu().numpy()]
         # node budget per partition, scaled with its ordered pairs (a multi-valued PA -- race: 20
         # pairs -- gets the budget a binary one gets per pair)
         budget = int(cfg.node_budget * max(1.0, Pp / 2.0))
@@ -247,7 +249,11 @@ class BetaBaBSolver:
             rest = {kk: v[nb:] for kk, v in pool.items()}
             levels += 1
             if cfg.probe_levels and levels == cfg.probe_levels + 1 and not is_root:
-                dec = int(np.isin(status[run], (SAT, UNSAT)).sum()) + int(self._closed_parts(pool, run, dev))
+                # progress in partitions: decided ones, plus closed pair trees of running ones in
+                # units of Pp (a race partition needs all 20 of its trees closed)
+                dec = int(np.isin(status[run], (SAT, UNSAT)).sum())
+                dec += self._closed_trees(pool, R0, tree_run, status) / Pp
+                self.stats["probe_yield"] = dec / run.size
                 if dec < cfg.probe_yield * run.size:
                     self.stats["probe_stop"] = self.stats.get("probe_stop", 0) + 1
                     status[run[status[run] == RUNNING]] = UNKNOWN
@@ -310,12 +316,12 @@ class BetaBaBSolver:
         return status, cex_x, cex_xp, nodes_np
 
     @staticmethod
-    def _closed_parts(pool, run, dev) -> int:
-        """RUNNING partitions of ``run`` with no node left in the pool (all their nodes closed)."""
-        left = torch.zeros(int(run.max()) + 1 if run.size else 1, dtype=torch.bool, device=dev)
-        if pool["part"].numel():
-            left[pool["part"]] = True
-        return int((~left[torch.from_numpy(run).to(dev)]).sum())
+    def _closed_trees(pool, R0: int, tree_run, status) -> int:
+        """Pair trees of RUNNING partitions with no node left in the pool."""
+        left = np.zeros(R0, dtype=bool)
+        if pool["tree"].numel():
+            left[pool["tree"].cpu().numpy()] = True
+        return int((~left & (status[tree_run] == RUNNING)).sum())
 
     def _tighten(self, cur, pa, ram=None):
         """Phase-aware bounds of the batch's nodes (both copies in one launch pair; copy B over x',

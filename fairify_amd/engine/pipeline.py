@@ -15,6 +15,7 @@ the work (BaB node expansions), so the 24 CSV columns keep their meaning.
 from __future__ import annotations
 
 import os
+import sys
 import time
 from dataclasses import dataclass, field, replace
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -280,8 +281,12 @@ def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes,
     bs = BetaBaBSolver(be, q, BetaConfig(node_budget=budget, batch_nodes=min(batch_nodes, 32768),
                                          time_budget=time_budget, probe_levels=probe_levels),
                        **({"timer": tm} if tm is not None else {}))
+    t0 = time.time()
     br = bs.solve(lo_np[unk], hi_np[unk], mlp)
     dec = np.isin(br.status, (SAT, UNSAT))
+    if os.environ.get("FAIRIFY_BETA_LOG"):
+        print(f"[beta] {unk.size} partitions, budget {budget}: decided {int(dec.sum())} in "
+              f"{time.time() - t0:.2f} s, {bs.stats}", file=sys.stderr, flush=True)
     hit = unk[dec]
     status[hit] = br.status[dec]
     stage[hit] = "beta"

@@ -227,17 +227,18 @@ def test_certify_matches_reference(cuda):
     assert bool((a.score[differ].abs() <= tol[differ]).all())
 
 
-@pytest.mark.parametrize("model", ["AC-3", "AC-7"])
-def test_sim_reg_kernel_relaxed_matches_tile_kernel(cuda, monkeypatch, model):
-    """Relaxed queries on the register-resident simulation kernel (x' rows with the tile kernel's RA
-    offsets): activation counts equal the 64-row tile kernel's up to rounding-ambiguous samples
-    (compared in total), every witness is an exact violation within the pair constraints, and the
-    found sets agree on >= 99 % of the partitions."""
+@pytest.mark.parametrize("model,relaxed", [("AC-3", True), ("AC-7", True), ("AC-3", False), ("AC-7", False)])
+def test_sim_reg_kernel_relaxed_matches_tile_kernel(cuda, monkeypatch, model, relaxed):
+    """The register-resident simulation kernel against the 64-row tile kernel, relaxed queries
+    (x' rows with the tile kernel's RA offsets) and a plain multi-valued PA (race): activation
+    counts equal up to rounding-ambiguous samples (compared in total), every witness is an exact
+    violation within the pair constraints, and the found sets agree on >= 99 % of the
+    partitions."""
     from fairify_amd.engine import exact
     from fairify_amd.engine.sim import simulate
     from fairify_amd.partition import Grid
 
-    q = Query(("sex",), ("age",), 5).resolve(ADULT)
+    q = (Query(("sex",), ("age",), 5) if relaxed else Query(("race",))).resolve(ADULT)
     grid = Grid.reference(ADULT, 10)
     ids = np.arange(0, 16000, 37)[:256]
     lo, hi = grid.decode(ids)
