@@ -132,8 +132,9 @@ class VerifyConfig:
     anytime_beta: int = 64               # anytime rounds: beta BaB nodes per partition of the first round
                                          # (x anytime_growth per round; 0 = off), independent of the
                                          # fixed-pass beta_budget
-    beta_probe_levels: int = 4           # fixed pass: the stage gives up after this many levels unless
-                                         # 2 % of its partitions are decided (0 = never)
+    # fixed pass: the stage gives up after this many levels unless 2 % of its partitions are decided
+    # (closed pair trees count 1 / Pp each; 0 = never)
+    beta_probe_levels: int = int(os.environ.get("FAIRIFY_BETA_PROBE", "4"))
     beta_min_width: int = 17             # ... on networks whose widest hidden layer is at least this
                                          # (the narrower ones go to the relu stage, whose exact-zero
                                          # concretisation their zero logits need)
