@@ -104,6 +104,12 @@ struct Net {
       d.pack_floats = d.pack_g * 256 + (d.n_layers - 1) * 256 + d.n_layers * 16;
       total_floats += d.pack_floats;
     }
+    // backward operand order block (ops/backend.py: mfma_back_block)
+    d.wback_off = total_floats;
+    int wb = 0;
+    for (int l = 0; l < d.n_layers; ++l) wb += ((dims[l] + 15) / 16) * ((dims[l + 1] + 15) / 16) * 256;
+    d.wback_floats = wb;
+    total_floats += wb;
   }
   int n_params;
   int total_floats;

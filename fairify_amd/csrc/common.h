@@ -41,6 +41,11 @@ struct NetDesc {
   int pack_g;
   int pack_off;
   int pack_floats;
+  // backward (transposed) operand order of every layer's W, read straight from global memory by
+  // the back-substitution kernel when the staged copy would crowd its per-row LDS state out
+  // (csrc/refine.hip, BM-4): per layer [ot][t][lane][i] = W[16 ot + (lane&15)][16 t + 4(lane>>4) + i]
+  int wback_off;
+  int wback_floats;
 };
 
 // lowbias32 (Wellons) — identical to ops/reference.py:hash32

@@ -107,7 +107,11 @@ __device__ __forceinline__ void fa_refine_records(const NetDesc& net, const Boun
   }
 }
 
-template <int TM>
+// WG: the weights are read from the global backward-order block (NetDesc.wback_off; w_lds are
+// offsets into it) instead of being staged: a 150-wide net's staged W (112 KB for BM-4) left LDS
+// for one box row per workgroup.  A wave reads one float4 per lane per 8 MFMAs (256 cycles),
+// ~4 B/clk, which L2 sustains for every wave of a CU.
+template <int TM, bool WG = false>
 __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a, RefineCfg cfg) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -117,17 +121,20 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
   for (int l = 0; l < LW; ++l) {
     const int nin = net.dims[l], nout = net.dims[l + 1];
     const int tin = (nin + 15) >> 4, tout = (nout + 15) >> 4;
-    const float* W = a.flat + net.w_off[l];
-    float* dst = smem + cfg.w_lds[l];
-    const int tot = tin * tout * 256;
-    for (int e = tid; e < tot; e += 256) {
-      const int i4 = e & 3, ln = (e >> 2) & 63, tt = e >> 8;
-      const int t = tt % tout, ot = tt / tout;
-      const int in = 16 * ot + (ln & 15), out = 16 * t + 4 * (ln >> 4) + i4;
-      dst[e] = (in < nin && out < nout) ? W[(size_t)in * nout + out] : 0.f;
+    if (!WG) {
+      const float* W = a.flat + net.w_off[l];
+      float* dst = smem + cfg.w_lds[l];
+      const int tot = tin * tout * 256;
+      for (int e = tid; e < tot; e += 256) {
+        const int i4 = e & 3, ln = (e >> 2) & 63, tt = e >> 8;
+        const int t = tt % tout, ot = tt / tout;
+        const int in = 16 * ot + (ln & 15), out = 16 * t + 4 * (ln >> 4) + i4;
+        dst[e] = (in < nin && out < nout) ? W[(size_t)in * nout + out] : 0.f;
+      }
     }
     for (int e = tid; e < nout; e += 256) smem[cfg.b_lds[l] + e] = a.flat[net.b_off[l] + e];
   }
+  const float* wsrc = WG ? a.flat + net.wback_off : smem;
   const int lane = tid & 63, col = lane & 15, grp = lane >> 4;
   const int wave = tid >> 6;
   const int n0 = net.dims[0];
@@ -205,7 +212,7 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
       const int ktop = net.dims[k];                  // width of h_{k-1}
       const int offk = net.neuron_off[k];
       const int tk = (nk + 15) >> 4;                 // output tiles of W_k (staged layout)
-      const float* wk = smem + cfg.w_lds[k];
+      const float* wk = wsrc + cfg.w_lds[k];
       // ---- the columns of this layer: both bounds of every UNSTABLE neuron of a running row (a
       // stable neuron's relaxation is exact whatever its interval, so tightening it buys nothing);
       // the logit: every running row
@@ -287,7 +294,7 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
               er += neg ? 3.f * u * (fabsf(m) * q.w + fabsf(tt)) : 0.f;
             }
           }
-          const float4* wb = reinterpret_cast<const float4*>(smem + cfg.w_lds[l]);
+          const float4* wb = reinterpret_cast<const float4*>(wsrc + cfg.w_lds[l]);
           const float gn = fa_rgam(2 * n + 1, u);
 #pragma unroll
           for (int ot = 0; ot < TM; ++ot) {
@@ -403,13 +410,21 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
 
 namespace {
 typedef void (*RefineKernel)(NetDesc, BoundArgs, RefineCfg);
-RefineKernel select_refine(int TM) {
+RefineKernel select_refine(int TM, bool wg) {
   if (TM <= 1) return fa_refine_kernel<1>;
   if (TM <= 2) return fa_refine_kernel<2>;
   if (TM <= 4) return fa_refine_kernel<4>;
-  if (TM <= 7) return fa_refine_kernel<7>;
-  if (TM <= 10) return fa_refine_kernel<10>;
+  if (TM <= 7) return wg ? fa_refine_kernel<7, true> : fa_refine_kernel<7>;
+  if (TM <= 10) return wg ? fa_refine_kernel<10, true> : fa_refine_kernel<10>;
   return nullptr;
+}
+
+// global-weights variant above this many staged bytes (FAIRIFY_REFINE_WG_KB: A/B and the
+// bitwise-equality test; 0 = never; read per launch)
+size_t refine_wg_bytes() {
+  const char* e = getenv("FAIRIFY_REFINE_WG_KB");
+  const long kb = e ? atol(e) : 64;
+  return kb > 0 ? (size_t)kb * 1024 : (size_t)-1;
 }
 
 int refine_cus() {
@@ -430,17 +445,19 @@ int backward_launch(const NetDesc& net, const BoundArgs& a, int full, int logit,
   const int L = net.n_layers;
   int TM = 1;
   for (int l = 0; l < L; ++l) TM = std::max(TM, (net.dims[l] + 15) / 16);
-  const RefineKernel k = select_refine(TM);
-  if (!k) return -1;
   RefineCfg cfg{};
   cfg.full = full;
   cfg.logit = logit;
   const int LW = (full || logit) ? L : L - 1;
   int offs = 0;
   for (int l = 0; l < LW; ++l) {
-    cfg.w_lds[l] = offs;
+    cfg.w_lds[l] = offs;   // the LDS layout, and (WG) the same offsets in the global block
     offs += ((net.dims[l] + 15) / 16) * ((net.dims[l + 1] + 15) / 16) * 256;
   }
+  const bool wg = (size_t)offs * sizeof(float) > refine_wg_bytes() && TM >= 5 && net.wback_floats >= offs;
+  const RefineKernel k = select_refine(TM, wg);
+  if (!k) return -1;
+  if (wg) offs = 0;        // nothing staged: the biases start the LDS
   for (int l = 0; l < LW; ++l) {
     cfg.b_lds[l] = offs;
     offs += net.dims[l + 1];
@@ -522,5 +539,6 @@ extern "C" int fa_backward_launch(const NetDesc& net, BoundArgs a, hipStream_t s
   return backward_launch(net, a, 1, 1, stream);
 }
 
+FA_LDS_REGISTER(FA_LDS_K((fa_refine_kernel<7, true>)), FA_LDS_K((fa_refine_kernel<10, true>)));
 FA_LDS_REGISTER(FA_LDS_K(fa_refine_kernel<1>), FA_LDS_K(fa_refine_kernel<2>), FA_LDS_K(fa_refine_kernel<4>),
                 FA_LDS_K(fa_refine_kernel<7>), FA_LDS_K(fa_refine_kernel<10>));

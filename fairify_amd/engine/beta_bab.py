@@ -53,9 +53,10 @@ class BetaConfig:
     tighten: bool = True             # children: re-bound every hidden neuron over the node's box and
     #                                  phase region (csrc/refine.hip with phases), intersected with
     #                                  the inherited bounds; an empty region closes the node
-    probe_levels: int = 0            # > 0: after this many levels, stop the call unless it has decided
-    probe_yield: float = 0.02        # at least this fraction of its partitions (a residue it does not
-    #                                  converge on -- random-init bench nets -- costs a few levels only)
+    probe_levels: int = 0            # > 0: once 2 x this many nodes per pair tree are expanded, stop
+    probe_yield: float = 0.02        # the call unless it has decided at least this fraction of its
+    #                                  partitions (closed pair trees count 1 / Pp each): a residue it
+    #                                  does not converge on -- random-init bench nets -- costs little
     beta_pos: bool = True            # split multipliers projected >= 0 (free-signed ones, which may
     #                                  use the interval side, make Adam oscillate around 0: measured
     #                                  8 / 10 -> 0 / 10 trained AC-7 partitions closed, tools/exp)
@@ -225,6 +226,7 @@ class BetaBaBSolver:
         # pairs -- gets the budget a binary one gets per pair)
         budget = int(cfg.node_budget * max(1.0, Pp / 2.0))
         levels = 0
+        probed = False
         timed_out = False
         while pool["part"].numel():
             if time.time() - t0 > time_budget:
@@ -248,7 +250,12 @@ class BetaBaBSolver:
             cur = {kk: v[:nb] for kk, v in pool.items()}
             rest = {kk: v[nb:] for kk, v in pool.items()}
             levels += 1
-            if cfg.probe_levels and levels == cfg.probe_levels + 1 and not is_root:
+            # the probe point: 2 probe_levels nodes expanded per pair tree (a binary tree of depth
+            # ~probe_levels - 1), not a batch count -- a race partition has 20 trees, and its first
+            # batches hold only a slice of one level
+            if cfg.probe_levels and not probed and not is_root and \
+                    int(nodes_np.sum()) >= 2 * cfg.probe_levels * R0:
+                probed = True
                 # progress in partitions: decided ones, plus closed pair trees of running ones in
                 # units of Pp (a race partition needs all 20 of its trees closed)
                 dec = int(np.isin(status[run], (SAT, UNSAT)).sum())

@@ -36,6 +36,24 @@ def mfma_weight_block(weights, biases) -> np.ndarray:
     return np.concatenate([out, np.zeros((-len(out)) % 4, np.float32)])
 
 
+def mfma_back_block(weights) -> np.ndarray:
+    """Weights in backward (transposed) MFMA operand order, read from global memory by
+    csrc/refine.hip when staging them would leave too little LDS for its per-row state: per layer
+    [ot][t][lane][i] = W[16 ot + (lane&15)][16 t + 4(lane>>4) + i] (zero padded), ot over input
+    tiles, t over output tiles -- the layout that kernel stages into LDS.  Must match
+    ``Net::wback_off`` / ``wback_floats`` in csrc/bindings.cpp (appended last)."""
+    parts = []
+    lane = np.arange(64)
+    for W in weights:
+        n_in, n_out = W.shape
+        tin, tout = (n_in + 15) // 16, (n_out + 15) // 16
+        Wp = np.zeros((16 * tin, 16 * tout), np.float32)
+        Wp[:n_in, :n_out] = W
+        ot, t, ln, i = np.meshgrid(np.arange(tin), np.arange(tout), lane, np.arange(4), indexing="ij")
+        parts.append(Wp[16 * ot + (ln & 15), 16 * t + 4 * (ln >> 4) + i].reshape(-1))
+    return np.concatenate(parts)
+
+
 def pack_groups(dims) -> int:
     """Boxes packed per 16-row MFMA tile by the symbolic kernel for narrow single-tile networks
     (csrc/symbolic.hip, ``PG``): inputs <= 16 and every hidden layer <= 8 wide.  Box g owns tile
@@ -115,6 +133,7 @@ class Backend:
             G = pack_groups([mlp.n_in] + mlp.widths)
             if G > 1:
                 flat = np.concatenate([flat, mfma_packed_block(mlp.weights, mlp.biases, G)])
+            flat = np.concatenate([flat, mfma_back_block(mlp.weights)])
             self.flat = torch.from_numpy(flat).to(self.device)
             dims = [mlp.n_in] + mlp.widths
             self.dims = torch.tensor(dims, dtype=torch.int32)

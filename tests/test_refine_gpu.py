@@ -311,3 +311,37 @@ def test_backward_kernel_with_dead_mask(cuda):
     assert bool((rg.dead.cpu() | ~dead.bool()).all())           # masked -> dead
     assert bool((rr.dead | ~dead.bool()).all())
     assert float((rg.dead.cpu() == rr.dead).double().mean()) >= 0.99
+
+
+@pytest.mark.parametrize("mode", ["refine", "refine_crown", "backward"])
+def test_global_weight_refine_bitwise_equals_staged(cuda, monkeypatch, mode):
+    """BM-4's shape (16-150-100-50): the back-substitution kernel reading W from the global
+    backward-order block (8 box rows per workgroup) gives bitwise the bounds of the LDS-staged
+    kernel (1 row per workgroup): same arithmetic, same order, per column."""
+    from fairify_amd.ops import ext
+    from fairify_amd.ops import hip as H
+
+    m = random_mlp(16, [150, 100, 50], seed=41, bias_scale=0.3)
+    lo, hi = _boxes(16, 203, 13)
+    gpu = Backend(m, cuda)
+    L_, H_ = lo.to(cuda), hi.to(cuda)
+    outs = []
+    for kb in ("64", "0"):                     # default (global weights) / never
+        monkeypatch.setenv("FAIRIFY_REFINE_WG_KB", kb)
+        if mode == "backward":
+            r = gpu.bounds(L_, H_, mode="backward", keep_layers=True)
+            outs.append([r.out_lb, r.out_ub, r.Lc, r.Uc, r.L0, r.U0, r.Le, r.Ue, torch.cat(r.layer_lb, 1),
+                         torch.cat(r.layer_ub, 1)])
+            continue
+        r = gpu.bounds(L_, H_, mode="symbolic", keep_layers=True)
+        if mode == "refine":
+            H.refine(gpu, L_, H_, r)
+        else:
+            ext().refine_crown(H._net(gpu), gpu.flat.data_ptr(), L_.contiguous().data_ptr(),
+                               H_.contiguous().data_ptr(), 0, L_.shape[0], r.out_lb.data_ptr(), r.out_ub.data_ptr(),
+                               r.Lc.data_ptr(), r.L0.data_ptr(), r.Le.data_ptr(), r.Uc.data_ptr(), r.U0.data_ptr(),
+                               r.Ue.data_ptr(), r.lay_lb_full.data_ptr(), r.lay_ub_full.data_ptr(), H._stream(cuda))
+        torch.cuda.synchronize()
+        outs.append([r.out_lb, r.out_ub, r.Lc, r.Uc, r.lay_lb_full, r.lay_ub_full])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
