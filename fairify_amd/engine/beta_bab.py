@@ -305,7 +305,9 @@ class BetaBaBSolver:
             grow &= run_t
             over = torch.from_numpy(nodes_np >= budget).to(dev)[cur["part"]] & grow
             if bool(over.any()):
-                status[np.unique(cur["part"][over].cpu().numpy())] = UNKNOWN
+                ob = np.unique(cur["part"][over].cpu().numpy())
+                self.stats["over_budget"] = self.stats.get("over_budget", 0) + int((status[ob] == RUNNING).sum())
+                status[ob] = UNKNOWN
                 grow &= ~over
             gi = torch.nonzero(grow).flatten()
             bi = lev.binit[gi] if cfg.warm_beta else torch.zeros_like(lev.binit[gi])
@@ -313,7 +315,9 @@ class BetaBaBSolver:
             pool = {kk: torch.cat([rest[kk], kids[kk]]) for kk in pool}
             if pool["part"].numel() > cfg.max_pool:
                 lost = torch.unique(pool["part"][cfg.max_pool:]).cpu().numpy()
-                status[lost[status[lost] == RUNNING]] = UNKNOWN
+                lost = lost[status[lost] == RUNNING]
+                self.stats["pool_lost"] = self.stats.get("pool_lost", 0) + int(lost.size)
+                status[lost] = UNKNOWN
                 pool = {kk: v[:cfg.max_pool] for kk, v in pool.items()}
         left = set(pool["part"].cpu().numpy().tolist()) if (timed_out and pool["part"].numel()) else set()
         for p in np.nonzero(status == RUNNING)[0]:
