@@ -450,6 +450,7 @@ SimRegKernel select_sim_reg(int TM) {
   if (TM <= 2) return fa_sim_reg_kernel<2>;
   if (TM <= 4) return fa_sim_reg_kernel<4>;
   if (TM <= 7) return fa_sim_reg_kernel<7>;
+  if (TM <= 10) return fa_sim_reg_kernel<10>;   // BM-4 (150-wide); the 64-row tile kernel before
   return nullptr;
 }
 // A/B switch (FAIRIFY_SIM_REG=0: the 64-row LDS tile kernel for every query)
@@ -634,4 +635,4 @@ extern "C" int fa_ascent_launch(const NetDesc& net, AscentArgs a, hipStream_t st
 
 FA_LDS_REGISTER(FA_LDS_K(fa_forward_kernel), FA_LDS_K(fa_sim_kernel), FA_LDS_K(fa_ascent_kernel),
                 FA_LDS_K(fa_sim_reg_kernel<1>), FA_LDS_K(fa_sim_reg_kernel<2>), FA_LDS_K(fa_sim_reg_kernel<4>),
-                FA_LDS_K(fa_sim_reg_kernel<7>));
+                FA_LDS_K(fa_sim_reg_kernel<7>), FA_LDS_K(fa_sim_reg_kernel<10>));

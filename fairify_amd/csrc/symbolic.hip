@@ -257,34 +257,30 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
     const bool isact = lb >= 0.f;
     if (nl_act && ob == 0 && jv && a.dead_out) a.dead_out[(size_t)r * net.n_hidden + noff + j] = isdead ? 1 : 0;
     const bool zero = isdead || forced || !jv;
-    float s, cnew, en, mgn, ivn;
-    if (ob == 0) {
-      // upper: identity (stable active, or the upper form T = U + eU >= 0 on the whole box:
-      // relu(z) <= T there, a chord from (aa, 0) would cut below it) / zero / chord over [aa, bb]
-      ivn = zero ? 0.f : fmaxf(ub, 0.f);
-      s = 1.f; cnew = c0; en = e; mgn = mg;
-      const float aa = mn - gc * mg + e;
-      if (zero) {
-        s = 0.f; cnew = 0.f; en = 0.f; mgn = 0.f;
-      } else if (!isact && !fact && aa < 0.f) {
-        const float bb = mx + gc * mg + e;
-        s = (bb / (bb - aa)) * (1.f + 4.f * unit);
-        const float shift = e - aa;
-        cnew = c0 * s + s * shift;
-        mgn = s * mgc * (1.f + 8.f * unit) + fabsf(cnew);
-        en = 4.f * unit * s * (mg + fabsf(shift));
-      }
-    } else {
-      // lower: lambda in {0,1} applied to L(x) - eL
-      ivn = zero ? 0.f : fmaxf(lb, 0.f);
-      const float aL = mn - gc * mg - e;
-      const float bL = mx + gc * mg - e;
-      const bool lam1 = !zero && (isact || ((bL > 0.f) && (bL > -aL)));
-      s = lam1 ? 1.f : 0.f;
-      cnew = lam1 ? c0 : 0.f;
-      en = lam1 ? e : 0.f;
-      mgn = lam1 ? mg : 0.f;
-    }
+    // both blocks' relaxations, then a per-lane select: the U and L lanes share every wave, so
+    // a branch on ob runs both sides anyway, plus the exec-mask juggling (SALU)
+    //   upper: identity (stable active, or the upper form T = U + eU >= 0 on the whole box:
+    //   relu(z) <= T there, a chord from (aa, 0) would cut below it) / zero / chord over [aa, bb]
+    const float aa = mn - gc * mg + e;
+    const float bb = mx + gc * mg + e;
+    const bool chord = !zero && !isact && !fact && aa < 0.f;
+    const float sc = (bb / (bb - aa)) * (1.f + 4.f * unit);     // used only where chord
+    const float shift = e - aa;
+    const float cc = c0 * sc + sc * shift;
+    const float sU = zero ? 0.f : (chord ? sc : 1.f);
+    const float cU = zero ? 0.f : (chord ? cc : c0);
+    const float mU = zero ? 0.f : (chord ? sc * mgc * (1.f + 8.f * unit) + fabsf(cc) : mg);
+    const float eU = zero ? 0.f : (chord ? 4.f * unit * sc * (mg + fabsf(shift)) : e);
+    //   lower: lambda in {0,1} applied to L(x) - eL
+    const float aL = mn - gc * mg - e;
+    const float bL = mx + gc * mg - e;
+    const bool lam1 = !zero && (isact || ((bL > 0.f) && (bL > -aL)));
+    const bool up = ob == 0;
+    const float ivn = zero ? 0.f : fmaxf(up ? ub : lb, 0.f);
+    const float s = up ? sU : (lam1 ? 1.f : 0.f);
+    const float cnew = up ? cU : (lam1 ? c0 : 0.f);
+    const float en = up ? eU : (lam1 ? e : 0.f);
+    const float mgn = up ? mU : (lam1 ? mg : 0.f);
     // new row: constant, error, interval, interval error (L errors negated), scaled coefficients
     const float mg_b = CR ? mgn + __shfl_xor(mgn, 16, 64) : mgn;            // C/R: both blocks
     const float iv_b = CR ? fmaxf(ivn, __shfl_xor(ivn, 16, 64)) : ivn;

@@ -279,6 +279,12 @@ def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes,
     after that many levels unless 2 % of the partitions are decided by then (BetaConfig)."""
     from .beta_bab import BetaBaBSolver, BetaConfig
 
+    # per model (Backend) and run: after 2 000 attempted partitions with under 1 % decided, the
+    # fixed pass stops trying this model's later chunks (relaxed/BM BM-4: 7 UNSAT + 202 SAT of ~11 K
+    # attempted for 15.6 s of kernel time, profiles/r5/s5_k/)
+    rec = getattr(be, "_beta_yield", None)
+    if probe_levels and rec is not None and rec[0] >= 2000 and rec[1] < 0.01 * rec[0]:
+        return 0
     bs = BetaBaBSolver(be, q, BetaConfig(node_budget=budget, batch_nodes=min(batch_nodes, 32768),
                                          time_budget=time_budget, probe_levels=probe_levels),
                        **({"timer": tm} if tm is not None else {}))
@@ -295,6 +301,9 @@ def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes,
     cex_x[unk[sb]] = br.cex_x[sb]
     cex_xp[unk[sb]] = br.cex_xp[sb]
     nodes[unk] += br.nodes
+    if probe_levels:
+        rec = getattr(be, "_beta_yield", None) or [0, 0]
+        be._beta_yield = [rec[0] + int(unk.size), rec[1] + int(dec.sum())]
     return int(dec.sum())
 
 

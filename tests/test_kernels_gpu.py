@@ -227,7 +227,8 @@ def test_certify_matches_reference(cuda):
     assert bool((a.score[differ].abs() <= tol[differ]).all())
 
 
-@pytest.mark.parametrize("model,relaxed", [("AC-3", True), ("AC-7", True), ("AC-3", False), ("AC-7", False)])
+@pytest.mark.parametrize("model,relaxed", [("AC-3", True), ("AC-7", True), ("AC-3", False), ("AC-7", False),
+                                           ("wide", True), ("wide", False)])
 def test_sim_reg_kernel_relaxed_matches_tile_kernel(cuda, monkeypatch, model, relaxed):
     """The register-resident simulation kernel against the 64-row tile kernel, relaxed queries
     (x' rows with the tile kernel's RA offsets) and a plain multi-valued PA (race): activation
@@ -244,7 +245,8 @@ def test_sim_reg_kernel_relaxed_matches_tile_kernel(cuda, monkeypatch, model, re
     lo, hi = grid.decode(ids)
     values = torch.from_numpy(q.pa_values(lo[0], hi[0])).to(cuda)
     pairs = torch.from_numpy(q.pa_pairs(values.cpu().numpy())).to(cuda)
-    m = get_model(model, weights="random", seed=0)
+    # "wide": a 150-100-50 net (BM-4's hidden shape, the 10-tile register kernel)
+    m = random_mlp(13, [150, 100, 50], seed=0) if model == "wide" else get_model(model, weights="random", seed=0)
     gpu = Backend(m, cuda)
     lo_t, hi_t = torch.from_numpy(lo).float().to(cuda), torch.from_numpy(hi).float().to(cuda)
     pid = torch.from_numpy(ids).to(cuda)
