@@ -53,10 +53,10 @@ class BetaConfig:
     tighten: bool = True             # children: re-bound every hidden neuron over the node's box and
     #                                  phase region (csrc/refine.hip with phases), intersected with
     #                                  the inherited bounds; an empty region closes the node
-    probe_levels: int = 0            # > 0: once 2 x this many nodes per pair tree are expanded, stop
-    probe_yield: float = 0.02        # the call unless it has decided at least this fraction of its
-    #                                  partitions (closed pair trees count 1 / Pp each): a residue it
-    #                                  does not converge on -- random-init bench nets -- costs little
+    probe_levels: int = 0            # > 0: a partition that has expanded 2 x this many nodes per pair
+    #                                  tree with none of its trees closed ends UNKNOWN (a residue the
+    #                                  stage does not converge on costs little; per partition, so the
+    #                                  verdicts do not depend on how partitions are grouped or sharded)
     beta_pos: bool = True            # split multipliers projected >= 0 (free-signed ones, which may
     #                                  use the interval side, make Adam oscillate around 0: measured
     #                                  8 / 10 -> 0 / 10 trained AC-7 partitions closed, tools/exp)
@@ -226,7 +226,11 @@ class BetaBaBSolver:
         # pairs -- gets the budget a binary one gets per pair)
         budget = int(cfg.node_budget * max(1.0, Pp / 2.0))
         levels = 0
-        probed = False
+        # the probe (per partition, so a verdict never depends on which partitions share the call):
+        # once a partition has expanded 2 probe_levels nodes per pair tree, it goes on only if one
+        # of its trees has closed
+        probed = np.zeros(P, dtype=bool)
+        probe_at = 2 * cfg.probe_levels * Pp
         timed_out = False
         while pool["part"].numel():
             if time.time() - t0 > time_budget:
@@ -250,21 +254,6 @@ class BetaBaBSolver:
             cur = {kk: v[:nb] for kk, v in pool.items()}
             rest = {kk: v[nb:] for kk, v in pool.items()}
             levels += 1
-            # the probe point: 2 probe_levels nodes expanded per pair tree (a binary tree of depth
-            # ~probe_levels - 1), not a batch count -- a race partition has 20 trees, and its first
-            # batches hold only a slice of one level
-            if cfg.probe_levels and not probed and not is_root and \
-                    int(nodes_np.sum()) >= 2 * cfg.probe_levels * R0:
-                probed = True
-                # progress in partitions: decided ones, plus closed pair trees of running ones in
-                # units of Pp (a race partition needs all 20 of its trees closed)
-                dec = int(np.isin(status[run], (SAT, UNSAT)).sum())
-                dec += self._closed_trees(pool, R0, tree_run, status) / Pp
-                self.stats["probe_yield"] = dec / run.size
-                if dec < cfg.probe_yield * run.size:
-                    self.stats["probe_stop"] = self.stats.get("probe_stop", 0) + 1
-                    status[run[status[run] == RUNNING]] = UNKNOWN
-                    break
             np.add.at(nodes_np, cur["part"].cpu().numpy(), 1)
             sc = 1.0 if is_root else cfg.child_lr
             empty = None
@@ -313,6 +302,8 @@ class BetaBaBSolver:
             bi = lev.binit[gi] if cfg.warm_beta else torch.zeros_like(lev.binit[gi])
             kids = self._children({kk: v[gi] for kk, v in cur.items()}, lev.split[gi], bi, NH, n0)
             pool = {kk: torch.cat([rest[kk], kids[kk]]) for kk in pool}
+            if cfg.probe_levels:
+                self._probe(pool, nodes_np, probed, probe_at, R0, tree_run, status)
             if pool["part"].numel() > cfg.max_pool:
                 lost = torch.unique(pool["part"][cfg.max_pool:]).cpu().numpy()
                 lost = lost[status[lost] == RUNNING]
@@ -326,13 +317,21 @@ class BetaBaBSolver:
         self.stats["nodes"] = self.stats.get("nodes", 0) + int(nodes_np.sum())
         return status, cex_x, cex_xp, nodes_np
 
-    @staticmethod
-    def _closed_trees(pool, R0: int, tree_run, status) -> int:
-        """Pair trees of RUNNING partitions with no node left in the pool."""
-        left = np.zeros(R0, dtype=bool)
+    def _probe(self, pool, nodes_np, probed, probe_at: int, R0: int, tree_run, status) -> None:
+        """Partitions past the probe point with no closed pair tree end UNKNOWN (their nodes are
+        dropped at the next level)."""
+        cand = np.nonzero((nodes_np >= probe_at) & ~probed & (status == RUNNING))[0]
+        if not cand.size:
+            return
+        probed[cand] = True
+        alive = np.zeros(R0, dtype=bool)
         if pool["tree"].numel():
-            left[pool["tree"].cpu().numpy()] = True
-        return int((~left & (status[tree_run] == RUNNING)).sum())
+            alive[pool["tree"].cpu().numpy()] = True
+        closed = np.bincount(tree_run[~alive], minlength=status.shape[0])
+        stop = cand[closed[cand] == 0]
+        if stop.size:
+            status[stop] = UNKNOWN
+            self.stats["probe_stop"] = self.stats.get("probe_stop", 0) + int(stop.size)
 
     def _tighten(self, cur, pa, ram=None):
         """Phase-aware bounds of the batch's nodes (both copies in one launch pair; copy B over x',

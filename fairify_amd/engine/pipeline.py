@@ -132,8 +132,8 @@ class VerifyConfig:
     anytime_beta: int = 64               # anytime rounds: beta BaB nodes per partition of the first round
                                          # (x anytime_growth per round; 0 = off), independent of the
                                          # fixed-pass beta_budget
-    # fixed pass: the stage gives up after this many levels unless 2 % of its partitions are decided
-    # (closed pair trees count 1 / Pp each; 0 = never)
+    # fixed pass: a partition gives up once it has expanded 2 x this many nodes per pair tree with none
+    # of its trees closed (0 = never)
     beta_probe_levels: int = int(os.environ.get("FAIRIFY_BETA_PROBE", "4"))
     beta_min_width: int = 17             # ... on networks whose widest hidden layer is at least this
                                          # (the narrower ones go to the relu stage, whose exact-zero
@@ -275,16 +275,11 @@ def _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, limit, worke
 def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes, status, stage, cex_x, cex_xp, nodes,
                 tm=None, probe_levels: int = 0):
     """beta-CROWN BaB (engine/beta_bab.py) on the partitions ``unk``: decided verdicts (sound SAT /
-    UNSAT) written into the stage arrays; returns how many it decided.  ``probe_levels``: give up
-    after that many levels unless 2 % of the partitions are decided by then (BetaConfig)."""
+    UNSAT) written into the stage arrays; returns how many it decided.  ``probe_levels``: a partition
+    gives up once it has expanded 2 x that many nodes per pair tree with none of its trees closed
+    (BetaConfig)."""
     from .beta_bab import BetaBaBSolver, BetaConfig
 
-    # per model (Backend) and run: after 2 000 attempted partitions with under 1 % decided, the
-    # fixed pass stops trying this model's later chunks (relaxed/BM BM-4: 7 UNSAT + 202 SAT of ~11 K
-    # attempted for 15.6 s of kernel time, profiles/r5/s5_k/)
-    rec = getattr(be, "_beta_yield", None)
-    if probe_levels and rec is not None and rec[0] >= 2000 and rec[1] < 0.01 * rec[0]:
-        return 0
     bs = BetaBaBSolver(be, q, BetaConfig(node_budget=budget, batch_nodes=min(batch_nodes, 32768),
                                          time_budget=time_budget, probe_levels=probe_levels),
                        **({"timer": tm} if tm is not None else {}))
@@ -301,9 +296,6 @@ def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes,
     cex_x[unk[sb]] = br.cex_x[sb]
     cex_xp[unk[sb]] = br.cex_xp[sb]
     nodes[unk] += br.nodes
-    if probe_levels:
-        rec = getattr(be, "_beta_yield", None) or [0, 0]
-        be._beta_yield = [rec[0] + int(unk.size), rec[1] + int(dec.sum())]
     return int(dec.sum())
 
 

@@ -229,3 +229,22 @@ def test_beta_bab_relaxed_matches_bruteforce(seed, tau):
             assert not truth, k
         decided += res.status[k] != UNKNOWN
     assert decided >= 0.5 * len(ids)
+
+
+def test_probe_verdicts_do_not_depend_on_grouping():
+    """With the probe on, each partition's verdict is its own: solving the partitions together, in
+    two halves, or one by one gives the same statuses (the product runner re-shards residues over
+    ranks, tests/test_dist_gloo.py::test_residual_redistribution_matches_one_rank)."""
+    pre = presets.get("src/AC-sex")
+    grid, q = pre.grid(), pre.resolved()
+    ids = processing_order(grid, 0)[:12]
+    lo, hi = grid.decode(ids)
+    m = random_mlp(13, [24, 12, 6], seed=5, bias_scale=0.5)
+    cfg = BetaConfig(node_budget=48, iters=10, root_iters=20, probe_levels=1)
+    be = Backend(m)
+    whole = BetaBaBSolver(be, q, cfg).solve(lo, hi, m).status
+    halves = np.concatenate([BetaBaBSolver(be, q, cfg).solve(lo[s], hi[s], m).status
+                             for s in (slice(0, 5), slice(5, 12))])
+    single = np.array([BetaBaBSolver(be, q, cfg).solve(lo[k:k + 1], hi[k:k + 1], m).status[0]
+                       for k in range(len(ids))])
+    assert np.array_equal(whole, halves) and np.array_equal(whole, single)
