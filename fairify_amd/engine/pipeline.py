@@ -138,6 +138,11 @@ class VerifyConfig:
     beta_min_width: int = 17             # ... on networks whose widest hidden layer is at least this
                                          # (the narrower ones go to the relu stage, whose exact-zero
                                          # concretisation their zero logits need)
+    beta_max_width: int = 128            # ... and at most this (fixed pass only): BM-4's 150-wide layer
+                                         # (transposed W beyond the kernel's LDS) decided 167 of 11 118
+                                         # residue partitions of relaxed/BM for 21 s of its 60 s
+                                         # (profiles/r5/s5_m/); a static rule, so verdicts stay
+                                         # independent of how partitions are sharded
     lp_budget: int = 4096                # verified-LP branch-and-bound (stage "lp", smt/lpbab.py) in
                                          # place of the untrusted MILP: LP nodes per partition (x growth
                                          # per anytime round); 0 = the round-2 MILP stage
@@ -619,7 +624,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     # partitions need phase splits as constraints on the region: Lagrangian split multipliers)
     from .beta_bab import supported as _beta_supported
 
-    beta_on = cfg.beta_budget > 0 and _beta_supported(q) and max(mlp.hidden or [0]) >= cfg.beta_min_width
+    beta_on = (cfg.beta_budget > 0 and _beta_supported(q)
+               and cfg.beta_min_width <= max(mlp.hidden or [0]) <= cfg.beta_max_width)
     if beta_on:
         unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
         if unk.size:
