@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--models", default="AC-1,AC-2,AC-3,AC-4,AC-5,AC-6,AC-7,AC-8,AC-9,AC-10,AC-11,AC-12")
     ap.add_argument("--limit", type=int, default=4000)
     ap.add_argument("--out", default="gpurun_out/residue")
+    ap.add_argument("--weights", default="random", help="random | zoo (trained weights)")
+    ap.add_argument("--big", action="store_true",
+                    help="the big-grid schedule of tools/baseline_configs.py (escalation to 8 192 nodes)")
     args = ap.parse_args()
     import torch
 
@@ -40,13 +43,14 @@ def main():
     grid, q = pre.grid(), pre.resolved()
     ids = processing_order(grid, seed=0)[:args.limit]
     cfg = VerifyConfig(sim_size=pre.sim_size, chunk=4096, soft_timeout=pre.soft_timeout, hard_timeout=pre.hard_timeout,
-                       node_budget=512, heuristic=False, heuristic_p=pre.heuristic_p, escalate_budget=32768,
-                       escalate_max_open=384, smt_backend="none",
-                       escalate_probation=((2048, 768), (4096, 768), (8192, 768), (16384, 1024)),
+                       node_budget=512, heuristic=False, heuristic_p=pre.heuristic_p,
+                       escalate_budget=8192 if args.big else 32768, escalate_max_open=384, smt_backend="none",
+                       escalate_probation=((2048, 768), (4096, 768)) if args.big else
+                       ((2048, 768), (4096, 768), (8192, 768), (16384, 1024)),
                        relu_budget=1024, relu_max_width=16, relu_escalate_cap=2048)
     os.makedirs(args.out, exist_ok=True)
     for name in args.models.split(","):
-        m = get_model(name, weights="random", seed=0)
+        m = get_model(name, weights=args.weights, seed=0)
         be = Backend(m, device=dev)
         t0 = time.time()
         recs = verify_chunk(be, m, q, grid, ids, cfg)
