@@ -1,0 +1,66 @@
+#!/usr/bin/env python
+"""beta stage settings on a dumped residue (tools/dump_residue.py): decided counts and time.
+
+    python tools/exp/beta_residue.py --preset relaxed/BM --model BM-8 --npz gpurun_out/res/BM-8.npz --n 400
+
+Each setting runs the stage alone (no probe) on the same UNKNOWN partitions; prints one line per
+setting: decided SAT / UNSAT, the stage's stats, wall seconds.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+from dataclasses import replace
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default="relaxed/BM")
+    ap.add_argument("--model", default="BM-8")
+    ap.add_argument("--weights", default="zoo")
+    ap.add_argument("--npz", required=True)
+    ap.add_argument("--n", type=int, default=400)
+    args = ap.parse_args()
+    import torch
+
+    from fairify_amd import presets
+    from fairify_amd.engine.beta_bab import SAT, UNSAT, BetaBaBSolver, BetaConfig
+    from fairify_amd.models.zoo import get_model
+    from fairify_amd.ops.backend import Backend
+
+    pre = presets.get(args.preset)
+    grid, q = pre.grid(), pre.resolved()
+    d = np.load(args.npz)
+    ids = d["grid_id"][d["verdict"] == "unknown"][:args.n]
+    lo, hi = grid.decode(ids)
+    m = get_model(args.model, weights=args.weights, seed=0)
+    be = Backend(m, device="cuda" if torch.cuda.device_count() else "cpu")
+    base = BetaConfig(node_budget=64)
+    settings = {
+        "default(64)": base,
+        "budget256": replace(base, node_budget=256),
+        "budget1024": replace(base, node_budget=1024),
+        "iters128": replace(base, iters=128, root_iters=400),
+        "lookahead16": replace(base, lookahead=16),
+        "no_tighten": replace(base, tighten=False),
+        "lr_x2": replace(base, lr_a=0.2, lr_b=1.0, lr_t=0.2),
+    }
+    print(f"{args.model}: {len(ids)} residue partitions", flush=True)
+    for name, cfg in settings.items():
+        t0 = time.time()
+        s = BetaBaBSolver(be, q, cfg)
+        r = s.solve(lo, hi, m)
+        if be.hip:
+            torch.cuda.synchronize()
+        print(f"{name:14s} sat {(r.status == SAT).sum():5d} unsat {(r.status == UNSAT).sum():5d} "
+              f"{time.time() - t0:7.2f}s {s.stats}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
