@@ -261,8 +261,10 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
           for (int t = 0; t < TM; ++t)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
+              // tiles t < the layer's input tiles are zero padded: load unguarded there
               const int in = 16 * t + 4 * grp + i;
-              lam[t][i] = in < ktop ? sgn * wk[jb + (t * tk * 64 + 4 * grp + i) * 4] : 0.f;
+              const float w = 16 * t < ktop ? wk[jb + (t * tk * 64 + 4 * grp + i) * 4] : 0.f;
+              lam[t][i] = in < ktop ? sgn * w : 0.f;
             }
         }
         float c = sgn * smem[cfg.b_lds[k] + j];
@@ -282,8 +284,12 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
             for (int i = 0; i < 4; ++i) {
               const int jj = 16 * t + 4 * grp + i;
               const bool jv = jj < n;
-              const float4 q = jv ? recg[off + jj] : make_float4(0.f, 0.f, 0.f, 0.f);
-              const float bj = jv ? b[jj] : 0.f;
+              // clamped index + select, not a guarded load (an exec-mask branch: SALU)
+              const int jc = min(jj, n - 1);
+              const float4 qr = recg[off + jc];
+              const float br = b[jc];
+              const float4 q = jv ? qr : make_float4(0.f, 0.f, 0.f, 0.f);
+              const float bj = jv ? br : 0.f;
               const float lm = lam[t][i];
               const bool neg = lm < 0.f;
               const float m = lm * (neg ? q.y : q.x);
@@ -296,6 +302,7 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
           }
           const float4* wb = reinterpret_cast<const float4*>(wsrc + cfg.w_lds[l]);
           const float gn = fa_rgam(2 * n + 1, u);
+          const int hoff = l > 0 ? net.neuron_off[l - 1] : 0;
 #pragma unroll
           for (int ot = 0; ot < TM; ++ot) {
             if (ot >= tin) break;
@@ -314,11 +321,9 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int in = 16 * ot + 4 * grp + i;
-              float hm = 0.f;
-              if (in < nin) {
-                if (l > 0) hm = hmg[net.neuron_off[l - 1] + in];
-                else hm = fmaxf(fabsf(bl[in]), fabsf(bl[n0 + in]));
-              }
+              const int ic = min(in, nin - 1);
+              const float hr = l > 0 ? hmg[hoff + ic] : fmaxf(fabsf(bl[ic]), fabsf(bl[n0 + ic]));
+              const float hm = in < nin ? hr : 0.f;
               lam[ot][i] = in < nin ? Z[i] : 0.f;
               er += gn * Q[i] * hm;
             }
@@ -340,16 +345,26 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
         // ---- concretise over the row's box
         float cp = 0.f, mp = 0.f;
 #pragma unroll
-        for (int t = 0; t < TM; ++t)
+        for (int t = 0; t < TM; ++t) {
+          if (16 * t >= n0) break;                            // uniform
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int in = 16 * t + 4 * grp + i;
-            if (in >= n0) continue;
-            const float xl = bl[in], xh = bl[n0 + in];
-            const float lm = lam[t][i];
-            cp += fminf(lm * xl, lm * xh);
-            mp += fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
+            if (TM <= 7) {   // clamped + select (10 tiles: the hoisted loads cost a wave per SIMD)
+              const int ic = min(in, n0 - 1);
+              const float xl = bl[ic], xh = bl[n0 + ic];
+              const float lm = lam[t][i];
+              const float dp = fminf(lm * xl, lm * xh), dm = fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
+              cp += in < n0 ? dp : 0.f;
+              mp += in < n0 ? dm : 0.f;
+            } else if (in < n0) {
+              const float xl = bl[in], xh = bl[n0 + in];
+              const float lm = lam[t][i];
+              cp += fminf(lm * xl, lm * xh);
+              mp += fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
+            }
           }
+        }
         cp += __shfl_xor(cp, 16); cp += __shfl_xor(cp, 32);
         mp += __shfl_xor(mp, 16); mp += __shfl_xor(mp, 32);
         const float conc = cp + c;

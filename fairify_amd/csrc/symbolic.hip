@@ -191,7 +191,10 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
     float v[16 * NT];
 #pragma unroll
     for (int c = 0; c < 16 * NT; ++c) v[c] = Trow[c];
-    const float b = jv ? sb[PG > 1 ? col : j] : 0.f;       // packed biases: 16 per layer, box g at g * PS
+    // packed biases: 16 per layer, box g at g * PS; clamped index + select (a guarded load is an
+    // exec-mask branch)
+    const float braw = sb[PG > 1 ? col : min(j, n_out - 1)];
+    const float b = jv ? braw : 0.f;
     // concretisation of the coefficient part over the box in centre/radius form:
     //   min / max = Σ v mid -+ Σ |v| rad,  magnitude Σ |v| m  (m >= |mid| + rad)
     // three FMAs per column (|v| is a free source modifier) instead of two products, a min, a max
