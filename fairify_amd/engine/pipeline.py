@@ -122,19 +122,21 @@ class VerifyConfig:
                                          # (profiles/r3/shard/diag_models_bench_config.jsonl: 38 % of a
                                          # bench step's nodes were AC-8 / AC-12 escalation spent on
                                          # partitions the relu stage then decided)
-    beta_budget: int = int(os.environ.get("FAIRIFY_BETA_BUDGET", "64"))
+    beta_budget: int = int(os.environ.get("FAIRIFY_BETA_BUDGET", "128"))
                                          # beta-CROWN phase-split BaB (stage "beta", engine/beta_bab.py)
                                          # on the residue: nodes per partition (0 = off); the trained
                                          # AC-7 residue closes in 10-60 nodes, the random-init bench
                                          # residue mostly does not (512 nodes: +3.4 s per step for 147
-                                         # verdicts, gpurun_out/s5_c); the anytime rounds grow it x
+                                         # verdicts, gpurun_out/s5_c); 128 with probe 8 over 64 with
+                                         # probe 4: targeted/AC AC-7 97.29 -> 98.30 % for +7 % time
+                                         # (profiles/r5/s5_u/); the anytime rounds grow it x
                                          # anytime_growth per round
     anytime_beta: int = 64               # anytime rounds: beta BaB nodes per partition of the first round
                                          # (x anytime_growth per round; 0 = off), independent of the
                                          # fixed-pass beta_budget
     # fixed pass: a partition gives up once it has expanded 2 x this many nodes per pair tree with none
     # of its trees closed (0 = never)
-    beta_probe_levels: int = int(os.environ.get("FAIRIFY_BETA_PROBE", "4"))
+    beta_probe_levels: int = int(os.environ.get("FAIRIFY_BETA_PROBE", "8"))
     beta_min_width: int = 17             # ... on networks whose widest hidden layer is at least this
                                          # (the narrower ones go to the relu stage, whose exact-zero
                                          # concretisation their zero logits need)
