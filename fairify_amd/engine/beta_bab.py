@@ -63,6 +63,8 @@ class BetaConfig:
     batch_nodes: int = 32768         # nodes per level launch
     time_budget: float = 1e9         # wall-clock seconds for the whole call
     max_pool: int = 1 << 21          # live nodes (more: the partitions losing nodes end UNKNOWN)
+    input_every: int = 0             # > 0 (experiment): every this many levels of a tree, split the
+    #                                  widest input dim (x, or x''s RA dims) instead of the kernel's choice
 
 
 def supported(q: ResolvedQuery) -> bool:
@@ -217,6 +219,7 @@ class BetaBaBSolver:
             "beA": torch.zeros(R0, NH, **f32), "beB": torch.zeros(R0, NH, **f32),
             "t": torch.full((R0,), 0.5, **f32),
             "root": torch.ones(R0, dtype=torch.bool, device=dev),
+            "depth": torch.zeros(R0, dtype=torch.int32, device=dev),
             # relaxed: Lagrange multipliers of the tie |x_r - x'_r| <= tau (RA dims)
             "gP": torch.zeros(R0, n0, **f32), "gM": torch.zeros(R0, n0, **f32),
             "tree": torch.arange(R0, device=dev),        # the (partition, ordered pair) root
@@ -300,7 +303,10 @@ class BetaBaBSolver:
                 grow &= ~over
             gi = torch.nonzero(grow).flatten()
             bi = lev.binit[gi] if cfg.warm_beta else torch.zeros_like(lev.binit[gi])
-            kids = self._children({kk: v[gi] for kk, v in cur.items()}, lev.split[gi], bi, NH, n0)
+            split = lev.split[gi]
+            if cfg.input_every > 0 and gi.numel():
+                split = self._force_input(cur, gi, split, pa, ra, n0, cfg.input_every)
+            kids = self._children({kk: v[gi] for kk, v in cur.items()}, split, bi, NH, n0)
             pool = {kk: torch.cat([rest[kk], kids[kk]]) for kk in pool}
             if cfg.probe_levels:
                 self._probe(pool, nodes_np, probed, probe_at, R0, tree_run, status)
@@ -370,6 +376,7 @@ class BetaBaBSolver:
         rep = torch.arange(R, device=dev).repeat_interleave(2)
         kid = {kk: v[rep].clone() for kk, v in nd.items()}
         kid["root"][:] = False
+        kid["depth"] += 1
         if R == 0:
             return kid
         sp = split[rep]
@@ -400,6 +407,27 @@ class BetaBaBSolver:
             kid[lk][ri[~low_child], d[~low_child]] = mid[~low_child] + 1
         # (plo / phi are read on the RA dims only; x' shares x's box everywhere else)
         return kid
+
+    @staticmethod
+    def _force_input(cur, gi, split, pa, ra, n0: int, every: int):
+        """Nodes at depth = every - 1 (mod every) split their widest input dim: x's (code -1 - d)
+        or x''s RA dims (code -1 - (n0 + d)); a node with no dim wider than a point keeps its split."""
+        dep = cur["depth"][gi]
+        sel = (dep % every) == (every - 1)
+        if not bool(sel.any()):
+            return split
+        w = (cur["hi"][gi] - cur["lo"][gi]).clone()
+        if pa:
+            w[:, pa] = -1.0
+        cols = [w]
+        if ra:
+            wp = torch.full_like(w, -1.0)
+            wp[:, ra] = (cur["phi"][gi] - cur["plo"][gi])[:, ra]
+            cols.append(wp)
+        W = torch.cat(cols, dim=1)
+        best, d = W.max(dim=1)
+        use = sel & (best >= 1.0)
+        return torch.where(use, (-1 - d).to(split.dtype), split)
 
     def _confirm(self, parts, xa, xb, status, cex_x, cex_xp, mlp_exact, lo_np, hi_np):
         X = xa.cpu().numpy().round().astype(np.int64)

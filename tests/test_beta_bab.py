@@ -156,15 +156,18 @@ def _brute_pair(m, lo, hi, pa):
     return bool((((z0 > 0) & (z1 < 0)) | ((z0 < 0) & (z1 > 0))).any())
 
 
-@pytest.mark.parametrize("seed", [3, 6])
-def test_beta_bab_matches_bruteforce(seed):
+@pytest.mark.parametrize("seed,input_every", [(3, 0), (6, 0), (3, 2)])
+def test_beta_bab_matches_bruteforce(seed, input_every):
+    """Decided verdicts equal lattice enumeration (input_every > 0: the experimental forced input
+    splits of BetaConfig)."""
     pre = presets.get("src/AC-sex")
     grid, q = pre.grid(), pre.resolved()
     ids = processing_order(grid, 0)[:24]
     lo, hi = grid.decode(ids)
     hi = np.minimum(hi, lo + 1)
     m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
-    res = BetaBaBSolver(Backend(m), q, BetaConfig(node_budget=256, iters=20, root_iters=40)).solve(lo, hi, m)
+    cfg = BetaConfig(node_budget=256, iters=20, root_iters=40, input_every=input_every)
+    res = BetaBaBSolver(Backend(m), q, cfg).solve(lo, hi, m)
     pa = q.pa_idx[0]
     assert (res.status != UNKNOWN).mean() > 0.5
     for k in range(len(ids)):
