@@ -376,7 +376,8 @@ class BetaBaBSolver:
         rep = torch.arange(R, device=dev).repeat_interleave(2)
         kid = {kk: v[rep].clone() for kk, v in nd.items()}
         kid["root"][:] = False
-        kid["depth"] += 1
+        if "depth" in kid:
+            kid["depth"] += 1
         if R == 0:
             return kid
         sp = split[rep]
