@@ -378,6 +378,17 @@ struct ReluLevelArgs {
   int cand_cap;
   float unit;
   float gmarg;              // gamma(2 n0 + 4)
+  // relaxed queries (|x_r - x'_r| <= tau on the RA dims, x' unclipped): every node also carries x''s
+  // box (equal to x's off the RA dims); copy B's row reads it, the certificate concretises the RA
+  // dims of the two copies separately (engine/relu_bab.py:certify_pair_relaxed), and a split may
+  // halve an x' RA dim (idim >= n0)
+  int nra;                  // 0: PA-only query
+  int ra_idx[FA_MAX_RA];
+  float tau;
+  const float* xplo;        // [Nn, n0]
+  const float* xphi;
+  float* oxplo;             // output pool
+  float* oxphi;
 };
 
 // beta-CROWN level of the ReLU-phase BaB (csrc/beta.hip, ops/beta.py:level_ref): one wave per node

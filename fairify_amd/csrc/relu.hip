@@ -326,7 +326,8 @@ __global__ void fa_relu_rows_kernel(ReluLevelArgs a) {
   for (long long e = (long long)blockIdx.x * FA_THREADS + threadIdx.x; e < tot; e += (long long)gridDim.x * FA_THREADS) {
     const int row = (int)(e / a.n0), d = (int)(e - (long long)row * a.n0);
     const int n = row >> 1, side = row & 1;
-    float lo = a.xlo[(size_t)n * a.n0 + d], hi = a.xhi[(size_t)n * a.n0 + d];
+    const bool xp = a.nra > 0 && side == 1;          // relaxed: copy B reads x''s box
+    float lo = (xp ? a.xplo : a.xlo)[(size_t)n * a.n0 + d], hi = (xp ? a.xphi : a.xhi)[(size_t)n * a.n0 + d];
     const int k = fa_pa_slot(a, d);
     if (k >= 0) {
       const int v = (int)a.pairs[2 * a.pair[n] + side];
@@ -342,8 +343,9 @@ __global__ void fa_relu_rows_kernel(ReluLevelArgs a) {
   }
 }
 
-// One thread per node.  NM >= n0 (register arrays).
-template <int NM>
+// One thread per node.  NM >= n0 (register arrays).  RX: relaxed query (a.nra > 0; the PA-only
+// instance keeps its registers: the x' arrays fold away)
+template <int NM, bool RX>
 __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs a) {
   const int n = blockIdx.x * FA_THREADS + threadIdx.x;
   if (n >= a.Nn) return;
@@ -353,10 +355,18 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
   uint8_t open = 0;
   int choice = -3, idim = -1;
   const int8_t st = a.status[p];
-  if ((st == ST_RUNNING || st == ST_STOPPING) && !(a.infeas[A] || a.infeas[B]) && !(a.olb[A] >= 0.f) &&
-      !(a.oub[B] <= 0.f)) {
+  // relaxed: x_r and x'_r boxes more than tau apart leave no admissible pair -- the node is closed
+  bool admissible = true;
+  for (int m = 0; RX && m < a.nra; ++m) {
+    const int d = a.ra_idx[m];
+    const size_t o = (size_t)n * n0 + d;
+    if (a.xplo[o] > a.xhi[o] + a.tau || a.xphi[o] < a.xlo[o] - a.tau) admissible = false;
+  }
+  if ((st == ST_RUNNING || st == ST_STOPPING) && admissible && !(a.infeas[A] || a.infeas[B]) &&
+      !(a.olb[A] >= 0.f) && !(a.oub[B] <= 0.f)) {
     const int vA = (int)a.pairs[2 * a.pair[n]], vB = (int)a.pairs[2 * a.pair[n] + 1];
-    float ca[NM], cb[NM], xl[NM], xh[NM];
+    float ca[NM], cb[NM], xl[NM], xh[NM], pl[NM], ph[NM];
+    bool rd[NM];                         // relaxed: RA dim (copies concretised separately)
     float fA = 0.f, fB = 0.f;
     float fmA = 0.f, fmB = 0.f;          // sum |ca_i v_k|: the folded products' rounding magnitude
 #pragma unroll
@@ -366,6 +376,13 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
       cb[i] = v ? a.Uc[(size_t)B * n0 + i] : 0.f;
       xl[i] = v ? a.xlo[(size_t)n * n0 + i] : 0.f;
       xh[i] = v ? a.xhi[(size_t)n * n0 + i] : 0.f;
+      bool r = false;
+      for (int m = 0; RX && m < a.nra; ++m) r = r || a.ra_idx[m] == i;
+      rd[i] = RX && v && r;
+      if (RX) {
+        pl[i] = rd[i] ? a.xplo[(size_t)n * n0 + i] : xl[i];
+        ph[i] = rd[i] ? a.xphi[(size_t)n * n0 + i] : xh[i];
+      }
     }
     for (int k = 0; k < a.npa; ++k) {   // fold the PA coordinates (fixed per row) into the constants
       const int d = a.pa_idx[k];
@@ -378,6 +395,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
           fmB += fabsf(cb[i] * a.values[vB * a.npa + k]);
           ca[i] = cb[i] = 0.f;
           xl[i] = xh[i] = 0.f;
+          if (RX) pl[i] = ph[i] = 0.f;
         }
     }
     const float LA0 = a.L0[A] - a.Le[A];
@@ -387,8 +405,9 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       const float mx = fmaxf(fabsf(xl[i]), fabsf(xh[i]));
+      const float mxb = RX ? fmaxf(fabsf(pl[i]), fabsf(ph[i])) : mx;   // copy B's box (x' on RA dims)
       magA += fabsf(ca[i]) * mx;
-      magB += fabsf(cb[i]) * mx;
+      magB += fabsf(cb[i]) * mxb;
       ca[i] = -ca[i];                      // A = -L_A
     }
     const float A0 = -(LA0 + fA), B0 = UB0 + fB;
@@ -397,8 +416,13 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
       float val = 0.f;
 #pragma unroll
       for (int i = 0; i < NM; ++i) {
-        const float cs = t * ca[i] + (1.f - t) * cb[i];
-        val += fmaxf(cs * xl[i], cs * xh[i]);
+        if (RX && rd[i]) {   // x_r and x'_r concretised separately (the tie only loosens when dropped)
+          const float ar = t * ca[i], br = (1.f - t) * cb[i];
+          val += fmaxf(ar * xl[i], ar * xh[i]) + fmaxf(br * pl[i], br * ph[i]);
+        } else {
+          const float cs = t * ca[i] + (1.f - t) * cb[i];
+          val += fmaxf(cs * xl[i], cs * xh[i]);
+        }
       }
       return val + t * A0 + (1.f - t) * B0 + a.gmarg * (t * magA + (1.f - t) * magB) + marg0;
     };
@@ -410,9 +434,11 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
 #pragma unroll 1
     for (int i = 0; i < n0; ++i) {
       float ai = 0.f, bi = 0.f;
+      bool ri = false;
 #pragma unroll
       for (int k = 0; k < NM; ++k)
-        if (k == i) { ai = ca[k]; bi = cb[k]; }
+        if (k == i) { ai = ca[k]; bi = cb[k]; ri = RX && rd[k]; }
+      if (ri) continue;                    // separate linear terms in t: no interior breakpoint
       const float den = ai - bi;
       if (den == 0.f) continue;
       const float t = -bi / den;
@@ -429,6 +455,24 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
         const float c = bt * ca[i] + (1.f - bt) * cb[i];
         const float x = c > 0.f ? a.xhi[(size_t)n * n0 + i] : a.xlo[(size_t)n * n0 + i];
         const int k = fa_pa_slot(a, i);
+        if (RX && rd[i]) {
+          // relaxed RA dim: x_r at copy A's vertex, x'_r at copy B's, pulled into [x_r - tau, x_r + tau]
+          const float xa = ca[i] > 0.f ? a.xhi[(size_t)n * n0 + i] : a.xlo[(size_t)n * n0 + i];
+          const float xb0 = cb[i] > 0.f ? a.xphi[(size_t)n * n0 + i] : a.xplo[(size_t)n * n0 + i];
+          a.cpts[(size_t)A * n0 + i] = xa;
+          a.cpts[(size_t)B * n0 + i] = fminf(fmaxf(xb0, xa - a.tau), xa + a.tau);
+          // input-split scores: x's dim by copy A's coefficient, x''s by copy B's (idim >= n0)
+          const float w = xh[i] - xl[i], wp = ph[i] - pl[i];
+          if (w > 0.f) {
+            const float s = fabsf(bt * ca[i]) * w + 1e-9f * w;
+            if (s > bs) { bs = s; idim = i; }
+          }
+          if (wp > 0.f) {
+            const float s = fabsf((1.f - bt) * cb[i]) * wp + 1e-9f * wp;
+            if (s > bs) { bs = s; idim = n0 + i; }
+          }
+          continue;
+        }
         a.cpts[(size_t)A * n0 + i] = k >= 0 ? a.values[vA * a.npa + k] : x;
         a.cpts[(size_t)B * n0 + i] = k >= 0 ? a.values[vB * a.npa + k] : x;
         const float w = xh[i] - xl[i];
@@ -496,7 +540,7 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_split_kernel(ReluLevelArgs
       a.opart[off + lane] = p;
       a.opair[off + lane] = a.pair[n];
     }
-    const int dsplit = ch == -1 ? a.idim[n] : -1;
+    const int dsplit = ch == -1 ? a.idim[n] : -1;    // >= n0: x''s RA dim dsplit - n0 (relaxed)
     for (int e = lane; e < 2 * n0; e += 64) {
       const int c = e / n0, d = e - c * n0;
       float lo = a.xlo[(size_t)n * n0 + d], hi = a.xhi[(size_t)n * n0 + d];
@@ -506,6 +550,15 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_split_kernel(ReluLevelArgs
       }
       a.oxlo[(size_t)(off + c) * n0 + d] = lo;
       a.oxhi[(size_t)(off + c) * n0 + d] = hi;
+      if (a.nra > 0) {
+        float plo = a.xplo[(size_t)n * n0 + d], phi = a.xphi[(size_t)n * n0 + d];
+        if (d + n0 == dsplit) {
+          const float mid = floorf(0.5f * (plo + phi));
+          if (c == 0) phi = mid; else plo = mid + 1.f;
+        }
+        a.oxplo[(size_t)(off + c) * n0 + d] = plo;
+        a.oxphi[(size_t)(off + c) * n0 + d] = phi;
+      }
     }
     const int kfix = ch >= 0 ? (ch >> 16) * a.nh + (ch & 0xffff) : -1;
     for (int e = lane; e < 2 * w2; e += 64) {
@@ -545,9 +598,17 @@ extern "C" int fa_relu_rows_launch(ReluLevelArgs a, hipStream_t stream) {
 extern "C" int fa_relu_cert_launch(ReluLevelArgs a, hipStream_t stream) {
   if (a.Nn <= 0) return 0;
   const dim3 g((a.Nn + FA_THREADS - 1) / FA_THREADS);
-  if (a.n0 <= 16) hipLaunchKernelGGL(fa_relu_cert_kernel<16>, g, dim3(FA_THREADS), 0, stream, a);
-  else if (a.n0 <= 32) hipLaunchKernelGGL(fa_relu_cert_kernel<32>, g, dim3(FA_THREADS), 0, stream, a);
-  else if (a.n0 <= 64) hipLaunchKernelGGL(fa_relu_cert_kernel<64>, g, dim3(FA_THREADS), 0, stream, a);
+  const bool rx = a.nra > 0;
+  if (a.n0 <= 16) {
+    if (rx) hipLaunchKernelGGL((fa_relu_cert_kernel<16, true>), g, dim3(FA_THREADS), 0, stream, a);
+    else hipLaunchKernelGGL((fa_relu_cert_kernel<16, false>), g, dim3(FA_THREADS), 0, stream, a);
+  } else if (a.n0 <= 32) {
+    if (rx) hipLaunchKernelGGL((fa_relu_cert_kernel<32, true>), g, dim3(FA_THREADS), 0, stream, a);
+    else hipLaunchKernelGGL((fa_relu_cert_kernel<32, false>), g, dim3(FA_THREADS), 0, stream, a);
+  } else if (a.n0 <= 64) {
+    if (rx) hipLaunchKernelGGL((fa_relu_cert_kernel<64, true>), g, dim3(FA_THREADS), 0, stream, a);
+    else hipLaunchKernelGGL((fa_relu_cert_kernel<64, false>), g, dim3(FA_THREADS), 0, stream, a);
+  }
   else return -4;
   return (int)hipGetLastError();
 }

@@ -59,13 +59,23 @@ float rgamma(int k, double unit) {
 class ReluRuntime {
  public:
   ReluRuntime(py::handle net, uintptr_t flat, std::vector<int> pa, std::vector<float> values_f,
-              std::vector<int64_t> pairs, int capacity, int batch_nodes, double unit, int refine)
+              std::vector<int64_t> pairs, int capacity, int batch_nodes, double unit, int refine,
+              std::vector<int> ra, double tau)
       : net_(fa_net_desc(net)), flat_((const float*)flat), pa_(std::move(pa)), cap_(capacity), batch_(batch_nodes),
-        unit_(unit), refine_(refine) {
+        unit_(unit), refine_(refine), ra_(std::move(ra)), tau_((float)tau) {
     n0_ = net_.dims[0];
     nh_ = net_.n_hidden;
     npa_ = (int)pa_.size();
     if (npa_ == 0 || npa_ > FA_CMAX_PA) throw std::invalid_argument("bad PA");
+    // relaxed queries (x' RA box per node): at most FA_MAX_RA dims, none of them a PA dim
+    relaxed_ = !ra_.empty() && tau_ > 0.f;
+    if (!relaxed_) ra_.clear();
+    if ((int)ra_.size() > FA_MAX_RA) throw std::invalid_argument("bad RA");
+    for (int d : ra_) {
+      if (d < 0 || d >= n0_) throw std::invalid_argument("RA dim out of range");
+      for (int k : pa_)
+        if (k == d) throw std::invalid_argument("RA dim is a PA dim");
+    }
     V_ = (int)(values_f.size() / npa_);
     Pp_ = (int)(pairs.size() / 2);
     vals_.ensure(values_f.size());
@@ -98,6 +108,8 @@ class ReluRuntime {
     exact_.is_pa.assign(n0_, 0);
     exact_.is_ra.assign(n0_, 0);
     for (int k : pa_) exact_.is_pa[k] = 1;
+    for (int k : ra_) exact_.is_ra[k] = 1;
+    exact_.tau = tau_;
   }
 
   py::tuple solve(py::array_t<float, py::array::c_style | py::array::forcecast> lo,
@@ -121,7 +133,8 @@ class ReluRuntime {
     if (n_root > cap_) throw std::invalid_argument("more root nodes than pool capacity");
     ensure_pool(0, std::max<long long>(n_root, 1));
     // staged host block: status | part | pair | lo | hi (one H2D copy), then device memsets
-    const size_t sb = (size_t)((P + 3) & ~3) + (size_t)n_root * (2 * sizeof(int) + 2 * n0_ * sizeof(float));
+    const int nbox = relaxed_ ? 4 : 2;     // lo, hi (+ relaxed: x' lo, hi)
+    const size_t sb = (size_t)((P + 3) & ~3) + (size_t)n_root * (2 * sizeof(int) + nbox * n0_ * sizeof(float));
     hstage_.ensure(sb);
     {
       unsigned char* h = hstage_.p;
@@ -130,6 +143,8 @@ class ReluRuntime {
       int* hq = hp + n_root;
       float* hl = reinterpret_cast<float*>(hq + n_root);
       float* hh = hl + n_root * n0_;
+      float* hpl = hh + n_root * n0_;        // relaxed only
+      float* hph = hpl + n_root * n0_;
       long long k = 0;
       for (int p : run)
         for (int q = 0; q < Pp_; ++q, ++k) {
@@ -138,6 +153,16 @@ class ReluRuntime {
           for (int d = 0; d < n0_; ++d) {
             hl[k * n0_ + d] = lo.data()[(size_t)p * n0_ + d];
             hh[k * n0_ + d] = hi.data()[(size_t)p * n0_ + d];
+          }
+          if (relaxed_) {                    // x': the RA dims widened by tau, unclipped
+            for (int d = 0; d < n0_; ++d) {
+              hpl[k * n0_ + d] = hl[k * n0_ + d];
+              hph[k * n0_ + d] = hh[k * n0_ + d];
+            }
+            for (int d : ra_) {
+              hpl[k * n0_ + d] -= tau_;
+              hph[k * n0_ + d] += tau_;
+            }
           }
         }
       stage_.ensure(sb);
@@ -152,6 +177,12 @@ class ReluRuntime {
       rck(hipMemcpyAsync(lo_[0].p, d, n_root * n0_ * sizeof(float), hipMemcpyDeviceToDevice, st), "cp lo");
       d += n_root * n0_ * sizeof(float);
       rck(hipMemcpyAsync(hi_[0].p, d, n_root * n0_ * sizeof(float), hipMemcpyDeviceToDevice, st), "cp hi");
+      d += n_root * n0_ * sizeof(float);
+      if (relaxed_) {
+        rck(hipMemcpyAsync(plo_[0].p, d, n_root * n0_ * sizeof(float), hipMemcpyDeviceToDevice, st), "cp plo");
+        d += n_root * n0_ * sizeof(float);
+        rck(hipMemcpyAsync(phi_[0].p, d, n_root * n0_ * sizeof(float), hipMemcpyDeviceToDevice, st), "cp phi");
+      }
       rck(hipMemsetAsync(phase_[0].p, 0, (size_t)n_root * 2 * nh_, st), "memset phase");
       rck(hipMemsetAsync(nodes_.p, 0, P * sizeof(int), st), "memset nodes");
       rck(hipMemsetAsync(nodes_start_.p, 0, P * sizeof(int), st), "memset nodes_start");
@@ -246,6 +277,13 @@ class ReluRuntime {
     a.cand_buf = reinterpret_cast<float*>(cand_host_.p); a.cand_count = counters_.p + 1; a.cand_cap = cand_alloc_;
     a.unit = (float)unit_;
     a.gmarg = rgamma(2 * n0_ + 4, unit_);
+    if (relaxed_) {
+      a.nra = (int)ra_.size();
+      for (int k = 0; k < a.nra; ++k) a.ra_idx[k] = ra_[k];
+      a.tau = tau_;
+      a.xplo = plo_[cur].p + s * n0_; a.xphi = phi_[cur].p + s * n0_;
+      a.oxplo = plo_[nxt].p; a.oxphi = phi_[nxt].p;
+    }
     rckl(fa_relu_rows_launch(a, st), "relu rows");
     const int R = 2 * nb;
     rck(hipMemsetAsync(infeas_.p, 0, R, st), "memset infeas");
@@ -298,6 +336,7 @@ class ReluRuntime {
     n = std::min(n, cap_);
     part_[i].ensure(n); pair_[i].ensure(n);
     lo_[i].ensure((size_t)n * n0_); hi_[i].ensure((size_t)n * n0_);
+    if (relaxed_) { plo_[i].ensure((size_t)n * n0_); phi_[i].ensure((size_t)n * n0_); }
     phase_[i].ensure((size_t)n * 2 * nh_);
     pool_[i] = n;
   }
@@ -382,6 +421,9 @@ class ReluRuntime {
   int cap_, batch_;
   double unit_;
   int refine_ = 0;          // phase-aware back-substituted hidden-layer bounds (ReluConfig.refine)
+  std::vector<int> ra_;     // relaxed queries: RA dims and tolerance (x' box per node)
+  float tau_ = 0.f;
+  bool relaxed_ = false;
   int n0_ = 0, nh_ = 0, npa_ = 0, V_ = 0, Pp_ = 0;
   int pool_[2] = {0, 0};
   int cand_alloc_ = 0;
@@ -391,7 +433,7 @@ class ReluRuntime {
   RBuf<float> vals_;
   RBuf<int64_t> pairs_;
   RBuf<int> part_[2], pair_[2];
-  RBuf<float> lo_[2], hi_[2];
+  RBuf<float> lo_[2], hi_[2], plo_[2], phi_[2];
   RBuf<int8_t> phase_[2];
   RBuf<float> rlo_, rhi_, olb_, oub_, Lc_, Uc_, L0_, Le_, U0_, Ue_, lay_lb_, lay_ub_, score_, cpts_, pe_lb_, pe_ub_;
   RBuf<int> rpart_, split_, choice_, idim_, counters_, nodes_, nodes_start_, idx_;
@@ -409,9 +451,10 @@ class ReluRuntime {
 void register_relu(py::module& m) {
   py::class_<ReluRuntime>(m, "ReluRuntime")
       .def(py::init<py::handle, uintptr_t, std::vector<int>, std::vector<float>, std::vector<int64_t>, int, int,
-                    double, int>(),
+                    double, int, std::vector<int>, double>(),
            py::arg("net"), py::arg("flat"), py::arg("pa"), py::arg("values_f"), py::arg("pairs"),
-           py::arg("capacity"), py::arg("batch_nodes"), py::arg("unit"), py::arg("refine") = 0)
+           py::arg("capacity"), py::arg("batch_nodes"), py::arg("unit"), py::arg("refine") = 0,
+           py::arg("ra") = std::vector<int>(), py::arg("tau") = 0.0)
       .def("solve", &ReluRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("confirm"), py::arg("stream"));
 }

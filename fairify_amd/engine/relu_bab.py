@@ -214,9 +214,12 @@ class ReluBaBSolver:
     # ------------------------------------------------------------------------------------------
     def _solve_group(self, lo_np, hi_np, mlp_exact, status, time_budget):
         values_np, pairs_np = _pa_table(self.q, lo_np, hi_np)
-        # relaxed queries: the torch path (with the HIP bound kernels on the GPU); the native level
-        # kernels carry one box per node
-        if self.be.hip and not self.q.relaxed and os.environ.get("FAIRIFY_TORCH_BAB") != "1":
+        # the native runtime (csrc/relu_runtime.cpp) on the GPU, PA-only and relaxed queries alike
+        # (relaxed: an x' RA box per node; the second orientation is solve()'s negated network);
+        # FAIRIFY_TORCH_BAB=1: the torch orchestration (the reference semantics of the CPU tests)
+        # (FAIRIFY_RELU_RELAXED_TORCH=1: relaxed queries only, the A/B of the native relaxed path)
+        torch_rx = self.q.relaxed and os.environ.get("FAIRIFY_RELU_RELAXED_TORCH") == "1"
+        if self.be.hip and os.environ.get("FAIRIFY_TORCH_BAB") != "1" and not torch_rx:
             return self._solve_native(lo_np, hi_np, mlp_exact, status, values_np, pairs_np, time_budget)
         return self._solve_torch(lo_np, hi_np, mlp_exact, status, values_np, pairs_np, time_budget)
 
@@ -444,13 +447,16 @@ class ReluBaBSolver:
         from .bab import refine_level
 
         rf = min(1, refine_level(self.cfg.refine, self.be.widths))
-        key = (tuple(self.q.pa_idx), values_np.tobytes(), pairs_np.tobytes(), int(self.cfg.batch_nodes), rf)
+        ra = list(self.q.ra_idx) if self.q.relaxed else []
+        tau = float(self.q.tau) if self.q.relaxed else 0.0
+        key = (tuple(self.q.pa_idx), values_np.tobytes(), pairs_np.tobytes(), int(self.cfg.batch_nodes), rf,
+               tuple(ra), tau)
 
         def make(cap):
             return ext().ReluRuntime(_net(self.be), self.be.flat.data_ptr(), list(self.q.pa_idx),
                                      values_np.astype(np.float32).reshape(-1).tolist(),
                                      pairs_np.astype(np.int64).reshape(-1).tolist(), int(cap),
-                                     int(self.cfg.batch_nodes), float(self.be.unit), rf)
+                                     int(self.cfg.batch_nodes), float(self.be.unit), rf, ra, tau)
 
         return checkout(self.be, "_relu_rt", key, max(self.cfg.max_pool, 2 * n_root), make)
 

@@ -139,3 +139,54 @@ def test_native_relu_closes_residue(cuda, name, min_closed):
     tor = ReluBaBSolver(Backend(m, "cpu"), q, ReluConfig(node_budget=1024)).solve(lo, hi, m)
     both = (nat.status != UNKNOWN) & (tor.status != UNKNOWN)
     assert np.array_equal(nat.status[both], tor.status[both])
+
+
+@pytest.mark.parametrize("seed,tau", [(21, 2), (22, 3), (23, 2)])
+def test_native_relu_relaxed_matches_bruteforce_and_torch(cuda, seed, tau):
+    """Relaxed queries on the native runtime (x' RA box per node in csrc/relu_runtime.cpp, the
+    certificate concretising the copies' RA dims separately, x' RA splits; the second orientation on
+    the negated network): every decided verdict equals enumeration of all (x, x') pairs, every SAT
+    pair is exactly confirmed, and the verdicts agree with the torch orchestration where both
+    decide (FAIRIFY_TORCH_BAB=1)."""
+    from fairify_amd.engine import exact
+    from fairify_amd.spec import ADULT, Query
+
+    q = Query(pa=("sex",), ra=("age",), tau=tau).resolve(ADULT)
+    grid = presets.get("src/AC-sex").grid()
+    ids = processing_order(grid, 0)[:16]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 1)
+    pa, ra = q.pa_idx[0], q.ra_idx[0]
+    m = random_mlp(13, [6, 6], seed=seed, bias_scale=0.0 if seed % 2 else 0.5)
+    res = ReluBaBSolver(Backend(m, cuda), q, ReluConfig(node_budget=8192)).solve(lo, hi, m)
+    decided = 0
+    for k in range(len(ids)):
+        pts = np.array(list(itertools.product(*[range(a, b + 1) for a, b in zip(lo[k], hi[k])])))
+        truth = False
+        for s1 in (0, 1):
+            x = pts.copy()
+            x[:, pa] = s1
+            z = m.logits(x)
+            for d in range(-tau, tau + 1):
+                xp = x.copy()
+                xp[:, pa] = 1 - s1
+                xp[:, ra] += d
+                zp = m.logits(xp)
+                if (((z < 0) & (zp > 0)) | ((z > 0) & (zp < 0))).any():
+                    truth = True
+        if res.status[k] == SAT:
+            assert truth, k
+            ok = exact.check_pair_constraints(res.cex_x[k:k + 1], res.cex_xp[k:k + 1], lo[k:k + 1], hi[k:k + 1],
+                                              q.pa_idx, q.ra_idx, q.tau)
+            assert ok[0] and exact.is_violation(m, res.cex_x[k:k + 1], res.cex_xp[k:k + 1])[0]
+        elif res.status[k] == UNSAT:
+            assert not truth, k
+        decided += res.status[k] != UNKNOWN
+    assert decided >= 0.9 * len(ids)
+    os.environ["FAIRIFY_TORCH_BAB"] = "1"
+    try:
+        tor = ReluBaBSolver(Backend(m, cuda), q, ReluConfig(node_budget=8192)).solve(lo, hi, m)
+    finally:
+        del os.environ["FAIRIFY_TORCH_BAB"]
+    both = (res.status != UNKNOWN) & (tor.status != UNKNOWN)
+    assert np.array_equal(res.status[both], tor.status[both])
