@@ -50,6 +50,9 @@ def main():
         "lookahead16": replace(base, lookahead=16),
         "no_tighten": replace(base, tighten=False),
         "lr_x2": replace(base, lr_a=0.2, lr_b=1.0, lr_t=0.2),
+        "lr_t_x10": replace(base, lr_t=1.0),
+        "lr_t_x10_b256": replace(base, lr_t=1.0, node_budget=256),
+        "lr_t_x30_it128_b256": replace(base, lr_t=3.0, iters=128, root_iters=400, node_budget=256),
         "input_every1_b256": replace(base, node_budget=256, input_every=1),
         "input_every2_b256": replace(base, node_budget=256, input_every=2),
         "input_every3_b256": replace(base, node_budget=256, input_every=3),
