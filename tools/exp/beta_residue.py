@@ -42,8 +42,12 @@ def main():
     m = get_model(args.model, weights=args.weights, seed=0)
     be = Backend(m, device="cuda" if torch.cuda.device_count() else "cpu")
     base = BetaConfig(node_budget=64)
+    only = os.environ.get("BETA_RES_ONLY")
     settings = {
         "default(64)": base,
+        "iters512_root2000": replace(base, iters=512, root_iters=2000),
+        "iters1024_root4000_lr_half": replace(base, iters=1024, root_iters=4000, lr_a=0.05, lr_b=0.25, lr_t=0.05,
+                                              decay=0.995),
         "budget256": replace(base, node_budget=256),
         "budget1024": replace(base, node_budget=1024),
         "iters128": replace(base, iters=128, root_iters=400),
@@ -59,6 +63,8 @@ def main():
     }
     print(f"{args.model}: {len(ids)} residue partitions", flush=True)
     for name, cfg in settings.items():
+        if only and name not in only.split(","):
+            continue
         t0 = time.time()
         s = BetaBaBSolver(be, q, cfg)
         r = s.solve(lo, hi, m)
