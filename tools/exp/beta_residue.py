@@ -46,6 +46,10 @@ def main():
     settings = {
         "default(64)": base,
         "iters512_root2000": replace(base, iters=512, root_iters=2000),
+        "la0_b256": replace(base, lookahead=0, node_budget=256),
+        "la0_b1024": replace(base, lookahead=0, node_budget=1024),
+        "la2_b1024": replace(base, lookahead=2, node_budget=1024),
+        "la0_input2_b1024": replace(base, lookahead=0, node_budget=1024, input_every=2),
         "iters1024_root4000_lr_half": replace(base, iters=1024, root_iters=4000, lr_a=0.05, lr_b=0.25, lr_t=0.05,
                                               decay=0.995),
         "budget256": replace(base, node_budget=256),
