@@ -46,6 +46,9 @@ def main():
     settings = {
         "default(64)": base,
         "iters512_root2000": replace(base, iters=512, root_iters=2000),
+        "it256_b1024": replace(base, iters=256, root_iters=1000, node_budget=1024),
+        "it256_b4096": replace(base, iters=256, root_iters=1000, node_budget=4096),
+        "b4096": replace(base, node_budget=4096),
         "la0_b256": replace(base, lookahead=0, node_budget=256),
         "la0_b1024": replace(base, lookahead=0, node_budget=1024),
         "la2_b1024": replace(base, lookahead=2, node_budget=1024),
