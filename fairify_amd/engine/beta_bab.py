@@ -63,6 +63,8 @@ class BetaConfig:
     batch_nodes: int = 32768         # nodes per level launch
     time_budget: float = 1e9         # wall-clock seconds for the whole call
     max_pool: int = 1 << 21          # live nodes (more: the partitions losing nodes end UNKNOWN)
+    branch: str = "kernel"           # "lpgap" (experiment): split the neuron with the largest chord
+    #                                  slack at x* / x'* (the LP-BaB's primal-gap rule), not the kernel's
     input_every: int = 0             # > 0 (experiment): every this many levels of a tree, split the
     #                                  widest input dim (x, or x''s RA dims) instead of the kernel's choice
 
@@ -304,6 +306,11 @@ class BetaBaBSolver:
             gi = torch.nonzero(grow).flatten()
             bi = lev.binit[gi] if cfg.warm_beta else torch.zeros_like(lev.binit[gi])
             split = lev.split[gi]
+            if cfg.branch == "lpgap" and gi.numel():
+                ns = self._lp_gap_split(cur, gi, lev, pa, ra, tau, NH)
+                moved = (split >= 0) & (ns >= 0) & (ns != split)
+                split = torch.where(moved, ns, split)
+                bi = torch.where(moved[:, None], torch.zeros_like(bi), bi)   # new neuron: beta from 0
             if cfg.input_every > 0 and gi.numel():
                 split = self._force_input(cur, gi, split, pa, ra, n0, cfg.input_every)
             kids = self._children({kk: v[gi] for kk, v in cur.items()}, split, bi, NH, n0)
@@ -408,6 +415,36 @@ class BetaBaBSolver:
             kid[lk][ri[~low_child], d[~low_child]] = mid[~low_child] + 1
         # (plo / phi are read on the RA dims only; x' shares x's box everywhere else)
         return kid
+
+    def _lp_gap_split(self, cur, gi, lev, pa, ra, tau: float, NH: int):
+        """Per node: the unfixed unstable neuron (either copy) with the largest chord slack
+        u (z - l) / (u - l) - relu(z) at the node's vertex pair (x*, x'* on copy B's RA dims) -- the
+        LP-BaB's branching rule evaluated at beta's concretising point; -1 if none."""
+        be = self.be
+        xa = lev.xstar[gi].clone().to(be.dtype)
+        xb = (lev.xpstar[gi] if lev.xpstar is not None else lev.xstar[gi]).clone().to(be.dtype)
+        if ra:
+            xb[:, ra] = torch.minimum(torch.maximum(xb[:, ra], xa[:, ra] - tau), xa[:, ra] + tau)
+        xa[:, pa] = cur["va"][gi].to(be.dtype)
+        xb[:, pa] = cur["vb"][gi].to(be.dtype)
+        scores = []
+        for x, ph, LB, UB in ((xa, cur["phA"][gi], cur["LBA"][gi], cur["UBA"][gi]),
+                              (xb, cur["phB"][gi], cur["LBB"][gi], cur["UBB"][gi])):
+            h, off, sc = x, 0, []
+            for W, b in zip(be.ws[:-1], be.bs[:-1]):
+                z = h @ W + b
+                w = z.shape[1]
+                p_ = ph[:, off:off + w]
+                l_, u_ = LB[:, off:off + w].to(z.dtype), UB[:, off:off + w].to(z.dtype)
+                unst = (l_ < 0) & (u_ > 0) & (p_ == 0)
+                chord = u_ * (z - l_) / torch.where(unst, u_ - l_, torch.ones_like(u_))
+                sc.append(torch.where(unst, (chord - torch.relu(z)).clamp(min=0), torch.full_like(z, -1.0)))
+                h = torch.where(p_ < 0, torch.zeros_like(z), torch.where(p_ > 0, z, torch.relu(z)))
+                off += w
+            scores.append(torch.cat(sc, 1))
+        S = torch.cat(scores, 1)                       # [n, 2 NH]: copy A neurons, then copy B
+        best, j = S.max(dim=1)
+        return torch.where(best > 0, j, torch.full_like(j, -1)).to(lev.split.dtype)
 
     @staticmethod
     def _force_input(cur, gi, split, pa, ra, n0: int, every: int):

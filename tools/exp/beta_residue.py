@@ -46,6 +46,8 @@ def main():
     settings = {
         "default(64)": base,
         "iters512_root2000": replace(base, iters=512, root_iters=2000),
+        "lpgap_b1024": replace(base, branch="lpgap", node_budget=1024),
+        "lpgap_b4096": replace(base, branch="lpgap", node_budget=4096),
         "it256_b1024": replace(base, iters=256, root_iters=1000, node_budget=1024),
         "it256_b4096": replace(base, iters=256, root_iters=1000, node_budget=4096),
         "b4096": replace(base, node_budget=4096),
