@@ -24,7 +24,8 @@ field of this line.
 JSON keys (rank 0 prints one line; tests/test_bench_launch.py checks every one is present):
 metric, value, unit, n_gpus, steps, warmup, ms_per_step, higher_is_better, scaling, vs_baseline,
 dtype, data, config, decided_per_s_all, pct_verified, pct_verified_sound, partitions_per_s, sat,
-unsat, unknown, unsat_sound, unsat_heuristic, sat_by_stage, unsat_by_stage, dist, baseline.
+unsat, unknown, unsat_sound, unsat_heuristic, sat_by_stage, unsat_by_stage, dist, baseline,
+vs_baseline_note, per_model.
 
 Multi-GPU: one process per GPU, ``torch.distributed`` backend ``nccl`` (= RCCL over xGMI).
 
@@ -375,6 +376,12 @@ def main() -> None:
     # counters: attempted, decided, sat, unsat, unsat_heuristic, sat per stage, unsat per stage
     # (STAGES order)
     NC = 5 + 2 * len(STAGES)
+    # per model: attempted, unknown (no verdict), sound-unknown (no SOUND verdict), node expansions per
+    # stage (engine/pipeline.py:STAGE_NODE_COLS)
+    from fairify_amd.engine.pipeline import STAGE_NODE_COLS
+
+    NPM = 3 + len(STAGE_NODE_COLS)
+    pm_tot = np.zeros((len(models), NPM))
 
     def one_item(k: int, j, ids: np.ndarray, uis=None, high: bool = False):
         m, be = models[k], backends[k]
@@ -394,6 +401,12 @@ def main() -> None:
         for i, name in enumerate(STAGES):
             out[5 + i] = (sat & (st == name)).sum()
             out[5 + len(STAGES) + i] = (uns & (st == name)).sum()
+        pm = np.zeros(NPM)
+        sound = (sat & (st != "heuristic")) | (uns & ~np.isin(st, UNSOUND_UNSAT))
+        pm[:3] = [len(recs), (~(sat | uns)).sum(), (~sound).sum()]
+        sn = recs.cols.get("stage_nodes")
+        if sn is not None:
+            pm[3:] = sn.sum(axis=0)
         costs = {}
         if uis is not None:      # per-unit cost of the next step's LPT: node expansions + fixed cost
             nodes = recs.cols["nodes"].astype(np.float64)
@@ -402,9 +415,9 @@ def main() -> None:
                 nu = len(BL.unit_ids(order, units[ui][1], U))
                 costs[ui] = node_w[k] * (float(nodes[o:o + nu].sum()) + FIXED_COST * nu)
                 o += nu
-        return out, costs
+        return out, costs, (k, pm)
 
-    def run_step(step: int):
+    def run_step(step: int, timed: bool = False):
         step_no[0], step_t0[0] = step, time.time()
         items = items_for_step(step)
         items.sort(key=lambda it: (-item_cost.get((it[0], it[1]), 0.0), -models[it[0]].n_neurons))
@@ -414,9 +427,12 @@ def main() -> None:
         else:
             res = [f.result() for f in [pool.submit(one_item, k, j, ids, uis, i < n_hi)
                                         for i, (k, j, ids, uis) in enumerate(items)]]
+        if timed:
+            for _, _, (k, pm) in res:
+                pm_tot[k] += pm
         if balanced:
             local = np.zeros(len(units))
-            for _, costs in res:
+            for _, costs, _ in res:
                 for ui, cval in costs.items():
                     local[ui] = cval
             if args.emulate_shard:
@@ -424,7 +440,7 @@ def main() -> None:
                     ucost[:] = local                             # every unit ran here
             else:
                 ucost[:] = D.all_reduce_sum(info, local)         # every unit ran on exactly one rank
-        return sum((o for o, _ in res), np.zeros(NC))
+        return sum((o for o, _, _ in res), np.zeros(NC))
 
     sync = (lambda: torch.cuda.synchronize(info.device)) if info.device.type == "cuda" else (lambda: None)
 
@@ -450,7 +466,7 @@ def main() -> None:
     t0 = time.time()
     tot = np.zeros(NC)
     for s in range(args.steps):
-        tot += run_step(args.warmup + s)
+        tot += run_step(args.warmup + s, timed=True)
     sync()
     marker(2)
     t_local = time.time() - t0          # this rank's own work, before waiting for the others
@@ -460,6 +476,7 @@ def main() -> None:
     dt_max = D.all_reduce_max(info, dt)
     rank_ms = D.all_gather_floats(info, 1000.0 * t_local / max(1, args.steps))
     tot = D.all_reduce_sum(info, tot)
+    pm_all = D.all_reduce_sum(info, pm_tot.reshape(-1)).reshape(pm_tot.shape) / max(1, args.steps)
     att, dec, sat, uns, uns_h = tot[:5].tolist()
     sat_stage = {name: int(tot[5 + i]) for i, name in enumerate(STAGES)}
     unsat_stage = {name: int(tot[5 + len(STAGES) + i]) for i, name in enumerate(STAGES)}
@@ -521,6 +538,18 @@ def main() -> None:
                  "native_mem": _mem_delta(mem0, _native_mem())},
         "baseline": {"decided_per_s": round(BASELINE_DECIDED_PER_S, 5), "pct_verified_of_attempted": 89.0,
                      "coverage_of_grid_pct": 0.29},
+        # vs_baseline divides this random-init rate by the reference's TRAINED-weight Table-V rate: a
+        # cross-regime ratio.  The trained-weight comparison at equal budgets is its own run
+        # (tools/baseline_configs.py --group tablev; profiles/r6/baseline_configs.md).
+        "vs_baseline_note": "cross-regime: random-init AC suite (this run) / trained-weight Table V AC-sex "
+                            "aggregate (553 decided in 22 144 s); trained Table V at one HEAD: "
+                            "profiles/r6/baseline_configs.md",
+        # per model and per timed step: attempted, unknown, sound-unknown (no sound verdict) and node
+        # expansions per stage
+        "per_model": {m.name: {"attempted": int(round(pm_all[k, 0])), "unknown": round(float(pm_all[k, 1]), 1),
+                               "unknown_sound": round(float(pm_all[k, 2]), 1),
+                               "nodes": {c: int(round(pm_all[k, 3 + i])) for i, c in enumerate(STAGE_NODE_COLS)}}
+                      for k, m in enumerate(models)},
     }
     if args.budget_pass > 0:
         # per-model wall budget B: every (model, chunk) item gets the chunk's share of B for its

@@ -416,6 +416,8 @@ struct BetaArgs {
   int lookahead;            // candidates per score of the filtered branching (0: best gap score)
   int beta_pos;             // project beta >= 0 (1) or keep it free-signed (0)
   int stall;                // 1: when no look-ahead candidate's children beat the node, split the input
+  int pgap;                 // 1: branch by the primal gap mean(h) - relu(mean(z)) of the optimisation's
+                            // averaged primal iterates (the verified LP's rule at its optimum)
   int wpb;                  // waves per workgroup
   int wt_lds;               // 1: transposed weights staged in LDS too
   double* bound;            // [R] rigorous lower bound of t N(x,va) - (1-t) N(x,vb) (+inf: empty region)

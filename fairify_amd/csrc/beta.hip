@@ -74,6 +74,8 @@ struct Slab {            // per-wave LDS workspace
   float* ub[2];
   float* lam[2];         // multiplier on h_j of the last backward pass [NH]
   float* z[2];           // linearised pre-activations at x* [NH]
+  float* zb[2];          // pgap: sums of z / of the relaxation outputs h over the optimisation steps
+  float* hb[2];          //   (the Lagrangian's primal iterates; their mean is the primal point) [NH]
   float* sc;             // branching scores [2 NH]
   int8_t* kd[2];         // relaxation kind of the last backward pass (0 off, 1 identity, 2 alpha, 3 chord)
   int8_t* ph[2];         // phases
@@ -253,8 +255,9 @@ __device__ T conc(const NetDesc& nd, const Slab& S, const Node& N, const T* cA, 
       part += ta + tb + tt;
       if (RIG) {
         mag += tabs(ta) + tabs(tb) + tabs(tt);
-        emag += (T)2 * (tabs(ca) * (T)fmaxf(fabsf(lo), fabsf(hi)) + tabs(cb) * (T)fmaxf(fabsf(plo), fabsf(phi)) +
-                        tabs(tt));
+        // fl(gp - gm) is off by u (gp + gm): charged on both copies' magnitudes (ca may cancel it)
+        const T mxa = (T)fmaxf(fabsf(lo), fabsf(hi)), mxb = (T)fmaxf(fabsf(plo), fabsf(phi));
+        emag += (T)2 * (tabs(ca) * mxa + tabs(cb) * mxb + tabs(tt) + (gp + gm) * (mxa + mxb));
       }
       if (WX) {
         S.xs[i] = xa;
@@ -286,9 +289,11 @@ __device__ T conc(const NetDesc& nd, const Slab& S, const Node& N, const T* cA, 
 }
 
 // Linearised network of copy c at S.xs (PA dims = v): records z per neuron, returns the logit.
+// zacc / hacc (pgap, optional): each neuron's z and relaxation output h are added to them (the
+// primal iterate of this optimisation step; neuron k is always handled by the same lane).
 template <typename T>
 __device__ T fwd(const NetDesc& nd, const float* Wf, const Slab& S, const Node& N, int c, const float* v,
-                 const float* __restrict__ al) {
+                 const float* __restrict__ al, float* zacc = nullptr, float* hacc = nullptr) {
   const int lane = threadIdx.x & 63;
   const int L = nd.n_layers;
   const int n0 = nd.dims[0];
@@ -321,6 +326,10 @@ __device__ T fwd(const NetDesc& nd, const float* Wf, const Slab& S, const Node& 
         h = ubj / (ubj - lbj) * (z - lbj);
       }
       h1[j] = h;
+      if (zacc) {
+        zacc[k] += (float)z;
+        hacc[k] += (float)h;
+      }
     }
     wsync();
     T* tmp = h0;
@@ -362,7 +371,7 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   const int NHp = (NH + 3) & ~3;
   const int n0p = (n0 + 3) & ~3;
   const int mwp = (mw + 3) & ~3;
-  const int slab = 11 * NHp + 4 * mwp + 13 * n0p + 32;
+  const int slab = 15 * NHp + 4 * mwp + 13 * n0p + 32;
   float* base = smem + tot4 * (WTL ? 2 : 1) + wave * slab;
   Slab S;
   S.lb[0] = base; S.ub[0] = base + NHp; S.lb[1] = base + 2 * NHp; S.ub[1] = base + 3 * NHp;
@@ -371,7 +380,8 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   S.sc = base + 8 * NHp;                                  // 2 NHp
   int8_t* bytes = reinterpret_cast<int8_t*>(base + 10 * NHp);
   S.kd[0] = bytes; S.kd[1] = bytes + NHp; S.ph[0] = bytes + 2 * NHp; S.ph[1] = bytes + 3 * NHp;
-  double* dbase = reinterpret_cast<double*>(base + 11 * NHp);  // 11 NHp is a multiple of 4: 16-B aligned
+  S.zb[0] = base + 11 * NHp; S.zb[1] = base + 12 * NHp; S.hb[0] = base + 13 * NHp; S.hb[1] = base + 14 * NHp;
+  double* dbase = reinterpret_cast<double*>(base + 15 * NHp);  // 15 NHp is a multiple of 4: 16-B aligned
   S.b0 = dbase; S.b1 = dbase + mwp;
   S.cf[0] = dbase + 2 * mwp; S.cf[1] = S.cf[0] + n0p; S.hm[0] = S.cf[1] + n0p; S.hm[1] = S.hm[0] + n0p;
   S.cft = reinterpret_cast<float*>(S.hm[1] + n0p);
@@ -447,8 +457,9 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
     }
     return;
   }
-  // every neuron's state is touched by the SAME lane everywhere (lane j of its layer), so no
-  // lane reads a global word another lane of the wave wrote
+  // every neuron's state (par / cur / Adam moments, the pgap sums) is touched by the SAME lane
+  // everywhere (lane j of its layer, j mod 64), so no lane reads a global word another lane of the
+  // wave wrote (the scores and the split neuron's binit use that mapping too)
   for (int l = 0; l < L - 1; ++l)
     for (int j = lane; j < nd.dims[l + 1]; j += 64)
       for (int q = 0; q < 4; ++q) {
@@ -456,6 +467,10 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         cur[k] = par[k];
         mom[k] = 0.f;
         vel[k] = 0.f;
+        S.zb[0][k - q * NH] = 0.f;     // (q-invariant: the sums of neuron nd.neuron_off[l] + j)
+        S.zb[1][k - q * NH] = 0.f;
+        S.hb[0][k - q * NH] = 0.f;
+        S.hb[1][k - q * NH] = 0.f;
       }
   float tc = a.t[r], tbest = tc, mt = 0.f, vt = 0.f;
   float best = -FLT_MAX;
@@ -474,6 +489,7 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   float* cB = reinterpret_cast<float*>(S.cf[1]);
   const float b1c = 0.9f, b2c = 0.999f;
   float p1 = 1.f, p2 = 1.f, dk = 1.f;
+  int nacc = 0;                                    // primal iterates summed (pgap)
   for (int it = 0; it < a.iters; ++it) {
     const float kA = bwd<float, false, true, WTL>(nd, Wf, Wt, S, 0, tc, cur, cur + 2 * NH, -1, 0, cA, nullptr,
                                                   nullptr);
@@ -492,8 +508,9 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
           for (int q = 0; q < 4; ++q) par[q * NH + nd.neuron_off[l] + j] = cur[q * NH + nd.neuron_off[l] + j];
     }
     if (best > 0.f) break;
-    const float oA = fwd<float>(nd, Wf, S, N, 0, N.va, cur);
-    const float oB = fwd<float>(nd, Wf, S, N, 1, N.vb, cur + NH);
+    const float oA = fwd<float>(nd, Wf, S, N, 0, N.va, cur, a.pgap ? S.zb[0] : nullptr, S.hb[0]);
+    const float oB = fwd<float>(nd, Wf, S, N, 1, N.vb, cur + NH, a.pgap ? S.zb[1] : nullptr, S.hb[1]);
+    ++nacc;
     // Adam (bias-corrected), gradient ascent, projected
     p1 *= b1c;
     p2 *= b2c;
@@ -591,24 +608,36 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
     }
     return;
   }
-  // ---- branching scores: |lam| x relaxation gap at x* of unfixed unstable neurons
+  // ---- branching scores of unfixed unstable neurons: |lam| x relaxation gap at x*, or (pgap) the
+  // primal gap mean(h) - relu(mean(z)) over the optimisation steps (the verified LP's rule,
+  // smt/lpbab.py:_lp_bab, at the ergodic primal point).  Same lane mapping as the writers of par.
+  const bool use_pg = a.pgap && nacc > 0;
+  const float inv_n = 1.f / (float)(nacc > 0 ? nacc : 1);
   for (int c = 0; c < 2; ++c)
-    for (int k = lane; k < NH; k += 64) {
-      const int kind = S.kd[c][k];
-      float s = 0.f;
-      if (kind >= 2 && S.ph[c][k] == 0) {
-        const float z = S.z[c][k];
-        const float rz = fmaxf(z, 0.f);
-        float gap;
-        if (kind == 2) gap = rz - par[c * NH + k] * z;
-        else {
+    for (int l = 0; l < L - 1; ++l)
+      for (int j = lane; j < nd.dims[l + 1]; j += 64) {
+        const int k = nd.neuron_off[l] + j;
+        const int kind = S.kd[c][k];
+        float s = 0.f;
+        if (use_pg) {
           const float lbj = S.lb[c][k], ubj = S.ub[c][k];
-          gap = ubj / (ubj - lbj) * (z - lbj) - rz;
+          if (S.ph[c][k] == 0 && lbj < 0.f && ubj > 0.f) {
+            const float zm = S.zb[c][k] * inv_n, hm = S.hb[c][k] * inv_n;
+            s = fmaxf(hm - fmaxf(zm, 0.f), 0.f);
+          }
+        } else if (kind >= 2 && S.ph[c][k] == 0) {
+          const float z = S.z[c][k];
+          const float rz = fmaxf(z, 0.f);
+          float gap;
+          if (kind == 2) gap = rz - par[c * NH + k] * z;
+          else {
+            const float lbj = S.lb[c][k], ubj = S.ub[c][k];
+            gap = ubj / (ubj - lbj) * (z - lbj) - rz;
+          }
+          s = fabsf(S.lam[c][k]) * fabsf(gap);
         }
-        s = fabsf(S.lam[c][k]) * fabsf(gap);
+        S.sc[c * NH + k] = s;
       }
-      S.sc[c * NH + k] = s;
-    }
   wsync();
   int j0;
   float mx;
@@ -692,21 +721,27 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
     if (a.stall && (double)bw <= Bd) mx = 0.f;
   }
   // ---- outputs
-  if (lane == 0) {
-    a.bound[r] = Bd;
-    float b_in = 0.f, b_ac = 0.f;
-    int sp;
-    if (mx > 0.f) {
-      sp = jsel;
-      const int c = jsel >= NH ? 1 : 0;
-      const int k = jsel - c * NH;
+  if (mx > 0.f) {
+    // the split neuron's child multipliers, written by the lane that owns its par entries
+    const int c = jsel >= NH ? 1 : 0;
+    const int k = jsel - c * NH;
+    int l = 0;
+    while (l < L - 2 && k >= nd.neuron_off[l + 1]) ++l;
+    if (lane == ((k - nd.neuron_off[l]) & 63)) {
       const float lam = S.lam[c][k];
       const int kind = S.kd[c][k];
       float slope = 0.f;
       if (kind == 2) slope = par[c * NH + k];
       else if (kind == 3) slope = S.ub[c][k] / (S.ub[c][k] - S.lb[c][k]);
-      b_in = lam * slope;
-      b_ac = lam * (1.f - slope);
+      a.binit[2 * r] = lam * slope;
+      a.binit[2 * r + 1] = lam * (1.f - slope);
+    }
+  }
+  if (lane == 0) {
+    a.bound[r] = Bd;
+    int sp;
+    if (mx > 0.f) {
+      sp = jsel;
     } else {
       // input split: |coefficient| x width over x's non-PA dims (an RA dim: copy A's coefficient)
       // and, relaxed, x''s RA dims (copy B's, code n0 + d); none left: a lattice leaf
@@ -738,8 +773,10 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
       sp = bd >= 0 ? -1 - bd : -(2 * n0 + 1);
     }
     a.split[r] = sp;
-    a.binit[2 * r] = b_in;
-    a.binit[2 * r + 1] = b_ac;
+    if (!(mx > 0.f)) {
+      a.binit[2 * r] = 0.f;
+      a.binit[2 * r + 1] = 0.f;
+    }
   }
 }
 
@@ -751,7 +788,7 @@ extern "C" size_t fa_beta_slab_floats(const NetDesc& nd) {
   const int NHp = (nd.n_hidden + 3) & ~3;
   const int n0p = (nd.dims[0] + 3) & ~3;
   const int mwp = (nd.max_width + 3) & ~3;
-  return (size_t)(11 * NHp + 4 * mwp + 13 * n0p + 32);
+  return (size_t)(15 * NHp + 4 * mwp + 13 * n0p + 32);
 }
 
 // Launch configuration: waves per workgroup and whether the transposed weights fit in LDS next to

@@ -548,7 +548,8 @@ PYBIND11_MODULE(_C, m) {
     a.decay = decay;
     a.lookahead = lookahead;
     a.beta_pos = beta_pos;
-    a.stall = stall;
+    a.stall = stall & 1;        // bit 1: primal-gap branching (ops/hip.py:beta_level)
+    a.pgap = (stall >> 1) & 1;
     a.bound = P<double>(bound);
     a.split = P<int>(split);
     a.xstar = P<float>(xstar);

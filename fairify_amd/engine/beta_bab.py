@@ -63,8 +63,10 @@ class BetaConfig:
     batch_nodes: int = 32768         # nodes per level launch
     time_budget: float = 1e9         # wall-clock seconds for the whole call
     max_pool: int = 1 << 21          # live nodes (more: the partitions losing nodes end UNKNOWN)
-    branch: str = "kernel"           # "lpgap" (experiment): split the neuron with the largest chord
-    #                                  slack at x* / x'* (the LP-BaB's primal-gap rule), not the kernel's
+    branch: str = "kernel"           # "pgap": the verified LP's rule (largest primal gap h - relu(z)) at the
+    #                                  averaged primal iterate of the node's optimisation (kernel-side;
+    #                                  with lookahead > 0 it supplies the first candidate list);
+    #                                  "lpgap" (experiment): the chord slack at the vertex x* / x'*
     input_every: int = 0             # > 0 (experiment): every this many levels of a tree, split the
     #                                  widest input dim (x, or x''s RA dims) instead of the kernel's choice
 
@@ -271,7 +273,7 @@ class BetaBaBSolver:
                                     cur["LBB"], cur["UBB"], cur["phA"], cur["phB"], cur["alA"], cur["alB"],
                                     cur["beA"], cur["beB"], cur["t"], cfg.root_iters if is_root else cfg.iters,
                                     cfg.lr_a * sc, cfg.lr_b * sc, cfg.lr_t * sc, cfg.decay, cfg.lookahead,
-                                    cfg.beta_pos, rx)
+                                    cfg.beta_pos, rx, pgap=cfg.branch == "pgap")
             if empty is not None:
                 lev.bound = torch.where(empty, torch.full_like(lev.bound, float("inf")), lev.bound)
             closed = lev.bound >= 0

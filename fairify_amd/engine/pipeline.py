@@ -519,6 +519,13 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     cex_xp[newly_sat] = res.cex_xp[newly_sat]
     status = res.status.copy()
     nodes = res.nodes.copy()
+    # node expansions per stage (STAGE_NODE_COLS; bench JSON / diagnostics): each stage's delta of `nodes`
+    stage_nodes = np.zeros((Pn, len(STAGE_NODE_COLS)), dtype=np.int64)
+    stage_nodes[:, 0] = res.nodes
+
+    def charge(col: int, before: np.ndarray) -> None:
+        stage_nodes[:, col] += (nodes - before).astype(np.int64)
+
     open_left = res.open_left
     forced = faults.forced_unknown(ids) & (stage == "bab")      # fault injection: solver "timeouts"
     if forced.any():
@@ -597,7 +604,9 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             t_bab += time.time() - t0
 
     if not esc_after_relu:
+        n0_ = nodes.copy()
         escalate()
+        charge(0, n0_)
 
     # ---------------- stage 3r: ReLU-phase branch-and-bound on the residue (rigorous GPU bounds
     # with neuron-phase splits: the exact-zero partitions input splitting cannot close)
@@ -605,6 +614,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         from .relu_bab import ReluBaBSolver, ReluConfig
 
         unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
+        n0_ = nodes.copy()
         if unk.size:
             t0 = time.time()
             el = time.time() - t_start
@@ -622,6 +632,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             nodes[unk] += rres.nodes
             sync()
             t_bab += time.time() - t0
+        charge(1, n0_)
     # ---------------- stage 3b': beta-CROWN phase-split BaB on the residue (the wide nets' UNSAT
     # partitions need phase splits as constraints on the region: Lagrangian split multipliers)
     from .beta_bab import supported as _beta_supported
@@ -633,13 +644,17 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         if unk.size:
             t0 = time.time()
             el = time.time() - t_start
+            n0_ = nodes.copy()
             with tm("beta"):
                 _beta_round(be, q, mlp, unk, lo_np, hi_np, cfg.beta_budget, max(0.0, budget - el), cfg.batch_nodes,
                             status, stage, cex_x, cex_xp, nodes, tm, probe_levels=cfg.beta_probe_levels)
+            charge(2, n0_)
             sync()
             t_bab += time.time() - t0
     if esc_after_relu:
+        n0_ = nodes.copy()
         escalate()
+        charge(0, n0_)
 
     # ---------------- stage 3c: exact host solver on the residue (the reference's Z3 check,
     # src/AC/Verify-AC.py:145-158): Z3 when installed, else the HiGHS MILP back-end fed the
@@ -687,6 +702,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
 
     # ---------------- stage 3d: anytime escalation on the residue (sound; before the heuristic)
     anytime_rounds = 0
+    n_any = nodes.copy()
     if cfg.anytime_seconds > 0:
         t0 = time.time()
         deadline = t0 + cfg.anytime_seconds
@@ -857,6 +873,8 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     masked: Dict[int, np.ndarray] = {}
     t_heur = 0.0
     unk = np.nonzero(status == UNKNOWN)[0]
+    charge(3, n_any)          # every anytime round (between n_any and here)
+    n_h = nodes.copy()
     if cfg.heuristic and unk.size and ibp_ub is not None:
         t0 = time.time()
         h_attempt[unk] = 1
@@ -900,6 +918,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             real = exact.is_violation(mlp, cex_x[hs], cex_xp[hs]) & ok
             stage[hs[real]] = "heuristic-confirmed"
         nodes[unk] += hres.nodes
+        charge(4, n_h)
         sync()
         t_heur = time.time() - t0
 
@@ -970,6 +989,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         h_attempt=h_attempt, h_success=h_success,
         b_cnt=b_cnt, s_cnt=s_cnt, st_cnt=st_cnt, h_cnt=h_cnt, t_cnt=t_cnt, agree=agree, tp=tp, fp=fp, nodes=nodes.astype(np.int64),
         c_check=c_check, v_accurate=v_acc, cex_x=cex_x, cex_xp=cex_xp)
+    core["stage_nodes"] = stage_nodes
     if mask_bits is not None:
         core["mask_bits"] = mask_bits
     return core, (Pn, t_sim + t_prune + t_bab, t_bab, t_heur, t_replay)
@@ -1050,6 +1070,9 @@ def concat_records(parts: Sequence["ChunkRecords"]) -> "ChunkRecords":
                         sim_size=parts[0].sim_size)
 
 
+# node expansions per stage (core["stage_nodes"] columns): input-split BaB with its escalation, the
+# ReLU-phase BaB, the fixed beta pass, every anytime round, the heuristic retry
+STAGE_NODE_COLS = ("bab", "relu", "beta", "anytime", "heuristic")
 CORE_COLUMNS = ("grid_id", "verdict", "stage", "h_attempt", "h_success", "b_cnt", "s_cnt", "st_cnt", "h_cnt",
                 "t_cnt", "agree", "tp", "fp", "nodes", "c_check", "v_accurate", "cex_x", "cex_xp")
 
@@ -1107,7 +1130,7 @@ class ChunkRecords(Sequence):
 
     _INT = ("grid_id", "h_attempt", "h_success", "c_check", "v_accurate", "nodes")
     _HIDE = ("cex_x", "cex_xp", "b_cnt", "s_cnt", "st_cnt", "h_cnt", "t_cnt", "agree", "tp", "fp", "pruned_f1",
-             "mask_bits")
+             "mask_bits", "stage_nodes")
 
     def __init__(self, core: Dict[str, np.ndarray], orig_acc: Optional[float] = None, segments=None,
                  n_neurons: int = 1, sim_size: int = 1):

@@ -38,7 +38,7 @@ from ..report.csv_report import PartitionCSV, format_table, table_v_row_columns,
 from ..utils import faults, heap
 from ..utils.timer import StageTimer
 from .stages import STAGES as _STAGES
-from .pipeline import PartitionRecord, StreamPool, VerifyConfig, concat_records, verify_chunk
+from .pipeline import STAGE_NODE_COLS, PartitionRecord, StreamPool, VerifyConfig, concat_records, verify_chunk
 
 VCODE = {"sat": 1, "unsat": 2, "unknown": 0}
 VNAME = {v: k for k, v in VCODE.items()}
@@ -338,6 +338,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         last_note = time.time()
         inflight = None      # (async gather handle, per-rank positions) of the previous round
         rank_work = [0.0, 0]  # this rank's BaB node expansions and partitions (balance report)
+        rank_snodes = np.zeros(len(STAGE_NODE_COLS))   # ... of them per stage (pipeline.STAGE_NODE_COLS)
 
         def flush(item):
             handle, rpos, retried, expect = item
@@ -423,6 +424,8 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                 codes = wire.verdict_codes(recs)
                 rank_work[0] += float(recs.core["nodes"].sum())
                 rank_work[1] += len(recs)
+                if "stage_nodes" in recs.core:
+                    rank_snodes += recs.core["stage_nodes"].sum(axis=0)
             retried = None
             if escalate > 1:
                 all_codes = D.all_gather_int8(info, codes)
@@ -461,6 +464,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
         wall = D.all_reduce_max(info, rank_busy)
         rank_nodes = D.all_gather_floats(info, rank_work[0])
         rank_parts = D.all_gather_floats(info, float(rank_work[1]))
+        snodes = D.all_reduce_sum(info, rank_snodes)
         if info.is_main:
             tc = {k: (np.concatenate(v) if v else np.zeros(0)) for k, v in table_cols.items()}
             stage_codes = tc.pop("stage").astype(np.int64)
@@ -489,6 +493,10 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
             row["balance"] = "queue" if queue else ("strided" if info.world > 1 else "none")
             row["rank_nodes"] = [int(v) for v in rank_nodes]
             row["rank_partitions"] = [int(v) for v in rank_parts]
+            # where the work went: node expansions per stage (all ranks) and rank 0's stage timers
+            # (host-thread wall seconds, summed over concurrent threads: a breakdown, not a wall time)
+            row["stage_nodes"] = {c: int(snodes[i]) for i, c in enumerate(STAGE_NODE_COLS)}
+            row["stage_s"] = {k: round(v, 3) for k, v in sorted(timer.t.items(), key=lambda kv: -kv[1])}
             if cfg.keep_masks and mask_parts:
                 from ..report.masks import write_masks
 

@@ -132,8 +132,9 @@ def _backward(ws, bs, LB, UB, ph, al, be, scale, hmax_in, rig: bool):
     return lam, c, err, rec
 
 
-def _forward_lin(ws, bs, x, LB, rec, al):
-    """Pre-activations of the linearised network (each neuron's chosen relaxation) at x; logit."""
+def _forward_lin(ws, bs, x, LB, rec, al, hs=None):
+    """Pre-activations of the linearised network (each neuron's chosen relaxation) at x; logit.
+    ``hs`` (a list): receives each layer's relaxation outputs h (the Lagrangian's primal iterate)."""
     h = x
     zs = []
     for l in range(len(ws) - 1):
@@ -142,6 +143,8 @@ def _forward_lin(ws, bs, x, LB, rec, al):
         lam, kind, s, _ = rec[l]
         h = torch.where(kind == 1, z, torch.where(kind == 2, al[l] * z,
                                                   torch.where(kind == 3, s * (z - LB[l]), torch.zeros_like(z))))
+        if hs is not None:
+            hs.append(h)
     return zs, (h @ ws[-1] + bs[-1][None])[:, 0]
 
 
@@ -204,8 +207,10 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
         mag = terms.abs().sum(1) + tA.abs().sum(1) + tB.abs().sum(1) + pA.abs().sum(1) + pB.abs().sum(1) + \
             kA.abs() + kB.abs() + ktie.abs()
         econ = U64 * (coef.abs() * torch.maximum(lo_.abs(), hi_.abs())).sum(1) + _g(2 * n0 + 4) * mag
-        if tie:     # the RA coefficient sums cA + (gP - gM) etc. and tau (gP + gM)
-            econ = econ + 2 * U64 * torch.where(ram[None], cAe.abs() * hmA + cBe.abs() * hmB, torch.zeros_like(cA)).sum(1) \
+        if tie:     # the RA coefficient sums cA + (gP - gM) etc. and tau (gP + gM); fl(gP - gM) is off by
+            # u (gP + gM), charged on both copies' magnitudes (cA may cancel it: |cAe| alone does not cover it)
+            econ = econ + 2 * U64 * torch.where(ram[None], cAe.abs() * hmA + cBe.abs() * hmB +
+                                                (gP + gM) * (hmA + hmB), torch.zeros_like(cA)).sum(1) \
                 + 2 * U64 * ktie.abs()
         B = B - (eA + eB + econ) * (1 + 1e-6)
     out = {"B": B, "xs": xs, "xps": xps, "cA": cAe, "cB": cBe, "coef": coef, "g": None, "lin": None}
@@ -214,8 +219,9 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
     xa, xb = xs.clone(), xps.clone()
     xa[:, pa] = va.to(dt)
     xb[:, pa] = vb.to(dt)
-    zA, oA = _forward_lin(ws, bs, xa, bA[0], rA, alA)
-    zB, oB = _forward_lin(ws, bs, xb, bB[0], rB, alB)
+    hA, hB = [], []
+    zA, oA = _forward_lin(ws, bs, xa, bA[0], rA, alA, hA)
+    zB, oB = _forward_lin(ws, bs, xb, bB[0], rB, alB, hB)
     g = {"t": oA + oB}
     if tie:
         g["gP"] = torch.where(ram[None], xs - xps - tau, torch.zeros_like(xs))
@@ -227,6 +233,7 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
                         for zz, p, be_, lb, ub in zip(z, ph, bet, bnd[0], bnd[1])]
     out["g"] = g
     out["lin"] = ((zA, rA), (zB, rB))
+    out["h"] = (hA, hB)
     return out
 
 
@@ -294,6 +301,19 @@ def _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, 
     return torch.where(torch.isfinite(bw) | (bw > 0), pick, j0), bw
 
 
+def primal_gap_scores(zsum, hsum, n, lb, ub, ph):
+    """[R, 2 NH] the LP-BaB branching score at the averaged primal point: for an unfixed neuron
+    unstable over the node's (phase-clamped) bounds, ``max(h_bar - relu(z_bar), 0)`` with z_bar /
+    h_bar the means of the linearised network's pre-activations / relaxation outputs over the ``n``
+    optimisation steps (fp32 sums, the kernel's order: one step at a time); 0 elsewhere."""
+    nn = n.clamp(min=1.0)[:, None]
+    zb = zsum.float() / nn
+    hb = hsum.float() / nn
+    gap = (hb - torch.relu(zb)).clamp(min=0)
+    un = (ph == 0) & (lb < 0) & (ub > 0)
+    return torch.where(un & (n[:, None] > 0), gap, torch.zeros_like(gap))
+
+
 def clamp_bounds(LB: torch.Tensor, UB: torch.Tensor, ph: torch.Tensor):
     """Phase-clamped pre-activation bounds [R, NH] and the rows whose region they prove empty."""
     lb = torch.where(ph > 0, LB.clamp(min=0), LB)
@@ -303,7 +323,7 @@ def clamp_bounds(LB: torch.Tensor, UB: torch.Tensor, ph: torch.Tensor):
 
 def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t,
               iters: int, lr_a: float, lr_b: float, lr_t: float, decay: float = 1.0,
-              lookahead: int = 0, beta_pos: bool = True, rx=None, stall: bool = True) -> BetaLevel:
+              lookahead: int = 0, beta_pos: bool = True, rx=None, stall: bool = True, pgap: bool = False) -> BetaLevel:
     """One BaB level of rows R (the HIP kernel's semantics, csrc/beta.hip): ``iters`` projected-Adam
     steps in fp32 from the rows' current (alpha, beta, t) -- updated IN PLACE to the best iterate --
     then the rigorous fp64 bound, the branching decision and x* at those parameters.
@@ -311,7 +331,14 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     lo, hi [R, n0]; va, vb [R, npa]; LB*/UB* [R, NH] partition bounds (unclamped); ph* [R, NH] int8;
     al*/be* [R, NH] float32; t [R] float32.  ``rx`` = (ra [n0] bool, plo, phi [R, n0]): relaxed
     queries, copy B's RA dims over their own box (:func:`evaluate`); x' RA dims are split too
-    (``split`` = -1 - (n0 + d))."""
+    (``split`` = -1 - (n0 + d)).
+
+    ``pgap``: branch by the verified LP's rule (smt/lpbab.py:_lp_bab) at a primal point of the node's
+    relaxation instead of at the vertex x*: the Lagrangian's primal iterates (x*, z, h of the
+    linearised network) are averaged over the optimisation steps -- the ergodic average of a dual
+    (sub)gradient method converges to a primal optimum of the LP it dualises -- and an unfixed
+    unstable neuron scores its primal gap ``mean(h) - relu(mean(z))`` (look-ahead, when on, takes its
+    first candidate list from these scores)."""
     R, n0 = lo.shape
     dev = lo.device
     lbA, ubA, infA = clamp_bounds(LBA, UBA, phA)
@@ -338,10 +365,19 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     vt = torch.zeros_like(t)
     b1, b2, eps = 0.9, 0.999, 1e-8
     act = ~infeas
+    zsum = hsum = None
+    nsum = torch.zeros(R, dtype=torch.float32, device=dev)
     for it in range(iters):
         ev = evaluate(ws32, bs32, lo, hi, pa, va, vb, bA32, bB32, pA, pB, L32(cur["alA"]), L32(cur["alB"]),
                       L32(cur["beA"]), L32(cur["beB"]), ct, rig=False, rx=rxc(cur))
         B, g = ev["B"], ev["g"]
+        if pgap:       # the primal iterate of rows still optimising (the kernel's accumulators)
+            zi = torch.cat([torch.cat(ev["lin"][0][0], 1), torch.cat(ev["lin"][1][0], 1)], 1)
+            hi_ = torch.cat([torch.cat(ev["h"][0], 1), torch.cat(ev["h"][1], 1)], 1)
+            a_ = act[:, None].to(zi.dtype)
+            zsum = zi * a_ if zsum is None else zsum + zi * a_
+            hsum = hi_ * a_ if hsum is None else hsum + hi_ * a_
+            nsum = nsum + act.to(torch.float32)
         imp = act & (B > best)
         best = torch.where(imp, B, best)
         for k in keys:
@@ -386,6 +422,9 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     B, lin, xs, coef = ev["B"], ev["lin"], ev["xs"], ev["coef"]
     B = torch.where(infeas, torch.full_like(B, float("inf")), B)
     sc = torch.cat([_scores(bA, lin[0], pA, alA64), _scores(bB, lin[1], pB, alB64)], 1)
+    if pgap and zsum is not None:
+        sc = primal_gap_scores(zsum, hsum, nsum, torch.cat([lbA, lbB], 1), torch.cat([ubA, ubB], 1),
+                               torch.cat([phA, phB], 1)).to(sc.dtype)
     mx, j = sc.max(1)
     if lookahead > 0:
         j, bw = _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, beA, beB,

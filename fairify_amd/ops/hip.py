@@ -614,7 +614,7 @@ def _beta_wt(be) -> torch.Tensor:
 
 
 def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t, iters, lr_a, lr_b, lr_t,
-               decay=1.0, lookahead=0, beta_pos=True, rx=None, stall=True):
+               decay=1.0, lookahead=0, beta_pos=True, rx=None, stall=True, pgap=False):
     """One beta-CROWN BaB level on the device (``fa_beta_kernel``, csrc/beta.hip): the rows'
     (alpha, beta, t) are optimised IN PLACE (kept at the best iterate) and their rigorous fp64
     bounds, branching decisions, concretising vertices and child multipliers returned
@@ -664,7 +664,8 @@ def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, b
                               lo_c.data_ptr(), hi_c.data_ptr(), va_c.data_ptr(), vb_c.data_ptr(),
                               *[x.data_ptr() for x in bnd], pA.data_ptr(), pB.data_ptr(), par.data_ptr(),
                               t.data_ptr(), scratch.data_ptr(), int(iters), float(lr_a), float(lr_b), float(lr_t),
-                              float(decay), int(lookahead), int(bool(beta_pos)), int(bool(stall)), bound.data_ptr(),
+                              float(decay), int(lookahead), int(bool(beta_pos)),
+                              int(bool(stall)) | (2 if pgap else 0), bound.data_ptr(),
                               split.data_ptr(),
                               xstar.data_ptr(), binit.data_ptr(), int(ramask), _ptr(plo_c), _ptr(phi_c),
                               xpstar.data_ptr(), _ptr(gt), float(tau), _stream(dev))

@@ -54,6 +54,17 @@ def test_self_launch_totals_match_one_rank():
     assert not missing, missing
     # honest accounting fields add up
     assert one["unsat_sound"] + one["unsat_heuristic"] == one["unsat"]
+    # per-model residue and stage node counts (per timed step) add up to the totals
+    pm = one["per_model"]
+    assert set(pm) == {"AC-8", "AC-9"}
+    assert sum(v["attempted"] for v in pm.values()) == one["sat"] + one["unsat"] + one["unknown"]
+    assert abs(sum(v["unknown"] for v in pm.values()) - one["unknown"]) < 1e-6
+    sound_dec = one["sat"] - one["sat_by_stage"]["heuristic"] + one["unsat_sound"]
+    assert abs(sum(v["unknown_sound"] for v in pm.values()) - (pm["AC-8"]["attempted"] + pm["AC-9"]["attempted"]
+                                                               - sound_dec)) < 1e-6
+    assert all(set(v["nodes"]) == {"bab", "relu", "beta", "anytime", "heuristic"} for v in pm.values())
+    assert sum(v["nodes"]["bab"] for v in pm.values()) > 0
+    assert "cross-regime" in one["vs_baseline_note"]
     assert sum(one["sat_by_stage"].values()) == one["sat"]
 
 

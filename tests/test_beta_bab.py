@@ -156,17 +156,18 @@ def _brute_pair(m, lo, hi, pa):
     return bool((((z0 > 0) & (z1 < 0)) | ((z0 < 0) & (z1 > 0))).any())
 
 
-@pytest.mark.parametrize("seed,input_every", [(3, 0), (6, 0), (3, 2)])
-def test_beta_bab_matches_bruteforce(seed, input_every):
+@pytest.mark.parametrize("seed,input_every,branch", [(3, 0, "kernel"), (6, 0, "kernel"), (3, 2, "kernel"),
+                                                     (3, 0, "pgap"), (6, 0, "pgap")])
+def test_beta_bab_matches_bruteforce(seed, input_every, branch):
     """Decided verdicts equal lattice enumeration (input_every > 0: the experimental forced input
-    splits of BetaConfig)."""
+    splits of BetaConfig; branch "pgap": the primal-gap rule at the averaged primal iterate)."""
     pre = presets.get("src/AC-sex")
     grid, q = pre.grid(), pre.resolved()
     ids = processing_order(grid, 0)[:24]
     lo, hi = grid.decode(ids)
     hi = np.minimum(hi, lo + 1)
     m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
-    cfg = BetaConfig(node_budget=256, iters=20, root_iters=40, input_every=input_every)
+    cfg = BetaConfig(node_budget=256, iters=20, root_iters=40, input_every=input_every, branch=branch)
     res = BetaBaBSolver(Backend(m), q, cfg).solve(lo, hi, m)
     pa = q.pa_idx[0]
     assert (res.status != UNKNOWN).mean() > 0.5
@@ -191,6 +192,36 @@ def test_beta_closes_trained_ac7_residue():
     lo, hi = grid.decode(ids)
     res = BetaBaBSolver(Backend(m), q, BetaConfig(node_budget=200)).solve(lo, hi, m)
     assert (res.status == UNSAT).sum() >= 5, res.status
+
+
+def _relaxed_truth(m, lo, hi, pa, ra, tau):
+    pts = _lattice(lo, hi)
+    for s1 in (0, 1):
+        x = pts.copy()
+        x[:, pa] = s1
+        z = m.logits(x)
+        for d in range(-tau, tau + 1):
+            xp = x.copy()
+            xp[:, pa] = 1 - s1
+            xp[:, ra] += d
+            zp = m.logits(xp)
+            if (((z < 0) & (zp > 0)) | ((z > 0) & (zp < 0))).any():
+                return True
+    return False
+
+
+def test_primal_gap_scores_rule():
+    """The LP rule's score: max(mean h - relu(mean z), 0) on unfixed neurons unstable over the node's
+    bounds, 0 on fixed / stable ones and on rows that took no optimisation step."""
+    z = torch.tensor([[2.0, -4.0, 1.0, 3.0], [1.0, 1.0, 1.0, 1.0]])
+    h = torch.tensor([[3.0, 1.0, 0.0, 5.0], [2.0, 2.0, 2.0, 2.0]])
+    n = torch.tensor([2.0, 0.0])
+    lb = torch.tensor([[-1.0, -1.0, -1.0, 0.5], [-1.0] * 4])
+    ub = torch.ones(2, 4)
+    ph = torch.tensor([[0, 0, 1, 0], [0, 0, 0, 0]], dtype=torch.int8)
+    s = B.primal_gap_scores(z, h, n, lb, ub, ph)
+    assert torch.allclose(s[0], torch.tensor([0.5, 0.5, 0.0, 0.0]))    # fixed (ph) / stable (lb > 0): 0
+    assert bool((s[1] == 0).all())
 
 
 @pytest.mark.parametrize("seed,tau", [(21, 2), (24, 3)])

@@ -28,7 +28,7 @@ def _params(R, NH, seed, neg):
     return al, be_, t
 
 
-def _both(cuda, seed, iters, neg=False, lookahead=0, fix=0.3, widths=(6, 5, 4)):
+def _both(cuda, seed, iters, neg=False, lookahead=0, fix=0.3, widths=(6, 5, 4), pgap=False):
     m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(seed, widths=widths, fix=fix)
     R = lo.shape[0]
     w = [x.shape[1] for x in ws[:-1]]
@@ -37,12 +37,13 @@ def _both(cuda, seed, iters, neg=False, lookahead=0, fix=0.3, widths=(6, 5, 4)):
     lr = dict(lr_a=0.1, lr_b=0.5, lr_t=0.1)
     cpu = [x.clone() for x in (al[0], al[1], be_[0], be_[1], t)]
     lr_ = B.level_ref(ws, bs, w, lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1], *cpu,
-                      iters=iters, lookahead=lookahead, beta_pos=not neg, **lr)
+                      iters=iters, lookahead=lookahead, beta_pos=not neg, pgap=pgap, **lr)
     gb = Backend(m, cuda)
     d = lambda x: x.to(cuda).contiguous()  # noqa: E731
     gpu = [d(x.clone()) for x in (al[0], al[1], be_[0], be_[1], t)]
     lg = hip.beta_level(gb, d(lo), d(hi), pa, d(va), d(vb), d(bnd[0][0]), d(bnd[0][1]), d(bnd[1][0]), d(bnd[1][1]),
-                        d(ph[0]), d(ph[1]), *gpu, iters=iters, lookahead=lookahead, beta_pos=not neg, **lr)
+                        d(ph[0]), d(ph[1]), *gpu, iters=iters, lookahead=lookahead, beta_pos=not neg, pgap=pgap,
+                        **lr)
     torch.cuda.synchronize()
     return m, w, (lo, hi, va, vb, ph, pa), lr_, lg, cpu, [x.cpu() for x in gpu]
 
@@ -89,6 +90,29 @@ def test_beta_kernel_split_and_binit_match_reference(cuda, seed):
     assert torch.allclose(lg.binit.cpu()[nb], lr_.binit[nb], rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("seed", [3, 4, 5])
+def test_beta_kernel_primal_gap_split_matches_reference(cuda, seed):
+    """pgap, a few optimisation steps (fp32 trajectories still agree): the kernel splits a neuron the
+    reference's primal-gap scores rank best (within fp32 summation noise), or both split the same
+    input dim; the rigorous bounds agree and the child multipliers reproduce the node's relaxation."""
+    m, w, _, lr_, lg, _, _ = _both(cuda, seed, 3, fix=0.1, pgap=True)
+    sg, sr, sc = lg.split.cpu(), lr_.split, lr_.scores
+    fin = torch.isfinite(lr_.bound)
+    assert torch.allclose(lg.bound.cpu()[fin], lr_.bound[fin], rtol=1e-5, atol=1e-5)
+    n_neu = 0
+    for r in range(sg.numel()):
+        if not torch.isfinite(lr_.bound[r]) or lr_.bound[r] >= 0:
+            continue
+        if sr[r] >= 0:
+            n_neu += 1
+            assert sg[r] >= 0, (r, int(sg[r]), int(sr[r]))
+            best = float(sc[r].max())
+            assert float(sc[r, sg[r]]) >= best * (1 - 1e-3) - 1e-5, (r, int(sg[r]), int(sr[r]))
+        else:
+            assert int(sg[r]) == int(sr[r]), (r, int(sg[r]), int(sr[r]))
+    assert n_neu > 0
+
+
 @pytest.mark.parametrize("seed", [3, 4])
 @pytest.mark.parametrize("look", [0, 4])
 def test_beta_kernel_optimises_soundly(cuda, seed, look):
@@ -115,15 +139,16 @@ def test_beta_kernel_wide_layers(cuda):
     assert torch.allclose(lg.bound.cpu()[fin], lr_.bound[fin], rtol=1e-9, atol=1e-9)
 
 
-@pytest.mark.parametrize("seed", [3, 6])
-def test_beta_bab_gpu_matches_bruteforce(cuda, seed):
+@pytest.mark.parametrize("seed,branch", [(3, "kernel"), (6, "kernel"), (3, "pgap"), (6, "pgap")])
+def test_beta_bab_gpu_matches_bruteforce(cuda, seed, branch):
     pre = presets.get("src/AC-sex")
     grid, q = pre.grid(), pre.resolved()
     ids = processing_order(grid, 0)[:24]
     lo, hi = grid.decode(ids)
     hi = np.minimum(hi, lo + 1)
     m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
-    res = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=256, iters=20, root_iters=40)).solve(lo, hi, m)
+    res = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=256, iters=20, root_iters=40,
+                                                        branch=branch)).solve(lo, hi, m)
     pa = q.pa_idx[0]
     assert (res.status != UNKNOWN).mean() > 0.5
     for k in range(len(ids)):
@@ -227,3 +252,34 @@ def test_beta_kernel_relaxed_matches_reference_and_is_sound(cuda, seed, tie):
         tm = _true_min_rx(m, lo[r].numpy(), hi[r].numpy(), plo[r].numpy(), phi[r].numpy(), pa, ra, va[r].numpy(),
                           vb[r].numpy(), ph[0][r].numpy(), ph[1][r].numpy(), float(t[r]), tau if tie else None)
         assert float(bg[r]) <= tm, (r, float(bg[r]), tm)
+
+
+@pytest.mark.parametrize("seed,tau,branch", [(21, 2, "kernel"), (24, 3, "kernel"), (21, 2, "pgap")])
+def test_beta_bab_gpu_relaxed_matches_bruteforce(cuda, seed, tau, branch):
+    """GPU twin of test_beta_bab.py::test_beta_bab_relaxed_matches_bruteforce: relaxed queries through
+    the HIP kernel (x' RA boxes, tie multipliers, both orientations, exact confirmation); every
+    decided verdict equals enumeration of all (x, x') pairs."""
+    from fairify_amd.spec import ADULT, Query
+    from test_beta_bab import _relaxed_truth
+
+    q = Query(pa=("sex",), ra=("age",), tau=tau).resolve(ADULT)
+    grid = presets.get("src/AC-sex").grid()
+    ids = processing_order(grid, 0)[:16]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 1)
+    pa, ra = q.pa_idx[0], q.ra_idx[0]
+    m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
+    res = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=512, iters=20, root_iters=40,
+                                                        branch=branch)).solve(lo, hi, m)
+    decided = 0
+    for k in range(len(ids)):
+        if res.status[k] == UNKNOWN:
+            continue
+        decided += 1
+        truth = _relaxed_truth(m, lo[k], hi[k], pa, ra, tau)
+        assert (res.status[k] == SAT) == truth, k
+        if res.status[k] == SAT:
+            ok = exact.check_pair_constraints(res.cex_x[k:k + 1], res.cex_xp[k:k + 1], lo[k:k + 1], hi[k:k + 1],
+                                              q.pa_idx, q.ra_idx, q.tau)
+            assert ok[0] and exact.is_violation(m, res.cex_x[k:k + 1], res.cex_xp[k:k + 1])[0]
+    assert decided >= 0.5 * len(ids)

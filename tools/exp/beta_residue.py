@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--weights", default="zoo")
     ap.add_argument("--npz", required=True)
     ap.add_argument("--n", type=int, default=400)
+    ap.add_argument("--set", action="append", default=[],
+                    help="extra setting 'name:key=value,key=value' over BetaConfig(node_budget=64) "
+                         "(e.g. pg_b1024:branch=pgap,node_budget=1024,lookahead=0); given: only these run")
     args = ap.parse_args()
     import torch
 
@@ -70,6 +73,16 @@ def main():
         "input_every2_b256": replace(base, node_budget=256, input_every=2),
         "input_every3_b256": replace(base, node_budget=256, input_every=3),
     }
+    if args.set:
+        settings = {}
+        for spec in args.set:
+            name, _, kv = spec.partition(":")
+            kw = {}
+            for item in filter(None, kv.split(",")):
+                k, v = item.split("=")
+                cur = getattr(base, k)
+                kw[k] = type(cur)(v) if not isinstance(cur, bool) else v in ("1", "true", "True")
+            settings[name] = replace(base, **kw)
     print(f"{args.model}: {len(ids)} residue partitions", flush=True)
     for name, cfg in settings.items():
         if only and name not in only.split(","):
