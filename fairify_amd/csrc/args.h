@@ -416,8 +416,9 @@ struct BetaArgs {
   int lookahead;            // candidates per score of the filtered branching (0: best gap score)
   int beta_pos;             // project beta >= 0 (1) or keep it free-signed (0)
   int stall;                // 1: when no look-ahead candidate's children beat the node, split the input
-  int pgap;                 // 1: branch by the primal gap mean(h) - relu(mean(z)) of the optimisation's
-                            // averaged primal iterates (the verified LP's rule at its optimum)
+  int pgap;                 // > 0: branch by the primal gap mean(h) - relu(mean(z)) of the optimisation's
+                            // averaged primal iterates (the verified LP's rule at its optimum); the
+                            // iterates' weights: 1 uniform, 2 it + 1, 3 the second half of the steps
   int wpb;                  // waves per workgroup
   int wt_lds;               // 1: transposed weights staged in LDS too
   double* bound;            // [R] rigorous lower bound of t N(x,va) - (1-t) N(x,vb) (+inf: empty region)
@@ -432,4 +433,51 @@ struct BetaArgs {
   float* gtie;              // [R, 2, n0] multipliers of the tie |x_r - x'_r| <= tau (in = start, out =
                             // best), or nullptr (tie dropped)
   float tau;
+  const int8_t* osg;        // [R] orientation (+1: N(x,va) < 0 < N(x',vb); -1: the reverse), or nullptr (+1)
+  const uint8_t* skip;      // [R] nodes closed before bounding (decided partition, empty region), or nullptr:
+                            // bound +inf, no branching
+  int ph_stride;            // row stride of phA / phB (0: NH; the native runtime's [R][2][NH] layout: 2 NH)
+};
+
+// Native beta-CROWN BaB level (csrc/beta_runtime.cpp, kernels csrc/beta_bab.hip): a device-resident
+// node pool, double-buffered, structure-of-arrays; node n of the current slice and its children in the
+// next pool.  Per node: partition, root tree, orientation, x box, x' box (relaxed), PA values of both
+// copies, partition / tightened pre-activation bounds of both copies, phases [2][NH], optimiser
+// parameters [4][NH] (alpha_A, alpha_B, beta_A, beta_B), t, tie multipliers [2][n0] (relaxed).
+struct BetaPoolArgs {
+  int N;                    // nodes in this slice
+  int n0, nh, nn;           // input dims, hidden neurons, all neurons (layer-bound row stride)
+  int npa;
+  int pa_idx[FA_MAX_PA];
+  int nra;
+  int ra_idx[FA_MAX_RA];
+  float tau;
+  int leaf;                 // split code of a lattice leaf (-(2 n0 + 1))
+  int warm_beta;            // children's split multiplier from binit (else 0)
+  int count;                // count kernel: 1 = add the slice's alive nodes to their partitions' counts,
+                            // 0 = write the slice's skip flags
+  // current slice
+  const int* part; const int* tree; const int8_t* osg;
+  const float* lo; const float* hi; const float* plo; const float* phi;
+  const float* va; const float* vb;
+  float* LBA; float* UBA; float* LBB; float* UBB;
+  const int8_t* ph; const float* par; const float* t; const float* gt;
+  // per partition / per tree
+  int8_t* status; int* part_nodes; int budget;
+  int* tree_cnt;
+  // level work buffers
+  uint8_t* skip;            // [N]
+  float* rlo; float* rhi; int* rpart;              // [2N, n0] tightening rows (x rows 2n, x' rows 2n+1)
+  const float* lay_lb; const float* lay_ub;        // [2N, nn]
+  const uint8_t* infeas;                           // [2N]
+  const double* bound; const int* split; const float* xstar; const float* xpstar; const float* binit;
+  float* cpts;                                     // [2N, n0] candidate points
+  const float* pe_lb; const float* pe_ub;          // [2N]
+  // next pool
+  int* opart; int* otree; int8_t* oosg;
+  float* olo; float* ohi; float* oplo; float* ophi; float* ova; float* ovb;
+  float* oLBA; float* oUBA; float* oLBB; float* oUBB;
+  int8_t* oph; float* opar; float* ot; float* ogt;
+  int* count_out; int cap;
+  float* cand_buf; int* cand_count; int cand_cap;  // pinned records (x [n0], x' [n0], partition)
 };

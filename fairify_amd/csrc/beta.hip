@@ -293,7 +293,7 @@ __device__ T conc(const NetDesc& nd, const Slab& S, const Node& N, const T* cA, 
 // primal iterate of this optimisation step; neuron k is always handled by the same lane).
 template <typename T>
 __device__ T fwd(const NetDesc& nd, const float* Wf, const Slab& S, const Node& N, int c, const float* v,
-                 const float* __restrict__ al, float* zacc = nullptr, float* hacc = nullptr) {
+                 const float* __restrict__ al, float* zacc = nullptr, float* hacc = nullptr, float wacc = 1.f) {
   const int lane = threadIdx.x & 63;
   const int L = nd.n_layers;
   const int n0 = nd.dims[0];
@@ -327,8 +327,8 @@ __device__ T fwd(const NetDesc& nd, const float* Wf, const Slab& S, const Node& 
       }
       h1[j] = h;
       if (zacc) {
-        zacc[k] += (float)z;
-        hacc[k] += (float)h;
+        zacc[k] += wacc * (float)z;
+        hacc[k] += wacc * (float)h;
       }
     }
     wsync();
@@ -412,7 +412,8 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   {
     const float* LB[2] = {a.LBA + (size_t)r * NH, a.LBB + (size_t)r * NH};
     const float* UB[2] = {a.UBA + (size_t)r * NH, a.UBB + (size_t)r * NH};
-    const int8_t* PH[2] = {a.phA + (size_t)r * NH, a.phB + (size_t)r * NH};
+    const size_t phs = a.ph_stride > 0 ? (size_t)a.ph_stride : (size_t)NH;
+    const int8_t* PH[2] = {a.phA + (size_t)r * phs, a.phB + (size_t)r * phs};
     for (int c = 0; c < 2; ++c)
       for (int k = lane; k < NH; k += 64) {
         const int p = PH[c][k];
@@ -444,6 +445,7 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   float* cur = a.scratch + (size_t)r * 12 * NH;     // current
   float* mom = cur + 4 * NH;
   float* vel = cur + 8 * NH;
+  if (a.skip && a.skip[r]) bad = 1;         // closed before bounding: same outputs as an empty region
   if (__any(bad)) {
     if (lane == 0) {
       a.bound[r] = __builtin_inf();
@@ -473,6 +475,8 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         S.hb[1][k - q * NH] = 0.f;
       }
   float tc = a.t[r], tbest = tc, mt = 0.f, vt = 0.f;
+  // orientation: the objective og (t N_A - (1 - t) N_B) rules out N_A < 0 < N_B (og = +1) or the reverse
+  const float og = a.osg ? (float)a.osg[r] : 1.f;
   float best = -FLT_MAX;
   // relaxed: the tie's multipliers of this lane's RA dim (lane = input dim; n0 <= 64)
   const bool my_ra = N.tie && lane < n0 && ((N.ramask >> lane) & 1ull);
@@ -489,11 +493,13 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   float* cB = reinterpret_cast<float*>(S.cf[1]);
   const float b1c = 0.9f, b2c = 0.999f;
   float p1 = 1.f, p2 = 1.f, dk = 1.f;
-  int nacc = 0;                                    // primal iterates summed (pgap)
+  // primal iterates summed (pgap): weight 1 (mode 1), it + 1 (mode 2: later iterates count more), or
+  // 1 on the second half of the steps only (mode 3)
+  float nacc = 0.f;
   for (int it = 0; it < a.iters; ++it) {
-    const float kA = bwd<float, false, true, WTL>(nd, Wf, Wt, S, 0, tc, cur, cur + 2 * NH, -1, 0, cA, nullptr,
+    const float kA = bwd<float, false, true, WTL>(nd, Wf, Wt, S, 0, og * tc, cur, cur + 2 * NH, -1, 0, cA, nullptr,
                                                   nullptr);
-    const float kB = bwd<float, false, true, WTL>(nd, Wf, Wt, S, 1, -(1.f - tc), cur + NH, cur + 3 * NH, -1, 0, cB,
+    const float kB = bwd<float, false, true, WTL>(nd, Wf, Wt, S, 1, -og * (1.f - tc), cur + NH, cur + 3 * NH, -1, 0, cB,
                                                   nullptr, nullptr);
     const float Bv = conc<float, false, true>(nd, S, N, cA, cB, kA, kB, 0.f);
     if (Bv > best) {
@@ -508,9 +514,11 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
           for (int q = 0; q < 4; ++q) par[q * NH + nd.neuron_off[l] + j] = cur[q * NH + nd.neuron_off[l] + j];
     }
     if (best > 0.f) break;
-    const float oA = fwd<float>(nd, Wf, S, N, 0, N.va, cur, a.pgap ? S.zb[0] : nullptr, S.hb[0]);
-    const float oB = fwd<float>(nd, Wf, S, N, 1, N.vb, cur + NH, a.pgap ? S.zb[1] : nullptr, S.hb[1]);
-    ++nacc;
+    const float wi = a.pgap == 2 ? (float)(it + 1) : (a.pgap == 3 ? (2 * it >= a.iters ? 1.f : 0.f) : 1.f);
+    const bool acc = a.pgap && wi > 0.f;
+    const float oA = fwd<float>(nd, Wf, S, N, 0, N.va, cur, acc ? S.zb[0] : nullptr, S.hb[0], wi);
+    const float oB = fwd<float>(nd, Wf, S, N, 1, N.vb, cur + NH, acc ? S.zb[1] : nullptr, S.hb[1], wi);
+    if (acc) nacc += wi;
     // Adam (bias-corrected), gradient ascent, projected
     p1 *= b1c;
     p2 *= b2c;
@@ -554,7 +562,7 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         }
       }
     {
-      const float g = oA + oB;
+      const float g = og * (oA + oB);
       mt = b1c * mt + (1.f - b1c) * g;
       vt = b2c * vt + (1.f - b2c) * g * g;
       tc = fminf(fmaxf(tc + a.lr_t * dk * (mt / c1) / (sqrtf(vt / c2) + 1e-8f), 0.f), 1.f);
@@ -586,9 +594,9 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
 
   // ---- rigorous fp64 bound at the kept parameters
   double eA = 0, eB = 0;
-  const double kA = bwd<double, true, true, WTL>(nd, Wf, Wt, S, 0, (double)tf, par, par + 2 * NH, -1, 0, S.cf[0],
+  const double kA = bwd<double, true, true, WTL>(nd, Wf, Wt, S, 0, (double)og * (double)tf, par, par + 2 * NH, -1, 0, S.cf[0],
                                                  &eA, nullptr);
-  const double kB = bwd<double, true, true, WTL>(nd, Wf, Wt, S, 1, -(1.0 - (double)tf), par + NH, par + 3 * NH, -1,
+  const double kB = bwd<double, true, true, WTL>(nd, Wf, Wt, S, 1, -(double)og * (1.0 - (double)tf), par + NH, par + 3 * NH, -1,
                                                  0, S.cf[1], &eB, nullptr);
   const double Bd = conc<double, true, true>(nd, S, N, S.cf[0], S.cf[1], kA, kB, eA + eB);
   (void)fwd<double>(nd, Wf, S, N, 0, N.va, par);
@@ -611,8 +619,8 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   // ---- branching scores of unfixed unstable neurons: |lam| x relaxation gap at x*, or (pgap) the
   // primal gap mean(h) - relu(mean(z)) over the optimisation steps (the verified LP's rule,
   // smt/lpbab.py:_lp_bab, at the ergodic primal point).  Same lane mapping as the writers of par.
-  const bool use_pg = a.pgap && nacc > 0;
-  const float inv_n = 1.f / (float)(nacc > 0 ? nacc : 1);
+  const bool use_pg = a.pgap && nacc > 0.f;
+  const float inv_n = 1.f / (nacc > 0.f ? nacc : 1.f);
   for (int c = 0; c < 2; ++c)
     for (int l = 0; l < L - 1; ++l)
       for (int j = lane; j < nd.dims[l + 1]; j += 64) {
@@ -699,8 +707,9 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
       float worst = FLT_MAX;
       for (int sg = -1; sg <= 1; sg += 2) {
         int inf = 0;
-        const float kc = bwd<float, false, false, WTL>(nd, Wf, Wt, S, c, c == 0 ? tf : -(1.f - tf), par + c * NH,
-                                                       par + (2 + c) * NH, k, sg, cA32, nullptr, &inf);
+        const float sc_c = c == 0 ? og * tf : -og * (1.f - tf);
+        const float kc = bwd<float, false, false, WTL>(nd, Wf, Wt, S, c, sc_c, par + c * NH, par + (2 + c) * NH, k, sg,
+                                                       cA32, nullptr, &inf);
         float* oth = reinterpret_cast<float*>(S.b1);       // the other copy's coefficients (fp32)
         for (int i = lane; i < n0; i += 64) oth[i] = (float)S.cf[1 - c][i];
         wsync();

@@ -118,6 +118,7 @@ struct Net {
 const NetDesc& fa_net_desc(py::handle h) { return h.cast<const Net&>().d; }
 void register_bab(py::module& m);
 void register_relu(py::module& m);
+void register_beta(py::module& m);
 extern "C" int fa_crown_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_refine_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
 extern "C" int fa_backward_launch(const NetDesc& net, BoundArgs a, hipStream_t stream);
@@ -516,7 +517,7 @@ PYBIND11_MODULE(_C, m) {
                          int stall,
                          uintptr_t bound, uintptr_t split, uintptr_t xstar, uintptr_t binit,
                          unsigned long long ramask, uintptr_t plo, uintptr_t phi, uintptr_t xpstar, uintptr_t gtie,
-                         float tau, uintptr_t stream) {
+                         float tau, uintptr_t osg, uintptr_t stream) {
     if (pa.size() > FA_MAX_PA) throw std::invalid_argument("beta_level: too many PA dims");
     for (size_t q = 0; q < pa.size(); ++q)
       if (pa[q] < 0 || pa[q] >= net.d.dims[0] || (q && pa[q] <= pa[q - 1]))
@@ -549,7 +550,7 @@ PYBIND11_MODULE(_C, m) {
     a.lookahead = lookahead;
     a.beta_pos = beta_pos;
     a.stall = stall & 1;        // bit 1: primal-gap branching (ops/hip.py:beta_level)
-    a.pgap = (stall >> 1) & 1;
+    a.pgap = (stall >> 1) & 3;
     a.bound = P<double>(bound);
     a.split = P<int>(split);
     a.xstar = P<float>(xstar);
@@ -560,6 +561,7 @@ PYBIND11_MODULE(_C, m) {
     a.xpstar = P<float>(xpstar);
     a.gtie = P<float>(gtie);
     a.tau = tau;
+    a.osg = P<const int8_t>(osg);
     if ((net.d.dims[0] < 64 && (ramask >> net.d.dims[0])) || (ramask && (!plo || !phi)))
       throw std::invalid_argument("beta_level: RA mask beyond the inputs or no x' box");
     return fa_beta_launch(net.d, a, reinterpret_cast<hipStream_t>(stream));
@@ -576,6 +578,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lds_registered", [] { return (int)fa_lds_registry().size(); });
   register_bab(m);
   register_relu(m);
+  register_beta(m);
   // caching allocator of the native runtimes (devmem.h): hipFree / hipHostFree calls reaching the
   // driver stay 0 in steady state
   m.def("mem_stats", [] {

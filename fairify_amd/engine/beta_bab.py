@@ -17,8 +17,10 @@ on the host (SAT), a single lattice point is decided exactly, and a partition wh
 closed is UNSAT.  A partition past its node budget ends UNKNOWN.
 
 Relaxed queries (|x_r - x'_r| <= tau, x' unclipped): every node also carries x''s box on the RA
-dims, split like the input dims, and the second orientation runs on the negated network.  CPU tests pin verdicts to brute-force
-enumeration (tests/test_beta_bab.py); the GPU kernel to this module's reference (tests/test_beta_gpu.py).
+dims, split like the input dims, and its orientation: N(x, va) < 0 < N(x', vb) or the reverse (x' may
+leave the box, so the swapped pair does not cover the second one); both orientations are roots of the
+same search (the objective's sign per node).  CPU tests pin verdicts to brute-force enumeration
+(tests/test_beta_bab.py); the GPU kernel to this module's reference (tests/test_beta_gpu.py).
 """
 from __future__ import annotations
 
@@ -67,8 +69,16 @@ class BetaConfig:
     #                                  averaged primal iterate of the node's optimisation (kernel-side;
     #                                  with lookahead > 0 it supplies the first candidate list);
     #                                  "lpgap" (experiment): the chord slack at the vertex x* / x'*
+    pgap_weights: int = 1            # branch "pgap": iterate weights of the primal average (1 uniform, 2 it + 1,
+    #                                  3 second half of the steps)
     input_every: int = 0             # > 0 (experiment): every this many levels of a tree, split the
     #                                  widest input dim (x, or x''s RA dims) instead of the kernel's choice
+    native: bool = True              # HIP device: the level loop in the native runtime (csrc/beta_runtime.cpp,
+    #                                  device-resident pool / budgets / probe); FAIRIFY_TORCH_BETA=1 or the
+    #                                  experiments (lpgap, input_every, merge_orient off): this module's loop
+    merge_orient: bool = True        # relaxed: both orientations as roots of ONE search (per-node sign of
+    #                                  the objective, ops/beta.py:evaluate osg) instead of a second solve on
+    #                                  the negated network for the partitions the first one closed
 
 
 def supported(q: ResolvedQuery) -> bool:
@@ -112,7 +122,7 @@ class BetaBaBSolver:
             return BaBResult(status, cex_x, cex_xp, nodes)
         self.stats = {"levels": 0, "nodes": 0}
         r1 = self._solve_all(lo_np, hi_np, mlp_exact, status, t0)
-        if not self.q.relaxed or getattr(self, "_second", False):
+        if not self.q.relaxed or getattr(self, "_second", False) or self.cfg.merge_orient:
             return r1
         closed = (r1.status == UNSAT) & (status == RUNNING)
         if not closed.any():
@@ -197,14 +207,17 @@ class BetaBaBSolver:
         f32 = dict(dtype=torch.float32, device=dev)
         values = torch.from_numpy(values_np.astype(np.float32)).to(dev)
         V = values.shape[0]
+        # orientations per ordered pair: relaxed queries with merge_orient carry both as roots
+        O = 2 if (relaxed and cfg.merge_orient) else 1
         lo_r = torch.from_numpy(lo_np[run].astype(np.float32)).to(dev)
         hi_r = torch.from_numpy(hi_np[run].astype(np.float32)).to(dev)
         with self.tm("beta.roots"):
             rlb, rub = self._root_bounds(lo_r, hi_r, values)
             rlbp, rubp = self._root_bounds(lo_r, hi_r, values, widen=True) if relaxed else (rlb, rub)
-        # one root per (running partition, ordered pair)
-        k = torch.arange(run.size, device=dev).repeat_interleave(Pp)
-        pr = torch.from_numpy(pairs_np.astype(np.int64)).to(dev).repeat(run.size, 1)
+        # one root per (running partition, ordered pair, orientation)
+        k = torch.arange(run.size, device=dev).repeat_interleave(Pp * O)
+        pr = torch.from_numpy(pairs_np.astype(np.int64)).to(dev).repeat_interleave(O, dim=0).repeat(run.size, 1)
+        osg = torch.tensor([1, -1][:O], dtype=torch.int8, device=dev).repeat(run.size * Pp)
         ia, ib = k * V + pr[:, 0], k * V + pr[:, 1]
         R0 = k.numel()
         plo = lo_r[k].clone()
@@ -226,18 +239,23 @@ class BetaBaBSolver:
             "depth": torch.zeros(R0, dtype=torch.int32, device=dev),
             # relaxed: Lagrange multipliers of the tie |x_r - x'_r| <= tau (RA dims)
             "gP": torch.zeros(R0, n0, **f32), "gM": torch.zeros(R0, n0, **f32),
-            "tree": torch.arange(R0, device=dev),        # the (partition, ordered pair) root
+            "tree": torch.arange(R0, device=dev),        # the (partition, ordered pair, orientation) root
+            "osg": osg,
         }
         tree_run = run[k.cpu().numpy()]
         # node budget per partition, scaled with its ordered pairs (a multi-valued PA -- race: 20
         # pairs -- gets the budget a binary one gets per pair)
-        budget = int(cfg.node_budget * max(1.0, Pp / 2.0))
+        budget = int(cfg.node_budget * max(1.0, Pp / 2.0) * O)
+        if self._use_native(O):
+            return self._solve_native(pool, R0, status, lo_np, hi_np, mlp_exact, budget,
+                                      2 * cfg.probe_levels * Pp * O if cfg.probe_levels else 0,
+                                      max(0.0, time_budget - (time.time() - t0)))
         levels = 0
         # the probe (per partition, so a verdict never depends on which partitions share the call):
         # once a partition has expanded 2 probe_levels nodes per pair tree, it goes on only if one
         # of its trees has closed
         probed = np.zeros(P, dtype=bool)
-        probe_at = 2 * cfg.probe_levels * Pp
+        probe_at = 2 * cfg.probe_levels * Pp * O
         timed_out = False
         while pool["part"].numel():
             if time.time() - t0 > time_budget:
@@ -273,7 +291,8 @@ class BetaBaBSolver:
                                     cur["LBB"], cur["UBB"], cur["phA"], cur["phB"], cur["alA"], cur["alB"],
                                     cur["beA"], cur["beB"], cur["t"], cfg.root_iters if is_root else cfg.iters,
                                     cfg.lr_a * sc, cfg.lr_b * sc, cfg.lr_t * sc, cfg.decay, cfg.lookahead,
-                                    cfg.beta_pos, rx, pgap=cfg.branch == "pgap")
+                                    cfg.beta_pos, rx, pgap=cfg.pgap_weights if cfg.branch == "pgap" else 0,
+                                    osg=cur["osg"] if O > 1 else None)
             if empty is not None:
                 lev.bound = torch.where(empty, torch.full_like(lev.bound, float("inf")), lev.bound)
             closed = lev.bound >= 0
@@ -289,9 +308,11 @@ class BetaBaBSolver:
                 xa[:, pa] = cur["va"][cand]
                 xb[:, pa] = cur["vb"][cand]
                 with self.tm("beta.cand"):
-                    alb, _ = be.point_bounds(xa)
-                    _, bub = be.point_bounds(xb)
+                    alb, aub = be.point_bounds(xa)
+                    blb, bub = be.point_bounds(xb)
                 poss = (alb < 0) & (bub > 0)
+                if O > 1:       # orientation -1: N(x, va) > 0 > N(x', vb)
+                    poss = torch.where(cur["osg"][cand] > 0, poss, (aub > 0) & (blb < 0))
                 ci = cand[poss]
                 if ci.numel():
                     self._confirm(cur["part"][ci].cpu().numpy(), xa[poss], xb[poss], status, cex_x, cex_xp,
@@ -331,6 +352,78 @@ class BetaBaBSolver:
         self.stats["levels"] = self.stats.get("levels", 0) + levels
         self.stats["nodes"] = self.stats.get("nodes", 0) + int(nodes_np.sum())
         return status, cex_x, cex_xp, nodes_np
+
+    def _use_native(self, O: int) -> bool:
+        import os
+
+        cfg = self.cfg
+        return (self.be.hip and cfg.native and os.environ.get("FAIRIFY_TORCH_BETA") != "1"
+                and cfg.branch in ("kernel", "pgap") and cfg.input_every == 0
+                and (O == 2 or not self.q.relaxed))
+
+    def _solve_native(self, pool, R0: int, status, lo_np, hi_np, mlp_exact, budget: int, probe_at: int,
+                      time_budget: float):
+        """The level loop on the device (csrc/beta_runtime.cpp): the roots of ``pool`` go to the native
+        runtime's node pool; verdicts, witnesses and per-partition node counts come back."""
+        from ..ops import ext
+        from ..ops.hip import _beta_wt, _net
+        from .rtpool import checkout
+
+        be, q, cfg = self.be, self.q, self.cfg
+        P, n0 = lo_np.shape
+        NH = be.n_hidden
+        relaxed = q.relaxed
+        ra = list(q.ra_idx) if relaxed else []
+        tau = float(q.tau) if relaxed else 0.0
+        i32 = lambda x: x.to(torch.int32).contiguous()  # noqa: E731
+        f32 = lambda x: x.to(torch.float32).contiguous()  # noqa: E731
+        arrs = [i32(pool["part"]), pool["osg"].to(torch.int8).contiguous(), f32(pool["lo"]), f32(pool["hi"]),
+                f32(pool["plo"]), f32(pool["phi"]), f32(pool["va"]), f32(pool["vb"]), f32(pool["LBA"]),
+                f32(pool["UBA"]), f32(pool["LBB"]), f32(pool["UBB"]),
+                torch.stack([pool["phA"], pool["phB"]], 1).to(torch.int8).contiguous(),
+                torch.stack([pool["alA"], pool["alB"], pool["beA"], pool["beB"]], 1).contiguous(),
+                f32(pool["t"]), torch.stack([pool["gP"], pool["gM"]], 1).contiguous()]
+        ptrs = [a.data_ptr() for a in arrs]
+        if not relaxed:
+            ptrs[4] = ptrs[5] = ptrs[15] = 0
+        tree_part = pool["part"].to(torch.int32).cpu().numpy()
+        cfgd = {"iters": int(cfg.iters), "root_iters": int(cfg.root_iters), "lr_a": float(cfg.lr_a),
+                "lr_b": float(cfg.lr_b), "lr_t": float(cfg.lr_t), "child_lr": float(cfg.child_lr),
+                "decay": float(cfg.decay), "lookahead": int(cfg.lookahead), "beta_pos": int(bool(cfg.beta_pos)),
+                "stall": 1, "pgap": int(cfg.pgap_weights) if cfg.branch == "pgap" else 0, "warm_beta": int(bool(cfg.warm_beta)),
+                "tighten": int(bool(cfg.tighten))}
+
+        def confirm(parts: np.ndarray, buf: np.ndarray) -> np.ndarray:
+            X = np.rint(buf[:, :n0]).astype(np.int64)
+            XP = np.rint(buf[:, n0:]).astype(np.int64)
+            ok = exact.check_pair_constraints(X, XP, lo_np[parts], hi_np[parts], q.pa_idx, q.ra_idx, q.tau)
+            out = np.zeros(len(parts), dtype=bool)
+            idx = np.nonzero(ok)[0]
+            if idx.size:
+                out[idx] = exact.is_violation(mlp_exact, X[idx], XP[idx])
+            return out
+
+        cap = int(max(cfg.max_pool, 2 * R0))
+        batch = int(min(cfg.batch_nodes, 32768))
+        key = (tuple(q.pa_idx), tuple(ra), tau, batch)
+
+        def make(c):
+            return ext().BetaRuntime(_net(be), be.flat.data_ptr(), _beta_wt(be).data_ptr(), list(q.pa_idx), ra, tau,
+                                     int(c), batch)
+
+        stream = torch.cuda.current_stream(self.dev).cuda_stream
+        with self.tm("beta.native"), checkout(be, "_beta_rt", key, cap, make) as rt:
+            st, cx, cxp, nodes, stats = rt.solve(ptrs, int(R0), status.astype(np.int8), tree_part,
+                                                 lo_np.astype(np.float32), hi_np.astype(np.float32), int(budget),
+                                                 int(probe_at), float(time_budget), cfgd, confirm, stream)
+        del arrs
+        stats = dict(stats)
+        self.stats["levels"] = self.stats.get("levels", 0) + int(stats["levels"])
+        self.stats["nodes"] = self.stats.get("nodes", 0) + int(stats["nodes"])
+        if stats.get("probe_stop"):
+            self.stats["probe_stop"] = self.stats.get("probe_stop", 0) + int(stats["probe_stop"])
+        self.stats["native"] = True
+        return (np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes, dtype=np.int64))
 
     def _probe(self, pool, nodes_np, probed, probe_at: int, R0: int, tree_run, status) -> None:
         """Partitions past the probe point with no closed pair tree end UNKNOWN (their nodes are

@@ -149,7 +149,7 @@ def _forward_lin(ws, bs, x, LB, rec, al, hs=None):
 
 
 def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t, rig: bool, need_lin: bool = True,
-             rx=None):
+             rx=None, osg=None):
     """The coupled bound of rows R at the given parameters (per-layer lists), in the dtype of
     ``ws``.  ``rig``: fp64 with every rounding term subtracted (the sound bound).
 
@@ -158,6 +158,10 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
     the two copies are concretised separately, and the tie |x_r - x'_r| <= tau enters through its
     own Lagrange multipliers gP, gM >= 0 [R, n0] (``f >= f + gP (x_r - x'_r - tau) + gM (x'_r - x_r -
     tau)`` on every admissible pair; all zero: the tie dropped, as the relu stage does).
+    ``osg`` [R] (+1 / -1, default +1): the orientation of the violation a row rules out -- +1: N(x, va)
+    < 0 < N(x', vb), objective t N_A - (1 - t) N_B; -1: N(x, va) > 0 > N(x', vb), the same objective
+    negated (both orientations of a relaxed query as rows of one search; a PA-only query has x' = x
+    off the PA dims, so its swapped ordered pair is the second orientation).
     Returns a dict: B [R], g (gradients), lin (per-copy records), xs (x*), xps (x'*), cA, cB."""
     dt = ws[0].dtype
     pa = list(pa)
@@ -176,8 +180,9 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
     hmB = torch.maximum(loB.abs(), hiB.abs())
     hmA[:, pa] = va.abs().to(dt)
     hmB[:, pa] = vb.abs().to(dt)
-    cA, kA, eA, rA = _backward(ws, bs, bA[0], bA[1], phA, alA, beA, t, hmA, rig)
-    cB, kB, eB, rB = _backward(ws, bs, bB[0], bB[1], phB, alB, beB, -(1 - t), hmB, rig)
+    og = torch.ones_like(t) if osg is None else osg.to(t.dtype)
+    cA, kA, eA, rA = _backward(ws, bs, bA[0], bA[1], phA, alA, beA, og * t, hmA, rig)
+    cB, kB, eB, rB = _backward(ws, bs, bB[0], bB[1], phB, alB, beB, -og * (1 - t), hmB, rig)
     pA = cA[:, pa] * va.to(dt)
     pB = cB[:, pa] * vb.to(dt)
     shared = free & ~ram
@@ -222,7 +227,7 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
     hA, hB = [], []
     zA, oA = _forward_lin(ws, bs, xa, bA[0], rA, alA, hA)
     zB, oB = _forward_lin(ws, bs, xb, bB[0], rB, alB, hB)
-    g = {"t": oA + oB}
+    g = {"t": og * (oA + oB)}
     if tie:
         g["gP"] = torch.where(ram[None], xs - xps - tau, torch.zeros_like(xs))
         g["gM"] = torch.where(ram[None], xps - xs - tau, torch.zeros_like(xs))
@@ -262,7 +267,7 @@ def _intercepts(bnd, lin, ph):
 
 
 def _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, beA, beB, t, sc, lin,
-               K: int, j0, rx=None):
+               K: int, j0, rx=None, osg=None):
     """Filtered branching: the top-K neurons by relaxation-gap score and the top-K by chord intercept
     are each tried -- both children bounded at the node's parameters with the new multiplier at 0
     (one backward pass each) -- and the neuron whose worse child is best wins."""
@@ -292,7 +297,7 @@ def _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, 
                                    (rx[0], rx[1][rows], rx[2][rows], rx[3], rx[4][rows], rx[5][rows]))
     Bc = evaluate(ws32, bs32, lo[rows], hi[rows], pa, va[rows], vb[rows], (L(lA), L(uA)), (L(lB), L(uB)),
                   L(pA2), L(pB2), L(alA[rows]), L(alB[rows]), L(beA[rows]), L(beB[rows]), t[rows],
-                  rig=False, need_lin=False, rx=rxr)["B"]
+                  rig=False, need_lin=False, rx=rxr, osg=None if osg is None else osg[rows])["B"]
     Bc = torch.where(iA | iB, torch.full_like(Bc, float("inf")), Bc.float())
     worst = Bc.reshape(R, C, 2).min(2).values
     worst = torch.where(valid, worst, torch.full_like(worst, -float("inf")))
@@ -323,7 +328,8 @@ def clamp_bounds(LB: torch.Tensor, UB: torch.Tensor, ph: torch.Tensor):
 
 def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t,
               iters: int, lr_a: float, lr_b: float, lr_t: float, decay: float = 1.0,
-              lookahead: int = 0, beta_pos: bool = True, rx=None, stall: bool = True, pgap: bool = False) -> BetaLevel:
+              lookahead: int = 0, beta_pos: bool = True, rx=None, stall: bool = True, pgap: int = 0,
+              osg=None) -> BetaLevel:
     """One BaB level of rows R (the HIP kernel's semantics, csrc/beta.hip): ``iters`` projected-Adam
     steps in fp32 from the rows' current (alpha, beta, t) -- updated IN PLACE to the best iterate --
     then the rigorous fp64 bound, the branching decision and x* at those parameters.
@@ -331,14 +337,15 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     lo, hi [R, n0]; va, vb [R, npa]; LB*/UB* [R, NH] partition bounds (unclamped); ph* [R, NH] int8;
     al*/be* [R, NH] float32; t [R] float32.  ``rx`` = (ra [n0] bool, plo, phi [R, n0]): relaxed
     queries, copy B's RA dims over their own box (:func:`evaluate`); x' RA dims are split too
-    (``split`` = -1 - (n0 + d)).
+    (``split`` = -1 - (n0 + d)).  ``osg`` [R] int8: each row's orientation (:func:`evaluate`).
 
     ``pgap``: branch by the verified LP's rule (smt/lpbab.py:_lp_bab) at a primal point of the node's
     relaxation instead of at the vertex x*: the Lagrangian's primal iterates (x*, z, h of the
     linearised network) are averaged over the optimisation steps -- the ergodic average of a dual
     (sub)gradient method converges to a primal optimum of the LP it dualises -- and an unfixed
     unstable neuron scores its primal gap ``mean(h) - relu(mean(z))`` (look-ahead, when on, takes its
-    first candidate list from these scores)."""
+    first candidate list from these scores).  The iterates' weights: ``pgap`` 1 uniform, 2 ``it + 1``
+    (later iterates count more), 3 the second half of the steps only."""
     R, n0 = lo.shape
     dev = lo.device
     lbA, ubA, infA = clamp_bounds(LBA, UBA, phA)
@@ -369,15 +376,16 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     nsum = torch.zeros(R, dtype=torch.float32, device=dev)
     for it in range(iters):
         ev = evaluate(ws32, bs32, lo, hi, pa, va, vb, bA32, bB32, pA, pB, L32(cur["alA"]), L32(cur["alB"]),
-                      L32(cur["beA"]), L32(cur["beB"]), ct, rig=False, rx=rxc(cur))
+                      L32(cur["beA"]), L32(cur["beB"]), ct, rig=False, rx=rxc(cur), osg=osg)
         B, g = ev["B"], ev["g"]
-        if pgap:       # the primal iterate of rows still optimising (the kernel's accumulators)
+        wi = float(it + 1) if pgap == 2 else (float(2 * it >= iters) if pgap == 3 else 1.0)
+        if pgap and wi > 0:   # the primal iterate of rows still optimising (the kernel's accumulators)
             zi = torch.cat([torch.cat(ev["lin"][0][0], 1), torch.cat(ev["lin"][1][0], 1)], 1)
             hi_ = torch.cat([torch.cat(ev["h"][0], 1), torch.cat(ev["h"][1], 1)], 1)
-            a_ = act[:, None].to(zi.dtype)
+            a_ = act[:, None].to(zi.dtype) * wi
             zsum = zi * a_ if zsum is None else zsum + zi * a_
             hsum = hi_ * a_ if hsum is None else hsum + hi_ * a_
-            nsum = nsum + act.to(torch.float32)
+            nsum = nsum + act.to(torch.float32) * wi
         imp = act & (B > best)
         best = torch.where(imp, B, best)
         for k in keys:
@@ -418,7 +426,7 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     bA, bB = (L64(lbA), L64(ubA)), (L64(lbB), L64(ubB))
     alA64, alB64 = L64(alA), L64(alB)
     ev = evaluate(ws64, bs64, lo.to(d), hi.to(d), pa, va.to(d), vb.to(d), bA, bB, pA, pB, alA64, alB64, L64(beA),
-                  L64(beB), t.to(d), rig=True, rx=rxc(par))
+                  L64(beB), t.to(d), rig=True, rx=rxc(par), osg=osg)
     B, lin, xs, coef = ev["B"], ev["lin"], ev["xs"], ev["coef"]
     B = torch.where(infeas, torch.full_like(B, float("inf")), B)
     sc = torch.cat([_scores(bA, lin[0], pA, alA64), _scores(bB, lin[1], pB, alB64)], 1)
@@ -428,7 +436,7 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
     mx, j = sc.max(1)
     if lookahead > 0:
         j, bw = _lookahead(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, beA, beB,
-                           t, sc, lin, lookahead, j, rx)
+                           t, sc, lin, lookahead, j, rx, osg)
         if stall:
             # no candidate's children beat this node: the relaxations are not what keeps it open
             # -- split the input box instead (as the verified LP does)

@@ -614,7 +614,7 @@ def _beta_wt(be) -> torch.Tensor:
 
 
 def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t, iters, lr_a, lr_b, lr_t,
-               decay=1.0, lookahead=0, beta_pos=True, rx=None, stall=True, pgap=False):
+               decay=1.0, lookahead=0, beta_pos=True, rx=None, stall=True, pgap=False, osg=None):
     """One beta-CROWN BaB level on the device (``fa_beta_kernel``, csrc/beta.hip): the rows'
     (alpha, beta, t) are optimised IN PLACE (kept at the best iterate) and their rigorous fp64
     bounds, branching decisions, concretising vertices and child multipliers returned
@@ -659,16 +659,17 @@ def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, b
                 if tuple(x.shape) != (R, n0) or x.dtype != torch.float32:
                     raise ValueError(f"{nm}: expected float32 [{R}, {n0}]")
             gt = torch.stack([rx[4], rx[5]], 1).contiguous()       # [R, 2, n0]
+    osg_c = None if osg is None else _c(osg, torch.int8, (R,), "osg")
     if R:
         rc = ext().beta_level(_net(be), be.flat.data_ptr(), _beta_wt(be).data_ptr(), R, [int(d) for d in pa],
                               lo_c.data_ptr(), hi_c.data_ptr(), va_c.data_ptr(), vb_c.data_ptr(),
                               *[x.data_ptr() for x in bnd], pA.data_ptr(), pB.data_ptr(), par.data_ptr(),
                               t.data_ptr(), scratch.data_ptr(), int(iters), float(lr_a), float(lr_b), float(lr_t),
                               float(decay), int(lookahead), int(bool(beta_pos)),
-                              int(bool(stall)) | (2 if pgap else 0), bound.data_ptr(),
+                              int(bool(stall)) | (int(pgap) << 1), bound.data_ptr(),
                               split.data_ptr(),
                               xstar.data_ptr(), binit.data_ptr(), int(ramask), _ptr(plo_c), _ptr(phi_c),
-                              xpstar.data_ptr(), _ptr(gt), float(tau), _stream(dev))
+                              xpstar.data_ptr(), _ptr(gt), float(tau), _ptr(osg_c), _stream(dev))
         if rc != 0:
             raise RuntimeError(f"fa_beta_kernel launch failed ({rc}): network not supported by the beta kernel")
         if gt is not None:

@@ -2,7 +2,7 @@
 # round 6, call B: where AC-7's time goes on the big grids (stage timers + per-stage node counts on
 # slices of stress/AC and relaxed/AC), GPU stages only as in tools/baseline_configs.py
 set -o pipefail
-OUT=gpurun_out/r6b; mkdir -p $OUT
+OUT=gpurun_out/r6c; mkdir -p $OUT
 export PYTHONFAULTHANDLER=1
 for spec in "stress/AC:200000" "relaxed/AC:50000"; do
   pre=${spec%%:*}; n=${spec#*:}

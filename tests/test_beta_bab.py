@@ -96,6 +96,37 @@ def test_rigorous_bound_below_every_phase_feasible_point(seed, neg_beta):
         assert float(lev.bound[r]) <= tm, (r, float(lev.bound[r]), tm)
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_orientation_sign_equals_negated_network(seed):
+    """osg = -1 (the reverse orientation of a row) bounds exactly what the network with its logit
+    negated bounds with osg = +1 -- the merged-orientation search replaces the second solve on the
+    negated net -- and the bound stays below every phase-feasible point of that orientation."""
+    from fairify_amd.engine.relu_bab import negated
+
+    m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(seed)
+    R = lo.shape[0]
+    widths = [w.shape[1] for w in ws[:-1]]
+    NH = sum(widths)
+    g = torch.Generator().manual_seed(seed)
+    al = [torch.rand(R, NH, generator=g) for _ in range(2)]
+    be_ = [torch.rand(R, NH, generator=g) for _ in range(2)]
+    t = torch.rand(R, generator=g)
+    mn = negated(m)
+    wsn = [torch.tensor(np.asarray(w), dtype=torch.float32) for w in mn.weights]
+    bsn = [torch.tensor(np.asarray(b), dtype=torch.float32).reshape(-1) for b in mn.biases]
+    args = (lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1])
+    cp = lambda: [x.clone() for x in (al[0], al[1], be_[0], be_[1], t)]  # noqa: E731
+    neg = B.level_ref(ws, bs, widths, *args, *cp(), iters=0, lr_a=0.1, lr_b=0.5, lr_t=0.1,
+                      osg=torch.full((R,), -1, dtype=torch.int8))
+    ref_ = B.level_ref(wsn, bsn, widths, *args, *cp(), iters=0, lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    assert torch.equal(neg.bound, ref_.bound)
+    assert torch.equal(neg.split, ref_.split)
+    for r in range(R):
+        tm = _true_min(mn, lo[r].numpy(), hi[r].numpy(), pa, va[r].numpy(), vb[r].numpy(), ph[0][r].numpy(),
+                       ph[1][r].numpy(), float(t[r]), widths)
+        assert float(neg.bound[r]) <= tm
+
+
 @pytest.mark.parametrize("seed", [3, 4])
 def test_optimised_bound_sound_and_not_worse(seed):
     m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(seed, fix=0.15)
@@ -224,8 +255,8 @@ def test_primal_gap_scores_rule():
     assert bool((s[1] == 0).all())
 
 
-@pytest.mark.parametrize("seed,tau", [(21, 2), (24, 3)])
-def test_beta_bab_relaxed_matches_bruteforce(seed, tau):
+@pytest.mark.parametrize("seed,tau,merge", [(21, 2, True), (24, 3, True), (21, 2, False)])
+def test_beta_bab_relaxed_matches_bruteforce(seed, tau, merge):
     """Relaxed queries (|x_r - x'_r| <= tau on RA = age, x' unclipped): nodes carry x''s box on the
     RA dims (split like input dims), the second orientation runs on the negated network; every
     decided verdict equals enumeration of all (x, x') pairs, every SAT pair is exactly confirmed."""
@@ -238,7 +269,8 @@ def test_beta_bab_relaxed_matches_bruteforce(seed, tau):
     hi = np.minimum(hi, lo + 1)
     pa, ra = q.pa_idx[0], q.ra_idx[0]
     m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
-    res = BetaBaBSolver(Backend(m), q, BetaConfig(node_budget=512, iters=20, root_iters=40)).solve(lo, hi, m)
+    res = BetaBaBSolver(Backend(m), q, BetaConfig(node_budget=512, iters=20, root_iters=40,
+                                                  merge_orient=merge)).solve(lo, hi, m)
     decided = 0
     for k in range(len(ids)):
         pts = _lattice(lo[k], hi[k])

@@ -90,7 +90,7 @@ def test_beta_kernel_split_and_binit_match_reference(cuda, seed):
     assert torch.allclose(lg.binit.cpu()[nb], lr_.binit[nb], rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("seed", [3, 4, 5])
+@pytest.mark.parametrize("seed", [5, 8, 12])      # seeds with open nodes the reference splits on a neuron
 def test_beta_kernel_primal_gap_split_matches_reference(cuda, seed):
     """pgap, a few optimisation steps (fp32 trajectories still agree): the kernel splits a neuron the
     reference's primal-gap scores rank best (within fp32 summation noise), or both split the same
@@ -139,16 +139,21 @@ def test_beta_kernel_wide_layers(cuda):
     assert torch.allclose(lg.bound.cpu()[fin], lr_.bound[fin], rtol=1e-9, atol=1e-9)
 
 
-@pytest.mark.parametrize("seed,branch", [(3, "kernel"), (6, "kernel"), (3, "pgap"), (6, "pgap")])
-def test_beta_bab_gpu_matches_bruteforce(cuda, seed, branch):
+@pytest.mark.parametrize("seed,branch,native", [(3, "kernel", True), (6, "kernel", True), (3, "pgap", True),
+                                                (6, "pgap", True), (3, "kernel", False), (6, "pgap", False)])
+def test_beta_bab_gpu_matches_bruteforce(cuda, seed, branch, native):
+    """Decided verdicts equal lattice enumeration: the native level loop (csrc/beta_runtime.cpp) and the
+    torch loop over the same kernel."""
     pre = presets.get("src/AC-sex")
     grid, q = pre.grid(), pre.resolved()
     ids = processing_order(grid, 0)[:24]
     lo, hi = grid.decode(ids)
     hi = np.minimum(hi, lo + 1)
     m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
-    res = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=256, iters=20, root_iters=40,
-                                                        branch=branch)).solve(lo, hi, m)
+    sol = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=256, iters=20, root_iters=40, branch=branch,
+                                                        native=native))
+    res = sol.solve(lo, hi, m)
+    assert bool(sol.stats.get("native")) == native
     pa = q.pa_idx[0]
     assert (res.status != UNKNOWN).mean() > 0.5
     for k in range(len(ids)):
@@ -254,8 +259,9 @@ def test_beta_kernel_relaxed_matches_reference_and_is_sound(cuda, seed, tie):
         assert float(bg[r]) <= tm, (r, float(bg[r]), tm)
 
 
-@pytest.mark.parametrize("seed,tau,branch", [(21, 2, "kernel"), (24, 3, "kernel"), (21, 2, "pgap")])
-def test_beta_bab_gpu_relaxed_matches_bruteforce(cuda, seed, tau, branch):
+@pytest.mark.parametrize("seed,tau,branch,native", [(21, 2, "kernel", True), (24, 3, "kernel", True),
+                                                    (21, 2, "pgap", True), (21, 2, "kernel", False)])
+def test_beta_bab_gpu_relaxed_matches_bruteforce(cuda, seed, tau, branch, native):
     """GPU twin of test_beta_bab.py::test_beta_bab_relaxed_matches_bruteforce: relaxed queries through
     the HIP kernel (x' RA boxes, tie multipliers, both orientations, exact confirmation); every
     decided verdict equals enumeration of all (x, x') pairs."""
@@ -269,8 +275,10 @@ def test_beta_bab_gpu_relaxed_matches_bruteforce(cuda, seed, tau, branch):
     hi = np.minimum(hi, lo + 1)
     pa, ra = q.pa_idx[0], q.ra_idx[0]
     m = random_mlp(13, [8, 6, 4], seed=seed, bias_scale=0.5)
-    res = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=512, iters=20, root_iters=40,
-                                                        branch=branch)).solve(lo, hi, m)
+    sol = BetaBaBSolver(Backend(m, cuda), q, BetaConfig(node_budget=512, iters=20, root_iters=40, branch=branch,
+                                                        native=native))
+    res = sol.solve(lo, hi, m)
+    assert bool(sol.stats.get("native")) == native
     decided = 0
     for k in range(len(ids)):
         if res.status[k] == UNKNOWN:
@@ -283,3 +291,53 @@ def test_beta_bab_gpu_relaxed_matches_bruteforce(cuda, seed, tau, branch):
                                               q.pa_idx, q.ra_idx, q.tau)
             assert ok[0] and exact.is_violation(m, res.cex_x[k:k + 1], res.cex_xp[k:k + 1])[0]
     assert decided >= 0.5 * len(ids)
+
+
+@pytest.mark.parametrize("seed", [0, 2])
+def test_beta_kernel_orientation_sign_matches_reference(cuda, seed):
+    """osg = -1 rows through the kernel: the rigorous bounds equal the reference's (which equal the
+    negated network's, tests/test_beta_bab.py::test_orientation_sign_equals_negated_network)."""
+    m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(seed)
+    R = lo.shape[0]
+    w = [x.shape[1] for x in ws[:-1]]
+    NH = sum(w)
+    al, be_, t = _params(R, NH, seed, False)
+    osg = torch.tensor([1, -1] * (R // 2) + [1] * (R % 2), dtype=torch.int8)
+    lr = dict(lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    cpu = [x.clone() for x in (al[0], al[1], be_[0], be_[1], t)]
+    lr_ = B.level_ref(ws, bs, w, lo, hi, pa, va, vb, bnd[0][0], bnd[0][1], bnd[1][0], bnd[1][1], ph[0], ph[1], *cpu,
+                      iters=0, osg=osg, **lr)
+    d = lambda x: x.to(cuda).contiguous()  # noqa: E731
+    gpu = [d(x.clone()) for x in (al[0], al[1], be_[0], be_[1], t)]
+    lg = hip.beta_level(Backend(m, cuda), d(lo), d(hi), pa, d(va), d(vb), d(bnd[0][0]), d(bnd[0][1]), d(bnd[1][0]),
+                        d(bnd[1][1]), d(ph[0]), d(ph[1]), *gpu, iters=0, osg=d(osg), **lr)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(lr_.bound)
+    assert torch.allclose(lg.bound.cpu()[fin], lr_.bound[fin], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("relaxed", [False, True])
+def test_beta_native_agrees_with_torch_loop(cuda, relaxed):
+    """The native runtime and the torch loop run the same kernel on the same trees: wherever both
+    decide a partition they agree, and neither decides much less than the other (their level / budget
+    granularity differs: whole BFS levels vs FIFO batches)."""
+    from fairify_amd.spec import ADULT, Query
+
+    pre = presets.get("src/AC-sex")
+    grid = pre.grid()
+    q = Query(pa=("sex",), ra=("age",), tau=2).resolve(ADULT) if relaxed else pre.resolved()
+    ids = processing_order(grid, 0)[:48]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 2)
+    m = random_mlp(13, [16, 8, 4], seed=9, bias_scale=0.5)
+    be = Backend(m, cuda)
+    out = {}
+    for native in (True, False):
+        sol = BetaBaBSolver(be, q, BetaConfig(node_budget=256, iters=24, root_iters=48, native=native))
+        out[native] = sol.solve(lo, hi, m).status
+        assert bool(sol.stats.get("native")) == native
+    a, b = out[True], out[False]
+    both = (a != UNKNOWN) & (b != UNKNOWN)
+    assert both.sum() >= 0.5 * len(ids)
+    assert bool((a[both] == b[both]).all())
+    assert abs(int((a != UNKNOWN).sum()) - int((b != UNKNOWN).sum())) <= 0.1 * len(ids)
