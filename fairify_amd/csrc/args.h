@@ -336,6 +336,9 @@ struct ReluLevelArgs {
   int pa_idx[FA_CMAX_PA];
   const int64_t* pairs;     // [Pp, 2] indices into values
   const float* values;      // [V, npa]
+  int neg_from;             // > 0: nodes with pair >= neg_from rule out the reverse orientation
+                            // N(x, va) > 0 > N(x', vb) (relaxed queries: both orientations in one search;
+                            // the pairs table holds every ordered pair twice)
   // input pool
   const int* part;          // [Nn]
   const int* pair;          // [Nn]

@@ -127,7 +127,8 @@ class BetaRuntime {
                   py::array_t<int, py::array::c_style | py::array::forcecast> tree_part,
                   py::array_t<float, py::array::c_style | py::array::forcecast> box_lo,
                   py::array_t<float, py::array::c_style | py::array::forcecast> box_hi, int budget, int probe_at,
-                  double time_budget, py::dict cfg, py::object confirm, uintptr_t stream_i) {
+                  double time_budget, py::dict cfg, py::object confirm, uintptr_t stream_i,
+                  py::array_t<int, py::array::c_style | py::array::forcecast> closed0) {
     hipStream_t st = (hipStream_t)stream_i;
     const auto t0 = std::chrono::steady_clock::now();
     const int P = (int)status0.shape(0);
@@ -149,11 +150,14 @@ class BetaRuntime {
     status_.ensure(P); nodes_.ensure(P); probed_.ensure(P); part_closed_.ensure(P);
     tree_cnt_.ensure(std::max(R0, 1)); tree_done_.ensure(std::max(R0, 1)); tree_part_.ensure(std::max(R0, 1));
     ensure_pool(0, std::max(R0, 1));
-    // staged host block: status | tree_part (one H2D copy), then device memsets
-    const size_t sb = (size_t)((P + 3) & ~3) + (size_t)R0 * sizeof(int);
+    // staged host block: status | tree_part | closed0 (trees closed before the search: the probe's count)
+    if (closed0.ndim() != 1 || closed0.shape(0) != P) throw std::invalid_argument("beta solve: closed0 shape");
+    const size_t o_tp = (size_t)((P + 3) & ~3), o_c0 = o_tp + (size_t)R0 * sizeof(int);
+    const size_t sb = o_c0 + (size_t)P * sizeof(int);
     hstage_.ensure(sb);
     std::memcpy(hstage_.p, status0.data(), P);
-    std::memcpy(hstage_.p + ((P + 3) & ~3), tree_part.data(), (size_t)R0 * sizeof(int));
+    std::memcpy(hstage_.p + o_tp, tree_part.data(), (size_t)R0 * sizeof(int));
+    std::memcpy(hstage_.p + o_c0, closed0.data(), (size_t)P * sizeof(int));
     stage_.ensure(sb);
     bck(hipMemcpyAsync(stage_.p, hstage_.p, sb, hipMemcpyHostToDevice, st), "cp stage");
     bck(hipMemcpyAsync(status_.p, stage_.p, P, hipMemcpyDeviceToDevice, st), "cp status");
@@ -161,7 +165,8 @@ class BetaRuntime {
                        st), "cp tree_part");
     bck(hipMemsetAsync(nodes_.p, 0, P * sizeof(int), st), "memset nodes");
     bck(hipMemsetAsync(probed_.p, 0, P, st), "memset probed");
-    bck(hipMemsetAsync(part_closed_.p, 0, P * sizeof(int), st), "memset closed");
+    bck(hipMemcpyAsync(part_closed_.p, stage_.p + o_c0, (size_t)P * sizeof(int), hipMemcpyDeviceToDevice, st),
+        "cp closed0");
     bck(hipMemsetAsync(tree_done_.p, 0, std::max(R0, 1), st), "memset tree_done");
     bck(hipMemsetAsync(counters_.p, 0, 4 * sizeof(int), st), "memset counters");   // [2]: probe stops
     copy_roots(roots, R0, st);
@@ -522,5 +527,5 @@ void register_beta(py::module& m) {
            py::arg("capacity"), py::arg("batch_nodes"))
       .def("solve", &BetaRuntime::solve, py::arg("roots"), py::arg("R0"), py::arg("status"), py::arg("tree_part"),
            py::arg("box_lo"), py::arg("box_hi"), py::arg("budget"), py::arg("probe_at"), py::arg("time_budget"),
-           py::arg("cfg"), py::arg("confirm"), py::arg("stream"));
+           py::arg("cfg"), py::arg("confirm"), py::arg("stream"), py::arg("closed0"));
 }

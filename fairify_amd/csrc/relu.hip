@@ -326,7 +326,11 @@ __global__ void fa_relu_rows_kernel(ReluLevelArgs a) {
   for (long long e = (long long)blockIdx.x * FA_THREADS + threadIdx.x; e < tot; e += (long long)gridDim.x * FA_THREADS) {
     const int row = (int)(e / a.n0), d = (int)(e - (long long)row * a.n0);
     const int n = row >> 1, side = row & 1;
-    const bool xp = a.nra > 0 && side == 1;          // relaxed: copy B reads x''s box
+    // relaxed: copy B reads x''s box on the RA dims; every other dim is shared with x, and only x's box
+    // follows the input splits there (the x' box keeps its root values off the RA dims)
+    bool xp = false;
+    if (a.nra > 0 && side == 1)
+      for (int k = 0; k < a.nra; ++k) xp = xp || a.ra_idx[k] == d;
     float lo = (xp ? a.xplo : a.xlo)[(size_t)n * a.n0 + d], hi = (xp ? a.xphi : a.xhi)[(size_t)n * a.n0 + d];
     const int k = fa_pa_slot(a, d);
     if (k >= 0) {
@@ -362,8 +366,12 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
     const size_t o = (size_t)n * n0 + d;
     if (a.xplo[o] > a.xhi[o] + a.tau || a.xphi[o] < a.xlo[o] - a.tau) admissible = false;
   }
+  // orientation -1 (pair >= neg_from): N(x, va) > 0 > N(x', vb) is N_A' < 0 < N_B' on the negated
+  // logit, whose lower form is -U and upper form -L: copy A's U forms / copy B's L forms, negated
+  const bool ng = a.neg_from > 0 && a.pair[n] >= a.neg_from;
+  const float lbA = ng ? -a.oub[A] : a.olb[A], ubB = ng ? -a.olb[B] : a.oub[B];
   if ((st == ST_RUNNING || st == ST_STOPPING) && admissible && !(a.infeas[A] || a.infeas[B]) &&
-      !(a.olb[A] >= 0.f) && !(a.oub[B] <= 0.f)) {
+      !(lbA >= 0.f) && !(ubB <= 0.f)) {
     const int vA = (int)a.pairs[2 * a.pair[n]], vB = (int)a.pairs[2 * a.pair[n] + 1];
     float ca[NM], cb[NM], xl[NM], xh[NM], pl[NM], ph[NM];
     bool rd[NM];                         // relaxed: RA dim (copies concretised separately)
@@ -372,8 +380,8 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       const bool v = i < n0;
-      ca[i] = v ? a.Lc[(size_t)A * n0 + i] : 0.f;
-      cb[i] = v ? a.Uc[(size_t)B * n0 + i] : 0.f;
+      ca[i] = v ? (ng ? -a.Uc[(size_t)A * n0 + i] : a.Lc[(size_t)A * n0 + i]) : 0.f;
+      cb[i] = v ? (ng ? -a.Lc[(size_t)B * n0 + i] : a.Uc[(size_t)B * n0 + i]) : 0.f;
       xl[i] = v ? a.xlo[(size_t)n * n0 + i] : 0.f;
       xh[i] = v ? a.xhi[(size_t)n * n0 + i] : 0.f;
       bool r = false;
@@ -398,8 +406,9 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
           if (RX) pl[i] = ph[i] = 0.f;
         }
     }
-    const float LA0 = a.L0[A] - a.Le[A];
-    const float UB0 = a.U0[B] + a.Ue[B];
+    // lower constant of copy A's (oriented) logit less its error; upper constant of copy B's plus its error
+    const float LA0 = ng ? -(a.U0[A] + a.Ue[A]) : a.L0[A] - a.Le[A];
+    const float UB0 = ng ? -(a.L0[B] - a.Le[B]) : a.U0[B] + a.Ue[B];
     // with several PA dims the folded sum can cancel: the margin takes the terms' magnitudes
     float magA = fabsf(LA0) + fmA, magB = fabsf(UB0) + fmB;
 #pragma unroll
@@ -484,8 +493,9 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_cert_kernel(ReluLevelArgs 
       if (idim < 0) {
         choice = -2;                       // single lattice point: decided by the exact check
       } else {
-        const float gapA = -a.olb[A], gapB = a.oub[B];
-        const int sA = a.split[2 * A], sB = a.split[2 * B + 1];
+        // the bound closest to closing and its split: copy A's lower (oriented) bound, copy B's upper
+        const float gapA = -lbA, gapB = ubB;
+        const int sA = a.split[2 * A + (ng ? 1 : 0)], sB = a.split[2 * B + (ng ? 0 : 1)];
         const bool useA = sA >= 0 && (gapA <= gapB || sB < 0);
         const bool useB = !useA && sB >= 0;
         choice = useA ? sA : (useB ? 65536 + sB : -1);
@@ -508,8 +518,11 @@ __global__ void __launch_bounds__(FA_THREADS) fa_relu_split_kernel(ReluLevelArgs
     const int p = a.part[n];
     const int8_t st = a.status[p];
     if (st != ST_RUNNING && st != ST_STOPPING) continue;
-    // ---- the LP-optimal vertex pair, if its rigorous point bounds allow a violation
-    const bool poss = a.pe_lb[2 * n] < 0.f && a.pe_ub[2 * n + 1] > 0.f;
+    // ---- the LP-optimal vertex pair, if its rigorous point bounds allow a violation (of this node's
+    // orientation)
+    const bool ng = a.neg_from > 0 && a.pair[n] >= a.neg_from;
+    const bool poss = ng ? (a.pe_ub[2 * n] > 0.f && a.pe_lb[2 * n + 1] < 0.f)
+                         : (a.pe_lb[2 * n] < 0.f && a.pe_ub[2 * n + 1] > 0.f);
     if (poss) {
       int slot = 0;
       if (lane == 0) slot = atomicAdd(a.cand_count, 1);

@@ -60,7 +60,7 @@ class ReluRuntime {
  public:
   ReluRuntime(py::handle net, uintptr_t flat, std::vector<int> pa, std::vector<float> values_f,
               std::vector<int64_t> pairs, int capacity, int batch_nodes, double unit, int refine,
-              std::vector<int> ra, double tau)
+              std::vector<int> ra, double tau, int norient)
       : net_(fa_net_desc(net)), flat_((const float*)flat), pa_(std::move(pa)), cap_(capacity), batch_(batch_nodes),
         unit_(unit), refine_(refine), ra_(std::move(ra)), tau_((float)tau) {
     n0_ = net_.dims[0];
@@ -77,6 +77,15 @@ class ReluRuntime {
         if (k == d) throw std::invalid_argument("RA dim is a PA dim");
     }
     V_ = (int)(values_f.size() / npa_);
+    // relaxed queries, norient = 2: both orientations are roots of the same search -- every ordered
+    // pair appears twice in the table, the second copy (index >= neg_from_) ruling out the reverse
+    // orientation N(x, va) > 0 > N(x', vb) (relu.hip reads the negated logit's forms)
+    if (norient == 2 && relaxed_ && !pairs.empty()) {
+      neg_from_ = (int)(pairs.size() / 2);
+      std::vector<int64_t> twice(pairs);
+      twice.insert(twice.end(), pairs.begin(), pairs.end());
+      pairs.swap(twice);
+    }
     Pp_ = (int)(pairs.size() / 2);
     vals_.ensure(values_f.size());
     pairs_.ensure(std::max<size_t>(pairs.size(), 2));
@@ -261,7 +270,7 @@ class ReluRuntime {
     ReluLevelArgs a{};
     a.Nn = nb; a.n0 = n0_; a.nh = nh_; a.npa = npa_;
     for (int k = 0; k < npa_; ++k) a.pa_idx[k] = pa_[k];
-    a.pairs = pairs_.p; a.values = vals_.p;
+    a.pairs = pairs_.p; a.values = vals_.p; a.neg_from = neg_from_;
     a.part = part_[cur].p + s; a.pair = pair_[cur].p + s;
     a.xlo = lo_[cur].p + s * n0_; a.xhi = hi_[cur].p + s * n0_;
     a.phase = phase_[cur].p + s * 2 * nh_;
@@ -425,6 +434,7 @@ class ReluRuntime {
   float tau_ = 0.f;
   bool relaxed_ = false;
   int n0_ = 0, nh_ = 0, npa_ = 0, V_ = 0, Pp_ = 0;
+  int neg_from_ = 0;        // > 0: pairs [neg_from_, Pp_) are the reverse orientation
   int pool_[2] = {0, 0};
   int cand_alloc_ = 0;
   fa_exact::ExactChecker exact_;
@@ -451,10 +461,10 @@ class ReluRuntime {
 void register_relu(py::module& m) {
   py::class_<ReluRuntime>(m, "ReluRuntime")
       .def(py::init<py::handle, uintptr_t, std::vector<int>, std::vector<float>, std::vector<int64_t>, int, int,
-                    double, int, std::vector<int>, double>(),
+                    double, int, std::vector<int>, double, int>(),
            py::arg("net"), py::arg("flat"), py::arg("pa"), py::arg("values_f"), py::arg("pairs"),
            py::arg("capacity"), py::arg("batch_nodes"), py::arg("unit"), py::arg("refine") = 0,
-           py::arg("ra") = std::vector<int>(), py::arg("tau") = 0.0)
+           py::arg("ra") = std::vector<int>(), py::arg("tau") = 0.0, py::arg("norient") = 1)
       .def("solve", &ReluRuntime::solve, py::arg("lo"), py::arg("hi"), py::arg("status"), py::arg("budget"),
            py::arg("time_budget"), py::arg("confirm"), py::arg("stream"));
 }

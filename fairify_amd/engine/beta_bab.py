@@ -43,8 +43,9 @@ from .bab import RUNNING, SAT, UNKNOWN, UNSAT, BaBResult, _pa_table, pa_groups
 @dataclass
 class BetaConfig:
     node_budget: int = 512           # nodes per partition (all its pair trees together; x Pp / 2)
-    iters: int = 64                  # optimisation steps per node (warm-started from the parent)
-    root_iters: int = 200            # ... per root node
+    iters: int = 128                 # optimisation steps per node (warm-started from the parent); 128 over
+    #                                  64: relaxed/BM BM-8 residue 48 vs 33 of 200 at 1 024 nodes with pgap
+    root_iters: int = 400            # ... per root node
     lr_a: float = 0.1                # Adam step of the slopes alpha
     lr_b: float = 0.5                # ... of the split multipliers beta
     lr_t: float = 0.1                # ... of the pair weight t
@@ -65,9 +66,10 @@ class BetaConfig:
     batch_nodes: int = 32768         # nodes per level launch
     time_budget: float = 1e9         # wall-clock seconds for the whole call
     max_pool: int = 1 << 21          # live nodes (more: the partitions losing nodes end UNKNOWN)
-    branch: str = "kernel"           # "pgap": the verified LP's rule (largest primal gap h - relu(z)) at the
+    branch: str = "pgap"             # "pgap": the verified LP's rule (largest primal gap h - relu(z)) at the
     #                                  averaged primal iterate of the node's optimisation (kernel-side;
     #                                  with lookahead > 0 it supplies the first candidate list);
+    #                                  "kernel": |lambda| x relaxation gap at the vertex x* (round 5);
     #                                  "lpgap" (experiment): the chord slack at the vertex x* / x'*
     pgap_weights: int = 1            # branch "pgap": iterate weights of the primal average (1 uniform, 2 it + 1,
     #                                  3 second half of the steps)
@@ -76,6 +78,8 @@ class BetaConfig:
     native: bool = True              # HIP device: the level loop in the native runtime (csrc/beta_runtime.cpp,
     #                                  device-resident pool / budgets / probe); FAIRIFY_TORCH_BETA=1 or the
     #                                  experiments (lpgap, input_every, merge_orient off): this module's loop
+    sign_prune: bool = True          # close the (pair, orientation) trees a per-value logit sign test settles
+    #                                  before their roots are bounded
     merge_orient: bool = True        # relaxed: both orientations as roots of ONE search (per-node sign of
     #                                  the objective, ops/beta.py:evaluate osg) instead of a second solve on
     #                                  the negated network for the partitions the first one closed
@@ -178,6 +182,7 @@ class BetaBaBSolver:
         NH = be.n_hidden
         lb = torch.cat([t.float() for t in res.layer_lb], 1)[:, :NH].contiguous()
         ub = torch.cat([t.float() for t in res.layer_ub], 1)[:, :NH].contiguous()
+        self._logit = (res.out_lb, res.out_ub)          # [P * V] rigorous logit bounds of the rows
         return lb, ub
 
     def _solve_group(self, lo_np, hi_np, mlp_exact, status, time_budget):
@@ -213,12 +218,31 @@ class BetaBaBSolver:
         hi_r = torch.from_numpy(hi_np[run].astype(np.float32)).to(dev)
         with self.tm("beta.roots"):
             rlb, rub = self._root_bounds(lo_r, hi_r, values)
+            olx = self._logit
             rlbp, rubp = self._root_bounds(lo_r, hi_r, values, widen=True) if relaxed else (rlb, rub)
+            olp = self._logit if relaxed else olx
         # one root per (running partition, ordered pair, orientation)
         k = torch.arange(run.size, device=dev).repeat_interleave(Pp * O)
         pr = torch.from_numpy(pairs_np.astype(np.int64)).to(dev).repeat_interleave(O, dim=0).repeat(run.size, 1)
         osg = torch.tensor([1, -1][:O], dtype=torch.int8, device=dev).repeat(run.size * Pp)
         ia, ib = k * V + pr[:, 0], k * V + pr[:, 1]
+        pre_closed = np.zeros(P, dtype=np.int32)
+        if cfg.sign_prune:
+            # per-value sign tests from the rows' rigorous logit bounds (the verified LP's shared sign
+            # tests, smt/lpbab.py:solve_partition): a tree whose copy A can never have the sign its
+            # orientation needs (N(x, va) < 0, or > 0 for the reverse) or whose copy B can never have
+            # the opposite one is closed before its root is bounded -- a race query has 20 ordered
+            # pairs x 2 orientations, most of them settled by one of 2 V such tests
+            pos = osg > 0
+            dead = torch.where(pos, (olx[0][ia] >= 0) | (olp[1][ib] <= 0), (olx[1][ia] <= 0) | (olp[0][ib] >= 0))
+            keep = ~dead
+            # the probe counts these trees as closed (progress on the partition)
+            pre_closed = np.bincount(run[k[dead].cpu().numpy()], minlength=P).astype(np.int32)
+            k, pr, osg, ia, ib = k[keep], pr[keep], osg[keep], ia[keep], ib[keep]
+            self.stats["sign_pruned"] = self.stats.get("sign_pruned", 0) + int(dead.sum())
+            if k.numel() == 0:
+                status[run] = UNSAT
+                return status, cex_x, cex_xp, nodes_np
         R0 = k.numel()
         plo = lo_r[k].clone()
         phi = hi_r[k].clone()
@@ -249,7 +273,7 @@ class BetaBaBSolver:
         if self._use_native(O):
             return self._solve_native(pool, R0, status, lo_np, hi_np, mlp_exact, budget,
                                       2 * cfg.probe_levels * Pp * O if cfg.probe_levels else 0,
-                                      max(0.0, time_budget - (time.time() - t0)))
+                                      max(0.0, time_budget - (time.time() - t0)), pre_closed)
         levels = 0
         # the probe (per partition, so a verdict never depends on which partitions share the call):
         # once a partition has expanded 2 probe_levels nodes per pair tree, it goes on only if one
@@ -339,7 +363,7 @@ class BetaBaBSolver:
             kids = self._children({kk: v[gi] for kk, v in cur.items()}, split, bi, NH, n0)
             pool = {kk: torch.cat([rest[kk], kids[kk]]) for kk in pool}
             if cfg.probe_levels:
-                self._probe(pool, nodes_np, probed, probe_at, R0, tree_run, status)
+                self._probe(pool, nodes_np, probed, probe_at, R0, tree_run, status, pre_closed)
             if pool["part"].numel() > cfg.max_pool:
                 lost = torch.unique(pool["part"][cfg.max_pool:]).cpu().numpy()
                 lost = lost[status[lost] == RUNNING]
@@ -362,7 +386,7 @@ class BetaBaBSolver:
                 and (O == 2 or not self.q.relaxed))
 
     def _solve_native(self, pool, R0: int, status, lo_np, hi_np, mlp_exact, budget: int, probe_at: int,
-                      time_budget: float):
+                      time_budget: float, pre_closed=None):
         """The level loop on the device (csrc/beta_runtime.cpp): the roots of ``pool`` go to the native
         runtime's node pool; verdicts, witnesses and per-partition node counts come back."""
         from ..ops import ext
@@ -415,7 +439,8 @@ class BetaBaBSolver:
         with self.tm("beta.native"), checkout(be, "_beta_rt", key, cap, make) as rt:
             st, cx, cxp, nodes, stats = rt.solve(ptrs, int(R0), status.astype(np.int8), tree_part,
                                                  lo_np.astype(np.float32), hi_np.astype(np.float32), int(budget),
-                                                 int(probe_at), float(time_budget), cfgd, confirm, stream)
+                                                 int(probe_at), float(time_budget), cfgd, confirm, stream,
+                                                 np.zeros(P, np.int32) if pre_closed is None else pre_closed)
         del arrs
         stats = dict(stats)
         self.stats["levels"] = self.stats.get("levels", 0) + int(stats["levels"])
@@ -425,7 +450,7 @@ class BetaBaBSolver:
         self.stats["native"] = True
         return (np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes, dtype=np.int64))
 
-    def _probe(self, pool, nodes_np, probed, probe_at: int, R0: int, tree_run, status) -> None:
+    def _probe(self, pool, nodes_np, probed, probe_at: int, R0: int, tree_run, status, pre_closed=None) -> None:
         """Partitions past the probe point with no closed pair tree end UNKNOWN (their nodes are
         dropped at the next level)."""
         cand = np.nonzero((nodes_np >= probe_at) & ~probed & (status == RUNNING))[0]
@@ -436,6 +461,8 @@ class BetaBaBSolver:
         if pool["tree"].numel():
             alive[pool["tree"].cpu().numpy()] = True
         closed = np.bincount(tree_run[~alive], minlength=status.shape[0])
+        if pre_closed is not None:
+            closed = closed + pre_closed
         stop = cand[closed[cand] == 0]
         if stop.size:
             status[stop] = UNKNOWN

@@ -145,6 +145,20 @@ class VerifyConfig:
                                          # residue partitions of relaxed/BM for 21 s of its 60 s
                                          # (profiles/r5/s5_m/); a static rule, so verdicts stay
                                          # independent of how partitions are sharded
+    beta_branch: str = os.environ.get("FAIRIFY_BETA_BRANCH", "pgap")
+                                         # BetaConfig.branch: "pgap" = the verified LP's primal-gap rule
+                                         # at the averaged primal iterate (relaxed/BM BM-8 residue: 33 vs
+                                         # 5 of 200 decided at 1 024 nodes, profiles/r6/), "kernel" =
+                                         # |lambda| x gap at the vertex x* (round 5)
+    beta_iters: int = int(os.environ.get("FAIRIFY_BETA_ITERS", "128"))
+                                         # optimisation steps per child node (root: x 3); 128 over 64:
+                                         # 48 vs 33 of 200 at 1 024 nodes (a converged dual gives the
+                                         # primal average its meaning)
+    beta_lookahead: int = 8              # filtered look-ahead candidates per score list
+    beta_escalate_cap: int = int(os.environ.get("FAIRIFY_BETA_ESC_CAP", "0"))
+                                         # networks the beta fixed pass runs on: cap the input-split
+                                         # escalation budget at this (their residue goes to beta instead
+                                         # of deep input splitting; 0 = no cap)
     lp_budget: int = 4096                # verified-LP branch-and-bound (stage "lp", smt/lpbab.py) in
                                          # place of the untrusted MILP: LP nodes per partition (x growth
                                          # per anytime round); 0 = the round-2 MILP stage
@@ -280,15 +294,19 @@ def _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, limit, worke
 
 
 def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes, status, stage, cex_x, cex_xp, nodes,
-                tm=None, probe_levels: int = 0):
+                tm=None, probe_levels: int = 0, cfg=None):
     """beta-CROWN BaB (engine/beta_bab.py) on the partitions ``unk``: decided verdicts (sound SAT /
     UNSAT) written into the stage arrays; returns how many it decided.  ``probe_levels``: a partition
     gives up once it has expanded 2 x that many nodes per pair tree with none of its trees closed
     (BetaConfig)."""
     from .beta_bab import BetaBaBSolver, BetaConfig
 
+    kw = {}
+    if cfg is not None:
+        kw = dict(branch=cfg.beta_branch, iters=cfg.beta_iters, root_iters=max(200, 3 * cfg.beta_iters),
+                  lookahead=cfg.beta_lookahead)
     bs = BetaBaBSolver(be, q, BetaConfig(node_budget=budget, batch_nodes=min(batch_nodes, 32768),
-                                         time_budget=time_budget, probe_levels=probe_levels),
+                                         time_budget=time_budget, probe_levels=probe_levels, **kw),
                        **({"timer": tm} if tm is not None else {}))
     t0 = time.time()
     br = bs.solve(lo_np[unk], hi_np[unk], mlp)
@@ -491,9 +509,14 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
     from .relu_bab import supported as _relu_supported
 
     relu_on = cfg.relu_budget > 0 and max(mlp.hidden or [0]) <= cfg.relu_max_width and _relu_supported(q)
-    if relu_on and cfg.relu_escalate_cap > 0 and cfg.escalate_budget > cfg.relu_escalate_cap:
-        # the residue of these networks goes to the relu stage: stop the input-split escalation early
-        cap = max(cfg.relu_escalate_cap, cfg.node_budget)
+    from .beta_bab import supported as _beta_supported
+
+    beta_on = (cfg.beta_budget > 0 and _beta_supported(q)
+               and cfg.beta_min_width <= max(mlp.hidden or [0]) <= cfg.beta_max_width)
+    esc_cap = cfg.relu_escalate_cap if relu_on else (cfg.beta_escalate_cap if beta_on else 0)
+    if esc_cap > 0 and cfg.escalate_budget > esc_cap:
+        # the residue of these networks goes to the relu / beta stage: stop the input-split escalation early
+        cap = max(esc_cap, cfg.node_budget)
         cfg = replace(cfg, escalate_budget=cap if cap > cfg.node_budget else 0,
                       escalate_probation=tuple(st for st in cfg.escalate_probation if st[0] < cap))
     # relu_first: the escalation pass (one budget, open-frontier gate) runs after stage 3r
@@ -635,10 +658,6 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
         charge(1, n0_)
     # ---------------- stage 3b': beta-CROWN phase-split BaB on the residue (the wide nets' UNSAT
     # partitions need phase splits as constraints on the region: Lagrangian split multipliers)
-    from .beta_bab import supported as _beta_supported
-
-    beta_on = (cfg.beta_budget > 0 and _beta_supported(q)
-               and cfg.beta_min_width <= max(mlp.hidden or [0]) <= cfg.beta_max_width)
     if beta_on:
         unk = np.nonzero((status == UNKNOWN) & ~forced)[0]
         if unk.size:
@@ -647,7 +666,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
             n0_ = nodes.copy()
             with tm("beta"):
                 _beta_round(be, q, mlp, unk, lo_np, hi_np, cfg.beta_budget, max(0.0, budget - el), cfg.batch_nodes,
-                            status, stage, cex_x, cex_xp, nodes, tm, probe_levels=cfg.beta_probe_levels)
+                            status, stage, cex_x, cex_xp, nodes, tm, probe_levels=cfg.beta_probe_levels, cfg=cfg)
             charge(2, n0_)
             sync()
             t_bab += time.time() - t0
@@ -743,7 +762,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                         # residue) the other stages keep their time
                         with tm("beta"):
                             ndec = _beta_round(be, q, mlp, unk, lo_np, hi_np, b_budget, 0.5 * left, cfg.batch_nodes,
-                                               status, stage, cex_x, cex_xp, nodes, tm)
+                                               status, stage, cex_x, cex_xp, nodes, tm, cfg=cfg)
                         if ndec < cfg.anytime_min_yield * unk.size:
                             beta_live = False
                     unk = np.nonzero((status == UNKNOWN) & ~forced)[0]

@@ -65,6 +65,10 @@ class ReluConfig:
     # step time, and on the trained AC-7 residue it closed none either way
     # (profiles/r4/relu_refine.md)
     refine: str = os.environ.get("FAIRIFY_RELU_REFINE", "off")
+    # relaxed queries on the native runtime: both orientations as roots of ONE search (the reverse
+    # orientation's nodes read the negated logit's forms, csrc/relu.hip) with the two solves' budgets
+    # pooled, instead of a second search on the negated network for the partitions the first closed
+    merge_orient: bool = os.environ.get("FAIRIFY_RELU_MERGE", "1") != "0"
 
 
 def supported(q: ResolvedQuery) -> bool:
@@ -178,7 +182,7 @@ class ReluBaBSolver:
         if not supported(self.q):
             status[status == RUNNING] = UNKNOWN
             return BaBResult(status, np.zeros((P, n), np.int64), np.zeros((P, n), np.int64), np.zeros(P, np.int64))
-        if self.q.relaxed and not getattr(self, "_second", False):
+        if self.q.relaxed and not getattr(self, "_second", False) and not self._merged():
             r1 = self._solve_groups_all(lo_np, hi_np, mlp_exact, status, t0)
             closed = (r1.status == UNSAT) & (status == RUNNING)
             if not closed.any():
@@ -197,6 +201,14 @@ class ReluBaBSolver:
             cx[s2], cxp[s2] = r2.cex_x[s2], r2.cex_xp[s2]
             return BaBResult(out, cx, cxp, r1.nodes + r2.nodes, 0, time.time() - t0)
         return self._solve_groups_all(lo_np, hi_np, mlp_exact, status, t0)
+
+    def _native(self) -> bool:
+        torch_rx = self.q.relaxed and os.environ.get("FAIRIFY_RELU_RELAXED_TORCH") == "1"
+        return self.be.hip and os.environ.get("FAIRIFY_TORCH_BAB") != "1" and not torch_rx
+
+    def _merged(self) -> bool:
+        """Relaxed query, both orientations in the native runtime's one search."""
+        return self.q.relaxed and self.cfg.merge_orient and self._native()
 
     def _solve_groups_all(self, lo_np, hi_np, mlp_exact, status, t0) -> BaBResult:
         P, n = lo_np.shape
@@ -218,8 +230,7 @@ class ReluBaBSolver:
         # (relaxed: an x' RA box per node; the second orientation is solve()'s negated network);
         # FAIRIFY_TORCH_BAB=1: the torch orchestration (the reference semantics of the CPU tests)
         # (FAIRIFY_RELU_RELAXED_TORCH=1: relaxed queries only, the A/B of the native relaxed path)
-        torch_rx = self.q.relaxed and os.environ.get("FAIRIFY_RELU_RELAXED_TORCH") == "1"
-        if self.be.hip and os.environ.get("FAIRIFY_TORCH_BAB") != "1" and not torch_rx:
+        if self._native():
             return self._solve_native(lo_np, hi_np, mlp_exact, status, values_np, pairs_np, time_budget)
         return self._solve_torch(lo_np, hi_np, mlp_exact, status, values_np, pairs_np, time_budget)
 
@@ -449,14 +460,15 @@ class ReluBaBSolver:
         rf = min(1, refine_level(self.cfg.refine, self.be.widths))
         ra = list(self.q.ra_idx) if self.q.relaxed else []
         tau = float(self.q.tau) if self.q.relaxed else 0.0
+        no = 2 if self._merged() else 1
         key = (tuple(self.q.pa_idx), values_np.tobytes(), pairs_np.tobytes(), int(self.cfg.batch_nodes), rf,
-               tuple(ra), tau)
+               tuple(ra), tau, no)
 
         def make(cap):
             return ext().ReluRuntime(_net(self.be), self.be.flat.data_ptr(), list(self.q.pa_idx),
                                      values_np.astype(np.float32).reshape(-1).tolist(),
                                      pairs_np.astype(np.int64).reshape(-1).tolist(), int(cap),
-                                     int(self.cfg.batch_nodes), float(self.be.unit), rf, ra, tau)
+                                     int(self.cfg.batch_nodes), float(self.be.unit), rf, ra, tau, no)
 
         return checkout(self.be, "_relu_rt", key, max(self.cfg.max_pool, 2 * n_root), make)
 
@@ -471,7 +483,8 @@ class ReluBaBSolver:
             status = status.copy()
             status[status == RUNNING] = UNKNOWN
             return status, np.zeros((P, n0), np.int64), np.zeros((P, n0), np.int64), np.zeros(P, np.int64)
-        n_root = int((status == RUNNING).sum()) * max(1, pairs_np.shape[0])
+        no = 2 if self._merged() else 1
+        n_root = int((status == RUNNING).sum()) * max(1, pairs_np.shape[0]) * no
         if pairs_np.shape[0] == 0:
             status = status.copy()
             status[status == RUNNING] = UNSAT
@@ -491,6 +504,6 @@ class ReluBaBSolver:
         stream = torch.cuda.current_stream(self.dev).cuda_stream
         with self.tm("relu.native"), self._runtime(values_np, pairs_np, n_root) as rt:
             st, cx, cxp, nodes, stats = rt.solve(lo_np.astype(np.float32), hi_np.astype(np.float32), status,
-                                                 int(self.cfg.node_budget), float(time_budget), confirm, stream)
+                                                 int(self.cfg.node_budget) * no, float(time_budget), confirm, stream)
         self.stats = dict(stats)
         return (np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes, dtype=np.int64))

@@ -297,6 +297,50 @@ def test_beta_bab_relaxed_matches_bruteforce(seed, tau, merge):
     assert decided >= 0.5 * len(ids)
 
 
+@pytest.mark.parametrize("relaxed", [False, True])
+def test_sign_pruned_roots_match_bruteforce(relaxed):
+    """Race (5 values: 20 ordered pairs, x 2 orientations when relaxed): the per-value logit sign tests
+    close many trees before their roots are bounded; the verdicts stay those of enumeration and of the
+    unpruned search."""
+    from fairify_amd.spec import ADULT, Query
+
+    q = Query(pa=("race",), ra=("age",) if relaxed else (), tau=2 if relaxed else 0).resolve(ADULT)
+    grid = presets.get("src/AC-race").grid()
+    ids = processing_order(grid, 0)[:12]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 1)
+    hi[:, q.pa_idx[0]] = np.maximum(hi[:, q.pa_idx[0]], lo[:, q.pa_idx[0]])
+    m = random_mlp(13, [8, 6, 4], seed=5, bias_scale=0.5)
+    be = Backend(m)
+    sols = {sp: BetaBaBSolver(be, q, BetaConfig(node_budget=256, iters=20, root_iters=40, sign_prune=sp))
+            for sp in (True, False)}
+    res = {sp: s.solve(lo, hi, m).status for sp, s in sols.items()}
+    assert sols[True].stats.get("sign_pruned", 0) > 0
+    both = (res[True] != UNKNOWN) & (res[False] != UNKNOWN)
+    assert bool((res[True][both] == res[False][both]).all())
+    assert (res[True] != UNKNOWN).sum() >= (res[False] != UNKNOWN).sum()
+    pa, ra = q.pa_idx[0], (q.ra_idx[0] if relaxed else None)
+    for k in np.nonzero(res[True] != UNKNOWN)[0]:
+        pts = _lattice(lo[k], hi[k])
+        vals = range(int(lo[k, pa]), int(hi[k, pa]) + 1)
+        truth = False
+        for v1 in vals:
+            x = pts.copy()
+            x[:, pa] = v1
+            z = m.logits(x)
+            for v2 in vals:
+                if v2 == v1:
+                    continue
+                for d in (range(-2, 3) if relaxed else (0,)):
+                    xp = x.copy()
+                    xp[:, pa] = v2
+                    if relaxed:
+                        xp[:, ra] += d
+                    zp = m.logits(xp)
+                    truth = truth or bool((((z < 0) & (zp > 0)) | ((z > 0) & (zp < 0))).any())
+        assert (res[True][k] == SAT) == truth, k
+
+
 def test_probe_verdicts_do_not_depend_on_grouping():
     """With the probe on, each partition's verdict is its own: solving the partitions together, in
     two halves, or one by one gives the same statuses (the product runner re-shards residues over

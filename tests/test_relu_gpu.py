@@ -190,3 +190,27 @@ def test_native_relu_relaxed_matches_bruteforce_and_torch(cuda, seed, tau):
         del os.environ["FAIRIFY_TORCH_BAB"]
     both = (res.status != UNKNOWN) & (tor.status != UNKNOWN)
     assert np.array_equal(res.status[both], tor.status[both])
+
+
+def test_native_relu_relaxed_wide_boxes_decide_like_torch(cuda):
+    """Wider boxes with a node budget that binds: copy B's rows follow x's input splits on the shared
+    dims (only the RA dims read x''s own box), so the native runtime decides about as many partitions
+    as the torch orchestration and agrees with it wherever both decide."""
+    from fairify_amd.spec import ADULT, Query
+
+    q = Query(pa=("sex",), ra=("age",), tau=2).resolve(ADULT)
+    grid = presets.get("src/AC-sex").grid()
+    ids = processing_order(grid, 0)[:64]
+    lo, hi = grid.decode(ids)
+    hi = np.minimum(hi, lo + 4)
+    m = random_mlp(13, [8, 6], seed=31, bias_scale=0.5)
+    nat = ReluBaBSolver(Backend(m, cuda), q, ReluConfig(node_budget=128)).solve(lo, hi, m)
+    os.environ["FAIRIFY_TORCH_BAB"] = "1"
+    try:
+        tor = ReluBaBSolver(Backend(m, cuda), q, ReluConfig(node_budget=128)).solve(lo, hi, m)
+    finally:
+        del os.environ["FAIRIFY_TORCH_BAB"]
+    both = (nat.status != UNKNOWN) & (tor.status != UNKNOWN)
+    assert np.array_equal(nat.status[both], tor.status[both])
+    dn, dt = int((nat.status != UNKNOWN).sum()), int((tor.status != UNKNOWN).sum())
+    assert dt > 0 and dn >= dt - max(2, dt // 10), (dn, dt)

@@ -83,6 +83,14 @@ def run_group(args) -> None:
                            ((2048, 768), (4096, 768), (8192, 768), (16384, 1024)),
                            relu_budget=1024, relu_escalate_cap=2048, smt_backend=args.smt or ("none" if big else "auto"),
                            chunk=8192)
+        if args.cfg:      # A/B overrides of VerifyConfig fields: --cfg key=value,key=value
+            from dataclasses import replace as _rp
+
+            kv = {}
+            for item in filter(None, args.cfg.split(",")):
+                k, v = item.split("=")
+                kv[k] = type(getattr(cfg, k))(v)
+            cfg = _rp(cfg, **kv)
         t0 = time.time()
         weights = {m: ("zoo" if has_weights(m) else "random") for m in models}
         rows = []
@@ -146,6 +154,7 @@ def main():
     ap.add_argument("--all-anytime", action="store_true", help="anytime mode for the other groups too")
     ap.add_argument("--max-partitions", type=int, default=None, help="CPU rehearsal: first N of each grid")
     ap.add_argument("--report", default=None)
+    ap.add_argument("--cfg", default="", help="VerifyConfig overrides 'key=value,...' (A/B runs)")
     ap.add_argument("--smt", default=None, help="host back-end (default: auto for tablev, none for the big grids)")
     ap.add_argument("--scratch", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "fairify_base"),
                     help="per-partition CSVs (not copied back)")
