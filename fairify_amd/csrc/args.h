@@ -440,6 +440,10 @@ struct BetaArgs {
   const uint8_t* skip;      // [R] nodes closed before bounding (decided partition, empty region), or nullptr:
                             // bound +inf, no branching
   int ph_stride;            // row stride of phA / phB (0: NH; the native runtime's [R][2][NH] layout: 2 NH)
+  int feas;                 // 1: infeasibility pass -- nodes still open (bound < 0) with a fixed phase: the
+                            // Lagrangian of the phase constraints alone (objective weight 0, multipliers
+                            // in [0, 1]) is optimised; a rigorous value > 0 proves the region empty (bound
+                            // := +inf); nothing else is written (scratch must hold [R, 16, NH])
 };
 
 // Native beta-CROWN BaB level (csrc/beta_runtime.cpp, kernels csrc/beta_bab.hip): a device-resident

@@ -442,10 +442,17 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
   }
   wsync();
   float* par = a.par + (size_t)r * 4 * NH;          // alpha_A, alpha_B, beta_A, beta_B (best)
-  float* cur = a.scratch + (size_t)r * 12 * NH;     // current
+  float* cur = a.scratch + (size_t)r * (a.feas ? 16 : 12) * NH;   // current
   float* mom = cur + 4 * NH;
   float* vel = cur + 8 * NH;
   if (a.skip && a.skip[r]) bad = 1;         // closed before bounding: same outputs as an empty region
+  if (a.feas) {
+    // infeasibility pass: only nodes the main pass left open and that fix some phase
+    int fixed = 0;
+    for (int c = 0; c < 2; ++c)
+      for (int k = lane; k < NH; k += 64) fixed |= S.ph[c][k] != 0;
+    if (__any(bad) || !__any(fixed) || !(a.bound[r] < 0.0)) return;
+  }
   if (__any(bad)) {
     if (lane == 0) {
       a.bound[r] = __builtin_inf();
@@ -466,7 +473,10 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
     for (int j = lane; j < nd.dims[l + 1]; j += 64)
       for (int q = 0; q < 4; ++q) {
         const int k = q * NH + nd.neuron_off[l] + j;
-        cur[k] = par[k];
+        // feas: the phase multipliers start at 0.5 on the fixed neurons (0 elsewhere), the slopes at the
+        // main pass's best
+        cur[k] = a.feas && q >= 2 ? (S.ph[q - 2][k - q * NH] != 0 ? 0.5f : 0.f) : par[k];
+        if (a.feas) cur[12 * NH + k] = cur[k];          // best iterate of the pass
         mom[k] = 0.f;
         vel[k] = 0.f;
         S.zb[0][k - q * NH] = 0.f;     // (q-invariant: the sums of neuron nd.neuron_off[l] + j)
@@ -475,16 +485,18 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         S.hb[1][k - q * NH] = 0.f;
       }
   float tc = a.t[r], tbest = tc, mt = 0.f, vt = 0.f;
-  // orientation: the objective og (t N_A - (1 - t) N_B) rules out N_A < 0 < N_B (og = +1) or the reverse
-  const float og = a.osg ? (float)a.osg[r] : 1.f;
+  // orientation: the objective og (t N_A - (1 - t) N_B) rules out N_A < 0 < N_B (og = +1) or the reverse;
+  // the infeasibility pass weighs it 0
+  const float og = (a.osg ? (float)a.osg[r] : 1.f) * (a.feas ? 0.f : 1.f);
+  float* fbest = cur + 12 * NH;                      // feas: the pass's best parameters (not par)
   float best = -FLT_MAX;
   // relaxed: the tie's multipliers of this lane's RA dim (lane = input dim; n0 <= 64)
   const bool my_ra = N.tie && lane < n0 && ((N.ramask >> lane) & 1ull);
   float* gio = N.tie ? a.gtie + (size_t)r * 2 * n0 : nullptr;
   float gbp = 0.f, gbm = 0.f, mgp = 0.f, vgp = 0.f, mgm = 0.f, vgm = 0.f;
   if (lane < n0) {
-    S.gt[0][lane] = my_ra ? gio[lane] : 0.f;
-    S.gt[1][lane] = my_ra ? gio[n0 + lane] : 0.f;
+    S.gt[0][lane] = my_ra && !a.feas ? gio[lane] : 0.f;
+    S.gt[1][lane] = my_ra && !a.feas ? gio[n0 + lane] : 0.f;
     gbp = S.gt[0][lane];
     gbm = S.gt[1][lane];
   }
@@ -509,9 +521,10 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         gbp = S.gt[0][lane];
         gbm = S.gt[1][lane];
       }
+      float* dst = a.feas ? fbest : par;
       for (int l = 0; l < L - 1; ++l)
         for (int j = lane; j < nd.dims[l + 1]; j += 64)
-          for (int q = 0; q < 4; ++q) par[q * NH + nd.neuron_off[l] + j] = cur[q * NH + nd.neuron_off[l] + j];
+          for (int q = 0; q < 4; ++q) dst[q * NH + nd.neuron_off[l] + j] = cur[q * NH + nd.neuron_off[l] + j];
     }
     if (best > 0.f) break;
     const float wi = a.pgap == 2 ? (float)(it + 1) : (a.pgap == 3 ? (2 * it >= a.iters ? 1.f : 0.f) : 1.f);
@@ -557,11 +570,12 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
           *m = mm;
           *v = vv;
           float nx = *x + a.lr_b * dk * (mm / c1) / (sqrtf(vv / c2) + 1e-8f);
-          if (a.beta_pos) nx = fmaxf(nx, 0.f);
+          if (a.beta_pos || a.feas) nx = fmaxf(nx, 0.f);
+          if (a.feas) nx = fminf(nx, 1.f);              // homogeneous: a box keeps the scale fixed
           *x = nx;
         }
       }
-    {
+    if (!a.feas) {
       const float g = og * (oA + oB);
       mt = b1c * mt + (1.f - b1c) * g;
       vt = b2c * vt + (1.f - b2c) * g * g;
@@ -574,23 +588,37 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
       vgp = b2c * vgp + (1.f - b2c) * gp * gp;
       mgm = b1c * mgm + (1.f - b1c) * gm;
       vgm = b2c * vgm + (1.f - b2c) * gm * gm;
-      S.gt[0][lane] = fmaxf(S.gt[0][lane] + a.lr_t * dk * (mgp / c1) / (sqrtf(vgp / c2) + 1e-8f), 0.f);
-      S.gt[1][lane] = fmaxf(S.gt[1][lane] + a.lr_t * dk * (mgm / c1) / (sqrtf(vgm / c2) + 1e-8f), 0.f);
+      const float gmax = a.feas ? 1.f : FLT_MAX;
+      S.gt[0][lane] = fminf(fmaxf(S.gt[0][lane] + a.lr_t * dk * (mgp / c1) / (sqrtf(vgp / c2) + 1e-8f), 0.f), gmax);
+      S.gt[1][lane] = fminf(fmaxf(S.gt[1][lane] + a.lr_t * dk * (mgm / c1) / (sqrtf(vgm / c2) + 1e-8f), 0.f), gmax);
     }
     dk *= a.decay;
     wsync();
   }
-  if (lane == 0) a.t[r] = a.iters > 0 ? tbest : tc;
+  if (lane == 0 && !a.feas) a.t[r] = a.iters > 0 ? tbest : tc;
   const float tf = a.iters > 0 ? tbest : tc;
   if (a.iters > 0 && lane < n0) {      // the kept (best) tie multipliers
     S.gt[0][lane] = gbp;
     S.gt[1][lane] = gbm;
-    if (my_ra) {
+    if (my_ra && !a.feas) {
       gio[lane] = gbp;
       gio[n0 + lane] = gbm;
     }
   }
   wsync();
+  if (a.feas) {
+    // rigorous value of the phase constraints' Lagrangian at the pass's best multipliers: > 0 proves
+    // that no point of the (relaxed) region satisfies every fixed phase -- the node is closed
+    const float* fp = a.iters > 0 ? fbest : cur;
+    double eA = 0, eB = 0;
+    const double kA = bwd<double, true, true, WTL>(nd, Wf, Wt, S, 0, 0.0, fp, fp + 2 * NH, -1, 0, S.cf[0], &eA,
+                                                   nullptr);
+    const double kB = bwd<double, true, true, WTL>(nd, Wf, Wt, S, 1, 0.0, fp + NH, fp + 3 * NH, -1, 0, S.cf[1], &eB,
+                                                   nullptr);
+    const double Bf = conc<double, true, false>(nd, S, N, S.cf[0], S.cf[1], kA, kB, eA + eB);
+    if (lane == 0 && Bf > 0.0) a.bound[r] = __builtin_inf();
+    return;
+  }
 
   // ---- rigorous fp64 bound at the kept parameters
   double eA = 0, eB = 0;

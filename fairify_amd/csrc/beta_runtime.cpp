@@ -90,7 +90,7 @@ class BetaRuntime {
     }
     if (batch_ <= 0) throw std::invalid_argument("beta runtime: batch_nodes must be > 0");
     const size_t B = (size_t)batch_;
-    skip_.ensure(B); scratch_.ensure(B * 12 * nh_); bound_.ensure(B); split_.ensure(B);
+    skip_.ensure(B); scratch_.ensure(B * 16 * nh_); bound_.ensure(B); split_.ensure(B);
     xstar_.ensure(B * n0_); xpstar_.ensure(B * n0_); binit_.ensure(2 * B);
     rlo_.ensure(2 * B * n0_); rhi_.ensure(2 * B * n0_); rpart_.ensure(2 * B);
     olb_.ensure(2 * B); oub_.ensure(2 * B); infeas_.ensure(2 * B);
@@ -145,6 +145,7 @@ class BetaRuntime {
     const int lookahead = cfg["lookahead"].cast<int>(), beta_pos = cfg["beta_pos"].cast<int>();
     const int stall = cfg["stall"].cast<int>(), pgap = cfg["pgap"].cast<int>();
     const int warm_beta = cfg["warm_beta"].cast<int>(), tighten = cfg["tighten"].cast<int>();
+    const int feas_iters = cfg.contains("feas_iters") ? cfg["feas_iters"].cast<int>() : 0;
     box_lo_ = box_lo.data();
     box_hi_ = box_hi.data();
     status_.ensure(P); nodes_.ensure(P); probed_.ensure(P); part_closed_.ensure(P);
@@ -204,7 +205,7 @@ class BetaRuntime {
           bckl(fa_bb_count_launch(a, st), "beta skip");          // a.count = 0: this slice's skip flags
           if (!root && tighten) tighten_slice(a, st);
           bound_slice(a, cur, s, nb, root ? root_iters : iters, lr_a * sc, lr_b * sc, lr_t * sc, decay, lookahead,
-                      beta_pos, stall, pgap, st);
+                      beta_pos, stall, pgap, st, root ? 0 : feas_iters, lr_a, lr_b, lr_t);
           bckl(fa_bb_cand_launch(a, st), "beta cand");
           screen_slice(nb, st);
           bckl(fa_bb_split_launch(a, st), "beta split");
@@ -325,7 +326,8 @@ class BetaRuntime {
   }
 
   void bound_slice(const BetaPoolArgs& pa, int cur, long long s, int nb, int iters, float lr_a, float lr_b,
-                   float lr_t, float decay, int lookahead, int beta_pos, int stall, int pgap, hipStream_t st) {
+                   float lr_t, float decay, int lookahead, int beta_pos, int stall, int pgap, hipStream_t st,
+                   int feas_iters, float flr_a, float flr_b, float flr_t) {
     Pool& c = pool_[cur];
     const size_t sn = (size_t)s;
     BetaArgs a;
@@ -358,6 +360,15 @@ class BetaRuntime {
     a.skip = skip_.p;
     const int rc = fa_beta_launch(net_, a, st);
     if (rc != 0) throw std::runtime_error("fa_beta_kernel launch failed, code " + std::to_string(rc));
+    if (feas_iters > 0) {
+      // the infeasibility pass on the nodes left open (phase constraints' Lagrangian alone): closes the
+      // empty regions the verified LP detects as infeasible; only bound_ can change
+      a.feas = 1;
+      a.iters = feas_iters;
+      a.lr_a = flr_a; a.lr_b = flr_b; a.lr_t = flr_t;     // a fresh optimisation: the roots' step sizes
+      const int rf = fa_beta_launch(net_, a, st);
+      if (rf != 0) throw std::runtime_error("fa_beta_kernel (feas) launch failed, code " + std::to_string(rf));
+    }
   }
 
   void screen_slice(int nb, hipStream_t st) {

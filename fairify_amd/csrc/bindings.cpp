@@ -551,6 +551,7 @@ PYBIND11_MODULE(_C, m) {
     a.beta_pos = beta_pos;
     a.stall = stall & 1;        // bit 1: primal-gap branching (ops/hip.py:beta_level)
     a.pgap = (stall >> 1) & 3;
+    a.feas = (stall >> 3) & 1;  // bit 3: the infeasibility pass (scratch [R, 16, NH])
     a.bound = P<double>(bound);
     a.split = P<int>(split);
     a.xstar = P<float>(xstar);

@@ -24,6 +24,7 @@ same search (the objective's sign per node).  CPU tests pin verdicts to brute-fo
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, replace
 from typing import Optional
@@ -78,6 +79,12 @@ class BetaConfig:
     native: bool = True              # HIP device: the level loop in the native runtime (csrc/beta_runtime.cpp,
     #                                  device-resident pool / budgets / probe); FAIRIFY_TORCH_BETA=1 or the
     #                                  experiments (lpgap, input_every, merge_orient off): this module's loop
+    feas_iters: int = int(os.environ.get("FAIRIFY_BETA_FEAS", "64"))
+    #                                  > 0: children left open after their optimisation get an infeasibility
+    #                                  pass of this many steps (the phase constraints' Lagrangian alone,
+    #                                  ops/beta.py:feasibility_ref) -- the verified LP closes most of its
+    #                                  tree as infeasible regions two or three phase splits deep
+    trees: tuple = ()                # experiment: only the trees (ordered-pair row, orientation) listed
     sign_prune: bool = True          # close the (pair, orientation) trees a per-value logit sign test settles
     #                                  before their roots are bounded
     merge_orient: bool = True        # relaxed: both orientations as roots of ONE search (per-node sign of
@@ -226,6 +233,13 @@ class BetaBaBSolver:
         pr = torch.from_numpy(pairs_np.astype(np.int64)).to(dev).repeat_interleave(O, dim=0).repeat(run.size, 1)
         osg = torch.tensor([1, -1][:O], dtype=torch.int8, device=dev).repeat(run.size * Pp)
         ia, ib = k * V + pr[:, 0], k * V + pr[:, 1]
+        self.stats["native"] = self._use_native(O)       # the loop this group runs on (tests / logs)
+        if cfg.trees:        # experiment: one tree at a time (tools/exp/beta_vs_lp.py)
+            jj = torch.arange(Pp, device=dev).repeat_interleave(O).repeat(run.size)
+            sel = torch.zeros_like(k, dtype=torch.bool)
+            for j_, o_ in cfg.trees:
+                sel |= (jj == j_) & (osg == o_)
+            k, pr, osg, ia, ib = k[sel], pr[sel], osg[sel], ia[sel], ib[sel]
         pre_closed = np.zeros(P, dtype=np.int32)
         if cfg.sign_prune:
             # per-value sign tests from the rows' rigorous logit bounds (the verified LP's shared sign
@@ -316,7 +330,9 @@ class BetaBaBSolver:
                                     cur["beA"], cur["beB"], cur["t"], cfg.root_iters if is_root else cfg.iters,
                                     cfg.lr_a * sc, cfg.lr_b * sc, cfg.lr_t * sc, cfg.decay, cfg.lookahead,
                                     cfg.beta_pos, rx, pgap=cfg.pgap_weights if cfg.branch == "pgap" else 0,
-                                    osg=cur["osg"] if O > 1 else None)
+                                    osg=cur["osg"] if O > 1 else None,
+                                    feas_iters=0 if is_root else cfg.feas_iters,
+                                    feas_lr=(cfg.lr_a, cfg.lr_b, cfg.lr_t))
             if empty is not None:
                 lev.bound = torch.where(empty, torch.full_like(lev.bound, float("inf")), lev.bound)
             closed = lev.bound >= 0
@@ -378,7 +394,6 @@ class BetaBaBSolver:
         return status, cex_x, cex_xp, nodes_np
 
     def _use_native(self, O: int) -> bool:
-        import os
 
         cfg = self.cfg
         return (self.be.hip and cfg.native and os.environ.get("FAIRIFY_TORCH_BETA") != "1"
@@ -415,7 +430,7 @@ class BetaBaBSolver:
                 "lr_b": float(cfg.lr_b), "lr_t": float(cfg.lr_t), "child_lr": float(cfg.child_lr),
                 "decay": float(cfg.decay), "lookahead": int(cfg.lookahead), "beta_pos": int(bool(cfg.beta_pos)),
                 "stall": 1, "pgap": int(cfg.pgap_weights) if cfg.branch == "pgap" else 0, "warm_beta": int(bool(cfg.warm_beta)),
-                "tighten": int(bool(cfg.tighten))}
+                "tighten": int(bool(cfg.tighten)), "feas_iters": int(cfg.feas_iters)}
 
         def confirm(parts: np.ndarray, buf: np.ndarray) -> np.ndarray:
             X = np.rint(buf[:, :n0]).astype(np.int64)
@@ -447,7 +462,6 @@ class BetaBaBSolver:
         self.stats["nodes"] = self.stats.get("nodes", 0) + int(stats["nodes"])
         if stats.get("probe_stop"):
             self.stats["probe_stop"] = self.stats.get("probe_stop", 0) + int(stats["probe_stop"])
-        self.stats["native"] = True
         return (np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes, dtype=np.int64))
 
     def _probe(self, pool, nodes_np, probed, probe_at: int, R0: int, tree_run, status, pre_closed=None) -> None:

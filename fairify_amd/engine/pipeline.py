@@ -155,6 +155,10 @@ class VerifyConfig:
                                          # 48 vs 33 of 200 at 1 024 nodes (a converged dual gives the
                                          # primal average its meaning)
     beta_lookahead: int = 8              # filtered look-ahead candidates per score list
+    beta_decay: float = float(os.environ.get("FAIRIFY_BETA_DECAY", "0.98"))
+                                         # step-size decay per optimisation step (BetaConfig.decay)
+    beta_feas_iters: int = int(os.environ.get("FAIRIFY_BETA_FEAS", "64"))
+                                         # infeasibility pass steps on open children (BetaConfig.feas_iters)
     beta_escalate_cap: int = int(os.environ.get("FAIRIFY_BETA_ESC_CAP", "0"))
                                          # networks the beta fixed pass runs on: cap the input-split
                                          # escalation budget at this (their residue goes to beta instead
@@ -304,7 +308,7 @@ def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes,
     kw = {}
     if cfg is not None:
         kw = dict(branch=cfg.beta_branch, iters=cfg.beta_iters, root_iters=max(200, 3 * cfg.beta_iters),
-                  lookahead=cfg.beta_lookahead)
+                  lookahead=cfg.beta_lookahead, decay=cfg.beta_decay, feas_iters=cfg.beta_feas_iters)
     bs = BetaBaBSolver(be, q, BetaConfig(node_budget=budget, batch_nodes=min(batch_nodes, 32768),
                                          time_budget=time_budget, probe_levels=probe_levels, **kw),
                        **({"timer": tm} if tm is not None else {}))

@@ -240,19 +240,21 @@ class Backend:
 
     def beta_level(self, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t, iters: int,
                    lr_a: float, lr_b: float, lr_t: float, decay: float = 1.0, lookahead: int = 0,
-                   beta_pos: bool = True, rx=None, stall: bool = True, pgap: int = 0, osg=None):
+                   beta_pos: bool = True, rx=None, stall: bool = True, pgap: int = 0, osg=None,
+                   feas_iters: int = 0, feas_lr=None):
         """One beta-CROWN BaB level (ops/beta.py): optimises the rows' (alpha, beta, t) IN PLACE and
         returns their rigorous fp64 bounds, branching decisions and concretising vertices."""
         if self.hip:
             from . import hip
 
             return hip.beta_level(self, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t,
-                                  iters, lr_a, lr_b, lr_t, decay, lookahead, beta_pos, rx, stall, pgap, osg)
+                                  iters, lr_a, lr_b, lr_t, decay, lookahead, beta_pos, rx, stall, pgap, osg,
+                                  feas_iters, feas_lr)
         from . import beta
 
         return beta.level_ref([w.float() for w in self.ws], [b.float() for b in self.bs], self.widths[:-1], lo, hi,
                               pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t, iters, lr_a, lr_b,
-                              lr_t, decay, lookahead, beta_pos, rx, stall, pgap, osg)
+                              lr_t, decay, lookahead, beta_pos, rx, stall, pgap, osg, feas_iters, feas_lr)
 
     # ----------------------------------------------------------------------------- BaB node test
     def pair_certify(self, res_x, res_xp, xlo, xhi, xplo, xphi, pairs, values, pa, shared, relaxed):

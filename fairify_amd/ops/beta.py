@@ -149,7 +149,7 @@ def _forward_lin(ws, bs, x, LB, rec, al, hs=None):
 
 
 def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t, rig: bool, need_lin: bool = True,
-             rx=None, osg=None):
+             rx=None, osg=None, obj: float = 1.0):
     """The coupled bound of rows R at the given parameters (per-layer lists), in the dtype of
     ``ws``.  ``rig``: fp64 with every rounding term subtracted (the sound bound).
 
@@ -180,7 +180,7 @@ def evaluate(ws, bs, lo, hi, pa, va, vb, bA, bB, phA, phB, alA, alB, beA, beB, t
     hmB = torch.maximum(loB.abs(), hiB.abs())
     hmA[:, pa] = va.abs().to(dt)
     hmB[:, pa] = vb.abs().to(dt)
-    og = torch.ones_like(t) if osg is None else osg.to(t.dtype)
+    og = (torch.ones_like(t) if osg is None else osg.to(t.dtype)) * obj    # obj = 0: constraints only
     cA, kA, eA, rA = _backward(ws, bs, bA[0], bA[1], phA, alA, beA, og * t, hmA, rig)
     cB, kB, eB, rB = _backward(ws, bs, bB[0], bB[1], phB, alB, beB, -og * (1 - t), hmB, rig)
     pA = cA[:, pa] * va.to(dt)
@@ -319,6 +319,69 @@ def primal_gap_scores(zsum, hsum, n, lb, ub, ph):
     return torch.where(un & (n[:, None] > 0), gap, torch.zeros_like(gap))
 
 
+def feasibility_ref(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, t, iters: int,
+                    lr_a: float, lr_b: float, lr_t: float, decay: float, rx, osg, run) -> torch.Tensor:
+    """[R] bool: rows whose phase region is proven EMPTY (the kernel's ``feas`` pass).
+
+    The Lagrangian of the fixed phases alone, ``min over the relaxed region of -sum_j beta_j s_j z_j``
+    (plus the tau tie's multipliers on relaxed rows), is <= 0 whenever some point satisfies every
+    phase; a rigorous value > 0 (Farkas) proves no point does -- the LP-BaB closes such nodes as
+    infeasible after two or three phase splits, where the objective's Lagrangian (weight 1 on the
+    logits) would need unboundedly large multipliers.  The value is positively homogeneous in the
+    multipliers, so they live in [0, 1]; projected Adam from 0.5 on the fixed neurons, the slopes
+    from the main pass's best, objective weight 0."""
+    R = lo.shape[0]
+    dev = lo.device
+    L32 = lambda v: _layers(v, widths)  # noqa: E731
+    bA32, bB32 = (L32(lbA), L32(ubA)), (L32(lbB), L32(ubB))
+    pA, pB = L32(phA), L32(phB)
+    half = torch.full_like(alA, 0.5)
+    cur = {"alA": alA.clone(), "alB": alB.clone(), "beA": torch.where(phA != 0, half, torch.zeros_like(alA)),
+           "beB": torch.where(phB != 0, half, torch.zeros_like(alB))}
+    tie = rx is not None and len(rx) > 3 and rx[4] is not None
+    if tie:
+        cur["gP"] = torch.zeros_like(rx[4])
+        cur["gM"] = torch.zeros_like(rx[5])
+    rxc = lambda c: rx if not tie else (rx[0], rx[1], rx[2], rx[3], c["gP"], c["gM"])  # noqa: E731
+    best = torch.full((R,), -float("inf"), dtype=torch.float32, device=dev)
+    bestp = {k: v.clone() for k, v in cur.items()}
+    m = {k: torch.zeros_like(v) for k, v in cur.items()}
+    vv = {k: torch.zeros_like(v) for k, v in cur.items()}
+    act = run.clone()
+    b1, b2, eps = 0.9, 0.999, 1e-8
+    for it in range(iters):
+        ev = evaluate(ws32, bs32, lo, hi, pa, va, vb, bA32, bB32, pA, pB, L32(cur["alA"]), L32(cur["alB"]),
+                      L32(cur["beA"]), L32(cur["beB"]), t, rig=False, rx=rxc(cur), osg=osg, obj=0.0)
+        Bv, g = ev["B"], ev["g"]
+        imp = act & (Bv > best)
+        best = torch.where(imp, Bv, best)
+        for k in cur:
+            bestp[k] = torch.where(imp[:, None], cur[k], bestp[k])
+        act = act & ~(best > 0)
+        if not bool(act.any()):
+            break
+        c1 = 1 - b1 ** (it + 1)
+        c2 = 1 - b2 ** (it + 1)
+        dk = decay ** it
+        for k in cur:
+            gk = torch.cat(g[k], 1) if isinstance(g[k], list) else g[k]
+            m[k] = b1 * m[k] + (1 - b1) * gk
+            vv[k] = b2 * vv[k] + (1 - b2) * gk * gk
+            lr = (lr_a if k.startswith("al") else (lr_t if k.startswith("g") else lr_b)) * dk
+            x = cur[k] + lr * (m[k] / c1) / ((vv[k] / c2).sqrt() + eps)
+            x = x.clamp(0, 1)
+            cur[k] = torch.where(act[:, None], x, cur[k])
+    fp = bestp if iters > 0 else cur
+    d = torch.float64
+    ws64 = [w.to(d) for w in ws32]
+    bs64 = [b.to(d) for b in bs32]
+    L64 = lambda v: _layers(v.to(d), widths)  # noqa: E731
+    ev = evaluate(ws64, bs64, lo.to(d), hi.to(d), pa, va.to(d), vb.to(d), (L64(lbA), L64(ubA)), (L64(lbB), L64(ubB)),
+                  pA, pB, L64(fp["alA"]), L64(fp["alB"]), L64(fp["beA"]), L64(fp["beB"]), t.to(d), rig=True,
+                  need_lin=False, rx=rxc(fp), osg=osg, obj=0.0)
+    return run & (ev["B"] > 0)
+
+
 def clamp_bounds(LB: torch.Tensor, UB: torch.Tensor, ph: torch.Tensor):
     """Phase-clamped pre-activation bounds [R, NH] and the rows whose region they prove empty."""
     lb = torch.where(ph > 0, LB.clamp(min=0), LB)
@@ -329,7 +392,7 @@ def clamp_bounds(LB: torch.Tensor, UB: torch.Tensor, ph: torch.Tensor):
 def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t,
               iters: int, lr_a: float, lr_b: float, lr_t: float, decay: float = 1.0,
               lookahead: int = 0, beta_pos: bool = True, rx=None, stall: bool = True, pgap: int = 0,
-              osg=None) -> BetaLevel:
+              osg=None, feas_iters: int = 0, feas_lr=None) -> BetaLevel:
     """One BaB level of rows R (the HIP kernel's semantics, csrc/beta.hip): ``iters`` projected-Adam
     steps in fp32 from the rows' current (alpha, beta, t) -- updated IN PLACE to the best iterate --
     then the rigorous fp64 bound, the branching decision and x* at those parameters.
@@ -429,6 +492,14 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
                   L64(beB), t.to(d), rig=True, rx=rxc(par), osg=osg)
     B, lin, xs, coef = ev["B"], ev["lin"], ev["xs"], ev["coef"]
     B = torch.where(infeas, torch.full_like(B, float("inf")), B)
+    if feas_iters > 0:
+        # the infeasibility pass (the kernel's second launch): nodes left open with a fixed phase
+        fixed = (phA != 0).any(1) | (phB != 0).any(1)
+        run = (B < 0) & fixed & ~infeas
+        if bool(run.any()):
+            emp = feasibility_ref(ws32, bs32, widths, lo, hi, pa, va, vb, lbA, ubA, lbB, ubB, phA, phB, alA, alB, t,
+                                  feas_iters, *(feas_lr or (lr_a, lr_b, lr_t)), decay, rx, osg, run)
+            B = torch.where(emp, torch.full_like(B, float("inf")), B)
     sc = torch.cat([_scores(bA, lin[0], pA, alA64), _scores(bB, lin[1], pB, alB64)], 1)
     if pgap and zsum is not None:
         sc = primal_gap_scores(zsum, hsum, nsum, torch.cat([lbA, lbB], 1), torch.cat([ubA, ubB], 1),

@@ -614,7 +614,8 @@ def _beta_wt(be) -> torch.Tensor:
 
 
 def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, beA, beB, t, iters, lr_a, lr_b, lr_t,
-               decay=1.0, lookahead=0, beta_pos=True, rx=None, stall=True, pgap=False, osg=None):
+               decay=1.0, lookahead=0, beta_pos=True, rx=None, stall=True, pgap=False, osg=None, feas_iters=0,
+               feas_lr=None):
     """One beta-CROWN BaB level on the device (``fa_beta_kernel``, csrc/beta.hip): the rows'
     (alpha, beta, t) are optimised IN PLACE (kept at the best iterate) and their rigorous fp64
     bounds, branching decisions, concretising vertices and child multipliers returned
@@ -641,7 +642,7 @@ def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, b
     if tuple(t.shape) != (R,) or t.dtype != torch.float32 or not t.is_contiguous():
         raise ValueError("t: expected contiguous float32 [R]")
     par = torch.stack([alA, alB, beA, beB], 1).contiguous()          # [R, 4, NH]
-    scratch = torch.empty(R, 12, NH, **f32)
+    scratch = torch.empty(R, 16 if feas_iters > 0 else 12, NH, **f32)
     bound = torch.empty(R, dtype=torch.float64, device=dev)
     split = torch.empty(R, dtype=torch.int32, device=dev)
     xstar = torch.empty(R, n0, **f32)
@@ -661,15 +662,19 @@ def beta_level(be, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, phB, alA, alB, b
             gt = torch.stack([rx[4], rx[5]], 1).contiguous()       # [R, 2, n0]
     osg_c = None if osg is None else _c(osg, torch.int8, (R,), "osg")
     if R:
-        rc = ext().beta_level(_net(be), be.flat.data_ptr(), _beta_wt(be).data_ptr(), R, [int(d) for d in pa],
-                              lo_c.data_ptr(), hi_c.data_ptr(), va_c.data_ptr(), vb_c.data_ptr(),
-                              *[x.data_ptr() for x in bnd], pA.data_ptr(), pB.data_ptr(), par.data_ptr(),
-                              t.data_ptr(), scratch.data_ptr(), int(iters), float(lr_a), float(lr_b), float(lr_t),
-                              float(decay), int(lookahead), int(bool(beta_pos)),
-                              int(bool(stall)) | (int(pgap) << 1), bound.data_ptr(),
-                              split.data_ptr(),
-                              xstar.data_ptr(), binit.data_ptr(), int(ramask), _ptr(plo_c), _ptr(phi_c),
-                              xpstar.data_ptr(), _ptr(gt), float(tau), _ptr(osg_c), _stream(dev))
+        def launch(n_it, flags, lra, lrb, lrt):
+            return ext().beta_level(_net(be), be.flat.data_ptr(), _beta_wt(be).data_ptr(), R, [int(d) for d in pa],
+                                    lo_c.data_ptr(), hi_c.data_ptr(), va_c.data_ptr(), vb_c.data_ptr(),
+                                    *[x.data_ptr() for x in bnd], pA.data_ptr(), pB.data_ptr(), par.data_ptr(),
+                                    t.data_ptr(), scratch.data_ptr(), int(n_it), float(lra), float(lrb), float(lrt),
+                                    float(decay), int(lookahead), int(bool(beta_pos)), flags, bound.data_ptr(),
+                                    split.data_ptr(), xstar.data_ptr(), binit.data_ptr(), int(ramask), _ptr(plo_c),
+                                    _ptr(phi_c), xpstar.data_ptr(), _ptr(gt), float(tau), _ptr(osg_c), _stream(dev))
+
+        rc = launch(iters, int(bool(stall)) | (int(pgap) << 1), lr_a, lr_b, lr_t)
+        if rc == 0 and feas_iters > 0:
+            # the infeasibility pass (bit 3) on the nodes left open: only their bounds can change
+            rc = launch(feas_iters, 8, *(feas_lr or (lr_a, lr_b, lr_t)))
         if rc != 0:
             raise RuntimeError(f"fa_beta_kernel launch failed ({rc}): network not supported by the beta kernel")
         if gt is not None:

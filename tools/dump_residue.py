@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--weights", default="random", help="random | zoo (trained weights)")
     ap.add_argument("--big", action="store_true",
                     help="the big-grid schedule of tools/baseline_configs.py (escalation to 8 192 nodes)")
+    ap.add_argument("--cfg", default="", help="VerifyConfig overrides 'key=value,...'")
     args = ap.parse_args()
     import torch
 
@@ -48,6 +49,14 @@ def main():
                        escalate_probation=((2048, 768), (4096, 768)) if args.big else
                        ((2048, 768), (4096, 768), (8192, 768), (16384, 1024)),
                        relu_budget=1024, relu_max_width=16, relu_escalate_cap=2048)
+    if args.cfg:      # VerifyConfig overrides 'key=value,...'
+        from dataclasses import replace as _rp
+
+        kv = {}
+        for item in filter(None, args.cfg.split(",")):
+            k, v = item.split("=")
+            kv[k] = type(getattr(cfg, k))(v)
+        cfg = _rp(cfg, **kv)
     os.makedirs(args.out, exist_ok=True)
     for name in args.models.split(","):
         m = get_model(name, weights=args.weights, seed=0)
@@ -58,8 +67,9 @@ def main():
             torch.cuda.synchronize()
         c = recs.cols
         v = c["verdict"]
-        np.savez(os.path.join(args.out, f"{name}.npz"), grid_id=c["grid_id"], verdict=v.astype(str),
-                 stage=c["stage"].astype(str), nodes=c["nodes"])
+        np.savez_compressed(os.path.join(args.out, f"{name}.npz"), grid_id=c["grid_id"], verdict=v.astype(str),
+                            stage=c["stage"].astype(str), nodes=c["nodes"],
+                            stage_nodes=c.get("stage_nodes", np.zeros((len(v), 0), np.int64)))
         print(f"{name}: {len(ids)} partitions in {time.time() - t0:.2f}s: sat {(v == 'sat').sum()} "
               f"unsat {(v == 'unsat').sum()} unknown {(v == 'unknown').sum()}", flush=True)
 

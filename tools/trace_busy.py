@@ -15,7 +15,8 @@ from collections import defaultdict
 
 MARK = "fa_trace_marker_kernel"
 rows = list(csv.DictReader(open(sys.argv[1])))
-iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].replace("(anonymous namespace)::", ""))
+            for r in rows)
 window = "--window" in sys.argv[2:]
 marks = [(s, e) for s, e, k in iv if k.startswith(MARK)]
 if window:
