@@ -23,11 +23,19 @@
 // nodes sharing one multiplier layout, which their per-node relaxation choices do not allow.
 #include <float.h>
 
+#include <algorithm>
+
 #include "args.h"
 
 namespace {
 
 constexpr double U64 = 1.1102230246251565e-16;   // 2^-53
+
+// waves per SIMD the register allocation targets (the kernel is latency bound: one wave64 per node,
+// dependent LDS / L2 round trips; at 186 VGPRs only 2 waves per SIMD fit)
+#ifndef FA_BETA_WPE
+#define FA_BETA_WPE 3
+#endif
 
 __device__ __forceinline__ double g64(int k) {    // Higham gamma_k in fp64, padded like ref.gamma
   const double ku = (k + 2) * U64;
@@ -197,13 +205,27 @@ __device__ T bwd(const NetDesc& nd, const float* Wf, const float* Wt, const Slab
     wsync();
     const float* wt = Wt + nd.w_off[l];
     for (int i = lane; i < win; i += 64) {
-      T acc = 0, aab = 0;
-      for (int j = 0; j < w; ++j) {
+      // four independent partial sums: the LDS reads of a chunk issue together instead of one
+      // dependent FMA (and its two LDS round trips) per multiplier (the rounding term covers any order)
+      T a0 = 0, a1 = 0, a2 = 0, a3 = 0, aab = 0;
+      int j = 0;
+      for (; j + 4 <= w; j += 4) {
+        const T w0 = (T)wt[j * win + i], w1 = (T)wt[(j + 1) * win + i];
+        const T w2 = (T)wt[(j + 2) * win + i], w3 = (T)wt[(j + 3) * win + i];
+        const T m0 = b1[j], m1 = b1[j + 1], m2 = b1[j + 2], m3 = b1[j + 3];
+        a0 += w0 * m0;
+        a1 += w1 * m1;
+        a2 += w2 * m2;
+        a3 += w3 * m3;
+        if (RIG) aab += (tabs(w0) * tabs(m0) + tabs(w1) * tabs(m1)) + (tabs(w2) * tabs(m2) + tabs(w3) * tabs(m3));
+      }
+      for (; j < w; ++j) {
         const T wv = (T)wt[j * win + i];
         const T m = b1[j];
-        acc += wv * m;
+        a0 += wv * m;
         if (RIG) aab += tabs(wv) * tabs(m);
       }
+      const T acc = (a0 + a1) + (a2 + a3);
       b0[i] = acc;
       if (RIG) {
         const T hmx = l > 0 ? (T)fmaxf(ubv[nd.neuron_off[l - 1] + i], 0.f) : (T)S.hm[c][i];
@@ -313,8 +335,16 @@ __device__ T fwd(const NetDesc& nd, const float* Wf, const Slab& S, const Node& 
     const float* W = Wf + nd.w_off[l];
     const float* bias = Wf + nd.b_off[l];
     for (int j = lane; j < w; j += 64) {
-      T z = (T)bias[j];
-      for (int i = 0; i < win; ++i) z += (T)W[i * w + j] * h0[i];
+      T z0 = (T)bias[j], z1 = 0, z2 = 0, z3 = 0;
+      int i = 0;
+      for (; i + 4 <= win; i += 4) {
+        z0 += (T)W[i * w + j] * h0[i];
+        z1 += (T)W[(i + 1) * w + j] * h0[i + 1];
+        z2 += (T)W[(i + 2) * w + j] * h0[i + 2];
+        z3 += (T)W[(i + 3) * w + j] * h0[i + 3];
+      }
+      for (; i < win; ++i) z0 += (T)W[i * w + j] * h0[i];
+      const T z = (z0 + z1) + (z2 + z3);
       const int k = off + j;
       S.z[c][k] = (float)z;
       const int kind = S.kd[c][k];
@@ -346,7 +376,8 @@ __device__ T fwd(const NetDesc& nd, const float* Wf, const Slab& S, const Node& 
 }
 
 template <bool WTL>
-__global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FA_BETA_WPE))) void fa_beta_kernel(NetDesc nd,
+                                                                                           BetaArgs a) {
   extern __shared__ float smem[];
   const int L = nd.n_layers;
   const int NH = nd.n_hidden;
@@ -543,36 +574,37 @@ __global__ __launch_bounds__(512) void fa_beta_kernel(NetDesc nd, BetaArgs a) {
         const float z = S.z[c][k];
         const int kind = S.kd[c][k];
         const int p = S.ph[c][k];
-        // alpha
+        // all six words of this neuron's state first (L2 round trips in flight together), then the
+        // updates: alpha (projected to [0, 1]) and beta (>= 0; the infeasibility pass boxes it in [0, 1])
+        float* xa = cur + c * NH + k;
+        float* ma = mom + c * NH + k;
+        float* va_ = vel + c * NH + k;
+        float* xb = cur + (2 + c) * NH + k;
+        float* mb = mom + (2 + c) * NH + k;
+        float* vb_ = vel + (2 + c) * NH + k;
+        const float xa0 = *xa, ma0 = *ma, va0 = *va_, xb0 = *xb, mb0 = *mb, vb0 = *vb_;
         {
           const float g = kind == 2 ? S.lam[c][k] * z : 0.f;
-          float* x = cur + c * NH + k;
-          float* m = mom + c * NH + k;
-          float* v = vel + c * NH + k;
-          const float mm = b1c * *m + (1.f - b1c) * g;
-          const float vv = b2c * *v + (1.f - b2c) * g * g;
-          *m = mm;
-          *v = vv;
-          *x = fminf(fmaxf(*x + a.lr_a * dk * (mm / c1) / (sqrtf(vv / c2) + 1e-8f), 0.f), 1.f);
+          const float mm = b1c * ma0 + (1.f - b1c) * g;
+          const float vv = b2c * va0 + (1.f - b2c) * g * g;
+          *ma = mm;
+          *va_ = vv;
+          *xa = fminf(fmaxf(xa0 + a.lr_a * dk * (mm / c1) / (sqrtf(vv / c2) + 1e-8f), 0.f), 1.f);
         }
-        // beta
         {
-          float* x = cur + (2 + c) * NH + k;
           float g = 0.f;
           if (p != 0) {
-            const float e = *x < 0.f ? (p > 0 ? S.ub[c][k] : S.lb[c][k]) : 0.f;
+            const float e = xb0 < 0.f ? (p > 0 ? S.ub[c][k] : S.lb[c][k]) : 0.f;
             g = -(float)p * (z - e);
           }
-          float* m = mom + (2 + c) * NH + k;
-          float* v = vel + (2 + c) * NH + k;
-          const float mm = b1c * *m + (1.f - b1c) * g;
-          const float vv = b2c * *v + (1.f - b2c) * g * g;
-          *m = mm;
-          *v = vv;
-          float nx = *x + a.lr_b * dk * (mm / c1) / (sqrtf(vv / c2) + 1e-8f);
+          const float mm = b1c * mb0 + (1.f - b1c) * g;
+          const float vv = b2c * vb0 + (1.f - b2c) * g * g;
+          *mb = mm;
+          *vb_ = vv;
+          float nx = xb0 + a.lr_b * dk * (mm / c1) / (sqrtf(vv / c2) + 1e-8f);
           if (a.beta_pos || a.feas) nx = fmaxf(nx, 0.f);
           if (a.feas) nx = fminf(nx, 1.f);              // homogeneous: a box keeps the scale fixed
-          *x = nx;
+          *xb = nx;
         }
       }
     if (!a.feas) {
@@ -829,28 +861,33 @@ extern "C" size_t fa_beta_slab_floats(const NetDesc& nd) {
 }
 
 // Launch configuration: waves per workgroup and whether the transposed weights fit in LDS next to
-// the forward copy, chosen for two workgroups per CU (<= 80 KB) when possible.  Returns 0 on
-// success, -1 when the network cannot run here (inputs > 64, no hidden layer, too many PA dims,
-// the weights alone over the LDS budget).
+// the forward copy, chosen to maximise the waves resident per CU -- the kernel is latency bound, so
+// resident waves are what hides its LDS / L2 round trips: min(workgroups per CU by LDS x waves per
+// workgroup, FA_BETA_WPE x 4 SIMDs by registers); ties keep the LDS-staged transposed weights.
+// Returns 0 on success, -1 when the network cannot run here (inputs > 64, no hidden layer, too many
+// PA dims, the weights alone over the LDS budget).
 extern "C" int fa_beta_config(const NetDesc& nd, int* wpb, int* wtl, size_t* bytes) {
   if (nd.dims[0] > 64 || nd.n_layers < 2 || nd.n_hidden <= 0) return -1;
   const int L = nd.n_layers;
   const size_t tot = (size_t)nd.b_off[L - 1] + nd.dims[L];
   const size_t tot4 = (tot + 3) & ~(size_t)3;
   const size_t slab = fa_beta_slab_floats(nd) * 4;
-  const size_t caps[2] = {80 * 1024, 160 * 1024 - 1024};
-  for (size_t cap : caps)
-    for (int w : {8, 4, 2, 1})
-      for (int t : {1, 0}) {
-        const size_t b = tot4 * 4 * (t ? 2 : 1) + w * slab;
-        if (b <= cap) {
-          *wpb = w;
-          *wtl = t;
-          *bytes = b;
-          return 0;
-        }
+  const size_t lds_cu = 160 * 1024, cap = 160 * 1024 - 1024;
+  const int reg_waves = 4 * FA_BETA_WPE;
+  int best = 0;
+  for (int t : {1, 0})
+    for (int w : {8, 4, 2, 1}) {
+      const size_t b = tot4 * 4 * (t ? 2 : 1) + w * slab;
+      if (b > cap) continue;
+      const int per_cu = std::min((int)(lds_cu / b) * w, reg_waves);
+      if (per_cu > best) {
+        best = per_cu;
+        *wpb = w;
+        *wtl = t;
+        *bytes = b;
       }
-  return -1;
+    }
+  return best > 0 ? 0 : -1;
 }
 
 extern "C" int fa_beta_launch(const NetDesc& nd, BetaArgs a, hipStream_t stream) {
