@@ -151,14 +151,18 @@ class BetaRuntime {
     status_.ensure(P); nodes_.ensure(P); probed_.ensure(P); part_closed_.ensure(P);
     tree_cnt_.ensure(std::max(R0, 1)); tree_done_.ensure(std::max(R0, 1)); tree_part_.ensure(std::max(R0, 1));
     ensure_pool(0, std::max(R0, 1));
-    // staged host block: status | tree_part | closed0 (trees closed before the search: the probe's count)
+    // staged host block: status | tree_part | closed0 (trees closed before the search: the probe's
+    // count) | root tree ids 0 .. R0 - 1
     if (closed0.ndim() != 1 || closed0.shape(0) != P) throw std::invalid_argument("beta solve: closed0 shape");
     const size_t o_tp = (size_t)((P + 3) & ~3), o_c0 = o_tp + (size_t)R0 * sizeof(int);
-    const size_t sb = o_c0 + (size_t)P * sizeof(int);
+    const size_t o_ti = o_c0 + (size_t)P * sizeof(int);
+    const size_t sb = o_ti + (size_t)R0 * sizeof(int);
     hstage_.ensure(sb);
     std::memcpy(hstage_.p, status0.data(), P);
     std::memcpy(hstage_.p + o_tp, tree_part.data(), (size_t)R0 * sizeof(int));
     std::memcpy(hstage_.p + o_c0, closed0.data(), (size_t)P * sizeof(int));
+    int* tid = reinterpret_cast<int*>(hstage_.p + o_ti);
+    for (int k = 0; k < R0; ++k) tid[k] = k;
     stage_.ensure(sb);
     bck(hipMemcpyAsync(stage_.p, hstage_.p, sb, hipMemcpyHostToDevice, st), "cp stage");
     bck(hipMemcpyAsync(status_.p, stage_.p, P, hipMemcpyDeviceToDevice, st), "cp status");
@@ -171,6 +175,8 @@ class BetaRuntime {
     bck(hipMemsetAsync(tree_done_.p, 0, std::max(R0, 1), st), "memset tree_done");
     bck(hipMemsetAsync(counters_.p, 0, 4 * sizeof(int), st), "memset counters");   // [2]: probe stops
     copy_roots(roots, R0, st);
+    bck(hipMemcpyAsync(pool_[0].tree.p, stage_.p + o_ti, (size_t)R0 * sizeof(int), hipMemcpyDeviceToDevice, st),
+        "root tree ids");
     std::vector<int64_t> cex_x((size_t)P * n0_, 0), cex_xp((size_t)P * n0_, 0);
     std::vector<char> got(P, 0);
     int cur = 0;
@@ -408,12 +414,6 @@ class BetaRuntime {
     cp(p.ph.p, r[12], R * 2 * nh_, "root ph");
     cp(p.par.p, r[13], R * 4 * nh_ * sizeof(float), "root par");
     cp(p.t.p, r[14], R * sizeof(float), "root t");
-    // tree ids: root k is tree k
-    std::vector<int> ids(R0);
-    for (int k = 0; k < R0; ++k) ids[k] = k;
-    htree_.ensure(std::max<size_t>(R * sizeof(int), 4));
-    std::memcpy(htree_.p, ids.data(), R * sizeof(int));
-    bck(hipMemcpyAsync(p.tree.p, htree_.p, R * sizeof(int), hipMemcpyHostToDevice, st), "root tree");
   }
 
   void ensure_pool(int i, int need) {
@@ -527,7 +527,7 @@ class BetaRuntime {
   fa_mem::HostBuf hcount_buf_{true};   // coherent: the settle kernel writes the level counters
   int* hcount_ = nullptr;
   // pinned staging (released / regrown only after the stream synchronisation that retires its copy)
-  fa_mem::HostBuf hstage_, hout_, htree_;
+  fa_mem::HostBuf hstage_, hout_;
   fa_mem::HostBuf cand_host_{true};   // candidate records (coherent pinned, written by the split kernel)
 };
 

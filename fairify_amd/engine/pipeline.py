@@ -145,11 +145,16 @@ class VerifyConfig:
                                          # residue partitions of relaxed/BM for 21 s of its 60 s
                                          # (profiles/r5/s5_m/); a static rule, so verdicts stay
                                          # independent of how partitions are sharded
-    beta_branch: str = os.environ.get("FAIRIFY_BETA_BRANCH", "pgap")
+    beta_branch: str = os.environ.get("FAIRIFY_BETA_BRANCH", "auto")
                                          # BetaConfig.branch: "pgap" = the verified LP's primal-gap rule
                                          # at the averaged primal iterate (relaxed/BM BM-8 residue: 33 vs
                                          # 5 of 200 decided at 1 024 nodes, profiles/r6/), "kernel" =
-                                         # |lambda| x gap at the vertex x* (round 5)
+                                         # |lambda| x gap at the vertex x* (round 5); "auto": pgap with
+                                         # beta_iters steps for a binary PA (2 ordered pairs), kernel with
+                                         # 64 for a multi-valued one -- measured per query at the fixed
+                                         # pass's budget: relaxed/BM BM-8 17 866 vs 22 785 UNKNOWN (pgap /
+                                         # kernel), stress/AC AC-7 4 466 vs 4 668, but relaxed/AC AC-7
+                                         # (race, 20 pairs) 1 840 vs 1 755 at 27.3 vs 18.9 s (profiles/r6/)
     beta_iters: int = int(os.environ.get("FAIRIFY_BETA_ITERS", "128"))
                                          # optimisation steps per child node (root: x 3); 128 over 64:
                                          # 48 vs 33 of 200 at 1 024 nodes (a converged dual gives the
@@ -157,8 +162,11 @@ class VerifyConfig:
     beta_lookahead: int = 8              # filtered look-ahead candidates per score list
     beta_decay: float = float(os.environ.get("FAIRIFY_BETA_DECAY", "0.98"))
                                          # step-size decay per optimisation step (BetaConfig.decay)
-    beta_feas_iters: int = int(os.environ.get("FAIRIFY_BETA_FEAS", "64"))
+    beta_feas_iters: int = int(os.environ.get("FAIRIFY_BETA_FEAS", "0"))
                                          # infeasibility pass steps on open children (BetaConfig.feas_iters)
+                                         # in the fixed pass: off -- at its 128-node budget with the probe
+                                         # it decided nothing more (relaxed/BM BM-8 17 866 vs 18 234 UNKNOWN,
+                                         # profiles/r6/); the anytime rounds (growing budgets) run 64 steps
     beta_escalate_cap: int = int(os.environ.get("FAIRIFY_BETA_ESC_CAP", "0"))
                                          # networks the beta fixed pass runs on: cap the input-split
                                          # escalation budget at this (their residue goes to beta instead
@@ -298,7 +306,7 @@ def _milp_round(be, mlp, q, unk, lo_np, hi_np, values_np, pairs_np, limit, worke
 
 
 def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes, status, stage, cex_x, cex_xp, nodes,
-                tm=None, probe_levels: int = 0, cfg=None):
+                tm=None, probe_levels: int = 0, cfg=None, anytime: bool = False):
     """beta-CROWN BaB (engine/beta_bab.py) on the partitions ``unk``: decided verdicts (sound SAT /
     UNSAT) written into the stage arrays; returns how many it decided.  ``probe_levels``: a partition
     gives up once it has expanded 2 x that many nodes per pair tree with none of its trees closed
@@ -307,8 +315,15 @@ def _beta_round(be, q, mlp, unk, lo_np, hi_np, budget, time_budget, batch_nodes,
 
     kw = {}
     if cfg is not None:
-        kw = dict(branch=cfg.beta_branch, iters=cfg.beta_iters, root_iters=max(200, 3 * cfg.beta_iters),
-                  lookahead=cfg.beta_lookahead, decay=cfg.beta_decay, feas_iters=cfg.beta_feas_iters)
+        branch, iters = cfg.beta_branch, cfg.beta_iters
+        if branch == "auto":
+            from .bab import _pa_table
+
+            _, pairs = _pa_table(q, lo_np[unk[:1]], hi_np[unk[:1]])
+            branch, iters = ("pgap", cfg.beta_iters) if pairs.shape[0] <= 2 else ("kernel", 64)
+        kw = dict(branch=branch, iters=iters, root_iters=max(200, 3 * iters),
+                  lookahead=cfg.beta_lookahead, decay=cfg.beta_decay,
+                  feas_iters=max(cfg.beta_feas_iters, 64) if anytime else cfg.beta_feas_iters)
     bs = BetaBaBSolver(be, q, BetaConfig(node_budget=budget, batch_nodes=min(batch_nodes, 32768),
                                          time_budget=time_budget, probe_levels=probe_levels, **kw),
                        **({"timer": tm} if tm is not None else {}))
@@ -766,7 +781,7 @@ def _verify_group(be: Backend, mlp: MLP, q: ResolvedQuery, ids: np.ndarray, lo_n
                         # residue) the other stages keep their time
                         with tm("beta"):
                             ndec = _beta_round(be, q, mlp, unk, lo_np, hi_np, b_budget, 0.5 * left, cfg.batch_nodes,
-                                               status, stage, cex_x, cex_xp, nodes, tm, cfg=cfg)
+                                               status, stage, cex_x, cex_xp, nodes, tm, cfg=cfg, anytime=True)
                         if ndec < cfg.anytime_min_yield * unk.size:
                             beta_live = False
                     unk = np.nonzero((status == UNKNOWN) & ~forced)[0]

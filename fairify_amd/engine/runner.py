@@ -274,7 +274,7 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
                max_partitions: Optional[int] = None, resume: bool = False, seed: int = 0,
                accuracy: bool = True, verbose: bool = True, escalate: int = 1,
                concurrency: int = 1, anytime_budget: Optional[float] = None,
-               metrics_csv: Optional[bool] = None, balance: str = "queue") -> List[Dict]:
+               metrics_csv: Optional[bool] = None, balance: str = "queue", start_partition: int = 0) -> List[Dict]:
     """``escalate`` > 1: every round's UNKNOWN partitions are re-distributed over all ranks and
     retried with ``escalate`` x the node budget (residual work stealing).  ``concurrency`` > 1:
     each rank verifies that many chunks of a round at once, one host thread + HIP stream each
@@ -298,6 +298,10 @@ def run_preset(preset: Preset, models: Optional[List[str]] = None, weights: str 
     grid = preset.grid(seed=seed)
     q = preset.resolved()
     order = processing_order(grid, seed=seed)
+    if start_partition:
+        # a contiguous block of the seeded order (one part of a run split over calls / jobs; the parts
+        # of a model partition its grid and their Table-V counts add up)
+        order = order[int(start_partition):]
     total = len(order) if max_partitions is None else min(len(order), int(max_partitions))
     cfg = cfg or VerifyConfig(sim_size=preset.sim_size, soft_timeout=preset.soft_timeout,
                               hard_timeout=preset.hard_timeout, heuristic_p=preset.heuristic_p, seed=seed)

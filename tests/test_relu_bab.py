@@ -165,8 +165,10 @@ def test_pipeline_relu_stage_and_anytime_rounds():
     base = dict(sim_size=200, node_budget=64, heuristic=False, smt_backend="none")
     off = verify_chunk(be, m, q, grid, ids, VerifyConfig(relu_budget=0, **base))
     on = verify_chunk(be, m, q, grid, ids, VerifyConfig(relu_budget=256, **base))
+    # (anytime_beta=0: the beta rounds, first in every anytime round, would take the relu rounds' share of
+    # the wall budget on a loaded host)
     wide = verify_chunk(be, m, q, grid, ids, VerifyConfig(relu_budget=256, relu_max_width=1, anytime_seconds=30,
-                                                          **base))
+                                                          anytime_beta=0, **base))
     for r in (on, wide):
         assert (r.cols["stage"] == "relu").sum() > 10
         assert (r.cols["verdict"] != "unknown").sum() > (off.cols["verdict"] != "unknown").sum()

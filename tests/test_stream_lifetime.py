@@ -36,7 +36,7 @@ def _host_operands(src: str):
     return out
 
 
-RUNTIMES = ("bab_runtime.cpp", "relu_runtime.cpp")
+RUNTIMES = ("bab_runtime.cpp", "relu_runtime.cpp", "beta_runtime.cpp")
 
 
 def _pinned_names(src: str):

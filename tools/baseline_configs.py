@@ -68,7 +68,7 @@ def run_group(args) -> None:
     for name in names:
         pre = presets.get(name)
         models = list(pre.models) if not args.models else args.models.split(",")
-        out = os.path.join(args.out, name.replace("/", "_"))
+        out = os.path.join(args.out, name.replace("/", "_") + (f"@{args.start}" if args.start else ""))
         os.makedirs(out, exist_ok=True)
         # per-partition CSVs (MBs per model) go to scratch: gpurun copies back <= 64 MiB of gpurun_out
         scratch = os.path.join(args.scratch, name.replace("/", "_"))
@@ -98,7 +98,8 @@ def run_group(args) -> None:
             cur["what"], cur["t"] = f"{name} {m}", time.time()
             r = run_preset(pre, models=[m], weights=weights[m], out_dir=os.path.join(scratch, m), cfg=cfg, info=info,
                            seed=0, accuracy=False, verbose=False, concurrency=4,
-                           anytime_budget=anytime or None, max_partitions=args.max_partitions)
+                           anytime_budget=anytime or None, max_partitions=args.max_partitions,
+                           start_partition=args.start)
             for row in r:
                 row["weights"] = weights[m]
                 rows.append(row)
@@ -108,6 +109,7 @@ def run_group(args) -> None:
             # after every model: a run cut by its time limit keeps the finished models
             with open(os.path.join(out, "summary.json"), "w") as f:
                 json.dump({"preset": name, "models": rows, "head": args.head, "wall_s": round(time.time() - t0, 2),
+                           "start": args.start, "max_partitions": args.max_partitions,
                            "anytime_budget_s": anytime, "heuristic": False, "smt": cfg.smt_backend,
                            "escalate_budget": cfg.escalate_budget}, f, indent=2)
         print(f"[{name}] done in {time.time() - t0:.1f}s", flush=True)
@@ -117,11 +119,31 @@ def run_group(args) -> None:
 def report(root: str) -> None:
     rows = []
     heads = set()
+    parts = {}
     for path in sorted(glob.glob(os.path.join(root, "*", "summary.json"))):
         s = json.load(open(path))
         heads.add(s.get("head"))
         for r in s["models"]:
+            if s.get("start") or s.get("max_partitions"):
+                # one part of a model's grid (--start / --max-partitions): counts and walls add up
+                key = (s["preset"], r["model"])
+                if key not in parts:
+                    parts[key] = (s["preset"], s.get("anytime_budget_s", 0), dict(r), [s.get("start", 0)])
+                    continue
+                m = parts[key][2]
+                for k in ("SAT", "UNSAT", "UNK", "UNSAT_heuristic", "UNSAT_sound", "#P"):
+                    if k in r:
+                        m[k] = m.get(k, 0) + r[k]
+                m["wall_s"] = round(float(m.get("wall_s", 0)) + float(r.get("wall_s", 0)), 3)
+                parts[key][3].append(s.get("start", 0))
+                continue
             rows.append((s["preset"], s.get("anytime_budget_s", 0), r))
+    for pre_, any_s, m, starts in parts.values():
+        sat_h = 0
+        m["Cov_sound%"] = round(100.0 * (m["SAT"] + m.get("UNSAT_sound", m["UNSAT"]) - sat_h) / max(1, m["Grid"]), 2)
+        m["partitions_per_s"] = round(m.get("#P", m["SAT"] + m["UNSAT"] + m["UNK"]) / max(1e-9, m["wall_s"]), 3)
+        m["parts"] = len(starts)
+        rows.append((pre_, any_s, m))
     print(f"# BASELINE configs at one HEAD ({', '.join(sorted(h or '?' for h in heads))}), sound verdicts only\n")
     print("`tools/baseline_configs.py` on 1x MI355X; heuristic retry off (every UNSAT a proof, every SAT an exactly "
           "confirmed pair).  Cov_sound% = (SAT + sound UNSAT) / grid.\n")
@@ -130,7 +152,8 @@ def report(root: str) -> None:
     print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     tot = {}
     for preset, any_s, r in rows:
-        print(f"| {preset} | {r['model']} | {r.get('weights', '?')} | {r['Grid']} | {r['SAT']} | {r['UNSAT']} | "
+        mname = r['model'] + (f" ({r['parts']} parts)" if r.get("parts", 1) > 1 else "")
+        print(f"| {preset} | {mname} | {r.get('weights', '?')} | {r['Grid']} | {r['SAT']} | {r['UNSAT']} | "
               f"{r['UNK']} | {r.get('Cov_sound%')} | {r.get('UNSAT_heuristic', 0)} | {any_s or '-'} | "
               f"{r.get('wall_s', '?')} | {r.get('partitions_per_s', '?')} |")
         t = tot.setdefault(preset, [0, 0, 0, 0.0])
@@ -155,6 +178,9 @@ def main():
     ap.add_argument("--max-partitions", type=int, default=None, help="CPU rehearsal: first N of each grid")
     ap.add_argument("--report", default=None)
     ap.add_argument("--cfg", default="", help="VerifyConfig overrides 'key=value,...' (A/B runs)")
+    ap.add_argument("--start", type=int, default=0,
+                    help="first position of the seeded order (with --max-partitions: one part of a model's grid; "
+                         "the report adds the parts of a (preset, model) up)")
     ap.add_argument("--smt", default=None, help="host back-end (default: auto for tablev, none for the big grids)")
     ap.add_argument("--scratch", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "fairify_base"),
                     help="per-partition CSVs (not copied back)")
