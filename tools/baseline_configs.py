@@ -68,7 +68,10 @@ def run_group(args) -> None:
     for name in names:
         pre = presets.get(name)
         models = list(pre.models) if not args.models else args.models.split(",")
-        out = os.path.join(args.out, name.replace("/", "_") + (f"@{args.start}" if args.start else ""))
+        # one directory per (preset, model subset, part): calls of one group never overwrite each other
+        sub = ("@" + args.models.replace(",", "+")) if args.models else ""
+        part = f"@{args.start}" if (args.start or args.max_partitions) else ""
+        out = os.path.join(args.out, name.replace("/", "_") + sub + part)
         os.makedirs(out, exist_ok=True)
         # per-partition CSVs (MBs per model) go to scratch: gpurun copies back <= 64 MiB of gpurun_out
         scratch = os.path.join(args.scratch, name.replace("/", "_"))
