@@ -375,23 +375,29 @@ __device__ T fwd(const NetDesc& nd, const float* Wf, const Slab& S, const Node& 
   return out;
 }
 
-template <bool WTL>
+// WM: where the weights live -- 1: both copies (forward W_l and the transposed backward operand) staged
+// in LDS; 0: the forward copy in LDS, the transposed one read from L2; 2: both from L2 (wide nets:
+// BM-4's 91 KB of weights would leave LDS for one or two waves per CU, L2 reads leave it for the slabs)
+template <int WM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FA_BETA_WPE))) void fa_beta_kernel(NetDesc nd,
                                                                                            BetaArgs a) {
+  constexpr bool WTL = WM == 1;
   extern __shared__ float smem[];
   const int L = nd.n_layers;
   const int NH = nd.n_hidden;
   const int n0 = nd.dims[0];
   const int mw = nd.max_width;
   const int tot = nd.b_off[L - 1] + nd.dims[L];
-  const int tot4 = (tot + 3) & ~3;
-  float* Wf = smem;
+  const int tot4 = WM == 2 ? 0 : (tot + 3) & ~3;
+  float* Wl = smem;
   float* Wtl = smem + tot4;
-  for (int k = threadIdx.x; k < tot; k += blockDim.x) {
-    Wf[k] = a.flat[k];
-    if (WTL) Wtl[k] = a.wt[k];
-  }
+  if (WM != 2)
+    for (int k = threadIdx.x; k < tot; k += blockDim.x) {
+      Wl[k] = a.flat[k];
+      if (WTL) Wtl[k] = a.wt[k];
+    }
   __syncthreads();
+  const float* Wf = WM == 2 ? a.flat : (const float*)Wl;
   const float* Wt = WTL ? (const float*)Wtl : a.wt;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -849,7 +855,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FA_BETA_WPE
   }
 }
 
-FA_LDS_REGISTER(FA_LDS_K(fa_beta_kernel<true>), FA_LDS_K(fa_beta_kernel<false>));
+FA_LDS_REGISTER(FA_LDS_K(fa_beta_kernel<1>), FA_LDS_K(fa_beta_kernel<0>), FA_LDS_K(fa_beta_kernel<2>));
 
 }  // namespace
 
@@ -875,9 +881,9 @@ extern "C" int fa_beta_config(const NetDesc& nd, int* wpb, int* wtl, size_t* byt
   const size_t lds_cu = 160 * 1024, cap = 160 * 1024 - 1024;
   const int reg_waves = 4 * FA_BETA_WPE;
   int best = 0;
-  for (int t : {1, 0})
+  for (int t : {1, 0, 2})             // (ties keep the earlier: more of the weights in LDS)
     for (int w : {8, 4, 2, 1}) {
-      const size_t b = tot4 * 4 * (t ? 2 : 1) + w * slab;
+      const size_t b = tot4 * 4 * (t == 1 ? 2 : (t == 0 ? 1 : 0)) + w * slab;
       if (b > cap) continue;
       const int per_cu = std::min((int)(lds_cu / b) * w, reg_waves);
       if (per_cu > best) {
@@ -900,9 +906,11 @@ extern "C" int fa_beta_launch(const NetDesc& nd, BetaArgs a, hipStream_t stream)
   a.wt_lds = wtl;
   const dim3 grid((a.R + wpb - 1) / wpb);
   const dim3 block(64 * wpb);
-  if (wtl)
-    hipLaunchKernelGGL(fa_beta_kernel<true>, grid, block, bytes, stream, nd, a);
+  if (wtl == 1)
+    hipLaunchKernelGGL(fa_beta_kernel<1>, grid, block, bytes, stream, nd, a);
+  else if (wtl == 2)
+    hipLaunchKernelGGL(fa_beta_kernel<2>, grid, block, bytes, stream, nd, a);
   else
-    hipLaunchKernelGGL(fa_beta_kernel<false>, grid, block, bytes, stream, nd, a);
+    hipLaunchKernelGGL(fa_beta_kernel<0>, grid, block, bytes, stream, nd, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -567,6 +567,12 @@ PYBIND11_MODULE(_C, m) {
       throw std::invalid_argument("beta_level: RA mask beyond the inputs or no x' box");
     return fa_beta_launch(net.d, a, reinterpret_cast<hipStream_t>(stream));
   });
+  m.def("beta_config", [](const Net& net) {
+    int w = 0, t = 0;
+    size_t b = 0;
+    const int rc = fa_beta_config(net.d, &w, &t, &b);
+    return py::make_tuple(rc, w, t, b);
+  });
   m.def("beta_fits", [](const Net& net) {
     int w = 0, t = 0;
     size_t b = 0;
