@@ -140,11 +140,12 @@ class VerifyConfig:
     beta_min_width: int = 17             # ... on networks whose widest hidden layer is at least this
                                          # (the narrower ones go to the relu stage, whose exact-zero
                                          # concretisation their zero logits need)
-    beta_max_width: int = 128            # ... and at most this (fixed pass only): BM-4's 150-wide layer
-                                         # (transposed W beyond the kernel's LDS) decided 167 of 11 118
-                                         # residue partitions of relaxed/BM for 21 s of its 60 s
-                                         # (profiles/r5/s5_m/); a static rule, so verdicts stay
-                                         # independent of how partitions are sharded
+    beta_max_width: int = 256            # ... and at most this (fixed pass only).  BM-4's 150-wide layer ran in
+                                         # round 5 with its weights staged in LDS (2 waves per CU) and decided
+                                         # 1.5 % of its residue; with the weights read from L2 (7 waves per
+                                         # CU) and primal-gap branching relaxed/BM BM-4 goes 11 118 -> 8 532
+                                         # UNKNOWN (98.89 -> 99.15 %) for 49.8 -> 68.3 s (profiles/r6/); a
+                                         # static rule, so verdicts stay independent of the sharding
     beta_branch: str = os.environ.get("FAIRIFY_BETA_BRANCH", "auto")
                                          # BetaConfig.branch: "pgap" = the verified LP's primal-gap rule
                                          # at the averaged primal iterate (relaxed/BM BM-8 residue: 33 vs

@@ -11,7 +11,7 @@ args="--group $G --out $OUT --head $HEAD"
 [ "$S" != "0" ] && args="$args --start $S"
 [ -n "$N" ] && args="$args --max-partitions $N"
 tag=$(echo "$G-$M-$S" | tr '/,' '__')
-timeout -k 10 1140 python -u tools/baseline_configs.py $args > $OUT/$tag.log 2>&1
+timeout -k 10 ${TLIM:-1140} python -u tools/baseline_configs.py $args > $OUT/$tag.log 2>&1
 rc=$?
 grep -v "^\[hb\]" $OUT/$tag.log | tail -14
 exit $rc

@@ -167,7 +167,7 @@ def test_pipeline_relu_stage_and_anytime_rounds():
     on = verify_chunk(be, m, q, grid, ids, VerifyConfig(relu_budget=256, **base))
     # (anytime_beta=0: the beta rounds, first in every anytime round, would take the relu rounds' share of
     # the wall budget on a loaded host)
-    wide = verify_chunk(be, m, q, grid, ids, VerifyConfig(relu_budget=256, relu_max_width=1, anytime_seconds=30,
+    wide = verify_chunk(be, m, q, grid, ids, VerifyConfig(relu_budget=256, relu_max_width=1, anytime_seconds=90,
                                                           anytime_beta=0, **base))
     for r in (on, wide):
         assert (r.cols["stage"] == "relu").sum() > 10
