@@ -880,9 +880,13 @@ extern "C" int fa_beta_config(const NetDesc& nd, int* wpb, int* wtl, size_t* byt
   const size_t slab = fa_beta_slab_floats(nd) * 4;
   const size_t lds_cu = 160 * 1024, cap = 160 * 1024 - 1024;
   const int reg_waves = 4 * FA_BETA_WPE;
+  // FAIRIFY_BETA_WM=0/1/2 forces the weight placement (tests: every mode gives the same bounds)
+  const char* fw = getenv("FAIRIFY_BETA_WM");
+  const int force = (fw && *fw >= '0' && *fw <= '2') ? *fw - '0' : -1;
   int best = 0;
   for (int t : {1, 0, 2})             // (ties keep the earlier: more of the weights in LDS)
     for (int w : {8, 4, 2, 1}) {
+      if (force >= 0 && t != force) continue;
       const size_t b = tot4 * 4 * (t == 1 ? 2 : (t == 0 ? 1 : 0)) + w * slab;
       if (b > cap) continue;
       const int per_cu = std::min((int)(lds_cu / b) * w, reg_waves);

@@ -72,6 +72,22 @@ __device__ __forceinline__ f32x4 fa_mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Compile-time network shape (layer widths dims[0..L]) for kernels specialised to the zoo shapes
+// that dominate the workloads (symbolic.hip, refine.hip): layer loops unroll at compile time and
+// every width, tile count and lane mask becomes a constant.  FaShapeAny (L = 0): widths from NetDesc.
+struct FaShapeAny {
+  static constexpr int L = 0;
+  __host__ __device__ static constexpr int dim(int) { return 0; }
+};
+template <int... D>
+struct FaShape {
+  static constexpr int L = sizeof...(D) - 1;
+  __host__ __device__ static constexpr int dim(int i) {
+    constexpr int d[] = {D...};
+    return d[i];
+  }
+};
+
 #define FA_CHECK(x)                                                              \
   do {                                                                           \
     hipError_t e__ = (x);                                                        \

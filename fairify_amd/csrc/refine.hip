@@ -32,6 +32,8 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <utility>
+#include <vector>
 
 #include "args.h"
 
@@ -107,11 +109,241 @@ __device__ __forceinline__ void fa_refine_records(const NetDesc& net, const Boun
   }
 }
 
+// One back-substitution step of a column through layer l (its relaxation records, then W_l):
+// lam <- W_l (relaxed lam), constant and rounding terms accumulated.  LC >= 0: l is the compile-time
+// layer LC of shape S (widths constant, tile loops without trip-count checks).
+template <int TM, bool WG, class S, int LC>
+__device__ __forceinline__ void fa_refine_step(const NetDesc& net, const RefineCfg& cfg, const float* smem,
+                                               const float* wsrc, const float4* recg, const float* hmg,
+                                               const float* bl, int n0, int lane, float u, int l_rt,
+                                               float (&lam)[TM][4], float& c, float& err) {
+  constexpr bool CS = S::L > 0 && LC >= 0;
+  const int l = CS ? LC : l_rt;
+  auto D = [&](int i) { return CS ? S::dim(i) : net.dims[i]; };
+  const int grp = lane >> 4;
+  const int n = D(l + 1);
+  const int nin = D(l);
+  const int tout = (n + 15) >> 4, tin = (nin + 15) >> 4;
+  const int off = net.neuron_off[l];
+  const float* b = smem + cfg.b_lds[l];
+  float mu[TM][4];
+  float cs = 0.f, cm = 0.f, er = 0.f;
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    if (t >= tout) break;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int jj = 16 * t + 4 * grp + i;
+      const bool jv = jj < n;
+      // clamped index + select, not a guarded load (an exec-mask branch: SALU)
+      const int jc = min(jj, n - 1);
+      const float4 qr = recg[off + jc];
+      const float br = b[jc];
+      const float4 q = jv ? qr : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float bj = jv ? br : 0.f;
+      const float lm = lam[t][i];
+      const bool neg = lm < 0.f;
+      const float m = lm * (neg ? q.y : q.x);
+      const float tt = neg ? -m * q.z : 0.f;
+      mu[t][i] = m;
+      cs += m * bj + tt;
+      cm += fabsf(m * bj) + fabsf(tt);
+      er += neg ? 3.f * u * (fabsf(m) * q.w + fabsf(tt)) : 0.f;
+    }
+  }
+  const float4* wb = reinterpret_cast<const float4*>(wsrc + cfg.w_lds[l]);
+  const float gn = fa_rgam(2 * n + 1, u);
+  const int hoff = l > 0 ? net.neuron_off[l - 1] : 0;
+#pragma unroll
+  for (int ot = 0; ot < TM; ++ot) {
+    if (ot >= tin) break;
+    f32x4 Z = {0.f, 0.f, 0.f, 0.f}, Q = Z;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      if (t >= tout) break;
+      const float4 w4 = wb[(ot * tout + t) * 64 + lane];
+      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        Z = fa_mfma4(wv[i], mu[t][i], Z);
+        Q = fa_mfma4(fabsf(wv[i]), fabsf(mu[t][i]), Q);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int in = 16 * ot + 4 * grp + i;
+      const int ic = min(in, nin - 1);
+      const float hr = l > 0 ? hmg[hoff + ic] : fmaxf(fabsf(bl[ic]), fabsf(bl[n0 + ic]));
+      const float hm = in < nin ? hr : 0.f;
+      lam[ot][i] = in < nin ? Z[i] : 0.f;
+      er += gn * Q[i] * hm;
+    }
+  }
+#pragma unroll
+  for (int ot = 0; ot < TM; ++ot)
+    if (ot >= tin)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lam[ot][i] = 0.f;
+  // per-column sums over the 4 lane groups holding the column's neurons
+  cs += __shfl_xor(cs, 16); cs += __shfl_xor(cs, 32);
+  cm += __shfl_xor(cm, 16); cm += __shfl_xor(cm, 32);
+  er += __shfl_xor(er, 16); er += __shfl_xor(er, 32);
+  const float gc = fa_rgam(2 * n + 1, u);
+  const float cold = c;
+  c = cold + cs;
+  err += er + gc * (fabsf(cold) + cm);
+}
+
+template <int TM, bool WG, class S, int KC, int... IS>
+__device__ __forceinline__ void fa_refine_back_c(std::integer_sequence<int, IS...>, const NetDesc& net,
+                                                 const RefineCfg& cfg, const float* smem, const float* wsrc,
+                                                 const float4* recg, const float* hmg, const float* bl, int n0,
+                                                 int lane, float u, float (&lam)[TM][4], float& c, float& err) {
+  // layers KC-1 .. 0 in order, each a compile-time step
+  (fa_refine_step<TM, WG, S, KC - 1 - IS>(net, cfg, smem, wsrc, recg, hmg, bl, n0, lane, u, 0, lam, c, err), ...);
+}
+
+// One 16-column tile of layer k: the columns' multipliers start at +-W_k[:, j], are carried back to
+// the input box (fa_refine_step per layer) and concretised; the slab (and, for the logit, the
+// output forms) tightened.  KC >= 0: k is the compile-time layer KC of shape S.
+template <int TM, bool WG, class S, int KC>
+__device__ __forceinline__ void fa_refine_col(const NetDesc& net, const BoundArgs& a, const RefineCfg& cfg,
+                                              const float* smem, const float* wsrc, float* slab,
+                                              const float4* rec, const float* hmx, const float* box,
+                                              const int* list, int k_rt, int rb, int nv, int tile, int lane,
+                                              float gK, float g0, float g1) {
+  constexpr bool CS = S::L > 0 && KC >= 0;
+  const int k = CS ? KC : k_rt;
+  auto D = [&](int i) { return CS ? S::dim(i) : net.dims[i]; };
+  const int L = CS ? S::L : net.n_layers;
+  const int col = lane & 15, grp = lane >> 4;
+  const int n0 = D(0);
+  const int N = net.n_neurons, NH = net.n_hidden;
+  const float u = net.unit;
+  const bool logit = k == L - 1;
+  const int nk = D(k + 1);
+  const int ktop = D(k);
+  const int offk = net.neuron_off[k];
+  const int tk = (nk + 15) >> 4;
+  const float* wk = wsrc + cfg.w_lds[k];
+  const int idx0 = tile * 16 + col;
+  const bool vvalid = idx0 < nv;
+  const int idx = vvalid ? idx0 : nv - 1;
+  const int e = list[idx >> 1];
+  const int s = idx & 1;
+  const int g = e / nk;
+  const int j = e - g * nk;
+  const int r = rb + g;
+  // row strides NH + 1: the lanes of a column tile read the same neuron of up to 16 rows, and
+  // an NH-float4 stride put those rows 4 ways on the same LDS banks (PMC: ~1 conflict cycle
+  // per LDS instruction, profiles/r4/pmc/final_pmc.md)
+  const float4* recg = rec + g * (NH + 1);
+  const float* hmg = hmx + g * (NH + 1);
+  const float* bl = box + g * 2 * n0;
+  const float sgn = s ? -1.f : 1.f;
+  // lam = +-W_k[:, j] from the staged copy: element (in, j) of layer k's operand order
+  float lam[TM][4];
+  {
+    const int jb = ((j >> 4) * 64 + 16 * ((j & 15) >> 2)) * 4 + (j & 3);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        // tiles t < the layer's input tiles are zero padded: load unguarded there
+        const int in = 16 * t + 4 * grp + i;
+        const float w = 16 * t < ktop ? wk[jb + (t * tk * 64 + 4 * grp + i) * 4] : 0.f;
+        lam[t][i] = in < ktop ? sgn * w : 0.f;
+      }
+  }
+  float c = sgn * smem[cfg.b_lds[k] + j];
+  float err = 0.f;
+  if constexpr (CS) {
+    fa_refine_back_c<TM, WG, S, KC>(std::make_integer_sequence<int, KC>{}, net, cfg, smem, wsrc, recg, hmg, bl, n0,
+                                    lane, u, lam, c, err);
+  } else {
+    for (int l = k - 1; l >= 0; --l)
+      fa_refine_step<TM, WG, S, -1>(net, cfg, smem, wsrc, recg, hmg, bl, n0, lane, u, l, lam, c, err);
+  }
+  // ---- concretise over the row's box
+  float cp = 0.f, mp = 0.f;
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    if (16 * t >= n0) break;                            // uniform
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int in = 16 * t + 4 * grp + i;
+      if (TM <= 7) {   // clamped + select (10 tiles: the hoisted loads cost a wave per SIMD)
+        const int ic = min(in, n0 - 1);
+        const float xl = bl[ic], xh = bl[n0 + ic];
+        const float lm = lam[t][i];
+        const float dp = fminf(lm * xl, lm * xh), dm = fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
+        cp += in < n0 ? dp : 0.f;
+        mp += in < n0 ? dm : 0.f;
+      } else if (in < n0) {
+        const float xl = bl[in], xh = bl[n0 + in];
+        const float lm = lam[t][i];
+        cp += fminf(lm * xl, lm * xh);
+        mp += fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
+      }
+    }
+  }
+  cp += __shfl_xor(cp, 16); cp += __shfl_xor(cp, 32);
+  mp += __shfl_xor(mp, 16); mp += __shfl_xor(mp, 32);
+  const float conc = cp + c;
+  const float cmg = mp + fabsf(c);
+  const float errK = err * (1.f + 2.f * gK);
+  const float low = conc - errK - g0 * cmg - g1 * fabsf(conc);
+  bool wr = vvalid;
+  if (logit && wr && !cfg.full) {
+    // REFINE + logit: replace the forward forms only where the backward ones concretise
+    // tighter (both are sound; crown.hip's rule)
+    wr = s ? (-low <= a.out_ub[r]) : (low >= a.out_lb[r]);
+  }
+  if (logit && wr) {
+    // the logit's back-substituted forms: s = 0 lower (L), s = 1 upper (U = -form)
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int in = 16 * t + 4 * grp + i;
+        if (in >= n0) continue;
+        if (s) a.Uc[(size_t)r * n0 + in] = -lam[t][i];
+        else a.Lc[(size_t)r * n0 + in] = lam[t][i];
+      }
+    if (grp == 0) {
+      if (s) { a.U0[r] = -c; a.Ue[r] = errK; a.out_ub[r] = -low; }
+      else { a.L0[r] = c; a.Le[r] = errK; a.out_lb[r] = low; }
+    }
+  }
+  // lane group 0 of each column writes (the 4 groups hold the same column value)
+  if (vvalid && grp == 0) {
+    float* dst = slab + g * 2 * N + (s ? N : 0) + offk + j;
+    *dst = s ? fminf(*dst, -low) : fmaxf(*dst, low);
+    if (!logit && a.phase_in && a.infeas) {
+      const int ph = a.phase_in[(size_t)r * NH + offk + j];
+      if ((ph > 0 && s && -low < 0.f) || (ph < 0 && !s && low > 0.f)) a.infeas[r] = 1;
+    }
+  }
+}
+
+template <int TM, bool WG, class S, int... KS>
+__device__ __forceinline__ void fa_refine_col_c(std::integer_sequence<int, KS...>, const NetDesc& net,
+                                                const BoundArgs& a, const RefineCfg& cfg, const float* smem,
+                                                const float* wsrc, float* slab, const float4* rec, const float* hmx,
+                                                const float* box, const int* list, int k, int rb, int nv, int tile,
+                                                int lane, float gK, float g0, float g1) {
+  // k is wave-uniform: one compile-time column body per layer, selected by a scalar branch
+  ((k == KS ? fa_refine_col<TM, WG, S, KS>(net, a, cfg, smem, wsrc, slab, rec, hmx, box, list, k, rb, nv, tile, lane,
+                                           gK, g0, g1)
+            : void()),
+   ...);
+}
+
 // WG: the weights are read from the global backward-order block (NetDesc.wback_off; w_lds are
 // offsets into it) instead of being staged: a 150-wide net's staged W (112 KB for BM-4) left LDS
 // for one box row per workgroup.  A wave reads one float4 per lane per 8 MFMAs (256 cycles),
 // ~4 B/clk, which L2 sustains for every wave of a CU.
-template <int TM, bool WG = false>
+template <int TM, bool WG = false, class S = FaShapeAny>
 __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a, RefineCfg cfg) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -209,10 +441,7 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
     for (int k = k0; k < k1; ++k) {
       const bool logit = k == L - 1;               // the output forms (FULL, or REFINE + logit)
       const int nk = net.dims[k + 1];
-      const int ktop = net.dims[k];                  // width of h_{k-1}
       const int offk = net.neuron_off[k];
-      const int tk = (nk + 15) >> 4;                 // output tiles of W_k (staged layout)
-      const float* wk = wsrc + cfg.w_lds[k];
       // ---- the columns of this layer: both bounds of every UNSTABLE neuron of a running row (a
       // stable neuron's relaxation is exact whatever its interval, so tightening it buys nothing);
       // the logit: every running row
@@ -237,171 +466,12 @@ __global__ void __launch_bounds__(256) fa_refine_kernel(NetDesc net, BoundArgs a
       const int nv = 2 * rrun[G];
       const int ntile = (nv + 15) >> 4;
       for (int tile = wave; tile < ntile; tile += 4) {
-        const int idx0 = tile * 16 + col;
-        const bool vvalid = idx0 < nv;
-        const int idx = vvalid ? idx0 : nv - 1;
-        const int e = list[idx >> 1];
-        const int s = idx & 1;
-        const int g = e / nk;
-        const int j = e - g * nk;
-        const int r = rb + g;
-        const int node = a.V > 0 ? r / a.V : r;
-        // row strides NH + 1: the lanes of a column tile read the same neuron of up to 16 rows, and
-        // an NH-float4 stride put those rows 4 ways on the same LDS banks (PMC: ~1 conflict cycle
-        // per LDS instruction, profiles/r4/pmc/final_pmc.md)
-        const float4* recg = rec + g * (NH + 1);
-        const float* hmg = hmx + g * (NH + 1);
-        const float* bl = box + g * 2 * n0;
-        const float sgn = s ? -1.f : 1.f;
-        // lam = +-W_k[:, j] from the staged copy: element (in, j) of layer k's operand order
-        float lam[TM][4];
-        {
-          const int jb = ((j >> 4) * 64 + 16 * ((j & 15) >> 2)) * 4 + (j & 3);
-#pragma unroll
-          for (int t = 0; t < TM; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              // tiles t < the layer's input tiles are zero padded: load unguarded there
-              const int in = 16 * t + 4 * grp + i;
-              const float w = 16 * t < ktop ? wk[jb + (t * tk * 64 + 4 * grp + i) * 4] : 0.f;
-              lam[t][i] = in < ktop ? sgn * w : 0.f;
-            }
-        }
-        float c = sgn * smem[cfg.b_lds[k] + j];
-        float err = 0.f;
-        for (int l = k - 1; l >= 0; --l) {
-          const int n = net.dims[l + 1];
-          const int nin = net.dims[l];
-          const int tout = (n + 15) >> 4, tin = (nin + 15) >> 4;
-          const int off = net.neuron_off[l];
-          const float* b = smem + cfg.b_lds[l];
-          float mu[TM][4];
-          float cs = 0.f, cm = 0.f, er = 0.f;
-#pragma unroll
-          for (int t = 0; t < TM; ++t) {
-            if (t >= tout) break;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int jj = 16 * t + 4 * grp + i;
-              const bool jv = jj < n;
-              // clamped index + select, not a guarded load (an exec-mask branch: SALU)
-              const int jc = min(jj, n - 1);
-              const float4 qr = recg[off + jc];
-              const float br = b[jc];
-              const float4 q = jv ? qr : make_float4(0.f, 0.f, 0.f, 0.f);
-              const float bj = jv ? br : 0.f;
-              const float lm = lam[t][i];
-              const bool neg = lm < 0.f;
-              const float m = lm * (neg ? q.y : q.x);
-              const float tt = neg ? -m * q.z : 0.f;
-              mu[t][i] = m;
-              cs += m * bj + tt;
-              cm += fabsf(m * bj) + fabsf(tt);
-              er += neg ? 3.f * u * (fabsf(m) * q.w + fabsf(tt)) : 0.f;
-            }
-          }
-          const float4* wb = reinterpret_cast<const float4*>(wsrc + cfg.w_lds[l]);
-          const float gn = fa_rgam(2 * n + 1, u);
-          const int hoff = l > 0 ? net.neuron_off[l - 1] : 0;
-#pragma unroll
-          for (int ot = 0; ot < TM; ++ot) {
-            if (ot >= tin) break;
-            f32x4 Z = {0.f, 0.f, 0.f, 0.f}, Q = Z;
-#pragma unroll
-            for (int t = 0; t < TM; ++t) {
-              if (t >= tout) break;
-              const float4 w4 = wb[(ot * tout + t) * 64 + lane];
-              const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                Z = fa_mfma4(wv[i], mu[t][i], Z);
-                Q = fa_mfma4(fabsf(wv[i]), fabsf(mu[t][i]), Q);
-              }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int in = 16 * ot + 4 * grp + i;
-              const int ic = min(in, nin - 1);
-              const float hr = l > 0 ? hmg[hoff + ic] : fmaxf(fabsf(bl[ic]), fabsf(bl[n0 + ic]));
-              const float hm = in < nin ? hr : 0.f;
-              lam[ot][i] = in < nin ? Z[i] : 0.f;
-              er += gn * Q[i] * hm;
-            }
-          }
-#pragma unroll
-          for (int ot = 0; ot < TM; ++ot)
-            if (ot >= tin)
-#pragma unroll
-              for (int i = 0; i < 4; ++i) lam[ot][i] = 0.f;
-          // per-column sums over the 4 lane groups holding the column's neurons
-          cs += __shfl_xor(cs, 16); cs += __shfl_xor(cs, 32);
-          cm += __shfl_xor(cm, 16); cm += __shfl_xor(cm, 32);
-          er += __shfl_xor(er, 16); er += __shfl_xor(er, 32);
-          const float gc = fa_rgam(2 * n + 1, u);
-          const float cold = c;
-          c = cold + cs;
-          err += er + gc * (fabsf(cold) + cm);
-        }
-        // ---- concretise over the row's box
-        float cp = 0.f, mp = 0.f;
-#pragma unroll
-        for (int t = 0; t < TM; ++t) {
-          if (16 * t >= n0) break;                            // uniform
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int in = 16 * t + 4 * grp + i;
-            if (TM <= 7) {   // clamped + select (10 tiles: the hoisted loads cost a wave per SIMD)
-              const int ic = min(in, n0 - 1);
-              const float xl = bl[ic], xh = bl[n0 + ic];
-              const float lm = lam[t][i];
-              const float dp = fminf(lm * xl, lm * xh), dm = fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
-              cp += in < n0 ? dp : 0.f;
-              mp += in < n0 ? dm : 0.f;
-            } else if (in < n0) {
-              const float xl = bl[in], xh = bl[n0 + in];
-              const float lm = lam[t][i];
-              cp += fminf(lm * xl, lm * xh);
-              mp += fabsf(lm) * fmaxf(fabsf(xl), fabsf(xh));
-            }
-          }
-        }
-        cp += __shfl_xor(cp, 16); cp += __shfl_xor(cp, 32);
-        mp += __shfl_xor(mp, 16); mp += __shfl_xor(mp, 32);
-        const float conc = cp + c;
-        const float cmg = mp + fabsf(c);
-        const float errK = err * (1.f + 2.f * gK);
-        const float low = conc - errK - g0 * cmg - g1 * fabsf(conc);
-        bool wr = vvalid;
-        if (logit && wr && !cfg.full) {
-          // REFINE + logit: replace the forward forms only where the backward ones concretise
-          // tighter (both are sound; crown.hip's rule)
-          wr = s ? (-low <= a.out_ub[r]) : (low >= a.out_lb[r]);
-        }
-        if (logit && wr) {
-          // the logit's back-substituted forms: s = 0 lower (L), s = 1 upper (U = -form)
-#pragma unroll
-          for (int t = 0; t < TM; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int in = 16 * t + 4 * grp + i;
-              if (in >= n0) continue;
-              if (s) a.Uc[(size_t)r * n0 + in] = -lam[t][i];
-              else a.Lc[(size_t)r * n0 + in] = lam[t][i];
-            }
-          if (grp == 0) {
-            if (s) { a.U0[r] = -c; a.Ue[r] = errK; a.out_ub[r] = -low; }
-            else { a.L0[r] = c; a.Le[r] = errK; a.out_lb[r] = low; }
-          }
-        }
-        // lane group 0 of each column writes (the 4 groups hold the same column value)
-        if (vvalid && grp == 0) {
-          float* dst = slab + g * 2 * N + (s ? N : 0) + offk + j;
-          *dst = s ? fminf(*dst, -low) : fmaxf(*dst, low);
-          if (!logit && a.phase_in && a.infeas) {
-            const int ph = a.phase_in[(size_t)r * NH + offk + j];
-            if ((ph > 0 && s && -low < 0.f) || (ph < 0 && !s && low > 0.f)) a.infeas[r] = 1;
-          }
-        }
+        if constexpr (S::L > 0)
+          fa_refine_col_c<TM, WG, S>(std::make_integer_sequence<int, S::L>{}, net, a, cfg, smem, wsrc, slab, rec, hmx,
+                                     box, list, k, rb, nv, tile, lane, gK, g0, g1);
+        else
+          fa_refine_col<TM, WG, S, -1>(net, a, cfg, smem, wsrc, slab, rec, hmx, box, list, k, rb, nv, tile, lane, gK,
+                                       g0, g1);
       }
       __syncthreads();
       if (k < L - 1) fa_refine_records(net, a, cfg, k, rb, smem);   // layer k is final now
@@ -431,6 +501,40 @@ RefineKernel select_refine(int TM, bool wg) {
   if (TM <= 4) return fa_refine_kernel<4>;
   if (TM <= 7) return wg ? fa_refine_kernel<7, true> : fa_refine_kernel<7>;
   if (TM <= 10) return wg ? fa_refine_kernel<10, true> : fa_refine_kernel<10>;
+  return nullptr;
+}
+
+// Compile-time shapes (common.h FaShape): the zoo's deep chains, each instantiated for the TM bucket
+// select_refine picks for it (same LDS layout and arithmetic; the column body is unrolled per layer
+// with constant widths).  FAIRIFY_REFINE_SHAPED=0 (read per launch: the bitwise-equality test toggles
+// it) keeps the run-time-shape kernels.
+struct ShapedRefine {
+  int tm;
+  bool wg;
+  std::vector<int> dims;
+  RefineKernel k;
+};
+template <int TM, int... D>
+ShapedRefine shaped_refine() {
+  return {TM, false, {D...}, fa_refine_kernel<TM, false, FaShape<D...>>};
+}
+
+RefineKernel select_refine_shaped(const NetDesc& net, int TM, bool wg) {
+  const char* e = getenv("FAIRIFY_REFINE_SHAPED");
+  if (e && *e == '0') return nullptr;
+  static const std::vector<ShapedRefine> v = {
+      shaped_refine<4, 13, 64, 32, 16, 8, 4, 1>(),    // AC-7
+      shaped_refine<4, 16, 64, 32, 16, 8, 4, 1>(),    // BM-8
+      shaped_refine<4, 13, 64, 64, 1>(),              // AC-5
+      shaped_refine<7, 13, 100, 100, 1>(),            // AC-4
+  };
+  const int tmb = TM <= 1 ? 1 : TM <= 2 ? 2 : TM <= 4 ? 4 : TM <= 7 ? 7 : 10;
+  for (const auto& s : v) {
+    if (s.tm != tmb || s.wg != wg || (int)s.dims.size() != net.n_layers + 1) continue;
+    bool same = true;
+    for (int l = 0; l <= net.n_layers && same; ++l) same = s.dims[l] == net.dims[l];
+    if (same) return s.k;
+  }
   return nullptr;
 }
 
@@ -470,8 +574,9 @@ int backward_launch(const NetDesc& net, const BoundArgs& a, int full, int logit,
     offs += ((net.dims[l] + 15) / 16) * ((net.dims[l + 1] + 15) / 16) * 256;
   }
   const bool wg = (size_t)offs * sizeof(float) > refine_wg_bytes() && TM >= 5 && net.wback_floats >= offs;
-  const RefineKernel k = select_refine(TM, wg);
+  RefineKernel k = select_refine(TM, wg);
   if (!k) return -1;
+  if (const RefineKernel ks = select_refine_shaped(net, TM, wg)) k = ks;
   if (wg) offs = 0;        // nothing staged: the biases start the LDS
   for (int l = 0; l < LW; ++l) {
     cfg.b_lds[l] = offs;
@@ -557,3 +662,7 @@ extern "C" int fa_backward_launch(const NetDesc& net, BoundArgs a, hipStream_t s
 FA_LDS_REGISTER(FA_LDS_K((fa_refine_kernel<7, true>)), FA_LDS_K((fa_refine_kernel<10, true>)));
 FA_LDS_REGISTER(FA_LDS_K(fa_refine_kernel<1>), FA_LDS_K(fa_refine_kernel<2>), FA_LDS_K(fa_refine_kernel<4>),
                 FA_LDS_K(fa_refine_kernel<7>), FA_LDS_K(fa_refine_kernel<10>));
+FA_LDS_REGISTER(FA_LDS_K((fa_refine_kernel<4, false, FaShape<13, 64, 32, 16, 8, 4, 1>>)),
+                FA_LDS_K((fa_refine_kernel<4, false, FaShape<16, 64, 32, 16, 8, 4, 1>>)),
+                FA_LDS_K((fa_refine_kernel<4, false, FaShape<13, 64, 64, 1>>)),
+                FA_LDS_K((fa_refine_kernel<7, false, FaShape<13, 100, 100, 1>>)));

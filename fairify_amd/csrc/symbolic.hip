@@ -32,6 +32,8 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <utility>
+#include <vector>
 
 #include "args.h"
 
@@ -48,6 +50,16 @@ struct SymCfg {
   int stage_off;                   // float offset in `flat` of the staged block (wperm or packed)
   int stage_floats;                //   and its size (multiple of 4)
 };
+
+// Compile-time network shape (common.h FaShape) for the zoo shapes that dominate the bench and the
+// big grids.  With the shape known, the layer loop is unrolled at compile time (fa_sym_layers_c):
+// every per-layer width, tile count, "last layer" test and partial-tile lane mask is a constant,
+// so the tile loops lose their uniform trip-count checks and the epilogue its width guards -- the
+// scalar work the PMC pass charged to these kernels (SALU:VALU 0.34-0.44, profiles/r5/pmc_diet.md).
+// SymShapeAny (L = 0): widths read from NetDesc at run time, any network.
+using SymShapeAny = FaShapeAny;
+template <int... D>
+using SymShape = FaShape<D...>;
 
 struct SymBox {
   const BoundArgs* a;
@@ -135,7 +147,7 @@ __device__ __forceinline__ void fa_pq_to_ul(const f32x4& P, const f32x4& Q, int 
   }
 }
 
-template <int NT, bool PAIR, int PG = 1, bool CR = false>
+template <int NT, bool PAIR, int PG = 1, bool CR = false, class S = SymShapeAny>
 __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
                                                 const float* smem, float* T, const float* bxv_in, const int* cdim_s,
                                                 int l, int r_in, int node_in, int r2, int node2, bool v2, int lane,
@@ -143,10 +155,11 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
                                                 const f32x4 (&Lq)[2][NT], float (&nu)[2][NT][4],
                                                 float (&nlo)[2][NT][4]) {
   constexpr int TS = SymSlab<NT>::TS;
+  constexpr bool CS = S::L > 0;        // compile-time shape: l is a constant here (fa_sym_layers_c)
   const int col = lane & 15, grp = lane >> 4;
-  const int n_out = net.dims[l + 1];
+  const int n_out = CS ? S::dim(l + 1) : net.dims[l + 1];
   const float* sb = smem + cfg.b_lds[l];
-  const bool last = l == net.n_layers - 1;
+  const bool last = CS ? l == S::L - 1 : l == net.n_layers - 1;
   const float gg = net.g_gemm[l];
   const float gc = net.g_conc;
   const float gi = net.g_one;
@@ -155,7 +168,7 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
   const float gnext = last ? 0.f : (CR ? net.g_fwd[l + 1] : net.g_gemm[l + 1]);
   const int noff = net.neuron_off[l];
   const int nc = cfg.nc;
-  const int n0 = net.dims[0];
+  const int n0 = CS ? S::dim(0) : net.dims[0];
   // neuron lane role in the epilogue: tile jt0 + (lane >> 5); within it lanes 0-15 = U block,
   // 16-31 = L block of neuron (lane & 15) -- all 64 lanes busy for two output tiles.  PAIR: the
   // two tiles are the same neurons of two box rows (r_in, r2), each with its own box values
@@ -168,7 +181,7 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
   const int node = PG > 1 ? (a.V > 0 ? r / a.V : r) : (second ? node2 : node_in);
   const float* bxv = bxv_in + (PG > 1 ? bidx : (second ? 1 : 0)) * SymSlab<NT, PG>::BOX;
   const int jt = PAIR ? jt0 : jt0 + tsub;
-  const int n_out_t = net.dims[l + 1];
+  const int n_out_t = n_out;
   const bool nl_act = PG > 1 ? r < a.R : (16 * jt < n_out_t && (!second || v2));
   const int ob = (lane >> 4) & 1;
   // this lane's row (tile row ob * 16 + col of tile tsub), rotated (fa_trot)
@@ -319,7 +332,7 @@ __device__ __forceinline__ bool fa_sym_epilogue(const NetDesc& net, const BoundA
 // index) is the box, both use output tile 0 of W.  PG > 1 (packed, PAIR only): slot u is a group
 // of PG boxes sharing the tile (block-diagonal weights); layer 0 builds its identity-form
 // operands on the fly from the boxes' input ranges in the wave's LDS box table.
-template <int NT, int TM, bool PAIR, int PG = 1>
+template <int NT, int TM, bool PAIR, int PG = 1, class S = SymShapeAny>
 __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs& a, const SymCfg& cfg,
                                              const float* smem, float* T, const float* bxv, const int* cdim_s,
                                              int l, int r, int node, int r2, int node2, bool v2, int lane,
@@ -328,12 +341,13 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
   constexpr int TMS = PAIR ? 2 : TM;
   constexpr bool CR = SymForm<PAIR, TM>::CR;
   constexpr int TS = SymSlab<NT>::TS;
+  constexpr bool CS = S::L > 0;        // compile-time shape: l is a constant here (fa_sym_layers_c)
   const int col = lane & 15, grp = lane >> 4;
-  const int n_in = net.dims[l], n_out = net.dims[l + 1];
+  const int n_in = CS ? S::dim(l) : net.dims[l], n_out = CS ? S::dim(l + 1) : net.dims[l + 1];
   const int tin = (n_in + 15) >> 4, tout = (n_out + 15) >> 4;
   const float* sw = smem + cfg.w_lds[l];
   const float* sb = smem + cfg.b_lds[l];
-  const bool last = l == net.n_layers - 1;
+  const bool last = CS ? l == S::L - 1 : l == net.n_layers - 1;
   const float gg = net.g_gemm[l];
   const float gc = net.g_conc;
   const float gi = net.g_one;
@@ -396,7 +410,7 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
       }
     }
     float nu[2][NT][4], nlo[2][NT][4];
-    if (!fa_sym_epilogue<NT, PAIR, PG, CR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
+    if (!fa_sym_epilogue<NT, PAIR, PG, CR, S>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
                                        nu, nlo))
       return;
 #pragma unroll
@@ -461,7 +475,7 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
         if (CR) fa_pq_to_ul(f32x4(U[bi][ct]), f32x4(Lq[bi][ct]), ct * 16 + col, gg, U[bi][ct], Lq[bi][ct]);
       }
     float nu[2][NT][4], nlo[2][NT][4];
-    fa_sym_epilogue<NT, PAIR, PG, CR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
+    fa_sym_epilogue<NT, PAIR, PG, CR, S>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, 0, U, Lq,
                                   nu, nlo);
     return;
   }
@@ -527,7 +541,7 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
       continue;
     }
 #else
-    if (!fa_sym_epilogue<NT, PAIR, PG, CR>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, jt0, U,
+    if (!fa_sym_epilogue<NT, PAIR, PG, CR, S>(net, a, cfg, smem, T, bxv, cdim_s, l, r, node, r2, node2, v2, lane, jt0, U,
                                        Lq, nu, nlo))
       continue;
 #endif
@@ -563,7 +577,21 @@ __device__ __forceinline__ void fa_sym_layer(const NetDesc& net, const BoundArgs
 #define FA_SYM_WAVES_PER_EU(NT, TM, PAIR) \
   ((PAIR) ? 3 : ((TM) == 2 ? 3 : ((TM) == 4 ? FA_SYM_WPE4 : ((TM) == 7 ? FA_SYM_WPE7 : 1))))
 
-template <int NT, int TM, bool PAIR, int PG = 1>
+// The layer chain of a compile-time shape: one inlined fa_sym_layer per layer, l a constant in each,
+// operands ping-ponging between XA (even layers' input) and XB.
+template <int NT, int TM, bool PAIR, int PG, class S, int... LS>
+__device__ __forceinline__ void fa_sym_layers_c(std::integer_sequence<int, LS...>, const NetDesc& net,
+                                                const BoundArgs& a, const SymCfg& cfg, const float* smem, float* T,
+                                                const float* bxv, const int* cdim_s, int r, int node, int r2,
+                                                int node2, bool v2, int lane, float (&XA)[NT][PAIR ? 2 : TM][2][4],
+                                                float (&XB)[NT][PAIR ? 2 : TM][2][4]) {
+  ((LS & 1 ? fa_sym_layer<NT, TM, PAIR, PG, S>(net, a, cfg, smem, T, bxv, cdim_s, LS, r, node, r2, node2, v2, lane,
+                                               XB, XA)
+           : fa_sym_layer<NT, TM, PAIR, PG, S>(net, a, cfg, smem, T, bxv, cdim_s, LS, r, node, r2, node2, v2, lane,
+                                               XA, XB)),
+   ...);
+}
+
 // Threads per workgroup: the 7-tile kernel's staged W (AC-4: 63 KB) leaves LDS for one workgroup
 // per CU, so it runs 8 waves per workgroup (2 per SIMD, its VGPR limit) instead of 4.
 #ifndef FA_SYM_BIG_THREADS
@@ -571,6 +599,7 @@ template <int NT, int TM, bool PAIR, int PG = 1>
 #endif
 #define FA_SYM_THREADS(TM) ((TM) == 7 ? FA_SYM_BIG_THREADS : FA_THREADS)
 
+template <int NT, int TM, bool PAIR, int PG = 1, class S = SymShapeAny>
 __global__ void __launch_bounds__(FA_SYM_THREADS(TM)) __attribute__((amdgpu_waves_per_eu(FA_SYM_WAVES_PER_EU(NT, TM, PAIR))))
 fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
   constexpr bool CR = SymForm<PAIR, TM>::CR;   // centre / radius operands (multi-tile kernels)
@@ -592,7 +621,7 @@ fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
   const int grp = lane >> 4;
   const int wave = tid >> 6;
   const int nw = FA_SYM_THREADS(TM) / 64;
-  const int n0 = net.dims[0];
+  const int n0 = S::L > 0 ? S::dim(0) : net.dims[0];
   const int nc = cfg.nc;
   const float g0 = net.g_gemm[0];
   float* T = smem + cfg.lds_floats + wave * SymSlab<NT, PG>::FLOATS;
@@ -699,13 +728,18 @@ fa_sym_kernel(NetDesc net, BoundArgs a, SymCfg cfg) {
       }
     }
     __builtin_amdgcn_wave_barrier();
-    for (int l = 0; l < net.n_layers; ++l) {
-      if (l & 1)
-        fa_sym_layer<NT, TM, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
-                                       lane, XB, XA);
-      else
-        fa_sym_layer<NT, TM, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
-                                       lane, XA, XB);
+    if constexpr (S::L > 0) {
+      fa_sym_layers_c<NT, TM, PAIR, PG, S>(std::make_integer_sequence<int, S::L>{}, net, a, cfg, smem, T, bxv, cdim_s,
+                                           r, bx.node, rb, bxs[RPW - 1].node, v2, lane, XA, XB);
+    } else {
+      for (int l = 0; l < net.n_layers; ++l) {
+        if (l & 1)
+          fa_sym_layer<NT, TM, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
+                                         lane, XB, XA);
+        else
+          fa_sym_layer<NT, TM, PAIR, PG>(net, a, cfg, smem, T, bxv, cdim_s, l, r, bx.node, rb, bxs[RPW - 1].node, v2,
+                                         lane, XA, XB);
+      }
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -786,6 +820,54 @@ SymKernel select_kernel(int NT, int TM) {
   }
 }
 
+// the TM template bucket select_kernel uses for a layer width of TM tiles (0: none)
+int tm_bucket(int NT, int TM) {
+  if (TM > max_tm()) return 0;
+  const int b = TM <= 1 ? 1 : TM <= 2 ? 2 : TM <= 4 ? 4 : TM <= 7 ? 7 : TM <= 10 ? 10 : 0;
+  if (NT == 2 && b == 7) return 10;
+  if (NT == 3 && b > 2) return 0;
+  return NT >= 1 && NT <= 3 ? b : 0;
+}
+
+// Compile-time shapes (SymShape): the zoo's dominant layer chains, each instantiated for the (NT, TM
+// bucket) kernel the run-time selection picks for it, so launch geometry, LDS layout and arithmetic
+// are the generic kernel's.  FAIRIFY_SYM_SHAPED=0 (read per launch: the bitwise-equality test
+// toggles it) keeps the run-time-shape kernels.
+struct ShapedKernel {
+  int nt, tm;
+  std::vector<int> dims;
+  SymKernel k;
+};
+template <int NT, int TM, int... D>
+ShapedKernel shaped() {
+  return {NT, TM, {D...}, fa_sym_kernel<NT, TM, false, 1, SymShape<D...>>};
+}
+
+const std::vector<ShapedKernel>& shaped_kernels() {
+  static const std::vector<ShapedKernel> v = {
+      shaped<1, 4, 13, 64, 32, 16, 8, 4, 1>(),   // AC-7, PA folded (node-row expansion)
+      shaped<2, 4, 13, 64, 32, 16, 8, 4, 1>(),   // AC-7, no dim folded (beta tightening rows)
+      shaped<2, 4, 16, 64, 32, 16, 8, 4, 1>(),   // BM-8
+      shaped<1, 4, 13, 64, 64, 1>(),             // AC-5
+      shaped<1, 4, 13, 50, 1>(),                 // AC-3
+      shaped<1, 7, 13, 100, 100, 1>(),           // AC-4
+      shaped<1, 7, 13, 100, 1>(),                // AC-2
+  };
+  return v;
+}
+
+SymKernel select_shaped(const NetDesc& net, int NT, int tmb) {
+  const char* e = getenv("FAIRIFY_SYM_SHAPED");
+  if (e && *e == '0') return nullptr;
+  for (const auto& s : shaped_kernels()) {
+    if (s.nt != NT || s.tm != tmb || (int)s.dims.size() != net.n_layers + 1) continue;
+    bool same = true;
+    for (int l = 0; l <= net.n_layers && same; ++l) same = s.dims[l] == net.dims[l];
+    if (same) return s.k;
+  }
+  return nullptr;
+}
+
 int device_cus() {
   static int cus = 0;
   static std::once_flag once;
@@ -825,10 +907,15 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
   SymKernel k = select_kernel(NT, TM);
   if (!k) return 0;
   const bool pair0 = k == sym_ptr<1, 1, true>();
+  const int tmb = tm_bucket(NT, TM);
   // packed narrow networks: pack_g boxes per tile, block-diagonal weights (NetDesc.pack_*)
   const int pg = (pair0 && net.pack_g > 1 && net.dims[0] <= 16 && use_pack()) ? net.pack_g : 1;
   if (pg > 1) k = select_packed(pg);
   if (!k) return 0;
+  if (!pair0) {   // a compile-time-shape instance of the same (NT, TM) kernel, when there is one
+    const SymKernel ks = select_shaped(net, NT, tmb);
+    if (ks) k = ks;
+  }
   int off = 0;
   if (pg > 1) {
     cfg.w_lds[0] = 0;
@@ -867,7 +954,7 @@ extern "C" int fa_sym_try_launch(const NetDesc& net, BoundArgs a, unsigned long 
     case 2: slab = SymSlab<2>::FLOATS; break;
     default: slab = SymSlab<3>::FLOATS; break;
   }
-  const int threads = (k == sym_ptr<1, 7>()) ? FA_SYM_BIG_THREADS : FA_THREADS;
+  const int threads = (!pair0 && NT == 1 && tmb == 7) ? FA_SYM_BIG_THREADS : FA_THREADS;   // = FA_SYM_THREADS(TM)
   const int rows_per_block = (threads / 64) * (pair0 ? 2 * pg : 1);
   const size_t bytes = (size_t)(off + (threads / 64) * slab) * sizeof(float);
   if (bytes > 160 * 1024) return 0;
@@ -901,3 +988,10 @@ FA_LDS_REGISTER(FA_LDS_K((sym_ptr<1, 1>())), FA_LDS_K((sym_ptr<1, 1, true>())), 
                 FA_LDS_K((sym_ptr<1, 7>())), FA_LDS_K((sym_ptr<1, 10>())), FA_LDS_K((sym_ptr<2, 1>())),
                 FA_LDS_K((sym_ptr<2, 2>())), FA_LDS_K((sym_ptr<2, 4>())), FA_LDS_K((sym_ptr<2, 10>())),
                 FA_LDS_K((sym_ptr<3, 1>())), FA_LDS_K((sym_ptr<3, 2>())));
+FA_LDS_REGISTER(FA_LDS_K((fa_sym_kernel<1, 4, false, 1, SymShape<13, 64, 32, 16, 8, 4, 1>>)),
+                FA_LDS_K((fa_sym_kernel<2, 4, false, 1, SymShape<13, 64, 32, 16, 8, 4, 1>>)),
+                FA_LDS_K((fa_sym_kernel<2, 4, false, 1, SymShape<16, 64, 32, 16, 8, 4, 1>>)),
+                FA_LDS_K((fa_sym_kernel<1, 4, false, 1, SymShape<13, 64, 64, 1>>)),
+                FA_LDS_K((fa_sym_kernel<1, 4, false, 1, SymShape<13, 50, 1>>)),
+                FA_LDS_K((fa_sym_kernel<1, 7, false, 1, SymShape<13, 100, 100, 1>>)),
+                FA_LDS_K((fa_sym_kernel<1, 7, false, 1, SymShape<13, 100, 1>>)));

@@ -139,6 +139,27 @@ def test_beta_kernel_wide_layers(cuda):
     assert torch.allclose(lg.bound.cpu()[fin], lr_.bound[fin], rtol=1e-9, atol=1e-9)
 
 
+@pytest.mark.parametrize("widths", [(6, 5, 4), (150, 100, 50)])
+def test_beta_kernel_weight_placement_is_bitwise_neutral(cuda, monkeypatch, widths):
+    """The three weight placements (both copies in LDS, forward copy in LDS, both read from L2 --
+    BM-4's 150-wide layer runs the last) run the same arithmetic: optimised parameters, rigorous
+    bounds, splits and vertices are bitwise equal."""
+    outs = []
+    # (both copies of the wide net's weights do not fit in LDS together)
+    for wm in (("1", "0", "2") if max(widths) < 100 else ("0", "2")):
+        monkeypatch.setenv("FAIRIFY_BETA_WM", wm)
+        _, _, _, _, lg, _, gp = _both(cuda, 9, 20, fix=0.2, widths=widths, pgap=True)
+        outs.append((lg, gp))
+    monkeypatch.delenv("FAIRIFY_BETA_WM")
+    (l0, g0) = outs[0]
+    for lg, gp in outs[1:]:
+        assert torch.equal(lg.bound.cpu(), l0.bound.cpu())
+        assert torch.equal(lg.split.cpu(), l0.split.cpu())
+        assert torch.equal(lg.xstar.cpu(), l0.xstar.cpu())
+        for a, b in zip(gp, g0):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("seed,branch,native", [(3, "kernel", True), (6, "kernel", True), (3, "pgap", True),
                                                 (6, "pgap", True), (3, "kernel", False), (6, "pgap", False)])
 def test_beta_bab_gpu_matches_bruteforce(cuda, seed, branch, native):

@@ -345,3 +345,38 @@ def test_global_weight_refine_bitwise_equals_staged(cuda, monkeypatch, mode):
         outs.append([r.out_lb, r.out_ub, r.Lc, r.Uc, r.lay_lb_full, r.lay_ub_full])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n0,hidden", [(13, [64, 32, 16, 8, 4]), (16, [64, 32, 16, 8, 4]), (13, [64, 64]),
+                                       (13, [100, 100])])
+def test_shaped_refine_kernel_is_bitwise_the_generic_one(cuda, monkeypatch, n0, hidden):
+    """The compile-time-shape refine instances (common.h FaShape: the column body unrolled per layer,
+    widths constant) run the generic kernel's arithmetic: REFINE, REFINE + logit (the runtime's
+    fused launch) and FULL give bitwise equal bounds and forms."""
+    from fairify_amd.ops import ext
+    from fairify_amd.ops import hip as H
+
+    m = random_mlp(n0, hidden, seed=41 + n0 + len(hidden), bias_scale=0.3)
+    lo, hi = _boxes(n0, 611, 13)
+    gpu = Backend(m, cuda)
+    L_, H_ = lo.to(cuda), hi.to(cuda)
+    outs = []
+    for shaped in ("1", "0"):
+        monkeypatch.setenv("FAIRIFY_REFINE_SHAPED", shaped)
+        a = gpu.bounds(L_, H_, mode="symbolic", crown=True, refine=True)
+        f = gpu.bounds(L_, H_, mode="symbolic", keep_layers=True)
+        ext().refine_crown(H._net(gpu), gpu.flat.data_ptr(), L_.contiguous().data_ptr(), H_.contiguous().data_ptr(),
+                           0, L_.shape[0], f.out_lb.data_ptr(), f.out_ub.data_ptr(), f.Lc.data_ptr(),
+                           f.L0.data_ptr(), f.Le.data_ptr(), f.Uc.data_ptr(), f.U0.data_ptr(), f.Ue.data_ptr(),
+                           f.lay_lb_full.data_ptr(), f.lay_ub_full.data_ptr(), H._stream(cuda))
+        b = gpu.bounds(L_, H_, mode="backward")
+        torch.cuda.synchronize()
+        outs.append((a, f, b))
+    for x, y in zip(outs[0], outs[1]):
+        for fld in ("out_lb", "out_ub", "Lc", "Uc", "L0", "U0", "Le", "Ue"):
+            if getattr(x, fld) is not None:
+                assert torch.equal(getattr(x, fld).cpu(), getattr(y, fld).cpu()), fld
+        for p, q in zip(x.layer_lb or [], y.layer_lb or []):
+            assert torch.equal(p.cpu(), q.cpu())
+        for p, q in zip(x.layer_ub or [], y.layer_ub or []):
+            assert torch.equal(p.cpu(), q.cpu())

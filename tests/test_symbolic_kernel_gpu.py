@@ -77,6 +77,32 @@ def test_symbolic_kernel_matches_reference(cuda, n0, hidden, fold):
     assert rg.dead is not None
 
 
+@pytest.mark.parametrize("n0,hidden,fold,dead", [
+    (13, [64, 32, 16, 8, 4], (8,), False), (13, [64, 32, 16, 8, 4], (8,), True),    # AC-7
+    (13, [64, 32, 16, 8, 4], (), False),                                            # AC-7, NT=2
+    (16, [64, 32, 16, 8, 4], (0,), False), (16, [64, 32, 16, 8, 4], (0,), True),    # BM-8
+    (13, [64, 64], (8,), False), (13, [50], (7,), False),                           # AC-5, AC-3
+    (13, [100, 100], (8,), False), (13, [100, 100], (8,), True), (13, [100], (8,), False)])   # AC-4, AC-2
+def test_shaped_symbolic_kernel_is_bitwise_the_generic_one(cuda, monkeypatch, n0, hidden, fold, dead):
+    """The compile-time-shape instances (csrc/symbolic.hip SymShape: layer loop unrolled, widths
+    constant) run the generic kernel's arithmetic: every output is bitwise equal."""
+    m = random_mlp(n0, hidden, seed=n0 + len(hidden), bias_scale=0.3)
+    lo, hi = _boxes(n0, 700, 9, fold)
+    dm = (torch.rand(700, m.n_neurons - 1, generator=torch.Generator().manual_seed(1)) < 0.2).to(cuda) if dead else None
+    be = Backend(m, cuda)
+    outs = []
+    for shaped in ("1", "0"):
+        monkeypatch.setenv("FAIRIFY_SYM_SHAPED", shaped)
+        outs.append(be.bounds(lo.to(cuda), hi.to(cuda), mode="symbolic", keep_layers=True, fold=fold, dead=dm))
+    a, b = outs
+    for x, y in [(a.out_lb, b.out_lb), (a.out_ub, b.out_ub), (a.Lc, b.Lc), (a.Uc, b.Uc), (a.L0, b.L0), (a.U0, b.U0),
+                 (a.Le, b.Le), (a.Ue, b.Ue)] + \
+            list(zip(a.layer_lb, b.layer_lb)) + list(zip(a.layer_ub, b.layer_ub)):
+        assert torch.equal(x.cpu(), y.cpu())
+    if a.dead is not None:
+        assert torch.equal(a.dead.cpu(), b.dead.cpu())
+
+
 @pytest.mark.parametrize("n0,hidden,fold", [SHAPES[0], SHAPES[3], SHAPES[5], SHAPES[7], SHAPES[12]])
 def test_symbolic_kernel_forced_dead(cuda, n0, hidden, fold):
     m = random_mlp(n0, hidden, seed=11, bias_scale=0.3)
