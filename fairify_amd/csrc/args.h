@@ -486,5 +486,6 @@ struct BetaPoolArgs {
   float* oLBA; float* oUBA; float* oLBB; float* oUBB;
   int8_t* oph; float* opar; float* ot; float* ogt;
   int* count_out; int cap;
+  int* nan_count;                    // nodes whose rigorous bound came back NaN (their partition stops)
   float* cand_buf; int* cand_count; int cand_cap;  // pinned records (x [n0], x' [n0], partition)
 };

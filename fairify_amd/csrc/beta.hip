@@ -445,7 +445,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FA_BETA_WPE
   // PA indices must be listed in increasing order for the popcount lookup (checked on the host)
 
   // ---- phase-clamped bounds, phases, |input| maxima
-  int bad = 0;
+  int bad = 0, fixd = 0;
   {
     const float* LB[2] = {a.LBA + (size_t)r * NH, a.LBB + (size_t)r * NH};
     const float* UB[2] = {a.UBA + (size_t)r * NH, a.UBB + (size_t)r * NH};
@@ -458,6 +458,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FA_BETA_WPE
         if (p > 0) lb = fmaxf(lb, 0.f);
         if (p < 0) ub = fminf(ub, 0.f);
         if (lb > ub) bad = 1;
+        if (p != 0) fixd = 1;
         S.lb[c][k] = lb;
         S.ub[c][k] = ub;
         S.ph[c][k] = (int8_t)p;
@@ -482,6 +483,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FA_BETA_WPE
   float* cur = a.scratch + (size_t)r * (a.feas ? 16 : 12) * NH;   // current
   float* mom = cur + 4 * NH;
   float* vel = cur + 8 * NH;
+  // crossed bounds prove the region empty only through a fixed phase: with none fixed they are not
+  // sound bounds of a non-empty box, so the node gets no bound (NaN: its partition stops, UNKNOWN)
+  const bool corrupt = __any(bad) && !__any(fixd);
   if (a.skip && a.skip[r]) bad = 1;         // closed before bounding: same outputs as an empty region
   if (a.feas) {
     // infeasibility pass: only nodes the main pass left open and that fix some phase
@@ -492,7 +496,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(FA_BETA_WPE
   }
   if (__any(bad)) {
     if (lane == 0) {
-      a.bound[r] = __builtin_inf();
+      a.bound[r] = (corrupt && !(a.skip && a.skip[r])) ? __builtin_nan("") : __builtin_inf();
       a.split[r] = -(2 * n0 + 1);
       a.binit[2 * r] = 0.f;
       a.binit[2 * r + 1] = 0.f;

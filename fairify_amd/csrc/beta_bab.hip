@@ -109,8 +109,17 @@ __global__ void __launch_bounds__(FA_THREADS) fa_bb_split_kernel(BetaPoolArgs a)
   for (int n = blockIdx.x * (FA_THREADS / 64) + wave; n < a.N; n += gridDim.x * (FA_THREADS / 64)) {
     if (a.skip[n]) continue;                                    // wave-uniform
     const double B = a.bound[n];
-    if (!(B < 0.0)) continue;                                   // closed (+inf: empty)
+    if (B >= 0.0) continue;                                     // closed (+inf: empty)
     const int p = a.part[n];
+    if (!(B < 0.0)) {
+      // NaN: the node has no bound, so its tree cannot close -- the partition stops (UNKNOWN), never
+      // counted as closed
+      if (lane == 0) {
+        a.status[p] = BB_STOPPING;
+        if (a.nan_count) atomicAdd(a.nan_count, 1);
+      }
+      continue;
+    }
     const int8_t st = a.status[p];
     if (st != BB_RUNNING && st != BB_STOPPING) continue;
     // ---- the concretising vertex pair, if its rigorous point bounds allow this orientation's violation

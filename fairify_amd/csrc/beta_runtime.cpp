@@ -234,13 +234,15 @@ class BetaRuntime {
     hout_.ensure(hn_off + (size_t)P * sizeof(int) + 16);
     bck(hipMemcpyAsync(hout_.p, status_.p, P, hipMemcpyDeviceToHost, st), "cp status out");
     bck(hipMemcpyAsync(hout_.p + hn_off, nodes_.p, P * sizeof(int), hipMemcpyDeviceToHost, st), "cp nodes out");
-    bck(hipMemcpyAsync(hout_.p + hn_off + (size_t)P * sizeof(int), counters_.p + 2, sizeof(int),
+    bck(hipMemcpyAsync(hout_.p + hn_off + (size_t)P * sizeof(int), counters_.p + 2, 2 * sizeof(int),
                        hipMemcpyDeviceToHost, st), "cp probe stops");
     bck(hipStreamSynchronize(st), "sync");
     const int8_t* hs = reinterpret_cast<const int8_t*>(hout_.p);
     const int* hn = reinterpret_cast<const int*>(hout_.p + hn_off);
     int probe_stops = 0;
     std::memcpy(&probe_stops, hout_.p + hn_off + (size_t)P * sizeof(int), sizeof(int));
+    int nan_nodes = 0;
+    std::memcpy(&nan_nodes, hout_.p + hn_off + (size_t)(P + 1) * sizeof(int), sizeof(int));
     std::vector<char> left(P, 0);
     if (timed_out && n_in > 0) {
       std::vector<int> lp((size_t)n_in);
@@ -266,6 +268,7 @@ class BetaRuntime {
     stats["nodes"] = total;
     stats["timed_out"] = timed_out;
     stats["probe_stop"] = probe_stops;
+    stats["nan_nodes"] = nan_nodes;
     stats["unknown"] = over;
     stats["time"] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return py::make_tuple(status_out, ax, axp, nodes_out, stats);
@@ -304,6 +307,7 @@ class BetaRuntime {
     a.oLBA = o.LBA.p; a.oUBA = o.UBA.p; a.oLBB = o.LBB.p; a.oUBB = o.UBB.p;
     a.oph = o.ph.p; a.opar = o.par.p; a.ot = o.t.p; a.ogt = relaxed_ ? o.gt.p : nullptr;
     a.count_out = counters_.p; a.cap = o.cap;
+    a.nan_count = counters_.p + 3;
     a.cand_buf = reinterpret_cast<float*>(cand_host_.p); a.cand_count = counters_.p + 1; a.cand_cap = cand_alloc_;
     return a;
   }

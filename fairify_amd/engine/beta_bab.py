@@ -336,6 +336,13 @@ class BetaBaBSolver:
             if empty is not None:
                 lev.bound = torch.where(empty, torch.full_like(lev.bound, float("inf")), lev.bound)
             closed = lev.bound >= 0
+            nan = torch.isnan(lev.bound)
+            if bool(nan.any()):
+                # a node without a bound cannot close its tree: its partition stops (UNKNOWN), as in the
+                # native loop (csrc/beta_bab.hip split kernel)
+                bad = np.unique(cur["part"][nan].cpu().numpy())
+                self.stats["nan_nodes"] = self.stats.get("nan_nodes", 0) + int(nan.sum())
+                status[bad[status[bad] == RUNNING]] = UNKNOWN
             leaf = lev.split == B.LEAF(n0)
             # candidate vertex pairs of the nodes that stay open (and the lattice leaves): rigorous
             # point bounds screen, then the exact check on the host
@@ -462,6 +469,8 @@ class BetaBaBSolver:
         self.stats["nodes"] = self.stats.get("nodes", 0) + int(stats["nodes"])
         if stats.get("probe_stop"):
             self.stats["probe_stop"] = self.stats.get("probe_stop", 0) + int(stats["probe_stop"])
+        if stats.get("nan_nodes"):
+            self.stats["nan_nodes"] = self.stats.get("nan_nodes", 0) + int(stats["nan_nodes"])
         return (np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes, dtype=np.int64))
 
     def _probe(self, pool, nodes_np, probed, probe_at: int, R0: int, tree_run, status, pre_closed=None) -> None:

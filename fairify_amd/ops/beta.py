@@ -492,6 +492,10 @@ def level_ref(ws32, bs32, widths, lo, hi, pa, va, vb, LBA, UBA, LBB, UBB, phA, p
                   L64(beB), t.to(d), rig=True, rx=rxc(par), osg=osg)
     B, lin, xs, coef = ev["B"], ev["lin"], ev["xs"], ev["coef"]
     B = torch.where(infeas, torch.full_like(B, float("inf")), B)
+    # crossed bounds with no fixed phase are not sound bounds of a non-empty box: no bound (NaN), the
+    # kernel's guard (csrc/beta.hip)
+    nofix = ~((phA != 0).any(1) | (phB != 0).any(1))
+    B = torch.where(infeas & nofix, torch.full_like(B, float("nan")), B)
     if feas_iters > 0:
         # the infeasibility pass (the kernel's second launch): nodes left open with a fixed phase
         fixed = (phA != 0).any(1) | (phB != 0).any(1)

@@ -358,3 +358,26 @@ def test_probe_verdicts_do_not_depend_on_grouping():
     single = np.array([BetaBaBSolver(be, q, cfg).solve(lo[k:k + 1], hi[k:k + 1], m).status[0]
                        for k in range(len(ids))])
     assert np.array_equal(whole, halves) and np.array_equal(whole, single)
+
+
+def test_crossed_bounds_without_a_fixed_phase_give_no_bound():
+    """A node whose pre-activation bounds cross (lb > ub) proves its region empty only through a fixed
+    phase.  With none fixed the bounds are not sound bounds of the (non-empty) box: the node gets no
+    bound (NaN) -- never +inf, which would close its tree -- in the reference and in the BaB loop."""
+    m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(3, fix=0.0)
+    R = lo.shape[0]
+    NH = bnd[0][0].shape[1]
+    LBA, UBA = bnd[0][0].clone(), bnd[0][1].clone()
+    LBA[0, 2] = UBA[0, 2] + 1.0            # row 0: crossed, no phase fixed
+    ph1 = [p.clone() for p in ph]
+    LBA[1, 3] = UBA[1, 3] + 1.0            # row 1: crossed on a neuron fixed inactive -> empty (inf)
+    ph1[0][1, 3] = 1
+    g = torch.Generator().manual_seed(0)
+    al = [torch.rand(R, NH, generator=g) for _ in range(2)]
+    be_ = [torch.zeros(R, NH) for _ in range(2)]
+    t = torch.full((R,), 0.5)
+    lev = B.level_ref(ws, bs, [x.shape[1] for x in ws[:-1]], lo, hi, pa, va, vb, LBA, UBA, bnd[1][0], bnd[1][1],
+                      ph1[0], ph1[1], al[0], al[1], be_[0], be_[1], t, iters=0, lr_a=0.1, lr_b=0.5, lr_t=0.1)
+    assert torch.isnan(lev.bound[0])
+    assert float(lev.bound[1]) == float("inf")
+    assert bool(torch.isfinite(lev.bound[2:]).all())

@@ -362,3 +362,29 @@ def test_beta_native_agrees_with_torch_loop(cuda, relaxed):
     assert both.sum() >= 0.5 * len(ids)
     assert bool((a[both] == b[both]).all())
     assert abs(int((a != UNKNOWN).sum()) - int((b != UNKNOWN).sum())) <= 0.1 * len(ids)
+
+
+def test_beta_kernel_crossed_bounds_without_fixed_phase_give_no_bound(cuda):
+    """Kernel twin of test_beta_bab.py::test_crossed_bounds_without_a_fixed_phase_give_no_bound: crossed
+    bounds with no fixed phase -> NaN (the native loop stops the partition), through a fixed phase ->
+    +inf (empty region)."""
+    m, ws, bs, pa, lo, hi, va, vb, bnd, ph = _setup(3, fix=0.0)
+    R = lo.shape[0]
+    NH = bnd[0][0].shape[1]
+    LBA, UBA = bnd[0][0].clone(), bnd[0][1].clone()
+    LBA[0, 2] = UBA[0, 2] + 1.0
+    phA = ph[0].clone()
+    LBA[1, 3] = UBA[1, 3] + 1.0
+    phA[1, 3] = 1
+    gb = Backend(m, cuda)
+    d = lambda x: x.to(cuda).contiguous()  # noqa: E731
+    g = torch.Generator().manual_seed(0)
+    al = [d(torch.rand(R, NH, generator=g)) for _ in range(2)]
+    be_ = [d(torch.zeros(R, NH)) for _ in range(2)]
+    lg = hip.beta_level(gb, d(lo), d(hi), pa, d(va), d(vb), d(LBA), d(UBA), d(bnd[1][0]), d(bnd[1][1]), d(phA),
+                        d(ph[1]), al[0], al[1], be_[0], be_[1], d(torch.full((R,), 0.5)), iters=0, lr_a=0.1,
+                        lr_b=0.5, lr_t=0.1)
+    b = lg.bound.cpu()
+    assert torch.isnan(b[0])
+    assert float(b[1]) == float("inf")
+    assert bool(torch.isfinite(b[2:]).all())
