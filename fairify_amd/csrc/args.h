@@ -487,5 +487,7 @@ struct BetaPoolArgs {
   int8_t* oph; float* opar; float* ot; float* ogt;
   int* count_out; int cap;
   int* nan_count;                    // nodes whose rigorous bound came back NaN (their partition stops)
+  int* diag;                         // root level: [0] nodes skipped as not RUNNING, [1] as relaxed-dead
+  int root;
   float* cand_buf; int* cand_count; int cand_cap;  // pinned records (x [n0], x' [n0], partition)
 };

@@ -42,6 +42,7 @@ __global__ void fa_bb_count_kernel(BetaPoolArgs a) {
     if (alive) atomicAdd(&a.part_nodes[p], 1);
   } else {
     a.skip[n] = alive ? 0 : 1;
+    if (a.root && !alive && a.diag) atomicAdd(a.diag + (a.status[p] == BB_RUNNING ? 1 : 0), 1);
   }
 }
 

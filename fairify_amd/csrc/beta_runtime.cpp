@@ -98,7 +98,7 @@ class BetaRuntime {
     Ue_.ensure(2 * B);
     lay_lb_.ensure(2 * B * nn_); lay_ub_.ensure(2 * B * nn_);
     cpts_.ensure(2 * B * n0_); pe_lb_.ensure(2 * B); pe_ub_.ensure(2 * B);
-    counters_.ensure(4);
+    counters_.ensure(8);
     hcount_buf_.ensure(4 * sizeof(int));
     hcount_ = reinterpret_cast<int*>(hcount_buf_.p);
     // fp64 host copy of the network for the exact confirmation
@@ -173,7 +173,7 @@ class BetaRuntime {
     bck(hipMemcpyAsync(part_closed_.p, stage_.p + o_c0, (size_t)P * sizeof(int), hipMemcpyDeviceToDevice, st),
         "cp closed0");
     bck(hipMemsetAsync(tree_done_.p, 0, std::max(R0, 1), st), "memset tree_done");
-    bck(hipMemsetAsync(counters_.p, 0, 4 * sizeof(int), st), "memset counters");   // [2]: probe stops
+    bck(hipMemsetAsync(counters_.p, 0, 8 * sizeof(int), st), "memset counters");   // [2]: probe stops
     copy_roots(roots, R0, st);
     bck(hipMemcpyAsync(pool_[0].tree.p, stage_.p + o_ti, (size_t)R0 * sizeof(int), hipMemcpyDeviceToDevice, st),
         "root tree ids");
@@ -208,6 +208,7 @@ class BetaRuntime {
         for (long long s = 0; s < n_in; s += batch_) {
           const int nb = (int)std::min<long long>(batch_, n_in - s);
           BetaPoolArgs a = pool_args(cur, nxt, s, nb, P, budget, warm_beta);
+          a.root = root ? 1 : 0;
           bckl(fa_bb_count_launch(a, st), "beta skip");          // a.count = 0: this slice's skip flags
           if (!root && tighten) tighten_slice(a, st);
           bound_slice(a, cur, s, nb, root ? root_iters : iters, lr_a * sc, lr_b * sc, lr_t * sc, decay, lookahead,
@@ -231,18 +232,27 @@ class BetaRuntime {
     }
     // results
     const size_t hn_off = ((size_t)P + 15) & ~size_t(15);
-    hout_.ensure(hn_off + (size_t)P * sizeof(int) + 16);
+    const size_t hc_off = hn_off + (size_t)P * sizeof(int) + 32;
+    hout_.ensure(hc_off + (size_t)P * sizeof(int));
+    bck(hipMemcpyAsync(hout_.p + hc_off, part_closed_.p, (size_t)P * sizeof(int), hipMemcpyDeviceToHost, st),
+        "cp closed out");
+    int dev_next = 0;     // the last level's child count as the device has it (the loop saw 0)
+    bck(hipMemcpyAsync(hout_.p + hn_off + (size_t)P * sizeof(int) + 16, counters_.p, sizeof(int),
+                       hipMemcpyDeviceToHost, st), "cp next count");
     bck(hipMemcpyAsync(hout_.p, status_.p, P, hipMemcpyDeviceToHost, st), "cp status out");
     bck(hipMemcpyAsync(hout_.p + hn_off, nodes_.p, P * sizeof(int), hipMemcpyDeviceToHost, st), "cp nodes out");
-    bck(hipMemcpyAsync(hout_.p + hn_off + (size_t)P * sizeof(int), counters_.p + 2, 2 * sizeof(int),
+    bck(hipMemcpyAsync(hout_.p + hn_off + (size_t)P * sizeof(int), counters_.p + 2, 4 * sizeof(int),
                        hipMemcpyDeviceToHost, st), "cp probe stops");
     bck(hipStreamSynchronize(st), "sync");
+    std::memcpy(&dev_next, hout_.p + hn_off + (size_t)P * sizeof(int) + 16, sizeof(int));
+    const int* hclosed = reinterpret_cast<const int*>(hout_.p + hc_off);
     const int8_t* hs = reinterpret_cast<const int8_t*>(hout_.p);
     const int* hn = reinterpret_cast<const int*>(hout_.p + hn_off);
     int probe_stops = 0;
     std::memcpy(&probe_stops, hout_.p + hn_off + (size_t)P * sizeof(int), sizeof(int));
-    int nan_nodes = 0;
+    int nan_nodes = 0, diag[2] = {0, 0};
     std::memcpy(&nan_nodes, hout_.p + hn_off + (size_t)(P + 1) * sizeof(int), sizeof(int));
+    std::memcpy(diag, hout_.p + hn_off + (size_t)(P + 2) * sizeof(int), 2 * sizeof(int));
     std::vector<char> left(P, 0);
     if (timed_out && n_in > 0) {
       std::vector<int> lp((size_t)n_in);
@@ -251,11 +261,27 @@ class BetaRuntime {
     }
     py::array_t<int8_t> status_out(P);
     py::array_t<int64_t> nodes_out(P);
+    // UNSAT needs positive evidence: every (pair, orientation) tree of the partition closed on the device
+    // (settle kernel) or before the search (closed0) -- a partition still running whose trees are not
+    // all closed (a loop that ended early) is UNKNOWN, never UNSAT
+    std::vector<int> trees(P, 0);
+    for (int k = 0; k < R0; ++k) ++trees[tree_part.data()[k]];
+    int unclosed = 0;
     int over = 0;
     for (int p = 0; p < P; ++p) {
       int8_t v = hs[p];
-      if (got[p]) v = 1;
-      else if (v == 3 || v == 4) v = left[p] ? 0 : 2;     // every node of every tree closed => UNSAT
+      if (got[p]) {
+        v = 1;
+      } else if (v == 3 || v == 4) {
+        if (left[p]) {
+          v = 0;
+        } else if (hclosed[p] >= trees[p] + closed0.data()[p]) {
+          v = 2;                                            // every node of every tree closed => UNSAT
+        } else {
+          v = 0;
+          ++unclosed;
+        }
+      }
       if (v == 0 && status0.data()[p] == 3 && !got[p]) ++over;
       status_out.mutable_data()[p] = v;
       nodes_out.mutable_data()[p] = hn[p];
@@ -269,7 +295,11 @@ class BetaRuntime {
     stats["timed_out"] = timed_out;
     stats["probe_stop"] = probe_stops;
     stats["nan_nodes"] = nan_nodes;
+    stats["root_skip_status"] = diag[0];
+    stats["root_skip_tau"] = diag[1];
     stats["unknown"] = over;
+    stats["unclosed"] = unclosed;
+    stats["dev_next"] = (!timed_out && levels > 0) ? dev_next : 0;
     stats["time"] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return py::make_tuple(status_out, ax, axp, nodes_out, stats);
   }
@@ -308,6 +338,7 @@ class BetaRuntime {
     a.oph = o.ph.p; a.opar = o.par.p; a.ot = o.t.p; a.ogt = relaxed_ ? o.gt.p : nullptr;
     a.count_out = counters_.p; a.cap = o.cap;
     a.nan_count = counters_.p + 3;
+    a.diag = counters_.p + 4;
     a.cand_buf = reinterpret_cast<float*>(cand_host_.p); a.cand_count = counters_.p + 1; a.cand_cap = cand_alloc_;
     return a;
   }

@@ -25,6 +25,7 @@ same search (the objective's sign per node).  CPU tests pin verdicts to brute-fo
 from __future__ import annotations
 
 import os
+import sys
 import time
 from dataclasses import dataclass, replace
 from typing import Optional
@@ -463,14 +464,41 @@ class BetaBaBSolver:
                                                  lo_np.astype(np.float32), hi_np.astype(np.float32), int(budget),
                                                  int(probe_at), float(time_budget), cfgd, confirm, stream,
                                                  np.zeros(P, np.int32) if pre_closed is None else pre_closed)
-        del arrs
         stats = dict(stats)
+        if os.environ.get("FAIRIFY_BETA_CHECK") and int(stats["levels"]) == 1 and \
+                int((np.asarray(st) == UNSAT).sum()) == int((status == RUNNING).sum()) > 0:
+            # diagnostics of a whole group closed at the root level (tools: exp W/X)
+            c = lambda x: x.detach().cpu()  # noqa: E731
+            lba, uba, lbb, ubb = c(pool["LBA"]), c(pool["UBA"]), c(pool["LBB"]), c(pool["UBB"])
+            print(f"[beta-check] P={P} R0={R0} osg={np.unique(c(pool['osg']).numpy()).tolist()} "
+                  f"ph_nnz={int((c(pool['phA']) != 0).sum() + (c(pool['phB']) != 0).sum())} "
+                  f"crossedA={int((lba > uba).sum())} crossedB={int((lbb > ubb).sum())} "
+                  f"nan={int(torch.isnan(lba).sum() + torch.isnan(uba).sum())} "
+                  f"t={np.unique(c(pool['t']).numpy())[:4].tolist()} "
+                  f"box_w={float((c(pool['hi']) - c(pool['lo'])).sum(1).min())} stats={stats}",
+                  file=sys.stderr, flush=True)
+            # the same roots through the torch loop's kernel call (one level, fresh tensors)
+            lev = be.beta_level(pool["lo"], pool["hi"], list(q.pa_idx), pool["va"], pool["vb"], pool["LBA"],
+                                pool["UBA"], pool["LBB"], pool["UBB"], pool["phA"], pool["phB"],
+                                pool["alA"].clone(), pool["alB"].clone(), pool["beA"].clone(), pool["beB"].clone(),
+                                pool["t"].clone(), cfg.root_iters, cfg.lr_a, cfg.lr_b, cfg.lr_t, cfg.decay,
+                                cfg.lookahead, cfg.beta_pos,
+                                (torch.zeros(n0, dtype=torch.bool, device=self.dev).index_fill_(
+                                    0, torch.tensor(ra, dtype=torch.long, device=self.dev), True) if ra else None,
+                                 pool["plo"], pool["phi"], tau, pool["gP"].clone(), pool["gM"].clone())
+                                if relaxed else None,
+                                pgap=cfg.pgap_weights if cfg.branch == "pgap" else 0, osg=pool["osg"])
+            b = lev.bound.cpu()
+            print(f"[beta-check] torch-call root bounds: closed {int((b >= 0).sum())} of {b.numel()}, "
+                  f"min {float(b.min()):.4g}", file=sys.stderr, flush=True)
+        del arrs
         self.stats["levels"] = self.stats.get("levels", 0) + int(stats["levels"])
         self.stats["nodes"] = self.stats.get("nodes", 0) + int(stats["nodes"])
         if stats.get("probe_stop"):
             self.stats["probe_stop"] = self.stats.get("probe_stop", 0) + int(stats["probe_stop"])
-        if stats.get("nan_nodes"):
-            self.stats["nan_nodes"] = self.stats.get("nan_nodes", 0) + int(stats["nan_nodes"])
+        for key in ("nan_nodes", "root_skip_status", "root_skip_tau", "unclosed", "dev_next"):
+            if stats.get(key):
+                self.stats[key] = self.stats.get(key, 0) + int(stats[key])
         return (np.asarray(st, dtype=np.int8), np.asarray(cx), np.asarray(cxp), np.asarray(nodes, dtype=np.int64))
 
     def _probe(self, pool, nodes_np, probed, probe_at: int, R0: int, tree_run, status, pre_closed=None) -> None:

@@ -7,6 +7,7 @@ GPU), and passes raw pointers + ``torch.cuda.current_stream().cuda_stream``.
 from __future__ import annotations
 
 import os
+import threading
 from typing import Optional, Sequence
 
 import torch
@@ -19,13 +20,23 @@ def _stream(dev) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
 
 
+# Per-backend / per-grid lazy device state is created under this lock: the runner's worker threads share
+# one Backend per model, and a second thread that built its own copy and published it over the first
+# freed the first thread's tensor while a native runtime still held its device pointer (the beta
+# runtime's transposed weights: whole chunks of beta roots bounded with freed memory, exp R6 W/X).
+_LAZY_LOCK = threading.Lock()
+
+
 def _net(be):
     n = getattr(be, "_hipnet", None)
     if n is None:
-        dims = [be.mlp.n_in] + be.mlp.widths
-        n = ext().Net(dims, be.unit)
-        assert n.total_floats == be.flat.numel(), (n.total_floats, be.flat.numel())
-        be._hipnet = n
+        with _LAZY_LOCK:
+            n = getattr(be, "_hipnet", None)
+            if n is None:
+                dims = [be.mlp.n_in] + be.mlp.widths
+                n = ext().Net(dims, be.unit)
+                assert n.total_floats == be.flat.numel(), (n.total_floats, be.flat.numel())
+                be._hipnet = n
     return n
 
 
@@ -60,10 +71,13 @@ def decode(grid, ids: torch.Tensor):
     tabs = grid.__dict__.setdefault("_dev_decode", {})
     key = str(dev)
     if key not in tabs:
-        d = grid.decode_desc()
-        cl = torch.from_numpy(d["chunk_lo"]).to(dev) if d["chunk_lo"].size else torch.zeros(1, device=dev)
-        ch = torch.from_numpy(d["chunk_hi"]).to(dev) if d["chunk_hi"].size else torch.zeros(1, device=dev)
-        tabs[key] = (d, cl, ch)
+        with _LAZY_LOCK:
+            if key not in tabs:
+                d = grid.decode_desc()
+                cl = torch.from_numpy(d["chunk_lo"]).to(dev) if d["chunk_lo"].size else torch.zeros(1, device=dev)
+                ch = torch.from_numpy(d["chunk_hi"]).to(dev) if d["chunk_hi"].size else torch.zeros(1, device=dev)
+                torch.cuda.current_stream(dev).synchronize()     # published tables are complete for every stream
+                tabs[key] = (d, cl, ch)
     d, cl, ch = tabs[key]
     n0 = int(d["radix"].shape[0])
     Pn = int(ids.shape[0])
@@ -605,11 +619,17 @@ def _beta_wt(be) -> torch.Tensor:
     if wt is None:
         import numpy as np
 
-        parts = []
-        for w, b in zip(be.mlp.weights, be.mlp.biases):
-            parts += [np.ascontiguousarray(np.asarray(w, np.float32).T).reshape(-1), np.zeros(np.size(b), np.float32)]
-        wt = torch.from_numpy(np.concatenate(parts)).to(be.device)
-        be._beta_wt = wt
+        with _LAZY_LOCK:          # built once: native runtimes keep its device pointer for the backend's life
+            wt = getattr(be, "_beta_wt", None)
+            if wt is None:
+                parts = []
+                for w, b in zip(be.mlp.weights, be.mlp.biases):
+                    parts += [np.ascontiguousarray(np.asarray(w, np.float32).T).reshape(-1),
+                              np.zeros(np.size(b), np.float32)]
+                wt = torch.from_numpy(np.concatenate(parts)).to(be.device)
+                if wt.is_cuda:
+                    torch.cuda.current_stream(wt.device).synchronize()   # complete for every stream
+                be._beta_wt = wt
     return wt
 
 

@@ -381,3 +381,29 @@ def test_crossed_bounds_without_a_fixed_phase_give_no_bound():
     assert torch.isnan(lev.bound[0])
     assert float(lev.bound[1]) == float("inf")
     assert bool(torch.isfinite(lev.bound[2:]).all())
+
+
+def test_beta_transposed_weights_are_built_once_under_concurrency():
+    """The runner's worker threads share one Backend per model; the native beta runtime keeps the device
+    pointer of the transposed weights (ops/hip.py:_beta_wt).  Racing first calls must all get the SAME
+    tensor -- a second copy published over the first freed the memory a runtime still read (whole chunks
+    of beta roots bounded with freed weights)."""
+    import threading
+
+    from fairify_amd.ops import hip
+
+    for trial in range(5):
+        be = Backend(random_mlp(6, [40, 30], seed=trial), device="cpu")
+        bar = threading.Barrier(12)
+        got = []
+
+        def one():
+            bar.wait()
+            got.append(hip._beta_wt(be))
+
+        th = [threading.Thread(target=one) for _ in range(12)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert len(got) == 12 and all(g is got[0] for g in got)
