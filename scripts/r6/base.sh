@@ -3,7 +3,7 @@
 # (tools/baseline_configs.py; GPU stages only for the big grids, Table V in anytime mode); one call
 # per part that fits the call limit, all parts under gpurun_out/r6base/ (report merges parts)
 set -o pipefail
-OUT=gpurun_out/r6base; mkdir -p $OUT
+OUT=${BASE_OUT:-gpurun_out/r6base}; mkdir -p $OUT
 G=$1; M=${2:-}; S=${3:-0}; N=${4:-}
 HEAD=$(cat HEAD_SHA 2>/dev/null || echo "")
 args="--group $G --out $OUT --head $HEAD"
